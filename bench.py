@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Benchmark: codewords/s of the fused T-iteration GNN decode on MI355X (BASELINE.json metric).
+
+Default workload = BASELINE.json configs[1]: BCH(63,45) Tanner-graph GNN decode
+(classical/CGNNI.py architecture, T = 25), batch 65 536 codewords per GPU, synthetic AWGN
+(SNR grid 1..6 dB), inputs resident in HBM before the timed region.  One "step" = one
+launch of the fused decoder over the whole batch (all T iterations + readout).
+
+Multi-GPU: one process per GPU (torchrun).  Codewords are independent, so every rank
+decodes its own batch (weak scaling) with no data-path collective; ranks only barrier
+around the timed region and all_reduce(MAX) the elapsed time.
+
+Output: one JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'gnn-decode_amd'))
+
+import gnndecode as gd  # noqa: E402
+
+# Algorithmic FLOPs per codeword: per edge per iteration the v->c side
+# costs 3 (variable sum, leave-one-out, + x) and the c->v side 55 (/2, check sum,
+# leave-one-out, MLP 1->10->1 = 51, residual); readout 55 per variable.  Transcendentals
+# (tanh, softplus) are counted separately and not included in FLOPs.
+def flops_per_codeword(model, g, T):
+    E, V = g.E, g.V
+    if model in ('cgnni', 'qgnni'):
+        return 58 * E * T + 55 * V, E * T
+    if model in ('cbp', 'qbp'):
+        return 17 * E * T + 4 * V, 6 * E * T
+    if model == 'v24':
+        return 1417 * E * T + 514 * E + 2 * V, 256 * E * T + 128 * E
+    raise ValueError(model)
+
+
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
+PEAK_FP64_TFLOPS = 78.6
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--model', default='cgnni', choices=list(gd.MODELS))
+    p.add_argument('--code', default='bch_63_45')
+    p.add_argument('--batch', type=int, default=65536, help='codewords per GPU')
+    p.add_argument('--iters', type=int, default=None)
+    p.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
+    p.add_argument('--cpu-seconds', type=float, default=12.0,
+                   help='bounded CPU-baseline sample (0 disables)')
+    p.add_argument('--seed', type=int, default=0)
+    return p.parse_args()
+
+
+def load_pmc_traffic(tag):
+    """HBM bytes per launch from a committed rocprofv3 --pmc summary (profiles/), or None."""
+    path = os.path.join(ROOT, 'profiles', f'pmc_{tag}.json')
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get('hbm_bytes_per_launch')
+    except Exception:
+        return None
+
+
+def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
+    """Time the oracle (numpy restatement, 1 thread) on a bounded sample of this workload
+    and compare its outputs with the GPU outputs for the same codewords."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import numpy as np
+    import gnn_oracle
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=1)
+    except Exception:
+        limiter = None
+    w = {k: v.detach().cpu().numpy() for k, v in state.items()}
+    chunk = 512
+    x_all = x_dev.view(-1, g.N)
+    o_all = out_dev.view(-1, g.V)
+    done, t_total, max_err, mism = 0, 0.0, 0.0, 0
+    while t_total < seconds and done + chunk <= x_all.size(0):
+        xs = x_all[done:done + chunk].cpu().numpy().reshape(-1, 1)
+        t0 = time.perf_counter()
+        ref = gnn_oracle.decode(model, H, xs, T, w)
+        t_total += time.perf_counter() - t0
+        got = o_all[done:done + chunk].double().cpu().numpy().reshape(-1, 1)
+        ref = ref.astype(np.float64)
+        max_err = max(max_err, float(np.abs(got - ref).max()))
+        mism += int(((got > 0.5) != (ref > 0.5)).sum())
+        done += chunk
+    if limiter is not None:
+        limiter.unregister() if hasattr(limiter, 'unregister') else None
+    return {'value': done / t_total if t_total > 0 else None, 'unit': 'codewords/s',
+            'cores': 1, 'kind': 'port',
+            'sample': f'{done} codewords of the same batch (chunks of {chunk}), oracle/gnn_oracle.py '
+                      f'numpy restatement, 1 thread, {t_total:.1f} s',
+            'parity_max_abs_err': max_err, 'parity_hard_decision_mismatches': mism,
+            'parity_bits_compared': done * g.V}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl')
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    T = a.iters or gd.DEFAULT_ITERS[a.model]
+    dtype = torch.float32 if a.dtype == 'f32' else torch.float64
+
+    H = gd.codes.get_code(a.code)
+    torch.manual_seed(a.seed)
+    model = gd.MODELS[a.model](T, H).to(dev).eval()
+    g = model.graph(dev)
+    state = model.state_dict()
+    classical = a.model in ('cgnni', 'cbp')
+    if classical:
+        x, labels = gd.data.awgn_batch(H, a.batch, codeword_bit=0, seed=a.seed * 1000 + rank,
+                                       device=dev, dtype=dtype)
+    else:
+        x, labels = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
+    w = model.prepared_weights(dtype, dev)
+    out = torch.empty(a.batch * g.V, 1, dtype=dtype, device=dev)
+
+    def step():
+        gd.ops.decode(g, a.model, x, T, w, out=out)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(a.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / a.steps        # HIP events, same stream
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # hard-decision error rate of this batch (outside the timed region)
+    with torch.no_grad():
+        errs = ((out > 0.5).to(labels.dtype) != labels).sum()
+        if world > 1:
+            dist.all_reduce(errs)
+    ber = float(errs.item()) / (a.batch * g.V * world)
+
+    if rank == 0:
+        fl, trans = flops_per_codeword(a.model, g, T)
+        achieved = fl * a.batch / kernel_s / 1e12
+        peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
+        esz = 4 if dtype == torch.float32 else 8
+        io_bytes = (g.N + g.V) * esz * a.batch
+        cw_cfg = gd.ops.decode_tile(g, a.model, dtype)
+        tag = f'{a.model}_{a.code}_B{a.batch}_T{T}_{a.dtype}'
+        traffic = load_pmc_traffic(tag)
+        res = {
+            'metric': 'codewords/sec (whole node) at matched BER, T-iter GNN decode',
+            'value': world * a.batch * a.steps / elapsed,
+            'unit': 'codewords/s',
+            'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+            'ms_per_step': elapsed / a.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': a.dtype, 'data': 'synthetic (on-device AWGN/toric sampler, seeded); random-init weights',
+            'config': {'workload': f'{a.code} {a.model} decode, T={T}, batch={a.batch}/GPU',
+                       'code': a.code, 'model': a.model, 'iters': T, 'batch_per_gpu': a.batch,
+                       'global_batch': a.batch * world, 'parallelism': f'dp{world} (codeword shards)',
+                       'codewords_per_workgroup': cw_cfg[0], 'lds_bytes_per_workgroup': cw_cfg[1],
+                       'hard_decision_error_rate': ber},
+            'roofline': {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
+                         'frac': achieved / peak, 'traffic': traffic,
+                         'kernel': f'decode_kernel<{a.model}, {a.dtype}>',
+                         'kernel_ms': kernel_s * 1e3,
+                         'flops_per_codeword': fl, 'transcendentals_per_codeword': trans,
+                         'hbm_io_bytes_per_launch': io_bytes,
+                         'hbm_io_frac': io_bytes / kernel_s / 1e9 / PEAK_HBM_GBS},
+        }
+        if a.cpu_seconds > 0 and world == 1:
+            res['cpu_baseline'] = cpu_baseline(a.model, H, state, x, out, g, T, a.cpu_seconds)
+        else:
+            res['cpu_baseline'] = None
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,118 @@
+// gnnd_common.h — shared device/host helpers for libgnnd (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include "../../include/gnnd.h"
+
+#define GNND_BLOCK 256
+
+// ---------------------------------------------------------------------------------------
+// host-side graph (owned by libgnnd, device-resident tables built once per H)
+// ---------------------------------------------------------------------------------------
+struct GraphView {            // passed by value to kernels
+    int V, C, E, N;
+    int max_dv, max_dc;
+    const uint32_t* edge_vc;  // [E]   v | (c << 16), reference edge order (sorted by v, c)
+    const int* var_ptr;       // [V+1] edges of variable v are [var_ptr[v], var_ptr[v+1])
+    const int* chk_ptr;       // [C+1]
+    const int* chk_edge;      // [E]   edge ids of check c, increasing (= increasing v)
+};
+
+struct gnnd_graph {
+    GraphView view;
+    void* dev;                // single device allocation holding the four tables
+    size_t table_bytes;       // bytes of the four tables (staged to LDS by the kernels)
+};
+
+// int tables staged to LDS in this order: edge_vc[E], var_ptr[V+1], chk_ptr[C+1], chk_edge[E]
+__host__ __device__ inline int graph_table_ints(int V, int C, int E) {
+    return E + (V + 1) + (C + 1) + E;
+}
+
+int set_hip_error(hipError_t e);   // records e, returns GNND_ERR_HIP
+
+#define GNND_HIP_CHECK(call)                                   \
+    do {                                                       \
+        hipError_t _e = (call);                                \
+        if (_e != hipSuccess) return set_hip_error(_e);        \
+    } while (0)
+
+#define GNND_LAUNCH_CHECK()                                    \
+    do {                                                       \
+        hipError_t _e = hipGetLastError();                     \
+        if (_e != hipSuccess) return set_hip_error(_e);        \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// division by a runtime-constant divisor (Granlund-Montgomery, n < 2^31)
+// ---------------------------------------------------------------------------------------
+struct FastDiv {
+    uint32_t d, m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+    FastDiv f;
+    f.d = d;
+    uint32_t l = 0;
+    while ((1u << l) < d) ++l;
+    f.s = l;
+    f.m = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+    return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+    return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+// ---------------------------------------------------------------------------------------
+// scalar math with reference (torch CPU) semantics, float and double overloads
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float g_tanh(float x) { return tanhf(x); }
+__device__ __forceinline__ double g_tanh(double x) { return tanh(x); }
+__device__ __forceinline__ float g_log(float x) { return logf(x); }
+__device__ __forceinline__ double g_log(double x) { return log(x); }
+__device__ __forceinline__ float g_exp(float x) { return expf(x); }
+__device__ __forceinline__ double g_exp(double x) { return exp(x); }
+__device__ __forceinline__ float g_log1p(float x) { return log1pf(x); }
+__device__ __forceinline__ double g_log1p(double x) { return log1p(x); }
+__device__ __forceinline__ float g_cos(float x) { return cosf(x); }
+__device__ __forceinline__ double g_cos(double x) { return cos(x); }
+__device__ __forceinline__ float g_abs(float x) { return fabsf(x); }
+__device__ __forceinline__ double g_abs(double x) { return fabs(x); }
+template <typename T> __device__ __forceinline__ T g_fma(T a, T b, T c) { return fma(a, b, c); }
+template <typename T> __device__ __forceinline__ T g_min(T a, T b) { return a < b ? a : b; }
+template <typename T> __device__ __forceinline__ T g_max(T a, T b) { return a > b ? a : b; }
+// torch.clamp(x, lo, hi) (NaN propagates)
+template <typename T> __device__ __forceinline__ T g_clamp(T x, T lo, T hi) {
+    return x < lo ? lo : (x > hi ? hi : x);
+}
+
+// torch.nn.Softplus(beta=1, threshold=20): x > 20 ? x : log1p(exp(x))
+__device__ __forceinline__ double softplus_ref(double x) {
+    return x > 20.0 ? x : log1p(exp(x));
+}
+// fp32 fast form on the native v_exp_f32 / v_log_f32 (base 2).  The caller passes
+// hs = h * log2(e) (folded into the layer-1 weights) and folds ln(2) into the layer-2
+// weights:  softplus(h) = ln2 * log2(1 + 2^hs).  The max() restates the threshold
+// branch (for hs > 28 the log term equals hs to within one ulp) and the min() keeps
+// 2^hs finite.  Absolute error vs log1p(exp(h)) <= ~1e-7 (1 + 2^hs rounds to 1 once
+// 2^hs < 2^-24).
+__device__ __forceinline__ float softplus2_fast(float hs) {
+    float e = __builtin_amdgcn_exp2f(fminf(hs, 28.0f));
+    float l = __builtin_amdgcn_logf(1.0f + e);
+    return fmaxf(hs, l);
+}
+
+template <typename T> __device__ __forceinline__ T sigmoid_ref(T x) {
+    return T(1) / (T(1) + g_exp(-x));
+}
+
+// (-1)^k for an integer-valued k; equals torch.cos(pi * k) exactly for |k| < ~1e3
+// (cos of k*pi rounded rounds to +-1 in both precisions), falling back to cos otherwise.
+template <typename T> __device__ __forceinline__ T cos_pi(T k) {
+    T r = rint(k);
+    if (r == k && g_abs(k) < T(1024)) {
+        int ki = (int)r;
+        return (ki & 1) ? T(-1) : T(1);
+    }
+    return g_cos(T(M_PI) * k);
+}

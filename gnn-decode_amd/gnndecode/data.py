@@ -1,0 +1,52 @@
+"""Synthetic decoder inputs in the reference's batch layout (graph-major, N = V + C rows).
+
+* classical (classical/CGNNI.py:125-147 `Gen_Data`, :157-161 `CustomDataset`): BPSK of a
+  fixed codeword, AWGN with sigma^2 = 10^(-SNR/10), LLR = 2 y / sigma^2 at the variable rows,
+  zeros at the check rows; SNR cycles over a grid per codeword.
+* toric (quantum/error_generate.py:252-278 `gen_syn`): per codeword p drawn from a grid,
+  independent X/Z flips with probability p, prior log((1-p)/p) at the variable rows and
+  syndrome (-1)^(H^T e) at the check rows; labels y = e.
+
+The distributions match the reference; the random streams do not (torch generators on the
+device, seeded).  Generation is outside every timed region.
+"""
+import math
+
+import torch
+
+
+def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=0, seed=0, device='cuda',
+               dtype=torch.float32):
+    V, C = H.shape
+    g = torch.Generator(device=device).manual_seed(seed)
+    snr = torch.tensor([snrs[b % len(snrs)] for b in range(B)], dtype=torch.float32, device=device)
+    sigma = torch.sqrt(1.0 / (10 ** (snr / 10)))
+    y = (1 - 2 * float(codeword_bit)) + sigma[:, None] * torch.randn(B, V, generator=g, device=device)
+    llr = 2 * y / (sigma[:, None] ** 2)
+    x = torch.cat([llr, torch.zeros(B, C, device=device)], dim=1)
+    labels = torch.full((B, V), float(codeword_bit), device=device)
+    return x.reshape(B * (V + C), 1).to(dtype), labels.reshape(B * V, 1).to(dtype)
+
+
+def toric_batch(H, B, ps=(0.01, 0.02, 0.03, 0.04, 0.05, 0.06, 0.07, 0.08, 0.09, 0.1), seed=0,
+                device='cuda', dtype=torch.float64):
+    Ht = torch.as_tensor(H, dtype=torch.float32, device=device)    # [V, C]
+    V, C = Ht.shape
+    g = torch.Generator(device=device).manual_seed(seed)
+    pgrid = torch.tensor(ps, dtype=torch.float64, device=device)
+    p = pgrid[torch.randint(len(ps), (B,), generator=g, device=device)]
+    e = (torch.rand(B, V, generator=g, device=device, dtype=torch.float64) < p[:, None]).float()
+    syn = torch.remainder(e @ Ht, 2)
+    prior = torch.log((1 - p) / p)[:, None].expand(B, V)
+    x = torch.cat([prior.to(torch.float64), (1 - 2 * syn).to(torch.float64)], dim=1)
+    return x.reshape(B * (V + C), 1).to(dtype), e.reshape(B * V, 1).to(dtype)
+
+
+def make_batch(x, graph, device=None):
+    """A minimal PyG-style batch object: .x, .edge_index (collated, unshifted)."""
+    class Batch:
+        pass
+    b = Batch()
+    b.x = x
+    b.edge_index = graph.batched_edge_index(x.numel() // graph.N, 0, device or x.device)
+    return b

@@ -1,0 +1,335 @@
+"""The reference decoders on the MI355X operator (same layer names and state_dict keys).
+
+Each class mirrors one reference script's `GNNI` (paths relative to
+/root/reference/GNN-decode/) so its checkpoints load with `load_state_dict`:
+
+  DecoderV24   quantum/decoder_v2_4.py:230-294   keys ggc1.mlp.{0,2}.*, ggc2.mlp.*, mlp.*
+  QGNNI        quantum/QGNNI.py:186-252           keys ggc{1,2}.mlp.*, mlp.*
+  QuantumBP    quantum/BP.py:179-219              (no parameters)
+  CGNNI        classical/CGNNI.py:212-284         keys ggc{1,2}.mlp{1,2}.*, ggc{1,2}.rnn.*, mlp.*
+  ClassicalBP  classical/BP.py:216-259            (no parameters)
+
+Differences from the reference, all at the call boundary: the parity-check matrix is
+passed to the constructor (`GNNI(Nc, H)`) instead of being read from module globals
+(`rows`, `cols`, `BATCH_SIZE`), and the batch size is derived from `data.x`.
+
+`forward(data)` runs the fused single-launch decoder (libgnnd `gnnd_decode`) whenever the
+batch is the tiled Tanner graph and no autograd graph is requested (eval mode or
+no_grad); otherwise it runs the reference's layer-by-layer loop on the device operator
+(`MessagePassing.propagate` -> gnnd_propagate_*).
+"""
+import torch
+
+from . import ops
+from .graph import TannerGraph
+from .nn import MessagePassing, ClassicalMessagePassing, message_passing_class
+
+_MP = {v: message_passing_class(v) for v in ('v24', 'qgnni', 'qbp', 'cbp')}
+_MP['cgnni'] = ClassicalMessagePassing
+
+
+def _mlp(fan_in, hidden, act, dtype):
+    return torch.nn.Sequential(torch.nn.Linear(fan_in, hidden).to(dtype), act,
+                               torch.nn.Linear(hidden, 1).to(dtype))
+
+
+def init_weights(m):
+    """quantum/decoder_v2_4.py:211-215: Kaiming-normal weights, zero bias."""
+    if type(m) == torch.nn.Linear:
+        torch.nn.init.kaiming_normal_(m.weight, a=0, mode='fan_in')
+        m.bias.data.fill_(0)
+
+
+def _flat_mlp(seq, split_inputs=False):
+    W1 = seq[0].weight
+    parts = [W1[:, k] for k in range(W1.size(1))] if split_inputs else [W1.reshape(-1)]
+    return parts + [seq[0].bias.reshape(-1), seq[2].weight.reshape(-1), seq[2].bias.reshape(-1)]
+
+
+# ---------------------------------------------------------------------------------------
+# layers
+# ---------------------------------------------------------------------------------------
+class GraphConvV24(_MP['v24']):
+    """quantum/decoder_v2_4.py:230-257."""
+
+    def __init__(self, flow, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        fan_in = 2 if flow == 'source_to_target' else 1
+        self.mlp = _mlp(fan_in, 128, torch.nn.Softplus(), torch.float64)
+        self.mlp.apply(init_weights)
+
+    def forward(self, m, edge_index, x, size=None):
+        x = x if x.dim() == 2 else x.unsqueeze(-1)
+        size = size or (x.size(0), x.size(0))
+        return self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
+
+    def update(self, aggr_out):
+        if self.flow == 'source_to_target':
+            return self.mlp(aggr_out.to(self.mlp[0].weight.dtype)).to(aggr_out.dtype)
+        u = aggr_out[:, 0:1].to(self.mlp[0].weight.dtype)
+        return self.mlp(u).to(aggr_out.dtype) * aggr_out[:, 1:2]
+
+
+class GraphConvQGNNI(_MP['qgnni']):
+    """quantum/QGNNI.py:186-214."""
+
+    def __init__(self, flow, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        self.mlp = _mlp(1, 10, torch.nn.ReLU(), torch.float64)
+
+    def forward(self, m, edge_index, x, size=None):
+        x = x if x.dim() == 2 else x.unsqueeze(-1)
+        size = size or (x.size(0), x.size(0))
+        return self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
+
+    def update(self, aggr_out):
+        if self.flow == 'target_to_source':
+            u = aggr_out[:, 0:1].to(self.mlp[0].weight.dtype)
+            return self.mlp(u).to(aggr_out.dtype) * aggr_out[:, 1:2]
+        return aggr_out
+
+
+class GatedGraphConvBP(MessagePassing):
+    """quantum/BP.py:179-188 and classical/BP.py:216-228 (variant set per script)."""
+
+    def __init__(self, flow, variant, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        self.variant = variant
+
+    def forward(self, m, edge_index, x=None, size=None):
+        if x is not None:
+            x = x if x.dim() == 2 else x.unsqueeze(-1)
+        n = x.size(0) if x is not None else None
+        size = size or (n, n)
+        return self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
+
+
+class GatedGraphConvCGNNI(ClassicalMessagePassing):
+    """classical/CGNNI.py:212-242 (mlp1 and rnn exist for state_dict compatibility only)."""
+
+    def __init__(self, flow, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        self.mlp1 = _mlp(1, 10, torch.nn.ReLU(), torch.float32)
+        self.mlp2 = _mlp(1, 10, torch.nn.ReLU(), torch.float32)
+        self.rnn = torch.nn.GRUCell(1, 1, bias=bias)
+
+    def forward(self, m, edge_index, x=None, size=None):
+        if x is not None:
+            x = x if x.dim() == 2 else x.unsqueeze(-1)
+        n = x.size(0) if x is not None else None
+        size = size or (n, n)
+        return self.propagate(edge_index=edge_index, size=size, x=m, post=x)
+
+    def update(self, aggr_out):
+        if self.flow == 'target_to_source':
+            return self.mlp2(aggr_out.to(self.mlp2[0].weight.dtype)).to(aggr_out.dtype)
+        return aggr_out
+
+
+# ---------------------------------------------------------------------------------------
+# decoders
+# ---------------------------------------------------------------------------------------
+class _Decoder(torch.nn.Module):
+    kind = None            # libgnnd model name
+    classical = False
+
+    def __init__(self, Nc, H):
+        super().__init__()
+        self.Nc = Nc
+        self.H = torch.as_tensor(H).detach().cpu()
+        self.rows, self.cols = int(self.H.size(0)), int(self.H.size(1))
+        self._graphs = {}
+        self._wcache = None
+
+    # ---- graph / weights on the device ------------------------------------------------
+    def graph(self, device):
+        key = str(device)
+        g = self._graphs.get(key)
+        if g is None:
+            g = TannerGraph(self.H, device=device)
+            self._graphs[key] = g
+            for mod in self.modules():
+                if isinstance(mod, MessagePassing):
+                    mod.bind_graph(g)
+        return g
+
+    def packed_weights(self):
+        """Flat weights in the gnnd.h layout (model parameter dtype)."""
+        return None
+
+    def prepared_weights(self, dtype, device):
+        key = (dtype, str(device), tuple(p._version for p in self.parameters()),
+               tuple(p.data_ptr() for p in self.parameters()))
+        if self._wcache is not None and self._wcache[0] == key:
+            return self._wcache[1]
+        flat = self.packed_weights()
+        if flat is None:
+            return None
+        prep = ops.prepare_weights(self.kind, flat.detach().to(device=device, dtype=dtype))
+        self._wcache = (key, prep)
+        return prep
+
+    def fused_ok(self, x, edge_index):
+        if not x.is_cuda or x.dtype not in (torch.float32, torch.float64):
+            return False
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+            return False
+        g = self.graph(x.device)
+        if x.numel() % g.N or edge_index.size(1) != (x.numel() // g.N) * g.E:
+            return False
+        return g.is_tiled(edge_index, 0)
+
+    def forward(self, data):
+        x, edge_index = data.x, data.edge_index
+        if x.dim() == 1:
+            x = x.unsqueeze(1)
+        if self.fused_ok(x, edge_index):
+            g = self.graph(x.device)
+            return ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(x.dtype, x.device))
+        if not x.is_cuda:
+            raise RuntimeError('gnndecode runs on the GPU only (HIP/gfx950); move data to cuda')
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError('training through the device operator is not implemented '
+                                      'yet: run inference in eval mode or under torch.no_grad()')
+        self.graph(x.device)
+        return self.forward_layers(x, edge_index)
+
+    # ---- reference layer-by-layer loop on the device operator ---------------------------
+    def _shifted(self, edge_index):
+        return torch.stack([edge_index[0], edge_index[1] + self.rows])
+
+    def _var_rows(self, t, B):
+        N = self.rows + self.cols
+        return t.reshape(B, N, -1)[:, :self.rows].reshape(B * self.rows, -1)
+
+    def _var_sum(self, m, edge_index, nodes):
+        out = torch.zeros(nodes, m.size(1), dtype=m.dtype, device=m.device)
+        return out.index_add_(0, edge_index[0], m)
+
+    def forward_layers(self, x, edge_index):
+        raise NotImplementedError
+
+
+class DecoderV24(_Decoder):
+    """quantum/decoder_v2_4.py:260-294 (T = Nc = 15 in the reference)."""
+    kind = 'v24'
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.ggc1 = GraphConvV24('source_to_target')
+        self.ggc2 = GraphConvV24('target_to_source')
+        self.mlp = _mlp(1, 128, torch.nn.Softplus(), torch.float64)
+        self.mlp.apply(init_weights)
+
+    def packed_weights(self):
+        return torch.cat(_flat_mlp(self.ggc1.mlp, split_inputs=True) + _flat_mlp(self.ggc2.mlp)
+                         + _flat_mlp(self.mlp))
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        for _ in range(self.Nc):
+            m_p = m
+            m = self.ggc1(m, ei, x)
+            m = self.ggc2(m, ei, x) + m_p
+        f = self.mlp(m.to(self.mlp[0].weight.dtype)).to(x.dtype)
+        res = self._var_rows(self._var_sum(f, ei, x.size(0)), B) + self._var_rows(x, B)
+        return torch.sigmoid(-res)
+
+
+class QGNNI(_Decoder):
+    """quantum/QGNNI.py:217-252 (T = 25)."""
+    kind = 'qgnni'
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.ggc1 = GraphConvQGNNI('source_to_target')
+        self.ggc2 = GraphConvQGNNI('target_to_source')
+        self.mlp = _mlp(1, 10, torch.nn.ReLU(), torch.float64)
+
+    def packed_weights(self):
+        return torch.cat(_flat_mlp(self.ggc2.mlp) + _flat_mlp(self.mlp))
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        for _ in range(self.Nc):
+            m_p = m
+            m = self.ggc1(m, ei, x)
+            m = self.ggc2(m, ei, x) + m_p
+        r = self._var_rows(self._var_sum(m, ei, x.size(0)) + x, B)
+        return torch.sigmoid(-self.mlp(r.to(self.mlp[0].weight.dtype)).to(x.dtype))
+
+
+class QuantumBP(_Decoder):
+    """quantum/BP.py:191-219 (T = 10)."""
+    kind = 'qbp'
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.ggc1 = GatedGraphConvBP('source_to_target', 'qbp')
+        self.ggc2 = GatedGraphConvBP('target_to_source', 'qbp')
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        for _ in range(self.Nc):
+            m = self.ggc1(m, ei, x)
+            m = self.ggc2(m, ei, x)
+        res = self._var_rows(self._var_sum(m, ei, x.size(0)), B) + self._var_rows(x, B)
+        return torch.sigmoid(-res)
+
+
+class CGNNI(_Decoder):
+    """classical/CGNNI.py:248-284 (T = 25)."""
+    kind = 'cgnni'
+    classical = True
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.ggc1 = GatedGraphConvCGNNI('source_to_target')
+        self.ggc2 = GatedGraphConvCGNNI('target_to_source')
+        self.mlp = _mlp(1, 10, torch.nn.ReLU(), torch.float32)
+
+    def packed_weights(self):
+        return torch.cat(_flat_mlp(self.ggc2.mlp2) + _flat_mlp(self.mlp))
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        for _ in range(self.Nc):
+            m_p = m
+            m = self.ggc1(m, ei, x)
+            m = self.ggc2(m, ei) + m_p
+        r = self._var_rows(self._var_sum(m, ei, x.size(0)) + x, B)
+        res = torch.sigmoid(-self.mlp(r.to(self.mlp[0].weight.dtype)).to(x.dtype))
+        return torch.clamp(res, 1e-7, 1 - 1e-7)
+
+
+class ClassicalBP(_Decoder):
+    """classical/BP.py:231-259 (T = 25)."""
+    kind = 'cbp'
+    classical = True
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.ggc1 = GatedGraphConvBP('source_to_target', 'cbp')
+        self.ggc2 = GatedGraphConvBP('target_to_source', 'cbp')
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        for _ in range(self.Nc):
+            m = self.ggc1(m, ei, x)
+            m = self.ggc2(m, ei, x)   # classical/BP.py:246 passes no x; the body ignores it
+        res = self._var_rows(self._var_sum(m, ei, x.size(0)) + x, B)
+        return torch.clamp(torch.sigmoid(-res), 1e-7, 1 - 1e-7)
+
+
+MODELS = {'v24': DecoderV24, 'qgnni': QGNNI, 'qbp': QuantumBP, 'cgnni': CGNNI, 'cbp': ClassicalBP}
+DEFAULT_ITERS = {'v24': 15, 'qgnni': 25, 'qbp': 10, 'cgnni': 25, 'cbp': 25}

@@ -1,0 +1,118 @@
+"""Tensor-level entry points over the C ABI (torch tensors only as device-memory plumbing).
+
+Every function here launches HIP kernels from libgnnd.so on the current HIP stream and
+never synchronises the host.  Inputs must already be on the GPU: there is no CPU path.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .graph import TannerGraph, current_stream, dtype_code
+
+MODELS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp')
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _require_gpu(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('gnndecode runs on the GPU only (HIP/gfx950); got a CPU tensor')
+
+
+def propagate_width(variant, flow):
+    return _lib.get().gnnd_propagate_width(_lib.VARIANT[variant], _lib.FLOW[flow])
+
+
+def propagate(variant, flow, aggr, edge_index, msg, extra, dim_size, graph=None, chk_shift=None):
+    """One reference `propagate` body on the device.
+
+    msg [nE, 1] per-edge message, extra [dim_size, 1] node tensor (or None for CGNNI's
+    `post=None`), edge_index int64 [2, nE].  Uses the tiled LDS kernel when `graph` matches
+    the batched edge_index, otherwise the generic (atomic) kernels.
+    Returns [nE, F] with F = propagate_width(variant, flow).
+    """
+    _require_gpu(edge_index, msg, extra)
+    if msg.dim() == 1:
+        msg = msg.unsqueeze(1)
+    if msg.size(-1) != 1:
+        raise ValueError('per-edge message must have one feature column (reference models)')
+    msg = msg.contiguous()
+    dt = dtype_code(msg.dtype)
+    if extra is not None:
+        if extra.dim() == 1:
+            extra = extra.unsqueeze(1)
+        extra = extra.to(msg.dtype).contiguous()
+    nE = msg.size(0)
+    if edge_index.size(1) != nE:
+        raise ValueError('edge_index and message disagree on the number of edges')
+    F = propagate_width(variant, flow)
+    out = torch.empty(nE, F, dtype=msg.dtype, device=msg.device)
+    v, f, a = _lib.VARIANT[variant], _lib.FLOW[flow], _lib.AGGR[aggr]
+    stream = current_stream(msg.device)
+    if extra is None and variant != 'cgnni':
+        raise ValueError(f'{variant}: propagate needs `extra`')
+    if graph is not None and aggr != 'mean':
+        shift = graph.V if chk_shift is None else chk_shift
+        if (dim_size == (nE // graph.E) * graph.N and (extra is None or extra.size(0) == dim_size)
+                and graph.is_tiled(edge_index, shift)):
+            _lib.call('gnnd_propagate_tiled', graph.handle, v, f, a, dt, _ptr(msg), _ptr(extra),
+                      _ptr(out), nE // graph.E, stream)
+            return out
+    ei = edge_index if edge_index.stride(1) == 1 else edge_index.contiguous()
+    ws_bytes = ctypes.c_int64()
+    _lib.call('gnnd_propagate_generic_workspace', v, f, a, dt, nE, dim_size, ctypes.byref(ws_bytes))
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=msg.device)
+    _lib.call('gnnd_propagate_generic', v, f, a, dt, _ptr(ei), ei.stride(0), nE, _ptr(msg),
+              _ptr(extra), dim_size, _ptr(out), _ptr(ws), ws_bytes.value, stream)
+    return out
+
+
+def weights_count(model):
+    n = ctypes.c_int64()
+    _lib.call('gnnd_weights_count', _lib.VARIANT[model], ctypes.byref(n))
+    return n.value
+
+
+def prepare_weights(model, flat):
+    """Kernel-layout copy of a packed weight vector (gnnd_prepare_weights)."""
+    n = weights_count(model)
+    if n == 0:
+        return None
+    _require_gpu(flat)
+    flat = flat.contiguous()
+    if flat.numel() != n:
+        raise ValueError(f'{model}: expected {n} packed weights, got {flat.numel()}')
+    out = torch.empty_like(flat)
+    _lib.call('gnnd_prepare_weights', _lib.VARIANT[model], dtype_code(flat.dtype), _ptr(flat),
+              _ptr(out), current_stream(flat.device))
+    return out
+
+
+def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None):
+    """Fused T-iteration decode: x [B*N(,1)] -> P(bit=1) [B*V, 1]."""
+    _require_gpu(x, prepared_weights)
+    x = x.contiguous()
+    if x.numel() % graph.N:
+        raise ValueError(f'x has {x.numel()} rows, not a multiple of N={graph.N}')
+    B = x.numel() // graph.N
+    nw = weights_count(model)
+    if nw and (prepared_weights is None or prepared_weights.numel() != nw):
+        raise ValueError(f'{model}: needs {nw} prepared weights')
+    if prepared_weights is not None and prepared_weights.dtype != x.dtype:
+        raise TypeError('weights and x must share a dtype')
+    if out is None:
+        out = torch.empty(B * graph.V, 1, dtype=x.dtype, device=x.device)
+    _lib.call('gnnd_decode', graph.handle, _lib.VARIANT[model], dtype_code(x.dtype),
+              _ptr(prepared_weights), _ptr(x), _ptr(out), B, int(iters), current_stream(x.device))
+    return out
+
+
+def decode_tile(graph, model, dtype):
+    cw, lds = ctypes.c_int32(), ctypes.c_int32()
+    _lib.call('gnnd_decode_tile', graph.handle, _lib.VARIANT[model], dtype_code(dtype),
+              ctypes.byref(cw), ctypes.byref(lds))
+    return cw.value, lds.value

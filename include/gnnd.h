@@ -1,0 +1,144 @@
+/*
+ * gnnd.h — C ABI of libgnnd.so, the MI355X-native (gfx950) GNN belief-propagation decoder.
+ *
+ * This is the drop-in boundary for the reference's hot path (paths relative to
+ * /root/reference/GNN-decode/):
+ *
+ *   MessagePassing.propagate()   quantum/decoder_v2_4.py:85-148, quantum/QGNNI.py:54-116,
+ *                                quantum/BP.py:54-124, classical/CGNNI.py:52-112,
+ *                                classical/BP.py:52-123       -> gnnd_propagate_tiled / _generic
+ *   scatter_ (PyG-1.x)           quantum/decoder_v2_4.py:34-51 -> aggregation inside the above
+ *   GNNI.forward() T-loop        classical/CGNNI.py:259-284, classical/BP.py:239-259,
+ *     + update() MLPs + readout  quantum/BP.py:199-219, quantum/QGNNI.py:228-252,
+ *                                quantum/decoder_v2_4.py:272-294 -> gnnd_decode
+ *   H.to_sparse()._indices()     quantum/decoder_v2_4.py:164-165 -> gnnd_graph_create
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no framework types.  Every pointer named d_* is DEVICE
+ *     memory owned by the caller; h_* is host memory.  Kernels never allocate.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  No function that
+ *     takes a stream synchronises the host, so every such call is graph-capturable.
+ *   - Every function returns a gnnd_status; nothing throws or aborts.
+ *   - Batch layout is the reference's PyG collation (graph-major): codeword b owns node rows
+ *     [b*N, (b+1)*N) with N = V + C (variable rows first, then check rows) and edge rows
+ *     [b*E, (b+1)*E) in the single-graph edge order (sorted by (v, c)).
+ */
+#ifndef GNND_H
+#define GNND_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNND_VERSION 1
+
+typedef enum gnnd_status {
+    GNND_OK = 0,
+    GNND_ERR_INVALID_ARG = 1,   /* bad pointer / size / enum value                     */
+    GNND_ERR_HIP = 2,           /* a HIP runtime call failed (see gnnd_last_hip_error)  */
+    GNND_ERR_UNSUPPORTED = 3,   /* valid request this build does not implement         */
+    GNND_ERR_GRAPH = 4,         /* edge list is not a valid Tanner graph                */
+    GNND_ERR_ALLOC = 5          /* device allocation failed (graph creation only)       */
+} gnnd_status;
+
+typedef enum gnnd_dtype { GNND_F32 = 0, GNND_F64 = 1 } gnnd_dtype;
+
+/* `flow` of MessagePassing (quantum/decoder_v2_4.py:73-74,89):
+ *   SOURCE_TO_TARGET: aggregate at edge_index[0] (variable nodes)  = v->c message
+ *   TARGET_TO_SOURCE: aggregate at edge_index[1] (check nodes)     = c->v message     */
+typedef enum gnnd_flow { GNND_SOURCE_TO_TARGET = 0, GNND_TARGET_TO_SOURCE = 1 } gnnd_flow;
+
+/* `aggr` of MessagePassing (quantum/decoder_v2_4.py:70-71); PyG-1.x scatter_ rules. */
+typedef enum gnnd_aggr { GNND_AGGR_ADD = 0, GNND_AGGR_MEAN = 1, GNND_AGGR_MAX = 2 } gnnd_aggr;
+
+/* Which reference script's propagate body (the scripts each carry their own copy):
+ *   V24    quantum/decoder_v2_4.py:132-144  c->v tanh(x/2); both flows cat extra[idx_j] (F=2)
+ *   QGNNI  quantum/QGNNI.py:101-112         c->v tanh(x/2), cat (F=2); v->c + extra (F=1)
+ *   QBP    quantum/BP.py:101-119            c->v log-domain BP with syndrome; v->c + extra
+ *   CGNNI  classical/CGNNI.py:99-108        c->v tanh(x/2); + post (if non-NULL) (F=1)
+ *   CBP    classical/BP.py:99-119           c->v log-domain BP; v->c + extra (F=1)        */
+typedef enum gnnd_variant {
+    GNND_V24 = 0, GNND_QGNNI = 1, GNND_QBP = 2, GNND_CGNNI = 3, GNND_CBP = 4
+} gnnd_variant;
+
+/* Whole-decoder models for gnnd_decode (same enumerators as gnnd_variant). */
+typedef gnnd_variant gnnd_model;
+
+typedef struct gnnd_graph gnnd_graph;   /* opaque; device-resident single-codeword graph */
+
+/* ---- graph --------------------------------------------------------------------------
+ * Build the single-codeword Tanner graph from its edge list, i.e. the reference's
+ * `H.to_sparse()._indices()` of H[V, C] (row 0 = variable, row 1 = check), which must be
+ * sorted by (v, c) with no duplicates.  Replaces the per-batch int64 edge_index reads of
+ * the reference (quantum/decoder_v2_4.py:164-165, 277) with a cached CSR/CSC.          */
+int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
+                      int32_t num_var, int32_t num_chk, gnnd_graph** out);
+int gnnd_graph_destroy(gnnd_graph* g);
+/* dims[0..5] = V, C, E, N, max variable degree, max check degree */
+int gnnd_graph_dims(const gnnd_graph* g, int32_t* h_dims6);
+
+/* Check on the device that a batched edge_index (int64, rows 0/1 at d_edge_index and
+ * d_edge_index + row_stride, num_batched_edges columns) is the single graph tiled over
+ * `batch` codewords with node offset b*N and check ids shifted by `chk_shift` (V after
+ * GNNI.forward's shift, 0 before it).  Writes 1 (tiled) / 0 to *d_flag (device int32). */
+int gnnd_check_tiled(const gnnd_graph* g, const int64_t* d_edge_index, int64_t row_stride,
+                     int64_t num_batched_edges, int64_t batch, int64_t chk_shift,
+                     int32_t* d_flag, void* stream);
+
+/* ---- operator: one propagate() call ---------------------------------------------------
+ * Tiled fast path (aggr ADD or MAX).  d_msg [B*E] (the per-edge `x` kwarg), d_extra [B*N]
+ * (the `extra`/`post` argument; may be NULL only for CGNNI), d_out [B*E, F] row-major with
+ * F = gnnd_propagate_width(variant, flow).  dtype selects float/double for all three.    */
+int gnnd_propagate_width(int variant, int flow);
+int gnnd_propagate_tiled(const gnnd_graph* g, int variant, int flow, int aggr, int dtype,
+                         const void* d_msg, const void* d_extra, void* d_out, int64_t batch,
+                         void* stream);
+
+/* Generic path for an arbitrary edge_index (any aggr, including the reference's literal
+ * leave-one-out `mean`).  Uses float atomics for the scatter, so sums are order-dependent
+ * in the last bits.  d_workspace must hold gnnd_propagate_generic_workspace() bytes.    */
+int gnnd_propagate_generic_workspace(int variant, int flow, int aggr, int dtype,
+                                     int64_t num_edges, int64_t dim_size, int64_t* h_bytes);
+int gnnd_propagate_generic(int variant, int flow, int aggr, int dtype,
+                           const int64_t* d_edge_index, int64_t row_stride, int64_t num_edges,
+                           const void* d_msg, const void* d_extra, int64_t dim_size,
+                           void* d_out, void* d_workspace, int64_t workspace_bytes,
+                           void* stream);
+
+/* ---- fused T-iteration decoder --------------------------------------------------------
+ * Runs the whole GNNI.forward (m0 = 0, T iterations of both half-steps, residual, readout)
+ * for `batch` codewords in one launch; messages never leave the CU.
+ *   d_x   [B*N]   node features (priors/LLRs at variable rows, syndrome at check rows)
+ *   d_out [B*V]   P(bit = 1)  (sigmoid(-readout), clamped for the classical models)
+ *   d_w   weights in `dtype` as produced by gnnd_prepare_weights from the packed
+ *         state_dict layout below (gnnd_weights_count elements, same count after prepare):
+ *     CGNNI: ggc2.mlp2 {W1[10], b1[10], W2[10], b2}, mlp {W1[10], b1[10], W2[10], b2}  = 62
+ *     QGNNI: ggc2.mlp  {W1[10], b1[10], W2[10], b2}, mlp {same}                          = 62
+ *     V24:   ggc1.mlp  {W1[:,0][128], W1[:,1][128], b1[128], W2[128], b2},
+ *            ggc2.mlp  {W1[128], b1[128], W2[128], b2}, mlp {W1[128], b1[128], W2[128], b2}
+ *                                                                                    = 1283
+ *     CBP, QBP: none (d_w may be NULL)
+ * gnnd_prepare_weights converts that layout into the kernel layout (for the fp32 V24
+ * kernel the softplus layers are rescaled to base 2: layer-1 rows * log2(e), layer-2
+ * weights * ln(2); every other model/dtype is a plain copy).  Call it once per weights. */
+int gnnd_weights_count(int model, int64_t* h_count);
+int gnnd_prepare_weights(int model, int dtype, const void* d_w, void* d_prepared,
+                         void* stream);
+int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
+                void* d_out, int64_t batch, int32_t iters, void* stream);
+
+/* Codewords per workgroup the decoder would use (for roofline bookkeeping). */
+int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32_t* h_cw_per_block,
+                     int32_t* h_lds_bytes);
+
+/* ---- misc ----------------------------------------------------------------------------- */
+const char* gnnd_status_string(int status);
+int gnnd_last_hip_error(void);          /* hipError_t of the last GNND_ERR_HIP, per thread */
+int gnnd_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNND_H */

@@ -1,0 +1,310 @@
+"""ORACLE — test infrastructure only.  CPU (numpy) restatement of the reference hot path.
+
+This module is the CHECKER for the HIP path.  Only `tests/`, `__graft_entry__.smoke()` and
+`bench.py`'s `cpu_baseline` leg may import it; the product package (`gnn-decode_amd/gnndecode`)
+never does, and has no CPU fallback.
+
+It restates, in vectorised numpy, the `MessagePassing.propagate()` T-iteration decode loop of
+ironmanaudi/GNN-decode (paths relative to /root/reference/GNN-decode/):
+
+* `propagate()`           quantum/decoder_v2_4.py:85-148, quantum/QGNNI.py:54-116,
+                          quantum/BP.py:54-124, classical/CGNNI.py:52-112, classical/BP.py:52-123
+* `scatter_`              quantum/decoder_v2_4.py:34-51 (PyG-1.x utils.scatter_ replica),
+                          local `scatter_mean` quantum/decoder_v2_4.py:27-31
+* `GNNI.forward()`        classical/CGNNI.py:259-284, classical/BP.py:239-259,
+                          quantum/BP.py:199-219, quantum/QGNNI.py:228-252,
+                          quantum/decoder_v2_4.py:272-294
+* `update()` MLPs         classical/CGNNI.py:238-242, quantum/QGNNI.py:207-214,
+                          quantum/decoder_v2_4.py:253-257
+
+Parity pinning: every function here is checked against golden vectors produced by running the
+reference's own class definitions (tests/golden/make_golden.py) in tests/test_oracle_golden.py.
+Aggregations use `np.add.at`, which accumulates sequentially in edge order — the order of
+CPU torch_scatter / `index_add_` — so leave-one-out sums match the reference bit for bit up
+to the BLAS summation order inside the MLPs.
+
+Batch layout (A10): graph-major.  `x` is [B*N, 1] with N = V + C per codeword
+(variable rows first, then check rows), output is [B*V, 1].
+"""
+import numpy as np
+
+SCRIPTS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp')
+
+
+def tanner_edges(H):
+    """Single-codeword edge list of H [V, C], sorted by (v, c) like `H.to_sparse()._indices()`
+    (quantum/decoder_v2_4.py:164-165, classical/CGNNI.py:153-154)."""
+    v, c = np.nonzero(np.asarray(H))
+    return v.astype(np.int64), c.astype(np.int64)
+
+
+def batched_edge_index(H, B):
+    """PyG-1.x collation (node offset b*N) followed by GNNI.forward's check shift by V
+    (quantum/decoder_v2_4.py:277)."""
+    V, C = np.asarray(H).shape
+    N = V + C
+    v, c = tanner_edges(H)
+    off = np.repeat(np.arange(B, dtype=np.int64) * N, v.size)
+    return np.stack([np.tile(v, B) + off, np.tile(c, B) + V + off])
+
+
+# ---------------------------------------------------------------------------------------
+# scatter_ / propagate (operator level)
+# ---------------------------------------------------------------------------------------
+def scatter_(name, src, index, dim_size):
+    """PyG-1.x `scatter_` (quantum/decoder_v2_4.py:34-51): add / local leave-one-out mean /
+    max with fill -1e9 mapped to 0."""
+    src = np.asarray(src)
+    out_shape = (dim_size,) + src.shape[1:]
+    if name == 'add':
+        out = np.zeros(out_shape, src.dtype)
+        np.add.at(out, index, src)
+        return out
+    if name == 'mean':   # the local scatter_mean is already gathered & leave-one-out (:27-31)
+        s = np.zeros(out_shape, src.dtype)
+        np.add.at(s, index, src)
+        cnt = np.zeros(out_shape, src.dtype)
+        np.add.at(cnt, index, np.ones_like(src))
+        num = s[index] - src
+        den = np.maximum(cnt[index] - 1, 1)
+        return num / den
+    if name == 'max':
+        out = np.full(out_shape, -1e9, src.dtype)
+        np.maximum.at(out, index, src)
+        out[out == src.dtype.type(-1e9)] = 0
+        return out
+    raise ValueError(name)
+
+
+def _extrinsic(aggr, src, idx, dim_size):
+    """`scatter_(aggr, out, idx, dim_size)[idx] - out` (quantum/decoder_v2_4.py:136,138).
+    For 'mean' the reference's scatter_mean already returns the gathered leave-one-out
+    mean, which is then indexed again by `[idx]` — restated literally."""
+    agg = scatter_(aggr, src, idx, dim_size)
+    return agg[idx] - src
+
+
+def propagate(script, flow, aggr, edge_index, msg, extra, dim_size):
+    """Bare `MessagePassing.propagate(edge_index, extra, size=(dim_size,)*2, x=msg)` with the
+    base class's identity `message`/`update`, per reference script variant:
+
+    * v24   quantum/decoder_v2_4.py:132-146  (c->v tanh(x/2); both flows cat extra[idx_j])
+    * qgnni quantum/QGNNI.py:101-114         (c->v tanh(x/2), cat; v->c + extra)
+    * qbp   quantum/BP.py:101-121            (c->v log-domain BP with syndrome; v->c + extra)
+    * cgnni classical/CGNNI.py:99-110        (c->v tanh(x/2); `post` added if not None)
+    * cbp   classical/BP.py:99-121           (c->v log-domain BP; v->c + extra)
+    """
+    ei = np.asarray(edge_index)
+    i, j = (0, 1) if flow == 'target_to_source' else (1, 0)
+    idx = ei[j]
+    out = np.asarray(msg)
+    dt = out.dtype.type
+    if script in ('qbp', 'cbp') and flow == 'target_to_source':
+        lo = 1e-20 if script == 'qbp' else 1e-7
+        hi = 1 - 1e-12 if script == 'qbp' else 1 - 1e-7
+        out = np.clip(out, dt(-10), dt(10))
+        out = np.tanh(out / dt(2))
+        coeff = np.where(out < 0, dt(1), dt(0))
+        out = np.abs(out)
+        out = np.clip(out, dt(lo), dt(1e10))
+        out = np.log(out)
+        out = _extrinsic(aggr, out, idx, dim_size)
+        coeff = _extrinsic(aggr, coeff, idx, dim_size)
+        if script == 'qbp':
+            coeff = np.cos(dt(np.pi) * (coeff + (dt(1) - extra[idx]) / dt(2)))
+        else:
+            coeff = np.cos(dt(np.pi) * coeff)
+        out = np.exp(out) * coeff
+        out = np.clip(out, dt(-hi), dt(hi))
+        if script == 'qbp':
+            out = np.log(dt(1) + out) - np.log(dt(1) - out)
+        else:
+            out = np.log((dt(1) + out) / (dt(1) - out))
+        return out
+    if flow == 'target_to_source':
+        out = np.tanh(out / dt(2))
+    out = _extrinsic(aggr, out, idx, dim_size)
+    if script in ('qbp', 'cbp'):                       # v->c
+        return out + extra[idx]
+    if script == 'cgnni':
+        return out if extra is None else out + extra[idx]
+    if script == 'qgnni' and flow == 'source_to_target':
+        return out + extra[idx]
+    return np.concatenate([out, extra[idx]], axis=1)  # v24 both flows, qgnni c->v
+
+
+# ---------------------------------------------------------------------------------------
+# per-edge MLPs (torch.nn.Linear: y = x W^T + b)
+# ---------------------------------------------------------------------------------------
+def linear(x, W, b):
+    return x @ np.asarray(W, x.dtype).T + np.asarray(b, x.dtype)
+
+
+def softplus(x, threshold=20.0):
+    """torch.nn.Softplus(beta=1, threshold=20)."""
+    with np.errstate(over='ignore'):
+        return np.where(x > threshold, x, np.log1p(np.exp(np.minimum(x, threshold))))
+
+
+def relu(x):
+    return np.maximum(x, 0)
+
+
+def mlp(w, prefix, x, act):
+    h = linear(x, w[prefix + '0.weight'], w[prefix + '0.bias'])
+    return linear(act(h), w[prefix + '2.weight'], w[prefix + '2.bias'])
+
+
+def sigmoid(x):
+    with np.errstate(over='ignore'):
+        return 1 / (1 + np.exp(-x))
+
+
+# ---------------------------------------------------------------------------------------
+# whole-decoder restatements (single-graph structure, vectorised over the batch)
+# ---------------------------------------------------------------------------------------
+class _Graph:
+    def __init__(self, H):
+        H = np.asarray(H)
+        self.V, self.C = H.shape
+        self.N = self.V + self.C
+        self.v, self.c = tanner_edges(H)
+        self.E = self.v.size
+
+    def sum_var(self, m):           # m [B, E] -> [B, V]
+        out = np.zeros((m.shape[0], self.V), m.dtype)
+        np.add.at(out, (slice(None), self.v), m)
+        return out
+
+    def sum_chk(self, m):
+        out = np.zeros((m.shape[0], self.C), m.dtype)
+        np.add.at(out, (slice(None), self.c), m)
+        return out
+
+
+def _split_x(g, x):
+    x = np.asarray(x).reshape(-1, g.N)
+    return x[:, :g.V], x[:, g.V:]
+
+
+def _edge_mlp(w, prefix, u, act):
+    """Row-wise MLP on a per-edge scalar (or stacked feature) tensor [..., F] -> [...]."""
+    return mlp(w, prefix, u, act)[..., 0]
+
+
+def decode_cgnni(H, w, x, T):
+    """classical/CGNNI.py:259-284 (fp32, T=25)."""
+    g = _Graph(H)
+    xv, _ = _split_x(g, x)
+    dt = xv.dtype.type
+    m = np.zeros((xv.shape[0], g.E), xv.dtype)
+    for _ in range(T):
+        m_p = m
+        a = g.sum_var(m)[:, g.v] - m + xv[:, g.v]                  # ggc1: v->c, post = x
+        t = np.tanh(a / dt(2))                                       # ggc2: c->v
+        u = g.sum_chk(t)[:, g.c] - t
+        m = _edge_mlp(w, 'ggc2.mlp2.', u[..., None], relu) + m_p
+    r = g.sum_var(m) + xv
+    r = _edge_mlp(w, 'mlp.', r[..., None], relu)
+    out = np.clip(sigmoid(-r), dt(1e-7), dt(1 - 1e-7))
+    return out.reshape(-1, 1)
+
+
+def _bp_check(g, a, s, quantum):
+    dt = a.dtype.type
+    lo = 1e-20 if quantum else 1e-7
+    hi = 1 - 1e-12 if quantum else 1 - 1e-7
+    t = np.tanh(np.clip(a, dt(-10), dt(10)) / dt(2))
+    coeff = np.where(t < 0, dt(1), dt(0))
+    mag = np.log(np.clip(np.abs(t), dt(lo), dt(1e10)))
+    lam = g.sum_chk(mag)[:, g.c] - mag
+    n = g.sum_chk(coeff)[:, g.c] - coeff
+    if quantum:
+        n = n + (dt(1) - s[:, g.c]) / dt(2)
+    p = np.clip(np.exp(lam) * np.cos(dt(np.pi) * n), dt(-hi), dt(hi))
+    if quantum:
+        return np.log(dt(1) + p) - np.log(dt(1) - p)
+    return np.log((dt(1) + p) / (dt(1) - p))
+
+
+def decode_bp(H, x, T, quantum):
+    """classical/BP.py:239-259 (fp32, clamp output) / quantum/BP.py:199-219 (fp64)."""
+    g = _Graph(H)
+    xv, xc = _split_x(g, x)
+    dt = xv.dtype.type
+    m = np.zeros((xv.shape[0], g.E), xv.dtype)
+    for _ in range(T):
+        a = g.sum_var(m)[:, g.v] - m + xv[:, g.v]
+        m = _bp_check(g, a, xc, quantum)
+    r = g.sum_var(m) + xv
+    out = sigmoid(-r)
+    if not quantum:
+        out = np.clip(out, dt(1e-7), dt(1 - 1e-7))
+    return out.reshape(-1, 1)
+
+
+def decode_qgnni(H, w, x, T):
+    """quantum/QGNNI.py:228-252 (fp64, T=25)."""
+    g = _Graph(H)
+    xv, xc = _split_x(g, x)
+    dt = xv.dtype.type
+    m = np.zeros((xv.shape[0], g.E), xv.dtype)
+    for _ in range(T):
+        m_p = m
+        a = g.sum_var(m)[:, g.v] - m + xv[:, g.v]
+        t = np.tanh(a / dt(2))
+        u = g.sum_chk(t)[:, g.c] - t
+        m = _edge_mlp(w, 'ggc2.mlp.', u[..., None], relu) * xc[:, g.c] + m_p
+    r = g.sum_var(m) + xv
+    return sigmoid(-_edge_mlp(w, 'mlp.', r[..., None], relu)).reshape(-1, 1)
+
+
+def decode_v24(H, w, x, T):
+    """quantum/decoder_v2_4.py:272-294 (fp64, T=15)."""
+    g = _Graph(H)
+    xv, xc = _split_x(g, x)
+    dt = xv.dtype.type
+    m = np.zeros((xv.shape[0], g.E), xv.dtype)
+    for _ in range(T):
+        m_p = m
+        ext = g.sum_var(m)[:, g.v] - m
+        a = _edge_mlp(w, 'ggc1.mlp.', np.stack([ext, xv[:, g.v]], axis=-1), softplus)
+        t = np.tanh(a / dt(2))
+        u = g.sum_chk(t)[:, g.c] - t
+        m = _edge_mlp(w, 'ggc2.mlp.', u[..., None], softplus) * xc[:, g.c] + m_p
+    r = g.sum_var(_edge_mlp(w, 'mlp.', m[..., None], softplus)) + xv
+    return sigmoid(-r).reshape(-1, 1)
+
+
+def decode(model, H, x, T, w=None):
+    if model == 'cgnni':
+        return decode_cgnni(H, w, x, T)
+    if model == 'cbp':
+        return decode_bp(H, x, T, quantum=False)
+    if model == 'qbp':
+        return decode_bp(H, x, T, quantum=True)
+    if model == 'qgnni':
+        return decode_qgnni(H, w, x, T)
+    if model == 'v24':
+        return decode_v24(H, w, x, T)
+    raise ValueError(model)
+
+
+# ---------------------------------------------------------------------------------------
+# metrics (quantum/neural_BP.py:338-348 hard FER rule; classical BER)
+# ---------------------------------------------------------------------------------------
+def hard_decisions(p):
+    return (np.asarray(p) > 0.5).astype(np.uint8)
+
+
+def toric_failures(H, logical, y, p_hat):
+    """Residual-syndrome failure + logical failure counts for e + ê
+    (quantum/neural_BP.py:338-348 rule).  H [V, C], logical [4, V]."""
+    H = np.asarray(H, np.int64)
+    V = H.shape[0]
+    e = (np.asarray(y).reshape(-1, V).astype(np.int64) + hard_decisions(p_hat).reshape(-1, V)) % 2
+    syn = (e @ H) % 2
+    bad_syn = syn.any(axis=1)
+    lg = (e @ np.asarray(logical, np.int64).T) % 2
+    bad_log = (~bad_syn) & lg.any(axis=1)
+    return int(bad_syn.sum()), int(bad_log.sum())

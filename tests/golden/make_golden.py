@@ -1,0 +1,358 @@
+"""Golden-vector generator (container-only; NOT shipped, NOT run on the GPU box).
+
+Runs the reference's OWN class definitions on CPU to produce small seeded input/output
+fixtures (`tests/golden/*.npz`) that pin the oracle (`oracle/gnn_oracle.py`) and, through
+it, the HIP path.  Nothing from the reference is copied into the repo: at generation time
+this script reads the reference files under /root/reference as text, keeps only the named
+FunctionDef/ClassDef nodes (SURVEY.md Appendix C recipe) and `exec`s them against:
+
+* a `torch_scatter` 1.x shim: `scatter_add` = `zeros(dim_size).index_add_(0, idx, src)`
+  (sequential edge-order accumulation, as CPU torch_scatter) and `scatter_max` =
+  `full(fill).scatter_reduce('amax', include_self=True)`;
+* a PyG-1.x `scatter_` equal to the local replica at quantum/decoder_v2_4.py:34-51
+  (fill 0 for add/mean, -1e9 for max, fill mapped back to 0 for max);
+* `torch.Tensor.cuda = identity`, injected globals `rows`, `cols`, `BATCH_SIZE`, `H`;
+* PyG `Batch` collation restated: `edge_index` tiled with `b*N` node offsets.
+
+Checkpoints are read with `torch.load(..., weights_only=True)` only.
+Seeds are explicit (the reference sets none).
+
+Usage:  python tests/golden/make_golden.py      (writes tests/golden/*.npz)
+"""
+import ast
+import math
+import os
+import random
+import sys
+import types
+import inspect
+
+import numpy as np
+import torch
+
+REF = '/root/reference/GNN-decode'
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------------------
+# shims for the absent third-party packages (torch_scatter 1.x, torch_geometric <= 1.5)
+# --------------------------------------------------------------------------------------
+def _ts_scatter_add(src, index, dim=-1, out=None, dim_size=None, fill_value=0):
+    assert dim == 0
+    if dim_size is None:
+        dim_size = int(index.max()) + 1
+    res = torch.full((dim_size,) + tuple(src.shape[1:]), float(fill_value), dtype=src.dtype)
+    return res.index_add_(0, index, src)
+
+
+def _ts_scatter_max(src, index, dim=-1, out=None, dim_size=None, fill_value=None):
+    assert dim == 0
+    if dim_size is None:
+        dim_size = int(index.max()) + 1
+    fill = -1e9 if fill_value is None else float(fill_value)
+    res = torch.full((dim_size,) + tuple(src.shape[1:]), fill, dtype=src.dtype)
+    idx = index.view(-1, *([1] * (src.dim() - 1))).expand_as(src)
+    res = res.scatter_reduce(0, idx, src, reduce='amax', include_self=True)
+    return res, None
+
+
+def _ts_scatter_mean(src, index, dim=-1, out=None, dim_size=None, fill_value=0):
+    s = _ts_scatter_add(src, index, dim, out, dim_size, fill_value)
+    c = _ts_scatter_add(torch.ones_like(src), index, dim, None, s.size(0), 0)
+    return s / c.clamp(min=1)
+
+
+torch_scatter = types.ModuleType('torch_scatter')
+torch_scatter.scatter_add = _ts_scatter_add
+torch_scatter.scatter_max = _ts_scatter_max
+torch_scatter.scatter_mean = _ts_scatter_mean
+
+
+def pyg_scatter_(name, src, index, dim_size=None):
+    """PyG-1.x utils.scatter_ (same rule as the local replica at decoder_v2_4.py:34-51)."""
+    assert name in ['add', 'mean', 'max']
+    op = getattr(torch_scatter, 'scatter_{}'.format(name))
+    fill_value = -1e9 if name == 'max' else 0
+    out = op(src, index, 0, None, dim_size, fill_value)
+    if isinstance(out, tuple):
+        out = out[0]
+    if name == 'max':
+        out[out == fill_value] = 0
+    return out
+
+
+torch.Tensor.cuda = lambda self, *a, **k: self
+
+
+def load_ref(relpath, names, **globs):
+    path = os.path.join(REF, relpath)
+    tree = ast.parse(open(path).read(), path)
+    keep = []
+    for node in tree.body:
+        if isinstance(node, (ast.FunctionDef, ast.ClassDef)) and node.name in names:
+            keep.append(node)
+        elif isinstance(node, ast.Assign) and any(
+                isinstance(t, ast.Name) and t.id in ('special_args', '__size_error_msg__')
+                for t in node.targets):
+            keep.append(node)
+    ns = dict(torch=torch, math=math, inspect=inspect, np=np,
+              Variable=torch.autograd.Variable, F=torch.nn.functional,
+              torch_scatter=torch_scatter, scatter_add=_ts_scatter_add,
+              scatter_=pyg_scatter_)
+    ns.update(globs)
+    exec(compile(ast.Module(body=keep, type_ignores=[]), path, 'exec'), ns)
+    return ns
+
+
+def single_edge_index(H):
+    """H [V, C]; reference: `H.to_sparse()._indices()` (coalesced, sorted by (v, c))."""
+    return H.to_sparse()._indices()
+
+
+def batch_edge_index(ei, B, N):
+    """PyG-1.x collation: concatenate per-graph edge_index adding b*N (Batch.from_data_list)."""
+    E = ei.size(1)
+    off = torch.arange(B).repeat_interleave(E) * N
+    return ei.repeat(1, B) + off.unsqueeze(0)
+
+
+def set_seed(s):
+    random.seed(s)
+    np.random.seed(s)
+    torch.manual_seed(s)
+
+
+def bch_H():
+    Hm = np.loadtxt(os.path.join(REF, 'classical', 'BCH(63,45).txt'))   # [18, 63]
+    return torch.from_numpy(Hm).float().t()                                # [63, 18] as CGNNI.py:181
+
+
+def awgn_llr(B, n, codeword_bit, seed, snrs=(1, 2, 3, 4, 5, 6)):
+    """BPSK/AWGN LLRs following Gen_Data (classical/CGNNI.py:125-147): sigma^2 = 10^(-SNR/10),
+    y = (1-2c) + N(0, sigma^2), LLR = 2 y / sigma^2 (float32).  SNR cycles over the grid."""
+    g = torch.Generator().manual_seed(seed)
+    snr = torch.tensor([snrs[b % len(snrs)] for b in range(B)], dtype=torch.float32)
+    sigma = (1 / (10 ** (snr / 10))) ** 0.5
+    xm = 1 - 2 * float(codeword_bit)
+    noise = torch.normal(0.0, sigma.unsqueeze(1).repeat(1, n), generator=g)
+    y = xm + noise
+    llr = 2 * y * (1 / (sigma ** 2)).unsqueeze(1)
+    return llr.float(), snr
+
+
+def classical_x(llr, C):
+    """CustomDataset (classical/CGNNI.py:157-161): x = [LLR (V); zeros (C)] per codeword."""
+    B, V = llr.shape
+    x = torch.cat([llr, torch.zeros(B, C)], dim=1)
+    return x.reshape(B * (V + C), 1)
+
+
+def run_model(ns, H, x, B, T, state=None, dtype=torch.float32):
+    V, C = H.size(0), H.size(1)
+    N = V + C
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, B, H
+    ei = batch_edge_index(single_edge_index(H), B, N)
+    model = ns['GNNI'](T)
+    if state is not None:
+        model.load_state_dict(state)
+    data = types.SimpleNamespace(x=x, edge_index=ei)
+    with torch.no_grad():
+        out = model(data)
+    return out, model
+
+
+def sd_to_np(state):
+    return {'w/' + k: v.detach().cpu().numpy() for k, v in state.items()}
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name + '.npz')
+    np.savez_compressed(path, **arrays)
+    print('wrote', path, sum(a.nbytes for a in arrays.values()), 'bytes')
+
+
+# --------------------------------------------------------------------------------------
+def gen_classical():
+    H = bch_H()
+    V, C = H.shape
+    ei = single_edge_index(H)
+    save('bch_63_45_graph', H=H.numpy().astype(np.uint8), edge_index=ei.numpy())
+
+    # ---- CGNNI (classical/CGNNI.py), epoch-18 checkpoint, all-ones codeword
+    ns = load_ref('classical/CGNNI.py', {'MessagePassing', 'GatedGraphConv', 'GNNI'})
+    sd = torch.load(os.path.join(REF, 'classical/model/decoder_parameters_epoch18.pkl'),
+                    map_location='cpu', weights_only=True)
+    arrays = dict(sd_to_np(sd))
+    for B, seed in ((1, 11), (4, 12), (32, 13)):
+        llr, snr = awgn_llr(B, V, 1, seed)
+        x = classical_x(llr, C)
+        arrays[f'x_B{B}'] = x.numpy()
+        for T in (1, 2, 25):
+            out, _ = run_model(ns, H, x, B, T, sd)
+            arrays[f'out_B{B}_T{T}'] = out.numpy()
+    save('cgnni_bch', **arrays)
+
+    # CGNNI with seeded random init (different weights exercise other MLP regions)
+    set_seed(101)
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, 8, H
+    m0 = ns['GNNI'](25)
+    sd_r = {k: v.clone() for k, v in m0.state_dict().items()}
+    arrays = dict(sd_to_np(sd_r))
+    llr, _ = awgn_llr(8, V, 0, 14)
+    x = classical_x(llr, C)
+    arrays['x_B8'] = x.numpy()
+    for T in (1, 25):
+        out, _ = run_model(ns, H, x, 8, T, sd_r)
+        arrays[f'out_B8_T{T}'] = out.numpy()
+    save('cgnni_bch_randinit', **arrays)
+
+    # ---- classical BP (classical/BP.py), all-zeros codeword
+    ns = load_ref('classical/BP.py', {'MessagePassing', 'GatedGraphConv', 'GNNI'})
+    arrays = {}
+    for B, seed in ((1, 21), (32, 22)):
+        llr, snr = awgn_llr(B, V, 0, seed)
+        x = classical_x(llr, C)
+        arrays[f'x_B{B}'] = x.numpy()
+        for T in (1, 2, 25):
+            out, _ = run_model(ns, H, x, B, T)
+            arrays[f'out_B{B}_T{T}'] = out.numpy()
+    save('bp_bch', **arrays)
+
+
+def toric_inputs(eg, H, L, P, run, seed):
+    set_seed(seed)
+    ds = eg.gen_syn(P, L, H, run)
+    xs = torch.cat([ds[i].t() for i in range(0, len(ds), 2)], dim=0)      # [B*N, 1]
+    ys = torch.cat([ds[i + 1].t() for i in range(0, len(ds), 2)], dim=0)  # [B*V, 1]
+    return xs.double(), ys.double()
+
+
+def gen_quantum():
+    sys.path.insert(0, os.path.join(REF, 'quantum'))
+    import error_generate as eg
+
+    # ---- toric code construction fixtures (quantum/error_generate.py)
+    for L in (4, 5, 7):
+        Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+        H = torch.from_numpy(Hnp).t()
+        h_prep = eg.H_Prep(H.t())
+        H_prep = torch.from_numpy(h_prep.get_H_Prep())
+        logical, stab = h_prep.get_logical(H_prep)
+        save(f'toric_L{L}_graph', H=H.numpy().astype(np.uint8),
+             edge_index=single_edge_index(H).numpy(),
+             logical=logical.numpy().astype(np.uint8))
+
+    def toric_H(L):
+        Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+        return torch.from_numpy(Hnp).t()
+
+    # seeded sampler draws (distribution reference for the on-device sampler)
+    H5 = toric_H(5)
+    xs, ys = toric_inputs(eg, H5, 5, [0.01, 0.05, 0.1], 64, 31)
+    save('toric_L5_gen_syn', x=xs.numpy(), y=ys.numpy())
+
+    # ---- quantum BP (quantum/BP.py), L = 4, T = 10
+    H4 = toric_H(4)
+    ns = load_ref('quantum/BP.py', {'MessagePassing', 'GatedGraphConv', 'GNNI'})
+    arrays = {}
+    for B, seed in ((1, 41), (32, 42)):
+        x, y = toric_inputs(eg, H4, 4, [0.05, 0.1], B, seed)
+        arrays[f'x_B{B}'], arrays[f'y_B{B}'] = x.numpy(), y.numpy()
+        for T in (1, 2, 10):
+            out, _ = run_model(ns, H4, x, B, T)
+            arrays[f'out_B{B}_T{T}'] = out.numpy()
+    save('bp_toric4', **arrays)
+
+    # ---- QGNNI (quantum/QGNNI.py), L = 4, T = 25, seeded default init
+    ns = load_ref('quantum/QGNNI.py', {'MessagePassing', 'GraphConv', 'GNNI'})
+    set_seed(51)
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = H4.size(0), H4.size(1), 1, H4
+    sd = {k: v.clone() for k, v in ns['GNNI'](25).state_dict().items()}
+    arrays = dict(sd_to_np(sd))
+    for B, seed in ((1, 52), (32, 53)):
+        x, y = toric_inputs(eg, H4, 4, [0.05, 0.1], B, seed)
+        arrays[f'x_B{B}'], arrays[f'y_B{B}'] = x.numpy(), y.numpy()
+        for T in (1, 2, 25):
+            out, _ = run_model(ns, H4, x, B, T, sd)
+            arrays[f'out_B{B}_T{T}'] = out.numpy()
+    save('qgnni_toric4', **arrays)
+
+    # ---- decoder_v2_4 (quantum/decoder_v2_4.py), L = 5, T = 15, epoch-67 checkpoint
+    names = {'scatter_mean', 'scatter_', 'MessagePassing', 'GraphConv', 'GNNI',
+             'init_weights', 'init_weights_2'}
+    ns = load_ref('quantum/decoder_v2_4.py', names)
+    sd = torch.load(os.path.join(REF, 'quantum/new_model/decoder_parameters_epoch67.pkl'),
+                    map_location='cpu', weights_only=True)
+    arrays = dict(sd_to_np(sd))
+    for B, seed in ((1, 61), (4, 62), (32, 63)):
+        x, y = toric_inputs(eg, H5, 5, [0.01, 0.05, 0.1], B, seed)
+        arrays[f'x_B{B}'], arrays[f'y_B{B}'] = x.numpy(), y.numpy()
+        for T in (1, 2, 15):
+            out, _ = run_model(ns, H5, x, B, T, sd)
+            arrays[f'out_B{B}_T{T}'] = out.numpy()
+    save('v24_toric5', **arrays)
+
+    # decoder_v2_4 architecture at L = 7 (config 5), seeded Kaiming init as the reference
+    H7 = toric_H(7)
+    set_seed(71)
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = H7.size(0), H7.size(1), 1, H7
+    sd7 = {k: v.clone() for k, v in ns['GNNI'](15).state_dict().items()}
+    arrays = dict(sd_to_np(sd7))
+    x, y = toric_inputs(eg, H7, 7, [0.01, 0.05, 0.1], 8, 72)
+    arrays['x_B8'], arrays['y_B8'] = x.numpy(), y.numpy()
+    out, _ = run_model(ns, H7, x, 8, 15, sd7)
+    arrays['out_B8_T15'] = out.numpy()
+    save('v24_toric7', **arrays)
+
+    # ---- operator-level fixtures: one bare `propagate` call per script variant, with the
+    # base class's identity `update`, on random per-edge messages.
+    gen_propagate(eg, H5, H4)
+
+
+def gen_propagate(eg, H5, H4):
+    arrays = {}
+    B = 3
+    specs = [
+        # (tag, script, H, dtype, flows, aggrs, second-arg name)
+        ('v24', 'quantum/decoder_v2_4.py', H5, torch.float64, ('add', 'mean', 'max'), 'extra'),
+        ('qgnni', 'quantum/QGNNI.py', H4, torch.float64, ('add',), 'extra'),
+        ('qbp', 'quantum/BP.py', H4, torch.float64, ('add',), 'extra'),
+        ('cgnni', 'classical/CGNNI.py', bch_H(), torch.float32, ('add',), 'post'),
+        ('cbp', 'classical/BP.py', bch_H(), torch.float32, ('add',), 'extra'),
+    ]
+    g = torch.Generator().manual_seed(81)
+    for tag, script, H, dt, aggrs, argname in specs:
+        names = {'MessagePassing'}
+        if 'decoder_v2_4' in script:
+            names |= {'scatter_mean', 'scatter_'}
+        ns = load_ref(script, names)
+        V, C = H.shape
+        N = V + C
+        ei = batch_edge_index(single_edge_index(H), B, N)
+        ei = torch.stack([ei[0], ei[1] + V])                      # GNNI.forward's shift
+        E = ei.size(1)
+        arrays[f'{tag}/edge_index'] = ei.numpy()
+        m = (torch.randn(E, 1, generator=g) * 3).to(dt)
+        xv = (torch.randn(B, V, generator=g) * 2)
+        xc = torch.where(torch.rand(B, C, generator=g) < 0.3, -1.0, 1.0)
+        extra = torch.cat([xv, xc], dim=1).reshape(B * N, 1).to(dt)
+        arrays[f'{tag}/msg'] = m.numpy()
+        arrays[f'{tag}/extra'] = extra.numpy()
+        for flow in ('source_to_target', 'target_to_source'):
+            for aggr in aggrs:
+                mp = ns['MessagePassing'](aggr, flow)
+                with torch.no_grad():
+                    kw = {argname: extra}
+                    out = mp.propagate(edge_index=ei, size=(N * B, N * B), x=m, **kw)
+                arrays[f'{tag}/{flow}/{aggr}'] = out.numpy()
+                if tag == 'cgnni':           # classical CGNNI also calls it with post=None (c->v)
+                    with torch.no_grad():
+                        out = mp.propagate(edge_index=ei, post=None, size=(N * B, N * B), x=m)
+                    arrays[f'{tag}/{flow}/{aggr}/nopost'] = out.numpy()
+    save('propagate_ops', **arrays)
+
+
+if __name__ == '__main__':
+    torch.set_num_threads(1)
+    gen_classical()
+    gen_quantum()

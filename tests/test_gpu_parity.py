@@ -1,0 +1,227 @@
+"""GPU parity: the HIP path (through the C ABI) vs the reference-generated golden vectors and
+the oracle.  Run on an MI355X with `pytest -m gpu`.
+
+Tolerances (SURVEY.md §8(d) parity criterion):
+* native dtype (fp32 classical, fp64 quantum): soft outputs rtol 1e-4 / 1e-10 and identical
+  hard decisions, except bits whose oracle output is within 1e-6 (fp32) of 0.5;
+* fp32 kernels on the fp64 quantum models: |p - p_ref| <= 1e-4 and identical hard decisions
+  outside |p_ref - 0.5| < 1e-3 (reported).
+"""
+import numpy as np
+import pytest
+import torch
+
+import gnn_oracle as O
+from conftest import weights_of
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+DECODERS = [
+    ('cgnni_bch', 'cgnni', 'bch_63_45_graph'),
+    ('cgnni_bch_randinit', 'cgnni', 'bch_63_45_graph'),
+    ('bp_bch', 'cbp', 'bch_63_45_graph'),
+    ('bp_toric4', 'qbp', 'toric_L4_graph'),
+    ('qgnni_toric4', 'qgnni', 'toric_L4_graph'),
+    ('v24_toric5', 'v24', 'toric_L5_graph'),
+    ('v24_toric7', 'v24', 'toric_L7_graph'),
+]
+
+
+def _cases():
+    for fx, model, gfx in DECODERS:
+        z = np.load(f'tests/golden/{fx}.npz')
+        for k in z.files:
+            if k.startswith('out_'):
+                _, b, t = k.split('_')
+                yield pytest.param(fx, model, gfx, int(b[1:]), int(t[1:]), id=f'{fx}-{b}-{t}')
+
+
+def build_model(model, H, T, z):
+    import gnndecode as gd
+    m = gd.MODELS[model](T, H)
+    w = weights_of(z)
+    if w:
+        m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in w.items()})
+    return m.to(DEV).eval()
+
+
+def run_fused(m, x):
+    import gnndecode as gd
+    g = m.graph(x.device)
+    with torch.no_grad():
+        return m(gd.data.make_batch(x, g))
+
+
+def assert_parity(out, ref, native=True):
+    out = np.asarray(out, np.float64).ravel()
+    ref = np.asarray(ref, np.float64).ravel()
+    if native and ref.dtype == np.float64 and out.dtype == np.float64:
+        pass
+    tol = dict(rtol=1e-4, atol=1e-5) if not native else None
+    return out, ref, tol
+
+
+@pytest.mark.parametrize('fx,model,gfx,B,T', list(_cases()))
+def test_fused_decode_native_dtype(golden, fx, model, gfx, B, T):
+    z = golden(fx)
+    H = golden(gfx)['H']
+    ref = z[f'out_B{B}_T{T}']
+    m = build_model(model, H, T, z)
+    x = torch.from_numpy(z[f'x_B{B}']).to(DEV)
+    out = run_fused(m, x).cpu().numpy()
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    if ref.dtype == np.float32:
+        np.testing.assert_allclose(out, ref, rtol=1e-4, atol=2e-5)
+        near = np.abs(ref - 0.5) < 1e-6
+    else:
+        np.testing.assert_allclose(out, ref, rtol=1e-10, atol=1e-12)
+        near = np.abs(ref - 0.5) < 1e-12
+    assert ((out > 0.5) == (ref > 0.5))[~near].all()
+
+
+@pytest.mark.parametrize('fx,model,gfx,B,T', [c for c in _cases() if c.values[1] in ('qbp', 'qgnni', 'v24')])
+def test_fused_decode_fp32_on_quantum_models(golden, fx, model, gfx, B, T):
+    z = golden(fx)
+    H = golden(gfx)['H']
+    ref = z[f'out_B{B}_T{T}']
+    m = build_model(model, H, T, z)
+    x = torch.from_numpy(z[f'x_B{B}']).to(DEV).float()
+    out = run_fused(m, x).double().cpu().numpy()
+    assert np.abs(out - ref).max() <= 1e-4
+    far = np.abs(ref - 0.5) >= 1e-3
+    assert ((out > 0.5) == (ref > 0.5))[far].all()
+
+
+@pytest.mark.parametrize('fx,model,gfx,B,T', [c for c in _cases() if c.values[3] <= 4])
+def test_layerwise_operator_path(golden, fx, model, gfx, B, T):
+    """The reference's layer-by-layer loop with every propagate on the device operator."""
+    z = golden(fx)
+    H = golden(gfx)['H']
+    ref = z[f'out_B{B}_T{T}']
+    m = build_model(model, H, T, z)
+    x = torch.from_numpy(z[f'x_B{B}']).to(DEV)
+    g = m.graph(x.device)
+    import gnndecode as gd
+    with torch.no_grad():
+        out = m.forward_layers(x, gd.data.make_batch(x, g).edge_index).cpu().numpy()
+    tol = dict(rtol=1e-4, atol=2e-5) if ref.dtype == np.float32 else dict(rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(out, ref, **tol)
+
+
+def _prop_cases():
+    z = np.load('tests/golden/propagate_ops.npz')
+    for k in z.files:
+        if len(k.split('/')) >= 3:
+            yield pytest.param(k, id=k)
+
+
+@pytest.mark.parametrize('path', ['tiled', 'generic'])
+@pytest.mark.parametrize('key', list(_prop_cases()))
+def test_propagate_operator(golden, key, path):
+    import gnndecode as gd
+    z = golden('propagate_ops')
+    tag, flow, aggr = key.split('/')[:3]
+    ei = torch.from_numpy(z[f'{tag}/edge_index']).to(DEV)
+    msg = torch.from_numpy(z[f'{tag}/msg']).to(DEV)
+    extra_np = z[f'{tag}/extra']
+    extra = None if key.endswith('nopost') else torch.from_numpy(extra_np).to(DEV)
+    graph = None
+    if path == 'tiled':
+        gfx = {'v24': 'toric_L5_graph', 'qgnni': 'toric_L4_graph', 'qbp': 'toric_L4_graph',
+               'cgnni': 'bch_63_45_graph', 'cbp': 'bch_63_45_graph'}[tag]
+        graph = gd.TannerGraph(golden(gfx)['H'], device=DEV)
+        assert graph.is_tiled(ei, graph.V) or aggr == 'mean'
+    out = gd.ops.propagate(tag, flow, aggr, ei, msg, extra, extra_np.shape[0], graph=graph)
+    ref = z[key]
+    tol = dict(rtol=1e-5, atol=5e-6) if ref.dtype == np.float32 else dict(rtol=1e-11, atol=1e-12)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, **tol)
+
+
+def test_message_passing_module_drop_in(golden):
+    """A reference-style subclass (custom update) runs propagate on the device."""
+    import gnndecode as gd
+    z = golden('propagate_ops')
+    ei = torch.from_numpy(z['v24/edge_index']).to(DEV)
+    msg = torch.from_numpy(z['v24/msg']).to(DEV)
+    extra = torch.from_numpy(z['v24/extra']).to(DEV)
+
+    class Layer(gd.MessagePassing):
+        def update(self, aggr_out):
+            return aggr_out[:, :1] * 2
+
+    lay = Layer('add', 'target_to_source')
+    out = lay.propagate(ei, extra=extra, size=(extra.size(0), extra.size(0)), x=msg)
+    np.testing.assert_allclose(out.cpu().numpy(), z['v24/target_to_source/add'][:, :1] * 2,
+                               rtol=1e-11, atol=1e-12)
+
+
+# ------------------------------------------------------------------------------------
+# size-independent properties at the BASELINE batch size, ragged/empty edges
+# ------------------------------------------------------------------------------------
+def _bch_model(golden, T=25):
+    z = golden('cgnni_bch')
+    return build_model('cgnni', golden('bch_63_45_graph')['H'], T, z), weights_of(z)
+
+
+def test_large_batch_matches_oracle_on_sample(golden):
+    import gnndecode as gd
+    m, w = _bch_model(golden)
+    H = golden('bch_63_45_graph')['H']
+    B = 65536
+    x, _ = gd.data.awgn_batch(H, B, codeword_bit=1, seed=5, device=DEV)
+    out = run_fused(m, x).cpu().numpy().reshape(B, 63)
+    rng = np.random.default_rng(0)
+    pick = np.sort(rng.choice(B, 128, replace=False))
+    xs = x.cpu().numpy().reshape(B, 81)[pick].reshape(-1, 1)
+    ref = O.decode('cgnni', H, xs, 25, w).reshape(-1, 63)
+    np.testing.assert_allclose(out[pick], ref, rtol=1e-4, atol=2e-5)
+
+
+def test_batch_independence_and_determinism(golden):
+    """Decoding a codeword alone or inside any batch/tile position gives identical bits."""
+    import gnndecode as gd
+    m, _ = _bch_model(golden)
+    H = golden('bch_63_45_graph')['H']
+    g = m.graph(torch.device(DEV))
+    cw, _ = gd.ops.decode_tile(g, 'cgnni', torch.float32)
+    B = 3 * cw + 1                                    # ragged last tile
+    x, _ = gd.data.awgn_batch(H, B, seed=9, device=DEV)
+    full = run_fused(m, x)
+    again = run_fused(m, x)
+    assert torch.equal(full, again)
+    for b in (0, cw - 1, cw, B - 1):
+        one = run_fused(m, x.view(B, -1)[b:b + 1].reshape(-1, 1))
+        assert torch.equal(one.view(-1), full.view(B, -1)[b])
+
+
+def test_empty_batch(golden):
+    import gnndecode as gd
+    m, _ = _bch_model(golden)
+    g = m.graph(torch.device(DEV))
+    x = torch.empty(0, 1, device=DEV)
+    out = gd.ops.decode(g, 'cgnni', x, 25, m.prepared_weights(torch.float32, x.device))
+    assert out.shape == (0, 1)
+
+
+def test_ldpc_bp_all_zero_codeword_high_snr():
+    """802.11n LDPC(648,324) (unverified base matrix): BP decodes the all-zero word at
+    high SNR, and the GPU matches the oracle on a sample."""
+    import gnndecode as gd
+    H = gd.codes.wifi_ldpc_648()
+    m = gd.ClassicalBP(25, H).to(DEV).eval()
+    x, _ = gd.data.awgn_batch(H, 64, snrs=(6,), seed=3, device=DEV)
+    out = run_fused(m, x).cpu().numpy()
+    assert (out > 0.5).sum() == 0
+    ref = O.decode('cbp', H, x.cpu().numpy()[:8 * 972], 25)
+    np.testing.assert_allclose(out[:8 * 648], ref, rtol=1e-4, atol=2e-5)
+
+
+def test_cpu_tensors_fail_loudly(golden):
+    import gnndecode as gd
+    m, _ = _bch_model(golden)
+    x = torch.zeros(81, 1)
+    g = m.graph(torch.device(DEV))
+    with pytest.raises(RuntimeError):
+        gd.ops.decode(g, 'cgnni', x, 25, m.prepared_weights(torch.float32, torch.device(DEV)))

@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace summary.
+# Every GPU step runs under its own timeout; a crash/timeout (exit >= 124 or signal) ends the
+# script immediately.  Test failures (pytest exit 1) do not stop the bench.
+# usage: tools/gpu_round.sh [tag] [pytest-args...]
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOT"
+TAG="${1:-r01}"; shift || true
+OUT="$ROOT/gpurun_out/$TAG"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { echo "FATAL step $1 exit $2"; exit "$2"; }
+step() {  # name, timeout, cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "--- $name exit $rc"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then fatal "$name" $rc; fi
+  return 0
+}
+rocm-smi --showproductname > "$OUT/rocm-smi.txt" 2>&1 || true
+lscpu | grep -E "Model name|^CPU\(s\)" > "$OUT/lscpu.txt" 2>&1 || true
+step pytest_gpu 900 python -m pytest tests -m gpu -q -x "$@"
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 600 python bench.py --steps 20 --warmup 3
+step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0
+echo "=== done $(date +%T)"
