@@ -17,12 +17,17 @@ struct GraphView {            // passed by value to kernels
     const int* var_ptr;       // [V+1] edges of variable v are [var_ptr[v], var_ptr[v+1])
     const int* chk_ptr;       // [C+1]
     const int* chk_edge;      // [E]   edge ids of check c, increasing (= increasing v)
+    // check-group slot plan of the fused decoder: check c owns G lanes x R slots,
+    // slot (c, lane g, r) = c*G*R + g*R + r holds its edges in increasing order, padded.
+    int G, logG, R;
+    const uint32_t* slot;     // [C*G*R]  v | (e << 16), kSlotPad for padding
 };
+#define GNND_SLOT_PAD 0xffffffffu
 
 struct gnnd_graph {
     GraphView view;
-    void* dev;                // single device allocation holding the four tables
-    size_t table_bytes;       // bytes of the four tables (staged to LDS by the kernels)
+    void* dev;                // single device allocation holding every table
+    size_t table_bytes;       // bytes of the four CSR/CSC tables (staged to LDS)
 };
 
 // int tables staged to LDS in this order: edge_vc[E], var_ptr[V+1], chk_ptr[C+1], chk_edge[E]
@@ -116,3 +121,35 @@ template <typename T> __device__ __forceinline__ T cos_pi(T k) {
     }
     return g_cos(T(M_PI) * k);
 }
+
+// ---------------------------------------------------------------------------------------
+// all-reduce sum over aligned groups of G lanes (G a power of two <= 64, wave-uniform).
+// Every lane of a group ends with the identical value (each step adds two operands in
+// both orders, and fp addition is commutative).  DPP for the in-row steps.
+// ---------------------------------------------------------------------------------------
+template <int CTRL> __device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float group_sum(float v, int G) {
+    if (G > 1) v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]  (lane ^ 1)
+    if (G > 2) v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]  (lane ^ 2)
+    if (G > 4) v += dpp_mov<0x141>(v);   // row_half_mirror      (other quad of the 8)
+    if (G > 8) v += dpp_mov<0x140>(v);   // row_mirror           (other 8 of the 16)
+    if (G > 16) v += __shfl_xor(v, 16);
+    if (G > 32) v += __shfl_xor(v, 32);
+    return v;
+}
+__device__ __forceinline__ double group_sum(double v, int G) {
+    for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// tanh on the native base-2 exp and reciprocal (fp32 GNN path):
+// tanh(y) = sign(y) (1 - e) / (1 + e), e = exp(-2|y|) in (0, 1].  Absolute error ~1e-7
+// (1 - e is exact for e >= 1/2), i.e. at the rounding level of the reference's sums.
+__device__ __forceinline__ float tanh_fast(float y) {
+    float e = __builtin_amdgcn_exp2f(fabsf(y) * -2.8853900817779268f);
+    float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    return copysignf(t, y);
+}
+__device__ __forceinline__ double tanh_fast(double y) { return tanh(y); }

@@ -12,15 +12,11 @@
 // MI355X mapping.  Every codeword has the same Tanner graph, so the graph tables are
 // staged once per workgroup into LDS and each workgroup decodes a tile of CW codewords
 // whose per-edge messages live in LDS for all T iterations: HBM is touched only to read
-// x (N values per codeword) and write the V outputs.  One iteration is four phases
-// separated by workgroup barriers:
-//   A  variable sums   S_v = sum_{e in v} m_e          (thread per (cw, v), edge order)
-//   B  v->c edge op    a_e = (S_v - m_e) + x_v ; t_e = pre(a_e)       (thread per (cw, e))
-//   C  check sums      S_c = sum_{e in c} t_e          (thread per (cw, c), edge order)
-//   D  c->v edge op    m_e = update(S_c - t_e, s_c) + m_prev          (thread per (cw, e))
-// The node sums run in the reference's accumulation order (index_add in edge order from
-// 0), so the leave-one-out values match torch_scatter's bit for bit; only the MLP dot
-// products and transcendentals differ at the ulp level.
+// x (N values per codeword) and write the V outputs.  An iteration is two phases separated
+// by workgroup barriers (see decode_kernel): a check-group phase where G consecutive lanes
+// own one check's edges (R per lane), sum the check with a DPP butterfly and run both
+// message updates in registers, and a variable-sum phase in the reference's index_add
+// order.  Work is VALU/transcendental-bound (SURVEY.md §8(d) corrected in DESIGN.md).
 #include "gnnd_common.h"
 
 namespace {
@@ -98,130 +94,153 @@ template <typename T> __device__ __forceinline__ T cst(double v) { return (T)v; 
 // ---------------------------------------------------------------------------------------
 // the fused kernel
 // ---------------------------------------------------------------------------------------
-template <int MODEL, typename T>
+template <typename T> struct alignas(2 * sizeof(T)) SumX {
+    T s;   // S_v = sum of the variable's incoming c->v messages
+    T x;   // x_v (prior / LLR)
+};
+
+// Per iteration (two workgroup barriers):
+//  step 1  lanes = (codeword, check, lane-in-group): each lane owns R edge slots of its
+//          check (G lanes per check, consecutive and aligned inside the wave).  For every
+//          owned edge it forms the v->c message a_e = (S_v - m_e) + x_v from LDS, applies
+//          the v->c update and the c->v pre-op, sums the check with a G-lane butterfly
+//          (no LDS, no barrier), then writes m_e = update(S_c - t_e, s_c) (+ m_e) back to
+//          LDS in variable-major order.
+//  step 2  threads = (codeword, variable): S_v = sum of m over the variable's edges in
+//          the reference's index_add order.
+template <int MODEL, typename T, int R>
 __global__ void __launch_bounds__(GNND_BLOCK)
 decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
-              T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dV, FastDiv dC,
-              FastDiv dE) {
+              T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
+              FastDiv dN, FastDiv dE) {
     constexpr bool BP = ModelTraits<MODEL>::bp;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int V = g.V, C = g.C, E = g.E, N = g.N;
+    const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
 
-    // ---- LDS carve: graph tables, then per-codeword state
-    int* s_tab = (int*)smem;
-    const int nints = graph_table_ints(V, C, E);
-    const uint32_t* s_evc = (const uint32_t*)s_tab;
-    const int* s_vptr = s_tab + E;
-    const int* s_cptr = s_vptr + V + 1;
-    const int* s_cedge = s_cptr + C + 1;
-    size_t off = ((size_t)nints * 4 + 15) & ~(size_t)15;
-    T* s_m = (T*)(smem + off);          // [CW][E] messages m (c->v, persistent)
-    T* s_t = s_m + (size_t)CW * E;      // [CW][E] v->c quantity after pre-op
-    T* s_t2 = s_t + (size_t)CW * E;     // [CW][E] BP only: sign indicator
-    T* s_x = s_t2 + (BP ? (size_t)CW * E : 0);   // [CW][N] node features
-    T* s_vs = s_x + (size_t)CW * N;     // [CW][V] variable sums
-    T* s_cs = s_vs + (size_t)CW * V;    // [CW][C] check sums
-    T* s_cs2 = s_cs + (size_t)CW * C;   // [CW][C] BP only: sign-count sums
+    // ---- LDS carve: slot plan + variable CSR, then per-codeword state
+    const int nslot = C * G * R;
+    uint32_t* s_slot = (uint32_t*)smem;
+    int* s_vptr = (int*)(s_slot + nslot);
+    size_t off = (((size_t)nslot + V + 1) * 4 + 15) & ~(size_t)15;
+    T* s_m = (T*)(smem + off);                         // [CW][E]  c->v messages, var-major
+    SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * E);  // [CW][V]  {S_v, x_v}
+    T* s_xc = (T*)(s_sx + (size_t)CW * V);             // [CW][C]  check-row features
 
-    const int* gtab = (const int*)g.edge_vc;
-    for (int i = tid; i < nints; i += GNND_BLOCK) s_tab[i] = gtab[i];
-
+    for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot[i];
+    for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     const T* xg = x + b0 * N;
-    for (int i = tid; i < nb * N; i += GNND_BLOCK) s_x[i] = xg[i];
+    for (int i = tid; i < nb * N; i += GNND_BLOCK) {
+        int b = fdiv(i, dN), n = i - b * N;
+        T xv = xg[i];
+        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
+        else s_xc[b * C + n - V] = xv;
+    }
     for (int i = tid; i < nb * E; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
 
-    const int nV = nb * V, nC = nb * C, nE = nb * E;
+    const int IC = C * G;               // work items (lanes) per codeword
+    const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
+    const int nV = nb * V;
     for (int it = 0; it < iters; ++it) {
-        // A: variable sums (index_add order)
+        // ---------------- step 1: per check group
+        for (int f0 = 0; f0 < nItem; f0 += GNND_BLOCK) {
+            const int f = f0 + tid;
+            const bool act = f < nItem;
+            const int fc = act ? f : nItem - 1;          // idle groups compute on a copy
+            const int b = fdiv(fc, dItem);
+            const int rem = fc - b * IC;
+            const int c = rem >> logG;
+            const uint32_t* sl = s_slot + rem * R;       // (c*G + g)*R
+            T* mb = s_m + b * E;
+            const SumX<T>* sxb = s_sx + b * V;
+            uint32_t sv[R];
+            T mv[R], tv[R], cf[R];
+            T tsum = T(0), csum = T(0);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                sv[r] = sl[r];
+                const bool valid = sv[r] != GNND_SLOT_PAD;
+                const int v = valid ? (int)(sv[r] & 0xffffu) : 0;
+                const int e = valid ? (int)(sv[r] >> 16) : 0;
+                const T m = mb[e];
+                const SumX<T> p = sxb[v];
+                const T ext = p.s - m;
+                T t, cc = T(0);
+                if constexpr (MODEL == GNND_V24) {
+                    T a = mlp128x2_sp(w + kV24Ggc1, ext, p.x);
+                    t = tanh_fast(a / T(2));
+                } else if constexpr (BP) {
+                    T a = ext + p.x;
+                    T th = g_tanh(g_clamp(a, T(-10), T(10)) / T(2));
+                    cc = th < T(0) ? T(1) : T(0);
+                    const T lo = MODEL == GNND_QBP ? cst<T>(1e-20) : cst<T>(1e-7);
+                    t = g_log(g_clamp(g_abs(th), lo, cst<T>(1e10)));
+                } else {
+                    t = tanh_fast((ext + p.x) / T(2));
+                }
+                mv[r] = m;
+                tv[r] = valid ? t : T(0);
+                cf[r] = valid ? cc : T(0);
+                tsum += tv[r];
+                if constexpr (BP) csum += cf[r];
+            }
+            const T Sc = group_sum(tsum, G);
+            T Sc2 = T(0);
+            if constexpr (BP) Sc2 = group_sum(csum, G);
+            const T sc = s_xc[b * C + c];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!act || sv[r] == GNND_SLOT_PAD) continue;
+                const T u = Sc - tv[r];
+                T mn;
+                if constexpr (MODEL == GNND_V24) {
+                    mn = mlp128_sp(w + kV24Ggc2, u) * sc + mv[r];
+                } else if constexpr (MODEL == GNND_QGNNI) {
+                    mn = mlp10_relu(w + kMlp10Msg, u) * sc + mv[r];
+                } else if constexpr (MODEL == GNND_CGNNI) {
+                    mn = mlp10_relu(w + kMlp10Msg, u) + mv[r];
+                } else {   // BP: u = Lambda, n = sign count (leave-one-out)
+                    T n = Sc2 - cf[r];
+                    if constexpr (MODEL == GNND_QBP) n = n + (T(1) - sc) / T(2);
+                    const T hi = MODEL == GNND_QBP ? cst<T>(1 - 1e-12) : cst<T>(1 - 1e-7);
+                    T p = g_clamp(g_exp(u) * cos_pi(n), -hi, hi);
+                    if constexpr (MODEL == GNND_QBP)
+                        mn = g_log(T(1) + p) - g_log(T(1) - p);
+                    else
+                        mn = g_log((T(1) + p) / (T(1) - p));
+                }
+                mb[sv[r] >> 16] = mn;
+            }
+        }
+        __syncthreads();
+        if (it + 1 == iters) break;
+        // ---------------- step 2: variable sums
         for (int f = tid; f < nV; f += GNND_BLOCK) {
-            int b = fdiv(f, dV), v = f - b * V;
+            const int b = fdiv(f, dV), v = f - b * V;
             const T* mb = s_m + b * E;
             T s = T(0);
             for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[k];
-            s_vs[f] = s;
-        }
-        __syncthreads();
-        // B: v->c edge op and c->v pre-op
-        for (int f = tid; f < nE; f += GNND_BLOCK) {
-            int b = fdiv(f, dE), e = f - b * E;
-            int v = (int)(s_evc[e] & 0xffffu);
-            T mv = s_m[f];
-            T ext = s_vs[b * V + v] - mv;
-            T xv = s_x[b * N + v];
-            if constexpr (MODEL == GNND_V24) {
-                T a = mlp128x2_sp(w + kV24Ggc1, ext, xv);
-                s_t[f] = g_tanh(a / T(2));
-            } else if constexpr (BP) {
-                T a = ext + xv;
-                T t = g_tanh(g_clamp(a, T(-10), T(10)) / T(2));
-                s_t2[f] = t < T(0) ? T(1) : T(0);
-                const T lo = MODEL == GNND_QBP ? cst<T>(1e-20) : cst<T>(1e-7);
-                s_t[f] = g_log(g_clamp(g_abs(t), lo, cst<T>(1e10)));
-            } else {   // CGNNI, QGNNI: a = ext + x ; tanh(a/2)
-                T a = ext + xv;
-                s_t[f] = g_tanh(a / T(2));
-            }
-        }
-        __syncthreads();
-        // C: check sums
-        for (int f = tid; f < nC; f += GNND_BLOCK) {
-            int b = fdiv(f, dC), c = f - b * C;
-            const T* tb = s_t + b * E;
-            T s = T(0), s2 = T(0);
-            for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) {
-                int e = s_cedge[k];
-                s += tb[e];
-                if constexpr (BP) s2 += s_t2[b * E + e];
-            }
-            s_cs[f] = s;
-            if constexpr (BP) s_cs2[f] = s2;
-        }
-        __syncthreads();
-        // D: c->v edge op (+ residual)
-        for (int f = tid; f < nE; f += GNND_BLOCK) {
-            int b = fdiv(f, dE), e = f - b * E;
-            int c = (int)(s_evc[e] >> 16);
-            T u = s_cs[b * C + c] - s_t[f];
-            T sc = s_x[b * N + V + c];
-            T mn;
-            if constexpr (MODEL == GNND_V24) {
-                mn = mlp128_sp(w + kV24Ggc2, u) * sc + s_m[f];
-            } else if constexpr (MODEL == GNND_QGNNI) {
-                mn = mlp10_relu(w + kMlp10Msg, u) * sc + s_m[f];
-            } else if constexpr (MODEL == GNND_CGNNI) {
-                mn = mlp10_relu(w + kMlp10Msg, u) + s_m[f];
-            } else {   // BP: u = Lambda (sum of log|t| leave-one-out)
-                T n = s_cs2[b * C + c] - s_t2[f];
-                if constexpr (MODEL == GNND_QBP) n = n + (T(1) - sc) / T(2);
-                const T hi = MODEL == GNND_QBP ? cst<T>(1 - 1e-12) : cst<T>(1 - 1e-7);
-                T p = g_clamp(g_exp(u) * cos_pi(n), -hi, hi);
-                if constexpr (MODEL == GNND_QBP)
-                    mn = g_log(T(1) + p) - g_log(T(1) - p);
-                else
-                    mn = g_log((T(1) + p) / (T(1) - p));
-            }
-            s_m[f] = mn;
+            s_sx[f].s = s;
         }
         __syncthreads();
     }
 
     // ---- readout
-    T* og = out + b0 * V;
     if constexpr (MODEL == GNND_V24) {
-        // per-edge MLP_o(m_e) then variable sums (decoder_v2_4.py:291-292)
-        for (int f = tid; f < nE; f += GNND_BLOCK) s_t[f] = mlp128_sp(w + kV24Mlp, s_m[f]);
+        // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
+        for (int f = tid; f < nb * E; f += GNND_BLOCK) s_m[f] = mlp128_sp(w + kV24Mlp, s_m[f]);
         __syncthreads();
     }
+    T* og = out + b0 * V;
     for (int f = tid; f < nV; f += GNND_BLOCK) {
-        int b = fdiv(f, dV), v = f - b * V;
-        const T* mb = (MODEL == GNND_V24 ? s_t : s_m) + b * E;
+        const int b = fdiv(f, dV), v = f - b * V;
+        const T* mb = s_m + b * E;
         T s = T(0);
         for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[k];
-        T r = s + s_x[b * N + v];
+        const T r = s + s_sx[f].x;
         T o;
         if constexpr (MODEL == GNND_CGNNI) {
             o = g_clamp(sigmoid_ref(-mlp10_relu(w + kMlp10Out, r)), cst<T>(1e-7), cst<T>(1 - 1e-7));
@@ -263,18 +282,20 @@ int weights_count(int model) {
     }
 }
 
-size_t state_elems_per_cw(int model, const GraphView& g) {
-    const bool bp = model == GNND_CBP || model == GNND_QBP;
-    return (size_t)g.E * (bp ? 3 : 2) + g.N + g.V + (size_t)g.C * (bp ? 2 : 1);
+size_t state_bytes_per_cw(const GraphView& g, size_t esz) {
+    return esz * ((size_t)g.E + 2 * (size_t)g.V + g.C);
+}
+size_t table_bytes(const GraphView& g) {
+    return (((size_t)g.C * g.G * g.R + g.V + 1) * 4 + 15) & ~(size_t)15;
 }
 
 constexpr size_t kLdsTarget = 40 * 1024;     // ~4 workgroups (16 waves) per CU
 constexpr size_t kLdsMax = 160 * 1024;
 
-int choose_tile(int model, int dtype, const GraphView& g, int* cw, size_t* lds) {
+int choose_tile(int dtype, const GraphView& g, int* cw, size_t* lds) {
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
-    const size_t tab = ((size_t)graph_table_ints(g.V, g.C, g.E) * 4 + 15) & ~(size_t)15;
-    const size_t per = state_elems_per_cw(model, g) * esz;
+    const size_t tab = table_bytes(g);
+    const size_t per = state_bytes_per_cw(g, esz);
     if (tab + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     size_t n = tab + per >= kLdsTarget ? 1 : (kLdsTarget - tab) / per;
     if (n > 64) n = 64;
@@ -283,36 +304,48 @@ int choose_tile(int model, int dtype, const GraphView& g, int* cw, size_t* lds) 
     return GNND_OK;
 }
 
-template <int MODEL, typename T>
+template <int MODEL, typename T, int R>
 int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out, int64_t B,
                   int iters, hipStream_t st) {
     const GraphView& g = gr->view;
     int cw;
     size_t lds;
-    int rc = choose_tile(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &cw, &lds);
+    int rc = choose_tile(sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &cw, &lds);
     if (rc != GNND_OK) return rc;
-    auto kern = decode_kernel<MODEL, T>;
+    auto kern = decode_kernel<MODEL, T, R>;
     if (lds > 64 * 1024)
         GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int64_t blocks = (B + cw - 1) / cw;
     if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
     kern<<<(unsigned)blocks, GNND_BLOCK, lds, st>>>(
-        g, (const T*)w, (const T*)x, (T*)out, B, iters, cw, make_fastdiv(g.V), make_fastdiv(g.C),
-        make_fastdiv(g.E));
+        g, (const T*)w, (const T*)x, (T*)out, B, iters, cw, make_fastdiv(g.C * g.G),
+        make_fastdiv(g.V), make_fastdiv(g.N), make_fastdiv(g.E));
     GNND_LAUNCH_CHECK();
     return GNND_OK;
+}
+
+template <int MODEL, typename T>
+int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
+                    int iters, hipStream_t st) {
+    switch (g->view.R) {
+        case 1: return launch_decode<MODEL, T, 1>(g, w, x, out, B, iters, st);
+        case 2: return launch_decode<MODEL, T, 2>(g, w, x, out, B, iters, st);
+        case 3: return launch_decode<MODEL, T, 3>(g, w, x, out, B, iters, st);
+        case 4: return launch_decode<MODEL, T, 4>(g, w, x, out, B, iters, st);
+    }
+    return GNND_ERR_UNSUPPORTED;
 }
 
 template <typename T>
 int dispatch_decode(const gnnd_graph* g, int model, const void* w, const void* x, void* out,
                     int64_t B, int iters, hipStream_t st) {
     switch (model) {
-        case GNND_V24: return launch_decode<GNND_V24, T>(g, w, x, out, B, iters, st);
-        case GNND_QGNNI: return launch_decode<GNND_QGNNI, T>(g, w, x, out, B, iters, st);
-        case GNND_QBP: return launch_decode<GNND_QBP, T>(g, w, x, out, B, iters, st);
-        case GNND_CGNNI: return launch_decode<GNND_CGNNI, T>(g, w, x, out, B, iters, st);
-        case GNND_CBP: return launch_decode<GNND_CBP, T>(g, w, x, out, B, iters, st);
+        case GNND_V24: return launch_decode_r<GNND_V24, T>(g, w, x, out, B, iters, st);
+        case GNND_QGNNI: return launch_decode_r<GNND_QGNNI, T>(g, w, x, out, B, iters, st);
+        case GNND_QBP: return launch_decode_r<GNND_QBP, T>(g, w, x, out, B, iters, st);
+        case GNND_CGNNI: return launch_decode_r<GNND_CGNNI, T>(g, w, x, out, B, iters, st);
+        case GNND_CBP: return launch_decode_r<GNND_CBP, T>(g, w, x, out, B, iters, st);
         default: return GNND_ERR_INVALID_ARG;
     }
 }
@@ -351,7 +384,7 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     int cw;
     size_t lds;
-    int rc = choose_tile(model, dtype, g->view, &cw, &lds);
+    int rc = choose_tile(dtype, g->view, &cw, &lds);
     if (rc != GNND_OK) return rc;
     *h_cw = cw;
     *h_lds = (int32_t)lds;
@@ -362,9 +395,10 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
                            const void* d_x, void* d_out, int64_t batch, int32_t iters,
                            void* stream) {
     int nw = weights_count(model);
-    if (!g || nw < 0 || batch < 0 || iters < 0 || !d_x || !d_out) return GNND_ERR_INVALID_ARG;
-    if (nw > 0 && !d_w) return GNND_ERR_INVALID_ARG;
+    if (!g || nw < 0 || batch < 0 || iters < 0) return GNND_ERR_INVALID_ARG;
+    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     if (batch == 0) return GNND_OK;
+    if (!d_x || !d_out || (nw > 0 && !d_w)) return GNND_ERR_INVALID_ARG;
     if ((int64_t)batch * g->view.N > 0x7fffffffLL * 64) return GNND_ERR_UNSUPPORTED;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == GNND_F32) return dispatch_decode<float>(g, model, d_w, d_x, d_out, batch, iters, st);

@@ -37,8 +37,8 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     if (!out) return GNND_ERR_INVALID_ARG;
     *out = nullptr;
     if (!h_var || !h_chk || num_edges <= 0 || V <= 0 || C <= 0) return GNND_ERR_INVALID_ARG;
-    // 16-bit packing of (v, c) per edge; 65535 also bounds every degree
-    if (V > 65535 || C > 65535 || num_edges > (1 << 24)) return GNND_ERR_UNSUPPORTED;
+    // 16-bit packing of v, c and edge ids; 65535 also bounds every degree
+    if (V > 65535 || C > 65535 || num_edges > 65535) return GNND_ERR_UNSUPPORTED;
     const int E = (int)num_edges;
     std::vector<uint32_t> evc(E);
     std::vector<int> vptr(V + 1, 0), cptr(C + 1, 0), cedge(E);
@@ -60,18 +60,38 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         std::vector<int> fill(cptr.begin(), cptr.end() - 1);
         for (int e = 0; e < E; ++e) cedge[fill[h_chk[e]]++] = e;   // increasing e per check
     }
+    // check-group plan: R slots per lane, G (power of two) lanes per check, minimal padding
+    int bestG = 0, bestR = 0;
+    long best = -1;
+    for (int R = 1; R <= 4; ++R) {
+        int need = (max_dc + R - 1) / R, G = 1;
+        while (G < need) G <<= 1;
+        if (G > 64) continue;
+        long slots = (long)C * G * R;
+        if (best < 0 || slots < best) { best = slots; bestG = G; bestR = R; }
+    }
+    if (best < 0) return GNND_ERR_UNSUPPORTED;     // check degree > 256
+    const int nslot = C * bestG * bestR;
+    std::vector<uint32_t> slot(nslot, GNND_SLOT_PAD);
+    for (int c = 0; c < C; ++c)
+        for (int k = cptr[c], i = 0; k < cptr[c + 1]; ++k, ++i) {
+            int e = cedge[k];
+            slot[(size_t)c * bestG * bestR + i] = (evc[e] & 0xffffu) | ((uint32_t)e << 16);
+        }
+
     const int nints = graph_table_ints(V, C, E);
-    std::vector<int> table(nints);
+    std::vector<int> table(nints + nslot);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
     memcpy(table.data() + E + V + 1 + C + 1, cedge.data(), sizeof(int) * E);
+    memcpy(table.data() + nints, slot.data(), sizeof(int) * nslot);
 
     gnnd_graph* g = (gnnd_graph*)calloc(1, sizeof(gnnd_graph));
     if (!g) return GNND_ERR_ALLOC;
-    hipError_t err = hipMalloc(&g->dev, sizeof(int) * (size_t)nints);
+    hipError_t err = hipMalloc(&g->dev, sizeof(int) * table.size());
     if (err != hipSuccess) { free(g); set_hip_error(err); return GNND_ERR_ALLOC; }
-    err = hipMemcpy(g->dev, table.data(), sizeof(int) * (size_t)nints, hipMemcpyHostToDevice);
+    err = hipMemcpy(g->dev, table.data(), sizeof(int) * table.size(), hipMemcpyHostToDevice);
     if (err != hipSuccess) { (void)hipFree(g->dev); free(g); return set_hip_error(err); }
     int* d = (int*)g->dev;
     g->table_bytes = sizeof(int) * (size_t)nints;
@@ -82,6 +102,10 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     gv.var_ptr = d + E;
     gv.chk_ptr = d + E + V + 1;
     gv.chk_edge = d + E + V + 1 + C + 1;
+    gv.G = bestG; gv.R = bestR;
+    gv.logG = 0;
+    while ((1 << gv.logG) < bestG) ++gv.logG;
+    gv.slot = (const uint32_t*)(d + nints);
     *out = g;
     return GNND_OK;
 }

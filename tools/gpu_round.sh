@@ -26,5 +26,6 @@ lscpu | grep -E "Model name|^CPU\(s\)" > "$OUT/lscpu.txt" 2>&1 || true
 step pytest_gpu 900 python -m pytest tests -m gpu -q -x "$@"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
+step sweep 900 python tools/sweep.py --steps 5
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0
 echo "=== done $(date +%T)"
