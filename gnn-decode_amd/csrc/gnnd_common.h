@@ -144,12 +144,15 @@ __device__ __forceinline__ double group_sum(double v, int G) {
     return v;
 }
 
-// tanh on the native base-2 exp and reciprocal (fp32 GNN path):
-// tanh(y) = sign(y) (1 - e) / (1 + e), e = exp(-2|y|) in (0, 1].  Absolute error ~1e-7
+// tanh(a/2) on the native base-2 exp and reciprocal (fp32 GNN path):
+// tanh(a/2) = sign(a) (1 - e) / (1 + e), e = exp(-|a|) in (0, 1].  Absolute error ~1e-7
 // (1 - e is exact for e >= 1/2), i.e. at the rounding level of the reference's sums.
-__device__ __forceinline__ float tanh_fast(float y) {
-    float e = __builtin_amdgcn_exp2f(fabsf(y) * -2.8853900817779268f);
+__device__ __forceinline__ float tanh_half_fast(float a) {
+    float e = __builtin_amdgcn_exp2f(fabsf(a) * -1.4426950408889634f);
     float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
-    return copysignf(t, y);
+    return copysignf(t, a);
 }
-__device__ __forceinline__ double tanh_fast(double y) { return tanh(y); }
+__device__ __forceinline__ double tanh_half_fast(double a) { return tanh(a / 2.0); }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));

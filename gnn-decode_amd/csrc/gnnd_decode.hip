@@ -9,76 +9,23 @@
 //   V24    quantum/decoder_v2_4.py:272-294 (fp64 reference; v->c MLP 2->128->1 Softplus,
 //          c->v MLP 1->128->1 Softplus x syndrome, residual, per-edge readout MLP)
 //
-// MI355X mapping.  Every codeword has the same Tanner graph, so the graph tables are
-// staged once per workgroup into LDS and each workgroup decodes a tile of CW codewords
-// whose per-edge messages live in LDS for all T iterations: HBM is touched only to read
-// x (N values per codeword) and write the V outputs.  An iteration is two phases separated
-// by workgroup barriers (see decode_kernel): a check-group phase where G consecutive lanes
-// own one check's edges (R per lane), sum the check with a DPP butterfly and run both
-// message updates in registers, and a variable-sum phase in the reference's index_add
-// order.  Work is VALU/transcendental-bound (SURVEY.md §8(d) corrected in DESIGN.md).
+// MI355X mapping.  Every codeword has the same Tanner graph, so the graph tables and the
+// weights are staged once per workgroup into LDS and each workgroup decodes a tile of CW
+// codewords whose per-edge messages live in LDS for all T iterations: HBM is touched only
+// to read x (N values per codeword) and write the V outputs.  An iteration is two phases
+// separated by workgroup barriers (see decode_kernel): a check-group phase where G
+// consecutive lanes own one check's edges (R per lane), sum the check with a DPP butterfly
+// and run both message updates in registers, and a variable-sum phase in the reference's
+// index_add order.  The work is VALU/transcendental-bound, so the
+// fp32 MLPs run on packed FMAs (v_pk_fma_f32, two hidden units per instruction) with
+// weights in VGPRs (10-hidden) or broadcast from LDS (128-hidden), and the fp32 Softplus
+// and tanh use the native base-2 v_exp_f32 / v_log_f32 / v_rcp_f32.
 #include "gnnd_common.h"
 
 namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
-
-// ---------------------------------------------------------------------------------------
-// per-edge MLPs (torch.nn.Linear y = x W^T + b), weights uniform across lanes -> SGPRs
-// ---------------------------------------------------------------------------------------
-// Linear(1,10) -> ReLU -> Linear(10,1); w = {W1[10], b1[10], W2[10], b2}
-template <typename T>
-__device__ __forceinline__ T mlp10_relu(const T* __restrict__ w, T u) {
-    T acc = T(0);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        T h = g_fma(u, w[k], w[10 + k]);
-        acc = g_fma(g_max(h, T(0)), w[20 + k], acc);
-    }
-    return acc + w[30];
-}
-
-// Linear(1,128) -> Softplus -> Linear(128,1); w = {W1[128], b1[128], W2[128], b2}
-__device__ __forceinline__ double mlp128_sp(const double* __restrict__ w, double u) {
-    double acc = 0.0;
-#pragma unroll 8
-    for (int k = 0; k < 128; ++k) {
-        double h = fma(u, w[k], w[128 + k]);
-        acc = fma(softplus_ref(h), w[256 + k], acc);
-    }
-    return acc + w[384];
-}
-// fp32 prepared weights: W1, b1 pre-scaled by log2(e), W2 by ln(2)
-__device__ __forceinline__ float mlp128_sp(const float* __restrict__ w, float u) {
-    float acc = 0.f;
-#pragma unroll 16
-    for (int k = 0; k < 128; ++k) {
-        float hs = fmaf(u, w[k], w[128 + k]);
-        acc = fmaf(softplus2_fast(hs), w[256 + k], acc);
-    }
-    return acc + w[384];
-}
-
-// Linear(2,128) -> Softplus -> Linear(128,1); w = {W1[:,0][128], W1[:,1][128], b1[128], W2[128], b2}
-__device__ __forceinline__ double mlp128x2_sp(const double* __restrict__ w, double u0, double u1) {
-    double acc = 0.0;
-#pragma unroll 8
-    for (int k = 0; k < 128; ++k) {
-        double h = fma(u0, w[k], fma(u1, w[128 + k], w[256 + k]));
-        acc = fma(softplus_ref(h), w[384 + k], acc);
-    }
-    return acc + w[512];
-}
-__device__ __forceinline__ float mlp128x2_sp(const float* __restrict__ w, float u0, float u1) {
-    float acc = 0.f;
-#pragma unroll 16
-    for (int k = 0; k < 128; ++k) {
-        float hs = fmaf(u0, w[k], fmaf(u1, w[128 + k], w[256 + k]));
-        acc = fmaf(softplus2_fast(hs), w[384 + k], acc);
-    }
-    return acc + w[512];
-}
 
 // weight offsets in the packed layout (gnnd.h)
 constexpr int kV24Ggc1 = 0, kV24Ggc2 = 513, kV24Mlp = 898;
@@ -90,6 +37,107 @@ template <int MODEL> struct ModelTraits {
 
 // torch constants are Python doubles converted to the tensor dtype
 template <typename T> __device__ __forceinline__ T cst(double v) { return (T)v; }
+
+// ---------------------------------------------------------------------------------------
+// per-edge MLPs (torch.nn.Linear y = x W^T + b)
+// ---------------------------------------------------------------------------------------
+// Linear(1,10) -> ReLU -> Linear(10,1); w = {W1[10], b1[10], W2[10], b2}   (scalar form)
+template <typename T>
+__device__ __forceinline__ T mlp10_relu(const T* w, T u) {
+    T acc = T(0);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        T h = g_fma(u, w[k], w[10 + k]);
+        acc = g_fma(fmax(h, T(0)), w[20 + k], acc);
+    }
+    return acc + w[30];
+}
+
+// fp32 packed form with the 31 weights held in VGPRs (two hidden units per v_pk_fma_f32)
+struct Mlp10F32 {
+    f32x2 w1[5], b1[5], w2[5];
+    float b2;
+    __device__ __forceinline__ void load(const float* w) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            w1[k] = f32x2{w[2 * k], w[2 * k + 1]};
+            b1[k] = f32x2{w[10 + 2 * k], w[11 + 2 * k]};
+            w2[k] = f32x2{w[20 + 2 * k], w[21 + 2 * k]};
+        }
+        b2 = w[30];
+    }
+    __device__ __forceinline__ float operator()(float u) const {
+        const f32x2 uu = {u, u};
+        f32x2 acc = {0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            f32x2 h = __builtin_elementwise_fma(uu, w1[k], b1[k]);
+            h = __builtin_elementwise_max(h, f32x2{0.f, 0.f});
+            acc = __builtin_elementwise_fma(h, w2[k], acc);
+        }
+        return (acc.x + acc.y) + b2;
+    }
+};
+
+// fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1)
+__device__ __forceinline__ double mlp128_sp(const double* w, double u) {
+    double acc = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < 128; ++k) {
+        double h = fma(u, w[k], w[128 + k]);
+        acc = fma(softplus_ref(h), w[256 + k], acc);
+    }
+    return acc + w[384];
+}
+__device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double u1) {
+    double acc = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < 128; ++k) {
+        double h = fma(u0, w[k], fma(u1, w[128 + k], w[256 + k]));
+        acc = fma(softplus_ref(h), w[384 + k], acc);
+    }
+    return acc + w[512];
+}
+
+// fp32 forms on the prepared (interleaved, base-2 rescaled) layout of gnnd_prepare_weights:
+//   1-input:  [64] {W1[2j], W1[2j+1], b1[2j], b1[2j+1]} (x log2e), W2[128] (x ln2), b2
+//   2-input:  [64] {W1a[2j], W1a[2j+1], W1b[2j], W1b[2j+1]}, {b1[2j], b1[2j+1], W2[2j], W2[2j+1]}, b2
+__device__ __forceinline__ f32x2 softplus2_fast2(f32x2 hs) {
+    f32x2 e;
+    e.x = __builtin_amdgcn_exp2f(fminf(hs.x, 28.0f));
+    e.y = __builtin_amdgcn_exp2f(fminf(hs.y, 28.0f));
+    e = e + f32x2{1.0f, 1.0f};
+    f32x2 l;
+    l.x = __builtin_amdgcn_logf(e.x);
+    l.y = __builtin_amdgcn_logf(e.y);
+    return __builtin_elementwise_max(hs, l);
+}
+__device__ __forceinline__ float mlp128_sp(const float* w, float u) {
+    const f32x4* q = (const f32x4*)w;
+    const f32x2* w2 = (const f32x2*)(w + 256);
+    const f32x2 uu = {u, u};
+    f32x2 acc = {0.f, 0.f};
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) {
+        const f32x4 a = q[j];
+        f32x2 hs = __builtin_elementwise_fma(uu, f32x2{a.x, a.y}, f32x2{a.z, a.w});
+        acc = __builtin_elementwise_fma(softplus2_fast2(hs), w2[j], acc);
+    }
+    return (acc.x + acc.y) + w[384];
+}
+__device__ __forceinline__ float mlp128x2_sp(const float* w, float u0, float u1) {
+    const f32x4* q = (const f32x4*)w;
+    const f32x2 uu0 = {u0, u0}, uu1 = {u1, u1};
+    f32x2 acc = {0.f, 0.f};
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) {
+        const f32x4 a = q[2 * j], c = q[2 * j + 1];
+        f32x2 hs = __builtin_elementwise_fma(uu1, f32x2{a.z, a.w}, f32x2{c.x, c.y});
+        hs = __builtin_elementwise_fma(uu0, f32x2{a.x, a.y}, hs);
+        acc = __builtin_elementwise_fma(softplus2_fast2(hs), f32x2{c.z, c.w}, acc);
+    }
+    return (acc.x + acc.y) + w[512];
+}
 
 // ---------------------------------------------------------------------------------------
 // the fused kernel
@@ -110,23 +158,27 @@ template <typename T> struct alignas(2 * sizeof(T)) SumX {
 //          the reference's index_add order.
 template <int MODEL, typename T, int R>
 __global__ void __launch_bounds__(GNND_BLOCK)
-decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
+decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
               T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
-              FastDiv dN, FastDiv dE) {
+              FastDiv dN) {
     constexpr bool BP = ModelTraits<MODEL>::bp;
+    constexpr bool F32 = sizeof(T) == 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
 
-    // ---- LDS carve: slot plan + variable CSR, then per-codeword state
+    // ---- LDS carve: weights, slot plan + variable CSR, then per-codeword state
+    T* s_w = (T*)smem;
+    size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
     const int nslot = C * G * R;
-    uint32_t* s_slot = (uint32_t*)smem;
+    uint32_t* s_slot = (uint32_t*)(smem + off);
     int* s_vptr = (int*)(s_slot + nslot);
-    size_t off = (((size_t)nslot + V + 1) * 4 + 15) & ~(size_t)15;
+    off += (((size_t)nslot + V + 1) * 4 + 15) & ~(size_t)15;
     T* s_m = (T*)(smem + off);                         // [CW][E]  c->v messages, var-major
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * E);  // [CW][V]  {S_v, x_v}
     T* s_xc = (T*)(s_sx + (size_t)CW * V);             // [CW][C]  check-row features
 
+    for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
     for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot[i];
     for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
@@ -140,6 +192,11 @@ decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     }
     for (int i = tid; i < nb * E; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
+
+    // message-MLP weights of the 10-hidden models live in VGPRs for the whole decode
+    Mlp10F32 mlp_msg;
+    if constexpr (F32 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
+        mlp_msg.load((const float*)s_w + kMlp10Msg);
 
     const int IC = C * G;               // work items (lanes) per codeword
     const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
@@ -170,8 +227,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
                 const T ext = p.s - m;
                 T t, cc = T(0);
                 if constexpr (MODEL == GNND_V24) {
-                    T a = mlp128x2_sp(w + kV24Ggc1, ext, p.x);
-                    t = tanh_fast(a / T(2));
+                    t = tanh_half_fast(mlp128x2_sp(s_w + kV24Ggc1, ext, p.x));
                 } else if constexpr (BP) {
                     T a = ext + p.x;
                     T th = g_tanh(g_clamp(a, T(-10), T(10)) / T(2));
@@ -179,7 +235,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
                     const T lo = MODEL == GNND_QBP ? cst<T>(1e-20) : cst<T>(1e-7);
                     t = g_log(g_clamp(g_abs(th), lo, cst<T>(1e10)));
                 } else {
-                    t = tanh_fast((ext + p.x) / T(2));
+                    t = tanh_half_fast(ext + p.x);
                 }
                 mv[r] = m;
                 tv[r] = valid ? t : T(0);
@@ -191,29 +247,31 @@ decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
             T Sc2 = T(0);
             if constexpr (BP) Sc2 = group_sum(csum, G);
             const T sc = s_xc[b * C + c];
+            T mn[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (!act || sv[r] == GNND_SLOT_PAD) continue;
+            for (int r = 0; r < R; ++r) {   // every slot computes; only real edges store
                 const T u = Sc - tv[r];
-                T mn;
                 if constexpr (MODEL == GNND_V24) {
-                    mn = mlp128_sp(w + kV24Ggc2, u) * sc + mv[r];
-                } else if constexpr (MODEL == GNND_QGNNI) {
-                    mn = mlp10_relu(w + kMlp10Msg, u) * sc + mv[r];
-                } else if constexpr (MODEL == GNND_CGNNI) {
-                    mn = mlp10_relu(w + kMlp10Msg, u) + mv[r];
+                    mn[r] = mlp128_sp(s_w + kV24Ggc2, u) * sc + mv[r];
+                } else if constexpr (MODEL == GNND_QGNNI || MODEL == GNND_CGNNI) {
+                    T y;
+                    if constexpr (F32) y = mlp_msg(u);
+                    else y = mlp10_relu(s_w + kMlp10Msg, u);
+                    mn[r] = (MODEL == GNND_QGNNI ? y * sc : y) + mv[r];
                 } else {   // BP: u = Lambda, n = sign count (leave-one-out)
                     T n = Sc2 - cf[r];
                     if constexpr (MODEL == GNND_QBP) n = n + (T(1) - sc) / T(2);
                     const T hi = MODEL == GNND_QBP ? cst<T>(1 - 1e-12) : cst<T>(1 - 1e-7);
                     T p = g_clamp(g_exp(u) * cos_pi(n), -hi, hi);
                     if constexpr (MODEL == GNND_QBP)
-                        mn = g_log(T(1) + p) - g_log(T(1) - p);
+                        mn[r] = g_log(T(1) + p) - g_log(T(1) - p);
                     else
-                        mn = g_log((T(1) + p) / (T(1) - p));
+                        mn[r] = g_log((T(1) + p) / (T(1) - p));
                 }
-                mb[sv[r] >> 16] = mn;
             }
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (act && sv[r] != GNND_SLOT_PAD) mb[sv[r] >> 16] = mn[r];
         }
         __syncthreads();
         if (it + 1 == iters) break;
@@ -231,7 +289,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     // ---- readout
     if constexpr (MODEL == GNND_V24) {
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
-        for (int f = tid; f < nb * E; f += GNND_BLOCK) s_m[f] = mlp128_sp(w + kV24Mlp, s_m[f]);
+        for (int f = tid; f < nb * E; f += GNND_BLOCK) s_m[f] = mlp128_sp(s_w + kV24Mlp, s_m[f]);
         __syncthreads();
     }
     T* og = out + b0 * V;
@@ -243,9 +301,9 @@ decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
         const T r = s + s_sx[f].x;
         T o;
         if constexpr (MODEL == GNND_CGNNI) {
-            o = g_clamp(sigmoid_ref(-mlp10_relu(w + kMlp10Out, r)), cst<T>(1e-7), cst<T>(1 - 1e-7));
+            o = g_clamp(sigmoid_ref(-mlp10_relu(s_w + kMlp10Out, r)), cst<T>(1e-7), cst<T>(1 - 1e-7));
         } else if constexpr (MODEL == GNND_QGNNI) {
-            o = sigmoid_ref(-mlp10_relu(w + kMlp10Out, r));
+            o = sigmoid_ref(-mlp10_relu(s_w + kMlp10Out, r));
         } else if constexpr (MODEL == GNND_CBP) {
             o = g_clamp(sigmoid_ref(-r), cst<T>(1e-7), cst<T>(1 - 1e-7));
         } else {   // QBP, V24
@@ -256,21 +314,28 @@ decode_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
 }
 
 // ---------------------------------------------------------------------------------------
-template <typename T>
-__global__ void prepare_v24_f32_kernel(const T* __restrict__ in, T* __restrict__ outw) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 1283) return;
-    T v = in[i];
-    // ggc1: [0,384) layer 1 (W1a, W1b, b1), [384,512) W2, 512 b2
-    // ggc2 / mlp: [+0,+256) layer 1 (W1, b1), [+256,+384) W2, +384 b2
-    int seg, loc;
-    if (i < kV24Ggc2) { seg = 0; loc = i; }
-    else if (i < kV24Mlp) { seg = 1; loc = i - kV24Ggc2; }
-    else { seg = 2; loc = i - kV24Mlp; }
-    int l1 = seg == 0 ? 384 : 256, l2 = seg == 0 ? 512 : 384;
-    if (loc < l1) v = v * (T)kLog2e;
-    else if (loc < l2) v = v * (T)kLn2;
-    outw[i] = v;
+// weights: fp32 V24 gets the interleaved base-2 layout read by mlp128*_sp(float)
+// ---------------------------------------------------------------------------------------
+__global__ void prepare_v24_f32_kernel(const float* __restrict__ in, float* __restrict__ o) {
+    const int k = threadIdx.x;          // hidden unit, one block of 128 threads
+    const int j = k >> 1, h = k & 1;
+    // ggc1.mlp (plain: W1a[128], W1b[128], b1[128], W2[128], b2)
+    const float* a = in + kV24Ggc1;
+    float* q = o + kV24Ggc1;
+    q[8 * j + h] = a[k] * kLog2e;
+    q[8 * j + 2 + h] = a[128 + k] * kLog2e;
+    q[8 * j + 4 + h] = a[256 + k] * kLog2e;
+    q[8 * j + 6 + h] = a[384 + k] * kLn2;
+    if (k == 0) q[512] = a[512];
+    // ggc2.mlp and mlp (plain: W1[128], b1[128], W2[128], b2)
+    for (int seg = 0; seg < 2; ++seg) {
+        const float* s = in + (seg ? kV24Mlp : kV24Ggc2);
+        float* d = o + (seg ? kV24Mlp : kV24Ggc2);
+        d[4 * j + h] = s[k] * kLog2e;
+        d[4 * j + 2 + h] = s[128 + k] * kLog2e;
+        d[256 + k] = s[256 + k] * kLn2;
+        if (k == 0) d[384] = s[384];
+    }
 }
 
 int weights_count(int model) {
@@ -285,16 +350,17 @@ int weights_count(int model) {
 size_t state_bytes_per_cw(const GraphView& g, size_t esz) {
     return esz * ((size_t)g.E + 2 * (size_t)g.V + g.C);
 }
-size_t table_bytes(const GraphView& g) {
-    return (((size_t)g.C * g.G * g.R + g.V + 1) * 4 + 15) & ~(size_t)15;
+size_t fixed_bytes(const GraphView& g, int model, size_t esz) {
+    size_t wb = ((size_t)weights_count(model) * esz + 15) & ~(size_t)15;
+    return wb + ((((size_t)g.C * g.G * g.R + g.V + 1) * 4 + 15) & ~(size_t)15);
 }
 
 constexpr size_t kLdsTarget = 40 * 1024;     // ~4 workgroups (16 waves) per CU
 constexpr size_t kLdsMax = 160 * 1024;
 
-int choose_tile(int dtype, const GraphView& g, int* cw, size_t* lds) {
+int choose_tile(int model, int dtype, const GraphView& g, int* cw, size_t* lds) {
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
-    const size_t tab = table_bytes(g);
+    const size_t tab = fixed_bytes(g, model, esz);
     const size_t per = state_bytes_per_cw(g, esz);
     if (tab + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     size_t n = tab + per >= kLdsTarget ? 1 : (kLdsTarget - tab) / per;
@@ -310,7 +376,7 @@ int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out,
     const GraphView& g = gr->view;
     int cw;
     size_t lds;
-    int rc = choose_tile(sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &cw, &lds);
+    int rc = choose_tile(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &cw, &lds);
     if (rc != GNND_OK) return rc;
     auto kern = decode_kernel<MODEL, T, R>;
     if (lds > 64 * 1024)
@@ -319,8 +385,8 @@ int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out,
     int64_t blocks = (B + cw - 1) / cw;
     if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
     kern<<<(unsigned)blocks, GNND_BLOCK, lds, st>>>(
-        g, (const T*)w, (const T*)x, (T*)out, B, iters, cw, make_fastdiv(g.C * g.G),
-        make_fastdiv(g.V), make_fastdiv(g.N), make_fastdiv(g.E));
+        g, (const T*)w, weights_count(MODEL), (const T*)x, (T*)out, B, iters, cw,
+        make_fastdiv(g.C * g.G), make_fastdiv(g.V), make_fastdiv(g.N));
     GNND_LAUNCH_CHECK();
     return GNND_OK;
 }
@@ -364,17 +430,15 @@ extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void*
     int n = weights_count(model);
     if (n < 0 || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
     if (n == 0) return GNND_OK;
-    if (!d_w || !d_prepared) return GNND_ERR_INVALID_ARG;
+    if (!d_w || !d_prepared || d_w == d_prepared) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
     if (model == GNND_V24 && dtype == GNND_F32) {
-        prepare_v24_f32_kernel<float><<<(1283 + 255) / 256, 256, 0, st>>>(
-            (const float*)d_w, (float*)d_prepared);
+        prepare_v24_f32_kernel<<<1, 128, 0, st>>>((const float*)d_w, (float*)d_prepared);
         GNND_LAUNCH_CHECK();
         return GNND_OK;
     }
     size_t bytes = (size_t)n * (dtype == GNND_F64 ? 8 : 4);
-    if (d_w != d_prepared)
-        GNND_HIP_CHECK(hipMemcpyAsync(d_prepared, d_w, bytes, hipMemcpyDeviceToDevice, st));
+    GNND_HIP_CHECK(hipMemcpyAsync(d_prepared, d_w, bytes, hipMemcpyDeviceToDevice, st));
     return GNND_OK;
 }
 
@@ -384,7 +448,7 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     int cw;
     size_t lds;
-    int rc = choose_tile(dtype, g->view, &cw, &lds);
+    int rc = choose_tile(model, dtype, g->view, &cw, &lds);
     if (rc != GNND_OK) return rc;
     *h_cw = cw;
     *h_lds = (int32_t)lds;
@@ -399,9 +463,7 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     if (batch == 0) return GNND_OK;
     if (!d_x || !d_out || (nw > 0 && !d_w)) return GNND_ERR_INVALID_ARG;
-    if ((int64_t)batch * g->view.N > 0x7fffffffLL * 64) return GNND_ERR_UNSUPPORTED;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == GNND_F32) return dispatch_decode<float>(g, model, d_w, d_x, d_out, batch, iters, st);
-    if (dtype == GNND_F64) return dispatch_decode<double>(g, model, d_w, d_x, d_out, batch, iters, st);
-    return GNND_ERR_INVALID_ARG;
+    return dispatch_decode<double>(g, model, d_w, d_x, d_out, batch, iters, st);
 }
