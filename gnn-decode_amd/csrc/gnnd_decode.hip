@@ -18,7 +18,7 @@
 // and run both message updates in registers, and a variable-sum phase in the reference's
 // index_add order.  The work is VALU/transcendental-bound, so the
 // fp32 MLPs run on packed FMAs (v_pk_fma_f32, two hidden units per instruction) with
-// weights in VGPRs (10-hidden) or broadcast from LDS (128-hidden), and the fp32 Softplus
+// weights in VGPRs (10-hidden) or SGPRs (128-hidden, scalar loads), and the fp32 Softplus
 // and tanh use the native base-2 v_exp_f32 / v_log_f32 / v_rcp_f32.
 #include "gnnd_common.h"
 
@@ -193,6 +193,10 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     for (int i = tid; i < nb * E; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
 
+    // 128-hidden weights stream through the scalar cache into SGPRs (uniform addresses):
+    // no LDS traffic, one SGPR operand per packed FMA.  Broadcast ds_read_b128 of the same
+    // weights from LDS costs 4 LDS cycles per 4 floats per wave and saturated the LDS pipe.
+    const T* __restrict__ wv = w;
     // message-MLP weights of the 10-hidden models live in VGPRs for the whole decode
     Mlp10F32 mlp_msg;
     if constexpr (F32 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
@@ -227,7 +231,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                 const T ext = p.s - m;
                 T t, cc = T(0);
                 if constexpr (MODEL == GNND_V24) {
-                    t = tanh_half_fast(mlp128x2_sp(s_w + kV24Ggc1, ext, p.x));
+                    t = tanh_half_fast(mlp128x2_sp(wv + kV24Ggc1, ext, p.x));
                 } else if constexpr (BP) {
                     T a = ext + p.x;
                     T th = g_tanh(g_clamp(a, T(-10), T(10)) / T(2));
@@ -252,7 +256,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
             for (int r = 0; r < R; ++r) {   // every slot computes; only real edges store
                 const T u = Sc - tv[r];
                 if constexpr (MODEL == GNND_V24) {
-                    mn[r] = mlp128_sp(s_w + kV24Ggc2, u) * sc + mv[r];
+                    mn[r] = mlp128_sp(wv + kV24Ggc2, u) * sc + mv[r];
                 } else if constexpr (MODEL == GNND_QGNNI || MODEL == GNND_CGNNI) {
                     T y;
                     if constexpr (F32) y = mlp_msg(u);
@@ -289,7 +293,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     // ---- readout
     if constexpr (MODEL == GNND_V24) {
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
-        for (int f = tid; f < nb * E; f += GNND_BLOCK) s_m[f] = mlp128_sp(s_w + kV24Mlp, s_m[f]);
+        for (int f = tid; f < nb * E; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
         __syncthreads();
     }
     T* og = out + b0 * V;

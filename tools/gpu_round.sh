@@ -28,4 +28,6 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
 step sweep 900 python tools/sweep.py --steps 5
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0
+step pmc 1200 bash tools/pmc.sh "$OUT/pmc"
+python tools/pmc_summary.py "$OUT/pmc" cgnni_bch_63_45_B65536_T25_f32 "$OUT/pmc_cgnni_bch_63_45_B65536_T25_f32.json" > "$OUT/pmc_summary.log" 2>&1 || true
 echo "=== done $(date +%T)"

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Summarise tools/pmc.sh output for the dominant decode kernel.
+
+HBM traffic per launch follows MI355X_MICROARCH.md §HBM / cdna_hip_programming.md §7:
+FETCH_SIZE and WRITE_SIZE (KiB, separate passes), FETCH_SIZE doubled for the gfx950
+half-count of wide coalesced reads (reported both raw and corrected).
+usage: tools/pmc_summary.py PMCDIR TAG [OUTJSON]  (default profiles/pmc_TAG.json)
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(dirpath):
+    vals = defaultdict(list)
+    for f in glob.glob(os.path.join(dirpath, '**', '*counter_collection.csv'), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if 'decode_kernel' not in row.get('Kernel_Name', ''):
+                    continue
+                key = (row['Dispatch_Id'], row['Counter_Name'])
+                vals[key].append(float(row['Counter_Value']))
+    per = defaultdict(list)
+    for (disp, name), v in vals.items():
+        per[name].append(sum(v))          # sum over XCD/SE instances of one dispatch
+    return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
+
+
+def main():
+    d, tag = sys.argv[1], sys.argv[2]
+    res, counts = {}, {}
+    for sub in sorted(os.listdir(d)):
+        p = os.path.join(d, sub)
+        if os.path.isdir(p):
+            r, c = load(p)
+            res.update(r)
+            counts.update(c)
+    out = {'tag': tag, 'counters_per_dispatch_mean': res, 'dispatches': counts}
+    if 'FETCH_SIZE' in res and 'WRITE_SIZE' in res:
+        raw = (res['FETCH_SIZE'] + res['WRITE_SIZE']) * 1024
+        corr = (2 * res['FETCH_SIZE'] + res['WRITE_SIZE']) * 1024
+        out['hbm_bytes_per_launch_raw'] = raw
+        out['hbm_bytes_per_launch'] = corr
+        out['note'] = ('FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts 1/2 of wide '
+                       'coalesced reads); 4-B-per-lane access widths are uncalibrated')
+    if 'SQ_INSTS_VALU' in res and 'SQ_WAVES' in res:
+        out['valu_insts_per_wave'] = res['SQ_INSTS_VALU'] / res['SQ_WAVES']
+    if 'SQ_ACTIVE_INST_VALU' in res and 'SQ_BUSY_CYCLES' in res:
+        out['note_valu'] = 'SQ_* cycle counters are quad-cycles (MI355X_MICROARCH.md)'
+    path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, 'profiles', f'pmc_{tag}.json')
+    with open(path, 'w') as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == '__main__':
+    main()
