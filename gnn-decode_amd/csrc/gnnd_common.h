@@ -20,9 +20,10 @@ struct GraphView {            // passed by value to kernels
     // check-group slot plan of the fused decoder: check c owns G lanes x R slots,
     // slot (c, lane g, r) = c*G*R + g*R + r holds its edges in increasing order, padded.
     int G, logG, R;
-    const uint32_t* slot;     // [C*G*R]  v | (e << 16), kSlotPad for padding
+    const uint32_t* slot;     // [C*G*R]  variable of the slot's edge; GNND_SLOT_PAD if padding
+    const int* vslot;         // [E]      slot of edge e (reference edge order = var-major)
 };
-#define GNND_SLOT_PAD 0xffffffffu
+#define GNND_SLOT_PAD 0x80000000u   // padding slot: variable 0, flag bit 31
 
 struct gnnd_graph {
     GraphView view;

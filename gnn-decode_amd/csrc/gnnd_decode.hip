@@ -167,20 +167,24 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
 
-    // ---- LDS carve: weights, slot plan + variable CSR, then per-codeword state
+    // ---- LDS carve: weights, slot plan + variable CSR, then per-codeword state.
+    // Messages are stored in SLOT order (check-major, lane-contiguous): the check-group
+    // phase reads and writes them conflict-free; the variable sums gather via vslot.
     T* s_w = (T*)smem;
     size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
     const int nslot = C * G * R;
     uint32_t* s_slot = (uint32_t*)(smem + off);
     int* s_vptr = (int*)(s_slot + nslot);
-    off += (((size_t)nslot + V + 1) * 4 + 15) & ~(size_t)15;
-    T* s_m = (T*)(smem + off);                         // [CW][E]  c->v messages, var-major
-    SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * E);  // [CW][V]  {S_v, x_v}
-    T* s_xc = (T*)(s_sx + (size_t)CW * V);             // [CW][C]  check-row features
+    int* s_vslot = s_vptr + V + 1;
+    off += (((size_t)nslot + V + 1 + E) * 4 + 15) & ~(size_t)15;
+    T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
+    SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
+    T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
 
     for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
     for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot[i];
     for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
+    for (int i = tid; i < E; i += GNND_BLOCK) s_vslot[i] = g.vslot[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     const T* xg = x + b0 * N;
@@ -190,7 +194,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
         else s_xc[b * C + n - V] = xv;
     }
-    for (int i = tid; i < nb * E; i += GNND_BLOCK) s_m[i] = T(0);
+    for (int i = tid; i < nb * nslot; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
 
     // 128-hidden weights stream through the scalar cache into SGPRs (uniform addresses):
@@ -215,7 +219,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
             const int rem = fc - b * IC;
             const int c = rem >> logG;
             const uint32_t* sl = s_slot + rem * R;       // (c*G + g)*R
-            T* mb = s_m + b * E;
+            T* mb = s_m + b * nslot + rem * R;           // this lane's R message slots
             const SumX<T>* sxb = s_sx + b * V;
             uint32_t sv[R];
             T mv[R], tv[R], cf[R];
@@ -223,11 +227,9 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 sv[r] = sl[r];
-                const bool valid = sv[r] != GNND_SLOT_PAD;
-                const int v = valid ? (int)(sv[r] & 0xffffu) : 0;
-                const int e = valid ? (int)(sv[r] >> 16) : 0;
-                const T m = mb[e];
-                const SumX<T> p = sxb[v];
+                const bool valid = !(sv[r] & GNND_SLOT_PAD);
+                const T m = mb[r];
+                const SumX<T> p = sxb[sv[r] & 0xffffu];   // padding reads variable 0
                 const T ext = p.s - m;
                 T t, cc = T(0);
                 if constexpr (MODEL == GNND_V24) {
@@ -273,18 +275,19 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                         mn[r] = g_log((T(1) + p) / (T(1) - p));
                 }
             }
+            if (act) {                      // padding slots store too (never read back)
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (act && sv[r] != GNND_SLOT_PAD) mb[sv[r] >> 16] = mn[r];
+                for (int r = 0; r < R; ++r) mb[r] = mn[r];
+            }
         }
         __syncthreads();
         if (it + 1 == iters) break;
         // ---------------- step 2: variable sums
         for (int f = tid; f < nV; f += GNND_BLOCK) {
             const int b = fdiv(f, dV), v = f - b * V;
-            const T* mb = s_m + b * E;
+            const T* mb = s_m + b * nslot;
             T s = T(0);
-            for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[k];
+            for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[s_vslot[k]];
             s_sx[f].s = s;
         }
         __syncthreads();
@@ -293,15 +296,15 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     // ---- readout
     if constexpr (MODEL == GNND_V24) {
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
-        for (int f = tid; f < nb * E; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
+        for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
         __syncthreads();
     }
     T* og = out + b0 * V;
     for (int f = tid; f < nV; f += GNND_BLOCK) {
         const int b = fdiv(f, dV), v = f - b * V;
-        const T* mb = s_m + b * E;
+        const T* mb = s_m + b * nslot;
         T s = T(0);
-        for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[k];
+        for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[s_vslot[k]];
         const T r = s + s_sx[f].x;
         T o;
         if constexpr (MODEL == GNND_CGNNI) {
@@ -352,11 +355,11 @@ int weights_count(int model) {
 }
 
 size_t state_bytes_per_cw(const GraphView& g, size_t esz) {
-    return esz * ((size_t)g.E + 2 * (size_t)g.V + g.C);
+    return esz * ((size_t)g.C * g.G * g.R + 2 * (size_t)g.V + g.C);
 }
 size_t fixed_bytes(const GraphView& g, int model, size_t esz) {
     size_t wb = ((size_t)weights_count(model) * esz + 15) & ~(size_t)15;
-    return wb + ((((size_t)g.C * g.G * g.R + g.V + 1) * 4 + 15) & ~(size_t)15);
+    return wb + ((((size_t)g.C * g.G * g.R + g.V + 1 + g.E) * 4 + 15) & ~(size_t)15);
 }
 
 constexpr size_t kLdsTarget = 40 * 1024;     // ~4 workgroups (16 waves) per CU

@@ -73,19 +73,23 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     if (best < 0) return GNND_ERR_UNSUPPORTED;     // check degree > 256
     const int nslot = C * bestG * bestR;
     std::vector<uint32_t> slot(nslot, GNND_SLOT_PAD);
+    std::vector<int> vslot(E);
     for (int c = 0; c < C; ++c)
         for (int k = cptr[c], i = 0; k < cptr[c + 1]; ++k, ++i) {
             int e = cedge[k];
-            slot[(size_t)c * bestG * bestR + i] = (evc[e] & 0xffffu) | ((uint32_t)e << 16);
+            int pos = c * bestG * bestR + i;
+            slot[pos] = evc[e] & 0xffffu;
+            vslot[e] = pos;
         }
 
     const int nints = graph_table_ints(V, C, E);
-    std::vector<int> table(nints + nslot);
+    std::vector<int> table(nints + nslot + E);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
     memcpy(table.data() + E + V + 1 + C + 1, cedge.data(), sizeof(int) * E);
     memcpy(table.data() + nints, slot.data(), sizeof(int) * nslot);
+    memcpy(table.data() + nints + nslot, vslot.data(), sizeof(int) * E);
 
     gnnd_graph* g = (gnnd_graph*)calloc(1, sizeof(gnnd_graph));
     if (!g) return GNND_ERR_ALLOC;
@@ -106,6 +110,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     gv.logG = 0;
     while ((1 << gv.logG) < bestG) ++gv.logG;
     gv.slot = (const uint32_t*)(d + nints);
+    gv.vslot = d + nints + nslot;
     *out = g;
     return GNND_OK;
 }
