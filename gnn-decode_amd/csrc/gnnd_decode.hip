@@ -21,6 +21,7 @@
 // weights in VGPRs (10-hidden) or SGPRs (128-hidden, scalar loads), and the fp32 Softplus
 // and tanh use the native base-2 v_exp_f32 / v_log_f32 / v_rcp_f32.
 #include "gnnd_common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -146,6 +147,26 @@ template <typename T> struct alignas(2 * sizeof(T)) SumX {
     T s;   // S_v = sum of the variable's incoming c->v messages
     T x;   // x_v (prior / LLR)
 };
+
+// S_v = sum_{k in [k0, ke)} mb[vslot[k]] in k (= reference index_add) order.  The slot
+// indices and the messages are fetched eight at a time (independent LDS reads in flight,
+// clamped addresses, masked adds) instead of one dependent read pair per edge.
+template <typename T>
+__device__ __forceinline__ T var_sum(const T* mb, const int* vslot, int k0, int ke) {
+    T s = T(0);
+    for (int k = k0; k < ke; k += 8) {
+        int idx[8];
+        T val[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) idx[j] = vslot[min(k + j, ke - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) val[j] = mb[idx[j]];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (k + j < ke) s += val[j];
+    }
+    return s;
+}
 
 // Per iteration (two workgroup barriers):
 //  step 1  lanes = (codeword, check, lane-in-group): each lane owns R edge slots of its
@@ -285,10 +306,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         // ---------------- step 2: variable sums
         for (int f = tid; f < nV; f += GNND_BLOCK) {
             const int b = fdiv(f, dV), v = f - b * V;
-            const T* mb = s_m + b * nslot;
-            T s = T(0);
-            for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[s_vslot[k]];
-            s_sx[f].s = s;
+            s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
         }
         __syncthreads();
     }
@@ -302,9 +320,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     T* og = out + b0 * V;
     for (int f = tid; f < nV; f += GNND_BLOCK) {
         const int b = fdiv(f, dV), v = f - b * V;
-        const T* mb = s_m + b * nslot;
-        T s = T(0);
-        for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[s_vslot[k]];
+        const T s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
         const T r = s + s_sx[f].x;
         T o;
         if constexpr (MODEL == GNND_CGNNI) {
@@ -362,14 +378,25 @@ size_t fixed_bytes(const GraphView& g, int model, size_t esz) {
     return wb + ((((size_t)g.C * g.G * g.R + g.V + 1 + g.E) * 4 + 15) & ~(size_t)15);
 }
 
-constexpr size_t kLdsTarget = 40 * 1024;     // ~4 workgroups (16 waves) per CU
 constexpr size_t kLdsMax = 160 * 1024;
+
+// LDS budget per workgroup: 40 KiB -> 4 workgroups (16 waves) per CU.  GNND_LDS_TARGET
+// (bytes) overrides it for tuning sweeps.
+size_t lds_target() {
+    static size_t v = [] {
+        const char* e = getenv("GNND_LDS_TARGET");
+        long n = e ? atol(e) : 0;
+        return n >= 4096 && n <= (long)kLdsMax ? (size_t)n : (size_t)(40 * 1024);
+    }();
+    return v;
+}
 
 int choose_tile(int model, int dtype, const GraphView& g, int* cw, size_t* lds) {
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
     const size_t tab = fixed_bytes(g, model, esz);
     const size_t per = state_bytes_per_cw(g, esz);
     if (tab + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
+    const size_t kLdsTarget = lds_target();
     size_t n = tab + per >= kLdsTarget ? 1 : (kLdsTarget - tab) / per;
     if (n > 64) n = 64;
     *cw = (int)n;
