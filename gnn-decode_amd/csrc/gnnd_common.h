@@ -22,6 +22,7 @@ struct GraphView {            // passed by value to kernels
     int G, logG, R;
     const uint32_t* slot;     // [C*G*R]  variable of the slot's edge; GNND_SLOT_PAD if padding
     const int* vslot;         // [E]      slot of edge e (reference edge order = var-major)
+    const uint32_t* slot_ve;  // [C*G*R]  v | (e << 16); padding = 0 | (E << 16) (dummy edge)
 };
 #define GNND_SLOT_PAD 0x80000000u   // padding slot: variable 0, flag bit 31
 

@@ -1,340 +1,8 @@
-// gnnd_decode.hip — fused T-iteration GNN / BP decoder (one launch per batch).
-//
-// Restates GNNI.forward of the five reference decoders (paths relative to
-// /root/reference/GNN-decode/):
-//   CGNNI  classical/CGNNI.py:259-284   (fp32; c->v MLP 1->10->1 ReLU; residual; node MLP)
-//   CBP    classical/BP.py:239-259      (fp32; log-domain sum-product, no weights)
-//   QBP    quantum/BP.py:199-219        (fp64; syndrome-aware log-domain BP)
-//   QGNNI  quantum/QGNNI.py:228-252     (fp64; c->v MLP 1->10->1 ReLU x syndrome; residual)
-//   V24    quantum/decoder_v2_4.py:272-294 (fp64 reference; v->c MLP 2->128->1 Softplus,
-//          c->v MLP 1->128->1 Softplus x syndrome, residual, per-edge readout MLP)
-//
-// MI355X mapping.  Every codeword has the same Tanner graph, so the graph tables and the
-// weights are staged once per workgroup into LDS and each workgroup decodes a tile of CW
-// codewords whose per-edge messages live in LDS for all T iterations: HBM is touched only
-// to read x (N values per codeword) and write the V outputs.  An iteration is two phases
-// separated by workgroup barriers (see decode_kernel): a check-group phase where G
-// consecutive lanes own one check's edges (R per lane), sum the check with a DPP butterfly
-// and run both message updates in registers, and a variable-sum phase in the reference's
-// index_add order.  The work is VALU/transcendental-bound, so the
-// fp32 MLPs run on packed FMAs (v_pk_fma_f32, two hidden units per instruction) with
-// weights in VGPRs (10-hidden) or SGPRs (128-hidden, scalar loads), and the fp32 Softplus
-// and tanh use the native base-2 v_exp_f32 / v_log_f32 / v_rcp_f32.
-#include "gnnd_common.h"
-#include <stdlib.h>
+// gnnd_decode.hip — C ABI of the fused decoder (kernels: gnnd_decode_impl.h, instantiated
+// per model in gnnd_decode_<model>.hip) and the weight preparation kernel.
+#include "gnnd_decode_impl.h"
 
 namespace {
-
-constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kLn2 = 0.6931471805599453f;
-
-// weight offsets in the packed layout (gnnd.h)
-constexpr int kV24Ggc1 = 0, kV24Ggc2 = 513, kV24Mlp = 898;
-constexpr int kMlp10Msg = 0, kMlp10Out = 31;
-
-template <int MODEL> struct ModelTraits {
-    static constexpr bool bp = (MODEL == GNND_QBP || MODEL == GNND_CBP);
-};
-
-// torch constants are Python doubles converted to the tensor dtype
-template <typename T> __device__ __forceinline__ T cst(double v) { return (T)v; }
-
-// ---------------------------------------------------------------------------------------
-// per-edge MLPs (torch.nn.Linear y = x W^T + b)
-// ---------------------------------------------------------------------------------------
-// Linear(1,10) -> ReLU -> Linear(10,1); w = {W1[10], b1[10], W2[10], b2}   (scalar form)
-template <typename T>
-__device__ __forceinline__ T mlp10_relu(const T* w, T u) {
-    T acc = T(0);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        T h = g_fma(u, w[k], w[10 + k]);
-        acc = g_fma(fmax(h, T(0)), w[20 + k], acc);
-    }
-    return acc + w[30];
-}
-
-// fp32 packed form with the 31 weights held in VGPRs (two hidden units per v_pk_fma_f32)
-struct Mlp10F32 {
-    f32x2 w1[5], b1[5], w2[5];
-    float b2;
-    __device__ __forceinline__ void load(const float* w) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            w1[k] = f32x2{w[2 * k], w[2 * k + 1]};
-            b1[k] = f32x2{w[10 + 2 * k], w[11 + 2 * k]};
-            w2[k] = f32x2{w[20 + 2 * k], w[21 + 2 * k]};
-        }
-        b2 = w[30];
-    }
-    __device__ __forceinline__ float operator()(float u) const {
-        const f32x2 uu = {u, u};
-        f32x2 acc = {0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            f32x2 h = __builtin_elementwise_fma(uu, w1[k], b1[k]);
-            h = __builtin_elementwise_max(h, f32x2{0.f, 0.f});
-            acc = __builtin_elementwise_fma(h, w2[k], acc);
-        }
-        return (acc.x + acc.y) + b2;
-    }
-};
-
-// fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1)
-__device__ __forceinline__ double mlp128_sp(const double* w, double u) {
-    double acc = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < 128; ++k) {
-        double h = fma(u, w[k], w[128 + k]);
-        acc = fma(softplus_ref(h), w[256 + k], acc);
-    }
-    return acc + w[384];
-}
-__device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double u1) {
-    double acc = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < 128; ++k) {
-        double h = fma(u0, w[k], fma(u1, w[128 + k], w[256 + k]));
-        acc = fma(softplus_ref(h), w[384 + k], acc);
-    }
-    return acc + w[512];
-}
-
-// fp32 forms on the prepared (interleaved, base-2 rescaled) layout of gnnd_prepare_weights:
-//   1-input:  [64] {W1[2j], W1[2j+1], b1[2j], b1[2j+1]} (x log2e), W2[128] (x ln2), b2
-//   2-input:  [64] {W1a[2j], W1a[2j+1], W1b[2j], W1b[2j+1]}, {b1[2j], b1[2j+1], W2[2j], W2[2j+1]}, b2
-__device__ __forceinline__ f32x2 softplus2_fast2(f32x2 hs) {
-    f32x2 e;
-    e.x = __builtin_amdgcn_exp2f(fminf(hs.x, 28.0f));
-    e.y = __builtin_amdgcn_exp2f(fminf(hs.y, 28.0f));
-    e = e + f32x2{1.0f, 1.0f};
-    f32x2 l;
-    l.x = __builtin_amdgcn_logf(e.x);
-    l.y = __builtin_amdgcn_logf(e.y);
-    return __builtin_elementwise_max(hs, l);
-}
-__device__ __forceinline__ float mlp128_sp(const float* w, float u) {
-    const f32x4* q = (const f32x4*)w;
-    const f32x2* w2 = (const f32x2*)(w + 256);
-    const f32x2 uu = {u, u};
-    f32x2 acc = {0.f, 0.f};
-#pragma unroll 8
-    for (int j = 0; j < 64; ++j) {
-        const f32x4 a = q[j];
-        f32x2 hs = __builtin_elementwise_fma(uu, f32x2{a.x, a.y}, f32x2{a.z, a.w});
-        acc = __builtin_elementwise_fma(softplus2_fast2(hs), w2[j], acc);
-    }
-    return (acc.x + acc.y) + w[384];
-}
-__device__ __forceinline__ float mlp128x2_sp(const float* w, float u0, float u1) {
-    const f32x4* q = (const f32x4*)w;
-    const f32x2 uu0 = {u0, u0}, uu1 = {u1, u1};
-    f32x2 acc = {0.f, 0.f};
-#pragma unroll 8
-    for (int j = 0; j < 64; ++j) {
-        const f32x4 a = q[2 * j], c = q[2 * j + 1];
-        f32x2 hs = __builtin_elementwise_fma(uu1, f32x2{a.z, a.w}, f32x2{c.x, c.y});
-        hs = __builtin_elementwise_fma(uu0, f32x2{a.x, a.y}, hs);
-        acc = __builtin_elementwise_fma(softplus2_fast2(hs), f32x2{c.z, c.w}, acc);
-    }
-    return (acc.x + acc.y) + w[512];
-}
-
-// ---------------------------------------------------------------------------------------
-// the fused kernel
-// ---------------------------------------------------------------------------------------
-template <typename T> struct alignas(2 * sizeof(T)) SumX {
-    T s;   // S_v = sum of the variable's incoming c->v messages
-    T x;   // x_v (prior / LLR)
-};
-
-// S_v = sum_{k in [k0, ke)} mb[vslot[k]] in k (= reference index_add) order.  The slot
-// indices and the messages are fetched eight at a time (independent LDS reads in flight,
-// clamped addresses, masked adds) instead of one dependent read pair per edge.
-template <typename T>
-__device__ __forceinline__ T var_sum(const T* mb, const int* vslot, int k0, int ke) {
-    T s = T(0);
-    for (int k = k0; k < ke; k += 8) {
-        int idx[8];
-        T val[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) idx[j] = vslot[min(k + j, ke - 1)];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) val[j] = mb[idx[j]];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (k + j < ke) s += val[j];
-    }
-    return s;
-}
-
-// Per iteration (two workgroup barriers):
-//  step 1  lanes = (codeword, check, lane-in-group): each lane owns R edge slots of its
-//          check (G lanes per check, consecutive and aligned inside the wave).  For every
-//          owned edge it forms the v->c message a_e = (S_v - m_e) + x_v from LDS, applies
-//          the v->c update and the c->v pre-op, sums the check with a G-lane butterfly
-//          (no LDS, no barrier), then writes m_e = update(S_c - t_e, s_c) (+ m_e) back to
-//          LDS in variable-major order.
-//  step 2  threads = (codeword, variable): S_v = sum of m over the variable's edges in
-//          the reference's index_add order.
-template <int MODEL, typename T, int R>
-__global__ void __launch_bounds__(GNND_BLOCK)
-decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
-              T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
-              FastDiv dN) {
-    constexpr bool BP = ModelTraits<MODEL>::bp;
-    constexpr bool F32 = sizeof(T) == 4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
-    const int tid = threadIdx.x;
-
-    // ---- LDS carve: weights, slot plan + variable CSR, then per-codeword state.
-    // Messages are stored in SLOT order (check-major, lane-contiguous): the check-group
-    // phase reads and writes them conflict-free; the variable sums gather via vslot.
-    T* s_w = (T*)smem;
-    size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
-    const int nslot = C * G * R;
-    uint32_t* s_slot = (uint32_t*)(smem + off);
-    int* s_vptr = (int*)(s_slot + nslot);
-    int* s_vslot = s_vptr + V + 1;
-    off += (((size_t)nslot + V + 1 + E) * 4 + 15) & ~(size_t)15;
-    T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
-    SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
-    T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
-
-    for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
-    for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot[i];
-    for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
-    for (int i = tid; i < E; i += GNND_BLOCK) s_vslot[i] = g.vslot[i];
-    const int64_t b0 = (int64_t)blockIdx.x * CW;
-    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
-    const T* xg = x + b0 * N;
-    for (int i = tid; i < nb * N; i += GNND_BLOCK) {
-        int b = fdiv(i, dN), n = i - b * N;
-        T xv = xg[i];
-        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
-        else s_xc[b * C + n - V] = xv;
-    }
-    for (int i = tid; i < nb * nslot; i += GNND_BLOCK) s_m[i] = T(0);
-    __syncthreads();
-
-    // 128-hidden weights stream through the scalar cache into SGPRs (uniform addresses):
-    // no LDS traffic, one SGPR operand per packed FMA.  Broadcast ds_read_b128 of the same
-    // weights from LDS costs 4 LDS cycles per 4 floats per wave and saturated the LDS pipe.
-    const T* __restrict__ wv = w;
-    // message-MLP weights of the 10-hidden models live in VGPRs for the whole decode
-    Mlp10F32 mlp_msg;
-    if constexpr (F32 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
-        mlp_msg.load((const float*)s_w + kMlp10Msg);
-
-    const int IC = C * G;               // work items (lanes) per codeword
-    const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
-    const int nV = nb * V;
-    for (int it = 0; it < iters; ++it) {
-        // ---------------- step 1: per check group
-        for (int f0 = 0; f0 < nItem; f0 += GNND_BLOCK) {
-            const int f = f0 + tid;
-            const bool act = f < nItem;
-            const int fc = act ? f : nItem - 1;          // idle groups compute on a copy
-            const int b = fdiv(fc, dItem);
-            const int rem = fc - b * IC;
-            const int c = rem >> logG;
-            const uint32_t* sl = s_slot + rem * R;       // (c*G + g)*R
-            T* mb = s_m + b * nslot + rem * R;           // this lane's R message slots
-            const SumX<T>* sxb = s_sx + b * V;
-            uint32_t sv[R];
-            T mv[R], tv[R], cf[R];
-            T tsum = T(0), csum = T(0);
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                sv[r] = sl[r];
-                const bool valid = !(sv[r] & GNND_SLOT_PAD);
-                const T m = mb[r];
-                const SumX<T> p = sxb[sv[r] & 0xffffu];   // padding reads variable 0
-                const T ext = p.s - m;
-                T t, cc = T(0);
-                if constexpr (MODEL == GNND_V24) {
-                    t = tanh_half_fast(mlp128x2_sp(wv + kV24Ggc1, ext, p.x));
-                } else if constexpr (BP) {
-                    T a = ext + p.x;
-                    T th = g_tanh(g_clamp(a, T(-10), T(10)) / T(2));
-                    cc = th < T(0) ? T(1) : T(0);
-                    const T lo = MODEL == GNND_QBP ? cst<T>(1e-20) : cst<T>(1e-7);
-                    t = g_log(g_clamp(g_abs(th), lo, cst<T>(1e10)));
-                } else {
-                    t = tanh_half_fast(ext + p.x);
-                }
-                mv[r] = m;
-                tv[r] = valid ? t : T(0);
-                cf[r] = valid ? cc : T(0);
-                tsum += tv[r];
-                if constexpr (BP) csum += cf[r];
-            }
-            const T Sc = group_sum(tsum, G);
-            T Sc2 = T(0);
-            if constexpr (BP) Sc2 = group_sum(csum, G);
-            const T sc = s_xc[b * C + c];
-            T mn[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {   // every slot computes; only real edges store
-                const T u = Sc - tv[r];
-                if constexpr (MODEL == GNND_V24) {
-                    mn[r] = mlp128_sp(wv + kV24Ggc2, u) * sc + mv[r];
-                } else if constexpr (MODEL == GNND_QGNNI || MODEL == GNND_CGNNI) {
-                    T y;
-                    if constexpr (F32) y = mlp_msg(u);
-                    else y = mlp10_relu(s_w + kMlp10Msg, u);
-                    mn[r] = (MODEL == GNND_QGNNI ? y * sc : y) + mv[r];
-                } else {   // BP: u = Lambda, n = sign count (leave-one-out)
-                    T n = Sc2 - cf[r];
-                    if constexpr (MODEL == GNND_QBP) n = n + (T(1) - sc) / T(2);
-                    const T hi = MODEL == GNND_QBP ? cst<T>(1 - 1e-12) : cst<T>(1 - 1e-7);
-                    T p = g_clamp(g_exp(u) * cos_pi(n), -hi, hi);
-                    if constexpr (MODEL == GNND_QBP)
-                        mn[r] = g_log(T(1) + p) - g_log(T(1) - p);
-                    else
-                        mn[r] = g_log((T(1) + p) / (T(1) - p));
-                }
-            }
-            if (act) {                      // padding slots store too (never read back)
-#pragma unroll
-                for (int r = 0; r < R; ++r) mb[r] = mn[r];
-            }
-        }
-        __syncthreads();
-        if (it + 1 == iters) break;
-        // ---------------- step 2: variable sums
-        for (int f = tid; f < nV; f += GNND_BLOCK) {
-            const int b = fdiv(f, dV), v = f - b * V;
-            s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
-        }
-        __syncthreads();
-    }
-
-    // ---- readout
-    if constexpr (MODEL == GNND_V24) {
-        // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
-        for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
-        __syncthreads();
-    }
-    T* og = out + b0 * V;
-    for (int f = tid; f < nV; f += GNND_BLOCK) {
-        const int b = fdiv(f, dV), v = f - b * V;
-        const T s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
-        const T r = s + s_sx[f].x;
-        T o;
-        if constexpr (MODEL == GNND_CGNNI) {
-            o = g_clamp(sigmoid_ref(-mlp10_relu(s_w + kMlp10Out, r)), cst<T>(1e-7), cst<T>(1 - 1e-7));
-        } else if constexpr (MODEL == GNND_QGNNI) {
-            o = sigmoid_ref(-mlp10_relu(s_w + kMlp10Out, r));
-        } else if constexpr (MODEL == GNND_CBP) {
-            o = g_clamp(sigmoid_ref(-r), cst<T>(1e-7), cst<T>(1 - 1e-7));
-        } else {   // QBP, V24
-            o = sigmoid_ref(-r);
-        }
-        og[f] = o;
-    }
-}
 
 // ---------------------------------------------------------------------------------------
 // weights: fp32 V24 gets the interleaved base-2 layout read by mlp128*_sp(float)
@@ -361,91 +29,15 @@ __global__ void prepare_v24_f32_kernel(const float* __restrict__ in, float* __re
     }
 }
 
-int weights_count(int model) {
+
+int dispatch_decode(const gnnd_graph* g, int model, int dtype, const void* w, const void* x,
+                    void* out, int64_t B, int iters, hipStream_t st) {
     switch (model) {
-        case GNND_CGNNI: case GNND_QGNNI: return 62;
-        case GNND_V24: return 1283;
-        case GNND_CBP: case GNND_QBP: return 0;
-        default: return -1;
-    }
-}
-
-size_t state_bytes_per_cw(const GraphView& g, size_t esz) {
-    return esz * ((size_t)g.C * g.G * g.R + 2 * (size_t)g.V + g.C);
-}
-size_t fixed_bytes(const GraphView& g, int model, size_t esz) {
-    size_t wb = ((size_t)weights_count(model) * esz + 15) & ~(size_t)15;
-    return wb + ((((size_t)g.C * g.G * g.R + g.V + 1 + g.E) * 4 + 15) & ~(size_t)15);
-}
-
-constexpr size_t kLdsMax = 160 * 1024;
-
-// LDS budget per workgroup: 40 KiB -> 4 workgroups (16 waves) per CU.  GNND_LDS_TARGET
-// (bytes) overrides it for tuning sweeps.
-size_t lds_target() {
-    static size_t v = [] {
-        const char* e = getenv("GNND_LDS_TARGET");
-        long n = e ? atol(e) : 0;
-        return n >= 4096 && n <= (long)kLdsMax ? (size_t)n : (size_t)(40 * 1024);
-    }();
-    return v;
-}
-
-int choose_tile(int model, int dtype, const GraphView& g, int* cw, size_t* lds) {
-    const size_t esz = dtype == GNND_F64 ? 8 : 4;
-    const size_t tab = fixed_bytes(g, model, esz);
-    const size_t per = state_bytes_per_cw(g, esz);
-    if (tab + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
-    const size_t kLdsTarget = lds_target();
-    size_t n = tab + per >= kLdsTarget ? 1 : (kLdsTarget - tab) / per;
-    if (n > 64) n = 64;
-    *cw = (int)n;
-    *lds = tab + n * per;
-    return GNND_OK;
-}
-
-template <int MODEL, typename T, int R>
-int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out, int64_t B,
-                  int iters, hipStream_t st) {
-    const GraphView& g = gr->view;
-    int cw;
-    size_t lds;
-    int rc = choose_tile(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &cw, &lds);
-    if (rc != GNND_OK) return rc;
-    auto kern = decode_kernel<MODEL, T, R>;
-    if (lds > 64 * 1024)
-        GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int64_t blocks = (B + cw - 1) / cw;
-    if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
-    kern<<<(unsigned)blocks, GNND_BLOCK, lds, st>>>(
-        g, (const T*)w, weights_count(MODEL), (const T*)x, (T*)out, B, iters, cw,
-        make_fastdiv(g.C * g.G), make_fastdiv(g.V), make_fastdiv(g.N));
-    GNND_LAUNCH_CHECK();
-    return GNND_OK;
-}
-
-template <int MODEL, typename T>
-int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
-                    int iters, hipStream_t st) {
-    switch (g->view.R) {
-        case 1: return launch_decode<MODEL, T, 1>(g, w, x, out, B, iters, st);
-        case 2: return launch_decode<MODEL, T, 2>(g, w, x, out, B, iters, st);
-        case 3: return launch_decode<MODEL, T, 3>(g, w, x, out, B, iters, st);
-        case 4: return launch_decode<MODEL, T, 4>(g, w, x, out, B, iters, st);
-    }
-    return GNND_ERR_UNSUPPORTED;
-}
-
-template <typename T>
-int dispatch_decode(const gnnd_graph* g, int model, const void* w, const void* x, void* out,
-                    int64_t B, int iters, hipStream_t st) {
-    switch (model) {
-        case GNND_V24: return launch_decode_r<GNND_V24, T>(g, w, x, out, B, iters, st);
-        case GNND_QGNNI: return launch_decode_r<GNND_QGNNI, T>(g, w, x, out, B, iters, st);
-        case GNND_QBP: return launch_decode_r<GNND_QBP, T>(g, w, x, out, B, iters, st);
-        case GNND_CGNNI: return launch_decode_r<GNND_CGNNI, T>(g, w, x, out, B, iters, st);
-        case GNND_CBP: return launch_decode_r<GNND_CBP, T>(g, w, x, out, B, iters, st);
+        case GNND_V24: return gnnd_launch_v24(g, dtype, w, x, out, B, iters, st);
+        case GNND_QGNNI: return gnnd_launch_qgnni(g, dtype, w, x, out, B, iters, st);
+        case GNND_QBP: return gnnd_launch_qbp(g, dtype, w, x, out, B, iters, st);
+        case GNND_CGNNI: return gnnd_launch_cgnni(g, dtype, w, x, out, B, iters, st);
+        case GNND_CBP: return gnnd_launch_cbp(g, dtype, w, x, out, B, iters, st);
         default: return GNND_ERR_INVALID_ARG;
     }
 }
@@ -480,12 +72,11 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
                                 int32_t* h_lds) {
     if (!g || !h_cw || !h_lds || weights_count(model) < 0) return GNND_ERR_INVALID_ARG;
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
-    int cw;
-    size_t lds;
-    int rc = choose_tile(model, dtype, g->view, &cw, &lds);
+    Plan p;
+    int rc = make_plan(model, dtype, g->view, &p);
     if (rc != GNND_OK) return rc;
-    *h_cw = cw;
-    *h_lds = (int32_t)lds;
+    *h_cw = p.cw;
+    *h_lds = (int32_t)p.lds;
     return GNND_OK;
 }
 
@@ -498,6 +89,5 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
     if (batch == 0) return GNND_OK;
     if (!d_x || !d_out || (nw > 0 && !d_w)) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == GNND_F32) return dispatch_decode<float>(g, model, d_w, d_x, d_out, batch, iters, st);
-    return dispatch_decode<double>(g, model, d_w, d_x, d_out, batch, iters, st);
+    return dispatch_decode(g, model, dtype, d_w, d_x, d_out, batch, iters, st);
 }

@@ -1,0 +1,620 @@
+// gnnd_decode_impl.h — fused T-iteration GNN / BP decoder kernels (included by the
+// per-model translation units gnnd_decode_<model>.hip; C ABI in gnnd_decode.hip).
+//
+// Restates GNNI.forward of the five reference decoders (paths relative to
+// /root/reference/GNN-decode/):
+//   CGNNI  classical/CGNNI.py:259-284   (fp32; c->v MLP 1->10->1 ReLU; residual; node MLP)
+//   CBP    classical/BP.py:239-259      (fp32; log-domain sum-product, no weights)
+//   QBP    quantum/BP.py:199-219        (fp64; syndrome-aware log-domain BP)
+//   QGNNI  quantum/QGNNI.py:228-252     (fp64; c->v MLP 1->10->1 ReLU x syndrome; residual)
+//   V24    quantum/decoder_v2_4.py:272-294 (fp64 reference; v->c MLP 2->128->1 Softplus,
+//          c->v MLP 1->128->1 Softplus x syndrome, residual, per-edge readout MLP)
+//
+// MI355X mapping.  Every codeword has the same Tanner graph, so the graph tables and the
+// weights are staged once per workgroup into LDS and each workgroup decodes a tile of CW
+// codewords whose per-edge messages live in LDS for all T iterations: HBM is touched only
+// to read x (N values per codeword) and write the V outputs.  An iteration is two phases
+// separated by workgroup barriers (see decode_kernel): a check-group phase where G
+// consecutive lanes own one check's edges (R per lane), sum the check with a DPP butterfly
+// and run both message updates in registers, and a variable-sum phase in the reference's
+// index_add order.  The work is VALU/transcendental-bound, so the
+// fp32 MLPs run on packed FMAs (v_pk_fma_f32, two hidden units per instruction) with
+// weights in VGPRs (10-hidden) or SGPRs (128-hidden, scalar loads), and the fp32 Softplus
+// and tanh use the native base-2 v_exp_f32 / v_log_f32 / v_rcp_f32.
+#pragma once
+#include "gnnd_common.h"
+#include <stdlib.h>
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// weight offsets in the packed layout (gnnd.h)
+constexpr int kV24Ggc1 = 0, kV24Ggc2 = 513, kV24Mlp = 898;
+constexpr int kMlp10Msg = 0, kMlp10Out = 31;
+
+template <int MODEL> struct ModelTraits {
+    static constexpr bool bp = (MODEL == GNND_QBP || MODEL == GNND_CBP);
+};
+
+// torch constants are Python doubles converted to the tensor dtype
+template <typename T> __device__ __forceinline__ T cst(double v) { return (T)v; }
+
+// ---------------------------------------------------------------------------------------
+// per-edge MLPs (torch.nn.Linear y = x W^T + b)
+// ---------------------------------------------------------------------------------------
+// Linear(1,10) -> ReLU -> Linear(10,1); w = {W1[10], b1[10], W2[10], b2}   (scalar form)
+template <typename T>
+__device__ __forceinline__ T mlp10_relu(const T* w, T u) {
+    T acc = T(0);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        T h = g_fma(u, w[k], w[10 + k]);
+        acc = g_fma(fmax(h, T(0)), w[20 + k], acc);
+    }
+    return acc + w[30];
+}
+
+// fp32 packed form with the 31 weights held in VGPRs (two hidden units per v_pk_fma_f32)
+struct Mlp10F32 {
+    f32x2 w1[5], b1[5], w2[5];
+    float b2;
+    __device__ __forceinline__ void load(const float* w) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            w1[k] = f32x2{w[2 * k], w[2 * k + 1]};
+            b1[k] = f32x2{w[10 + 2 * k], w[11 + 2 * k]};
+            w2[k] = f32x2{w[20 + 2 * k], w[21 + 2 * k]};
+        }
+        b2 = w[30];
+    }
+    __device__ __forceinline__ float operator()(float u) const {
+        const f32x2 uu = {u, u};
+        f32x2 acc = {0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            f32x2 h = __builtin_elementwise_fma(uu, w1[k], b1[k]);
+            h = __builtin_elementwise_max(h, f32x2{0.f, 0.f});
+            acc = __builtin_elementwise_fma(h, w2[k], acc);
+        }
+        return (acc.x + acc.y) + b2;
+    }
+};
+
+// fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1)
+__device__ __forceinline__ double mlp128_sp(const double* w, double u) {
+    double acc = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < 128; ++k) {
+        double h = fma(u, w[k], w[128 + k]);
+        acc = fma(softplus_ref(h), w[256 + k], acc);
+    }
+    return acc + w[384];
+}
+__device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double u1) {
+    double acc = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < 128; ++k) {
+        double h = fma(u0, w[k], fma(u1, w[128 + k], w[256 + k]));
+        acc = fma(softplus_ref(h), w[384 + k], acc);
+    }
+    return acc + w[512];
+}
+
+// fp32 forms on the prepared (interleaved, base-2 rescaled) layout of gnnd_prepare_weights:
+//   1-input:  [64] {W1[2j], W1[2j+1], b1[2j], b1[2j+1]} (x log2e), W2[128] (x ln2), b2
+//   2-input:  [64] {W1a[2j], W1a[2j+1], W1b[2j], W1b[2j+1]}, {b1[2j], b1[2j+1], W2[2j], W2[2j+1]}, b2
+__device__ __forceinline__ f32x2 softplus2_fast2(f32x2 hs) {
+    f32x2 e;
+    e.x = __builtin_amdgcn_exp2f(fminf(hs.x, 28.0f));
+    e.y = __builtin_amdgcn_exp2f(fminf(hs.y, 28.0f));
+    e = e + f32x2{1.0f, 1.0f};
+    f32x2 l;
+    l.x = __builtin_amdgcn_logf(e.x);
+    l.y = __builtin_amdgcn_logf(e.y);
+    return __builtin_elementwise_max(hs, l);
+}
+__device__ __forceinline__ float mlp128_sp(const float* w, float u) {
+    const f32x4* q = (const f32x4*)w;
+    const f32x2* w2 = (const f32x2*)(w + 256);
+    const f32x2 uu = {u, u};
+    f32x2 acc = {0.f, 0.f};
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) {
+        const f32x4 a = q[j];
+        f32x2 hs = __builtin_elementwise_fma(uu, f32x2{a.x, a.y}, f32x2{a.z, a.w});
+        acc = __builtin_elementwise_fma(softplus2_fast2(hs), w2[j], acc);
+    }
+    return (acc.x + acc.y) + w[384];
+}
+__device__ __forceinline__ float mlp128x2_sp(const float* w, float u0, float u1) {
+    const f32x4* q = (const f32x4*)w;
+    const f32x2 uu0 = {u0, u0}, uu1 = {u1, u1};
+    f32x2 acc = {0.f, 0.f};
+#pragma unroll 8
+    for (int j = 0; j < 64; ++j) {
+        const f32x4 a = q[2 * j], c = q[2 * j + 1];
+        f32x2 hs = __builtin_elementwise_fma(uu1, f32x2{a.z, a.w}, f32x2{c.x, c.y});
+        hs = __builtin_elementwise_fma(uu0, f32x2{a.x, a.y}, hs);
+        acc = __builtin_elementwise_fma(softplus2_fast2(hs), f32x2{c.z, c.w}, acc);
+    }
+    return (acc.x + acc.y) + w[512];
+}
+
+// ---------------------------------------------------------------------------------------
+// the fused kernel
+// ---------------------------------------------------------------------------------------
+template <typename T> struct alignas(2 * sizeof(T)) SumX {
+    T s;   // S_v = sum of the variable's incoming c->v messages
+    T x;   // x_v (prior / LLR)
+};
+
+// S_v = sum_{k in [k0, ke)} mb[vslot[k]] in k (= reference index_add) order.  The slot
+// indices and the messages are fetched eight at a time (independent LDS reads in flight,
+// clamped addresses, masked adds) instead of one dependent read pair per edge.
+template <typename T>
+__device__ __forceinline__ T var_sum(const T* mb, const int* vslot, int k0, int ke) {
+    T s = T(0);
+    for (int k = k0; k < ke; k += 8) {
+        int idx[8];
+        T val[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) idx[j] = vslot[min(k + j, ke - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) val[j] = mb[idx[j]];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (k + j < ke) s += val[j];
+    }
+    return s;
+}
+
+
+// ---------------------------------------------------------------------------------------
+// per-edge model math shared by both kernels
+// ---------------------------------------------------------------------------------------
+template <int MODEL, typename T> struct EdgeMath {
+    static constexpr bool BP = ModelTraits<MODEL>::bp;
+    // v->c message update and c->v pre-op: a_e = (S_v - m_e) + x_v -> t_e (+ BP sign flag)
+    __device__ static __forceinline__ T pre(T ext, T xv, const T* __restrict__ wv, T& cc) {
+        cc = T(0);
+        if constexpr (MODEL == GNND_V24) {
+            return tanh_half_fast(mlp128x2_sp(wv + kV24Ggc1, ext, xv));
+        } else if constexpr (BP) {
+            T a = ext + xv;
+            T th = g_tanh(g_clamp(a, T(-10), T(10)) / T(2));
+            cc = th < T(0) ? T(1) : T(0);
+            const T lo = MODEL == GNND_QBP ? cst<T>(1e-20) : cst<T>(1e-7);
+            return g_log(g_clamp(g_abs(th), lo, cst<T>(1e10)));
+        } else {
+            return tanh_half_fast(ext + xv);
+        }
+    }
+    // c->v update: u = S_c - t_e (BP: Lambda), n2 = leave-one-out sign count (BP)
+    __device__ static __forceinline__ T post(T u, T n2, T sc, T mprev, const Mlp10F32& mlp,
+                                             const T* s_w, const T* __restrict__ wv) {
+        if constexpr (MODEL == GNND_V24) {
+            return mlp128_sp(wv + kV24Ggc2, u) * sc + mprev;
+        } else if constexpr (MODEL == GNND_QGNNI || MODEL == GNND_CGNNI) {
+            T y;
+            if constexpr (sizeof(T) == 4) y = mlp(u);
+            else y = mlp10_relu(s_w + kMlp10Msg, u);
+            return (MODEL == GNND_QGNNI ? y * sc : y) + mprev;
+        } else {
+            T n = n2;
+            if constexpr (MODEL == GNND_QBP) n = n + (T(1) - sc) / T(2);
+            const T hi = MODEL == GNND_QBP ? cst<T>(1 - 1e-12) : cst<T>(1 - 1e-7);
+            T p = g_clamp(g_exp(u) * cos_pi(n), -hi, hi);
+            if constexpr (MODEL == GNND_QBP) return g_log(T(1) + p) - g_log(T(1) - p);
+            else return g_log((T(1) + p) / (T(1) - p));
+        }
+    }
+    // readout of one variable from r = S_v(+x_v)
+    __device__ static __forceinline__ T readout(T r, const T* s_w) {
+        if constexpr (MODEL == GNND_CGNNI)
+            return g_clamp(sigmoid_ref(-mlp10_relu(s_w + kMlp10Out, r)), cst<T>(1e-7), cst<T>(1 - 1e-7));
+        else if constexpr (MODEL == GNND_QGNNI)
+            return sigmoid_ref(-mlp10_relu(s_w + kMlp10Out, r));
+        else if constexpr (MODEL == GNND_CBP)
+            return g_clamp(sigmoid_ref(-r), cst<T>(1e-7), cst<T>(1 - 1e-7));
+        else
+            return sigmoid_ref(-r);
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// streaming kernel (any model; V24 and graphs too large for the resident kernel)
+// ---------------------------------------------------------------------------------------
+// Per iteration (two workgroup barriers):
+//  step 1  lanes = (codeword, check, lane-in-group): each lane owns R edge slots of its
+//          check (G lanes per check, consecutive and aligned inside the wave).  For every
+//          owned edge it forms the v->c message a_e = (S_v - m_e) + x_v from LDS, applies
+//          the v->c update and the c->v pre-op, sums the check with a G-lane butterfly
+//          (no LDS, no barrier), then writes m_e = update(S_c - t_e, s_c) (+ m_e) back.
+//          Messages are stored in SLOT order (check-major, lane-contiguous).
+//  step 2  threads = (codeword, variable): S_v = sum of m over the variable's edges in
+//          the reference's index_add order (gathered through vslot).
+template <int MODEL, typename T, int R>
+__global__ void __launch_bounds__(GNND_BLOCK)
+decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
+              T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
+              FastDiv dN) {
+    using M = EdgeMath<MODEL, T>;
+    constexpr bool BP = ModelTraits<MODEL>::bp;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
+    const int tid = threadIdx.x;
+
+    T* s_w = (T*)smem;
+    size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
+    const int nslot = C * G * R;
+    uint32_t* s_slot = (uint32_t*)(smem + off);
+    int* s_vptr = (int*)(s_slot + nslot);
+    int* s_vslot = s_vptr + V + 1;
+    off += (((size_t)nslot + V + 1 + E) * 4 + 15) & ~(size_t)15;
+    T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
+    SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
+    T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
+
+    for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
+    for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot[i];
+    for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
+    for (int i = tid; i < E; i += GNND_BLOCK) s_vslot[i] = g.vslot[i];
+    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
+    const T* xg = x + b0 * N;
+    for (int i = tid; i < nb * N; i += GNND_BLOCK) {
+        int b = fdiv(i, dN), n = i - b * N;
+        T xv = xg[i];
+        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
+        else s_xc[b * C + n - V] = xv;
+    }
+    for (int i = tid; i < nb * nslot; i += GNND_BLOCK) s_m[i] = T(0);
+    __syncthreads();
+
+    // 128-hidden weights stream through the scalar cache into SGPRs (uniform addresses):
+    // no LDS traffic, one SGPR operand per packed FMA.  Broadcast ds_read_b128 of the same
+    // weights from LDS costs 4 LDS cycles per 4 floats per wave and saturated the LDS pipe.
+    const T* __restrict__ wv = w;
+    Mlp10F32 mlp_msg;   // 10-hidden message MLP weights live in VGPRs for the whole decode
+    if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
+        mlp_msg.load((const float*)s_w + kMlp10Msg);
+
+    const int IC = C * G;               // work items (lanes) per codeword
+    const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
+    const int nV = nb * V;
+    for (int it = 0; it < iters; ++it) {
+        for (int f0 = 0; f0 < nItem; f0 += GNND_BLOCK) {
+            const int f = f0 + tid;
+            const bool act = f < nItem;
+            const int fc = act ? f : nItem - 1;          // idle groups compute on a copy
+            const int b = fdiv(fc, dItem);
+            const int rem = fc - b * IC;
+            const int c = rem >> logG;
+            const uint32_t* sl = s_slot + rem * R;       // (c*G + g)*R
+            T* mb = s_m + b * nslot + rem * R;           // this lane's R message slots
+            const SumX<T>* sxb = s_sx + b * V;
+            T mv[R], tv[R], cf[R];
+            T tsum = T(0), csum = T(0);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t sv = sl[r];
+                const bool valid = !(sv & GNND_SLOT_PAD);
+                mv[r] = mb[r];
+                const SumX<T> p = sxb[sv & 0xffffu];      // padding reads variable 0
+                T cc;
+                T t = M::pre(p.s - mv[r], p.x, wv, cc);
+                tv[r] = valid ? t : T(0);
+                cf[r] = valid ? cc : T(0);
+                tsum += tv[r];
+                if constexpr (BP) csum += cf[r];
+            }
+            const T Sc = group_sum(tsum, G);
+            T Sc2 = T(0);
+            if constexpr (BP) Sc2 = group_sum(csum, G);
+            const T sc = s_xc[b * C + c];
+            T mn[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r)   // every slot computes; padding slots are never read
+                mn[r] = M::post(Sc - tv[r], Sc2 - cf[r], sc, mv[r], mlp_msg, s_w, wv);
+            if (act) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) mb[r] = mn[r];
+            }
+        }
+        __syncthreads();
+        if (it + 1 == iters) break;
+        for (int f = tid; f < nV; f += GNND_BLOCK) {
+            const int b = fdiv(f, dV), v = f - b * V;
+            s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
+        }
+        __syncthreads();
+    }
+
+    if constexpr (MODEL == GNND_V24) {
+        // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
+        for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
+        __syncthreads();
+    }
+    T* og = out + b0 * V;
+    for (int f = tid; f < nV; f += GNND_BLOCK) {
+        const int b = fdiv(f, dV), v = f - b * V;
+        const T s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
+        og[f] = M::readout(s + s_sx[f].x, s_w);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// resident kernel (light models: CGNNI, QGNNI, CBP, QBP)
+// ---------------------------------------------------------------------------------------
+// Same two-phase iteration, but every lane keeps the c->v messages of its QMAX work
+// items in registers for the whole decode, together with the items' slot entries
+// (variable, edge) and check feature.  Step 1 therefore touches LDS only to read
+// {S_v, x_v} and to publish m_e in VARIABLE-major order (E + 1 per codeword, the extra
+// slot absorbs padding writes), and step 2 sums contiguous rows with no indirection.
+template <int MODEL, typename T, int R, int QMAX>
+__global__ void __launch_bounds__(GNND_BLOCK, 4)   // 4 waves/SIMD: <= 128 VGPRs
+decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
+                       T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem,
+                       FastDiv dV, FastDiv dN) {
+    using M = EdgeMath<MODEL, T>;
+    constexpr bool BP = ModelTraits<MODEL>::bp;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
+    const int E1 = E + 1;
+    const int tid = threadIdx.x;
+
+    T* s_w = (T*)smem;
+    size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
+    int* s_vptr = (int*)(smem + off);
+    off += (((size_t)V + 1) * 4 + 15) & ~(size_t)15;
+    T* s_m = (T*)(smem + off);                             // [CW][E+1] messages, var-major
+    SumX<T>* s_sx = (SumX<T>*)(s_m + (((size_t)CW * E1 + 1) & ~(size_t)1));  // [CW][V]
+    T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
+
+    for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
+    for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
+    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
+    const T* xg = x + b0 * N;
+    for (int i = tid; i < nb * N; i += GNND_BLOCK) {
+        int b = fdiv(i, dN), n = i - b * N;
+        T xv = xg[i];
+        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
+        else s_xc[b * C + n - V] = xv;
+    }
+    __syncthreads();
+
+    Mlp10F32 mlp_msg;
+    if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
+        mlp_msg.load((const float*)s_w + kMlp10Msg);
+
+    // ---- per-lane resident state: item q = tid + q*256 (QMAX items; idle items of a
+    // partial last tile compute on a copy of the last real item and never store)
+    const int IC = C * G;
+    const int nItem = nb * IC;
+    uint32_t ve[QMAX][R];      // v | e << 16 (padding: 0 | E << 16)
+    T m[QMAX][R];
+    T sc[QMAX];
+    int cb[QMAX];              // codeword of the item
+    uint32_t actmask = 0;
+#pragma unroll
+    for (int q = 0; q < QMAX; ++q) {
+        const int f = tid + q * GNND_BLOCK;
+        const bool act = f < nItem;
+        const int fc = act ? f : nItem - 1;
+        const int b = fdiv(fc, dItem);
+        const int rem = fc - b * IC;
+        actmask |= (act ? 1u : 0u) << q;
+        sc[q] = s_xc[b * C + (rem >> logG)];
+        cb[q] = b;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            ve[q][r] = g.slot_ve[rem * R + r];
+            m[q][r] = T(0);
+        }
+    }
+
+    const int nV = nb * V;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int q = 0; q < QMAX; ++q) {
+            T tv[R], cf[R];
+            T tsum = T(0), csum = T(0);
+            const SumX<T>* sxb = s_sx + cb[q] * V;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t sv = ve[q][r];
+                const bool valid = (int)(sv >> 16) != E;
+                const SumX<T> p = sxb[sv & 0xffffu];
+                T cc;
+                T t = M::pre(p.s - m[q][r], p.x, w, cc);
+                tv[r] = valid ? t : T(0);
+                cf[r] = valid ? cc : T(0);
+                tsum += tv[r];
+                if constexpr (BP) csum += cf[r];
+            }
+            const T Sc = group_sum(tsum, G);
+            T Sc2 = T(0);
+            if constexpr (BP) Sc2 = group_sum(csum, G);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                m[q][r] = M::post(Sc - tv[r], Sc2 - cf[r], sc[q], m[q][r], mlp_msg, s_w, w);
+            if (actmask & (1u << q)) {
+                T* mb = s_m + cb[q] * E1;
+#pragma unroll
+                for (int r = 0; r < R; ++r) mb[ve[q][r] >> 16] = m[q][r];
+            }
+        }
+        __syncthreads();
+        for (int f = tid; f < nV; f += GNND_BLOCK) {
+            const int b = fdiv(f, dV), v = f - b * V;
+            const T* mb = s_m + b * E1;
+            T s = T(0);
+            for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[k];
+            if (it + 1 == iters) out[b0 * V + f] = M::readout(s + s_sx[f].x, s_w);
+            else s_sx[f].s = s;
+        }
+        __syncthreads();
+    }
+    if (iters == 0)
+        for (int f = tid; f < nV; f += GNND_BLOCK) out[b0 * V + f] = M::readout(s_sx[f].x, s_w);
+}
+
+int weights_count(int model) {
+    switch (model) {
+        case GNND_CGNNI: case GNND_QGNNI: return 62;
+        case GNND_V24: return 1283;
+        case GNND_CBP: case GNND_QBP: return 0;
+        default: return -1;
+    }
+}
+
+constexpr size_t kLdsMax = 160 * 1024;
+constexpr int kResidentQ[] = {3, 6, 9, 12};   // instantiated work items per lane
+constexpr int kResidentRegBudget = 88;          // Q * (2R + 2) state VGPRs (<= 128 total)
+
+// LDS budget per workgroup: 40 KiB -> 4 workgroups (16 waves) per CU.  GNND_LDS_TARGET
+// (bytes) overrides it for tuning sweeps; GNND_NO_RESIDENT=1 forces the streaming kernel.
+size_t lds_target() {
+    static size_t v = [] {
+        const char* e = getenv("GNND_LDS_TARGET");
+        long n = e ? atol(e) : 0;
+        return n >= 4096 && n <= (long)kLdsMax ? (size_t)n : (size_t)(40 * 1024);
+    }();
+    return v;
+}
+bool resident_disabled() {
+    static bool v = [] {
+        const char* e = getenv("GNND_NO_RESIDENT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+struct Plan {
+    bool resident;
+    int cw;       // codewords per workgroup
+    int q;        // work items per lane (resident)
+    size_t lds;   // bytes of dynamic LDS
+};
+
+size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+int make_plan(int model, int dtype, const GraphView& g, Plan* p) {
+    const size_t esz = dtype == GNND_F64 ? 8 : 4;
+    const size_t wb = align16((size_t)weights_count(model) * esz);
+    const size_t target = lds_target();
+    const int IC = g.C * g.G;
+    const bool light = model != GNND_V24;
+    if (light && dtype == GNND_F32 && !resident_disabled()) {
+        // resident layout: weights, var_ptr, then [CW][E+1] messages, [CW][V] {S, x}, [CW][C].
+        // Pick (CW, Q) with Q in kResidentQ maximising lane utilisation CW*IC / (Q*256),
+        // ties to the larger tile.
+        const size_t fixed = wb + align16(((size_t)g.V + 1) * 4);
+        auto lds_of = [&](int cw) {
+            return fixed + esz * (((size_t)cw * (g.E + 1) + 1) & ~(size_t)1) +
+                   esz * ((size_t)cw * (2 * (size_t)g.V + g.C));
+        };
+        int best = 0, bestq = 0;
+        double bestu = 0;
+        static const int force_q = [] {
+            const char* e = getenv("GNND_RESIDENT_Q");
+            return e ? atoi(e) : 0;
+        }();
+        for (int q : kResidentQ) {
+            if (q * (2 * g.R + 2) > kResidentRegBudget) continue;
+            if (force_q && q != force_q) continue;
+            int cw = q * GNND_BLOCK / IC;               // largest tile that fits q items/lane
+            if (cw > 64) cw = 64;
+            while (cw > 1 && lds_of(cw) > target) --cw;
+            if (cw < 1 || lds_of(cw) > kLdsMax || (cw * IC + GNND_BLOCK - 1) / GNND_BLOCK > q) continue;
+            double u = (double)cw * IC / ((double)q * GNND_BLOCK);
+            if (u > bestu + 1e-9 || (u > bestu - 1e-9 && cw > best)) { bestu = u; best = cw; bestq = q; }
+        }
+        if (best > 0 && bestu >= 0.5) {
+            p->resident = true;
+            p->cw = best;
+            p->q = bestq;
+            p->lds = lds_of(best);
+            return GNND_OK;
+        }
+    }
+    // streaming layout: weights, slot table, var_ptr, vslot, then [CW][nslot] messages,
+    // [CW][V] {S, x}, [CW][C]
+    const size_t nslot = (size_t)IC * g.R;
+    const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4);
+    const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
+    if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
+    size_t n = fixed + per >= target ? 1 : (target - fixed) / per;
+    if (n > 64) n = 64;
+    p->resident = false;
+    p->cw = (int)n;
+    p->q = 0;
+    p->lds = fixed + n * per;
+    return GNND_OK;
+}
+
+template <int MODEL, typename T, int R>
+int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out, int64_t B,
+                  int iters, hipStream_t st) {
+    const GraphView& g = gr->view;
+    Plan p;
+    int rc = make_plan(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p);
+    if (rc != GNND_OK) return rc;
+    int64_t blocks = (B + p.cw - 1) / p.cw;
+    if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
+    const int nw = weights_count(MODEL);
+    const FastDiv dI = make_fastdiv(g.C * g.G), dV = make_fastdiv(g.V), dN = make_fastdiv(g.N);
+    auto go = [&](auto kern) -> int {
+        if (p.lds > 64 * 1024)
+            GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
+        kern<<<(unsigned)blocks, GNND_BLOCK, p.lds, st>>>(g, (const T*)w, nw, (const T*)x, (T*)out,
+                                                          B, iters, p.cw, dI, dV, dN);
+        GNND_LAUNCH_CHECK();
+        return GNND_OK;
+    };
+    if constexpr (MODEL != GNND_V24 && sizeof(T) == 4) {
+        if (p.resident) {
+            switch (p.q) {
+                case 3: return go(decode_resident_kernel<MODEL, T, R, 3>);
+                case 6: return go(decode_resident_kernel<MODEL, T, R, 6>);
+                case 9: return go(decode_resident_kernel<MODEL, T, R, 9>);
+                case 12: return go(decode_resident_kernel<MODEL, T, R, 12>);
+            }
+            return GNND_ERR_UNSUPPORTED;
+        }
+    }
+    return go(decode_kernel<MODEL, T, R>);
+}
+
+
+template <int MODEL, typename T>
+int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
+                    int iters, hipStream_t st) {
+    switch (g->view.R) {
+        case 1: return launch_decode<MODEL, T, 1>(g, w, x, out, B, iters, st);
+        case 2: return launch_decode<MODEL, T, 2>(g, w, x, out, B, iters, st);
+        case 3: return launch_decode<MODEL, T, 3>(g, w, x, out, B, iters, st);
+        case 4: return launch_decode<MODEL, T, 4>(g, w, x, out, B, iters, st);
+    }
+    return GNND_ERR_UNSUPPORTED;
+}
+
+template <int MODEL>
+int launch_model(const gnnd_graph* g, int dtype, const void* w, const void* x, void* out,
+                 int64_t B, int iters, hipStream_t st) {
+    if (dtype == GNND_F32) return launch_decode_r<MODEL, float>(g, w, x, out, B, iters, st);
+    return launch_decode_r<MODEL, double>(g, w, x, out, B, iters, st);
+}
+
+}  // namespace
+
+// per-model launchers (one translation unit each, compiled in parallel)
+int gnnd_launch_v24(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_qgnni(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_qbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_cgnni(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_cbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

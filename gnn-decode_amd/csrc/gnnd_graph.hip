@@ -37,7 +37,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     if (!out) return GNND_ERR_INVALID_ARG;
     *out = nullptr;
     if (!h_var || !h_chk || num_edges <= 0 || V <= 0 || C <= 0) return GNND_ERR_INVALID_ARG;
-    // 16-bit packing of v, c and edge ids; 65535 also bounds every degree
+    // 16-bit packing of v, c and edge ids (E itself marks padding); bounds every degree
     if (V > 65535 || C > 65535 || num_edges > 65535) return GNND_ERR_UNSUPPORTED;
     const int E = (int)num_edges;
     std::vector<uint32_t> evc(E);
@@ -73,23 +73,26 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     if (best < 0) return GNND_ERR_UNSUPPORTED;     // check degree > 256
     const int nslot = C * bestG * bestR;
     std::vector<uint32_t> slot(nslot, GNND_SLOT_PAD);
+    std::vector<uint32_t> slot_ve(nslot, (uint32_t)E << 16);   // padding: v 0, dummy edge E
     std::vector<int> vslot(E);
     for (int c = 0; c < C; ++c)
         for (int k = cptr[c], i = 0; k < cptr[c + 1]; ++k, ++i) {
             int e = cedge[k];
             int pos = c * bestG * bestR + i;
             slot[pos] = evc[e] & 0xffffu;
+            slot_ve[pos] = (evc[e] & 0xffffu) | ((uint32_t)e << 16);
             vslot[e] = pos;
         }
 
     const int nints = graph_table_ints(V, C, E);
-    std::vector<int> table(nints + nslot + E);
+    std::vector<int> table(nints + nslot + E + nslot);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
     memcpy(table.data() + E + V + 1 + C + 1, cedge.data(), sizeof(int) * E);
     memcpy(table.data() + nints, slot.data(), sizeof(int) * nslot);
     memcpy(table.data() + nints + nslot, vslot.data(), sizeof(int) * E);
+    memcpy(table.data() + nints + nslot + E, slot_ve.data(), sizeof(int) * nslot);
 
     gnnd_graph* g = (gnnd_graph*)calloc(1, sizeof(gnnd_graph));
     if (!g) return GNND_ERR_ALLOC;
@@ -111,6 +114,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     while ((1 << gv.logG) < bestG) ++gv.logG;
     gv.slot = (const uint32_t*)(d + nints);
     gv.vslot = d + nints + nslot;
+    gv.slot_ve = (const uint32_t*)(d + nints + nslot + E);
     *out = g;
     return GNND_OK;
 }
