@@ -60,6 +60,8 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=12.0,
                    help='bounded CPU-baseline sample (0 disables)')
     p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--mode', default='decode', choices=['decode', 'train'],
+                   help='train = config 5: decoder_v2_4 training step (DP, RCCL all-reduce)')
     return p.parse_args()
 
 
@@ -111,6 +113,50 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
             'parity_bits_compared': done * g.V}
 
 
+def train_main(a, world, rank, dev):
+    """Config 5: decoder_v2_4 training on the toric code (default L=7), each rank a shard of
+    size --batch, one flat all_reduce(SUM) of the gradient per step (gnndecode.train)."""
+    code = a.code if a.code.startswith('toric') else 'toric_7'
+    model_name = a.model if a.model in ('v24', 'qgnni') else 'v24'
+    T = a.iters or gd.DEFAULT_ITERS[model_name]
+    dtype = torch.float64 if a.dtype == 'f64' else torch.float32
+    H = gd.codes.get_code(code)
+    torch.manual_seed(a.seed)
+    model = gd.MODELS[model_name](T, H).to(dev).to(dtype)
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
+                              logical_only=(model_name == 'qgnni')).to(dev)
+    tr = gd.train.Trainer(model, lf)
+    x, y = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
+    data = gd.data.make_batch(x, model.graph(dev))
+    for _ in range(a.warmup):
+        tr.step(data, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = tr.step(data, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({
+            'metric': 'training samples/sec (whole node), decoder_v2_4 step with RCCL grad all-reduce',
+            'value': world * a.batch * a.steps / elapsed, 'unit': 'samples/s', 'n_gpus': world,
+            'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': a.dtype,
+            'data': 'synthetic toric errors (on-device sampler, seeded); seeded Kaiming init',
+            'config': {'workload': f'{code} {model_name} training step, T={T}, batch={a.batch}/GPU',
+                       'global_batch': a.batch * world, 'parallelism': f'dp{world}',
+                       'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters())},
+            'roofline': None, 'cpu_baseline': None}), flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -120,6 +166,11 @@ def main():
         dist.init_process_group('nccl')
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    if a.mode == 'train':
+        train_main(a, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     T = a.iters or gd.DEFAULT_ITERS[a.model]
     dtype = torch.float32 if a.dtype == 'f32' else torch.float64
 

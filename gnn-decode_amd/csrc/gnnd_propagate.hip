@@ -389,6 +389,163 @@ bool valid_common(int var, int flow, int aggr, int dtype) {
            aggr >= AG_ADD && aggr <= AG_MAX && (dtype == GNND_F32 || dtype == GNND_F64);
 }
 
+
+// ---------------------------------------------------------------------------------------
+// backward of one propagate call w.r.t. the per-edge message (aggr 'add', non-BP bodies).
+// out_e[0] = S_j(pre(msg))_e - pre(msg_e) (+ extra or cat extra, which carry no msg
+// gradient), so grad_pre_e = sum_{e' at node j(e)} g_e' - g_e (the same leave-one-out
+// aggregation applied to the output gradient), times d pre / d msg:
+//   c->v tanh(msg/2):  (grad * (1 - t*t)) / 2   (torch tanh_backward then div_backward)
+// ---------------------------------------------------------------------------------------
+template <int VAR, int FLOW, typename T>
+__device__ __forceinline__ T pre_grad(T msg, T gpre) {
+    if constexpr (FLOW == GNND_TARGET_TO_SOURCE) {
+        T t = g_tanh(msg / T(2));
+        return (gpre * (T(1) - t * t)) / T(2);
+    } else {
+        return gpre;
+    }
+}
+
+template <int VAR, int FLOW, typename T>
+__global__ void __launch_bounds__(GNND_BLOCK)
+propagate_tiled_bwd_kernel(GraphView g, const T* __restrict__ msg, const T* __restrict__ gout,
+                           T* __restrict__ gmsg, int64_t B, int CW, FastDiv dNode, FastDiv dE) {
+    constexpr bool VARSIDE = FLOW == GNND_SOURCE_TO_TARGET;
+    constexpr int F = out_width(VAR, FLOW);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int V = g.V, C = g.C, E = g.E;
+    const int tid = threadIdx.x;
+    int* s_tab = (int*)smem;
+    const int nints = graph_table_ints(V, C, E);
+    const uint32_t* s_evc = (const uint32_t*)s_tab;
+    const int* s_vptr = s_tab + E;
+    const int* s_cptr = s_vptr + V + 1;
+    const int* s_cedge = s_cptr + C + 1;
+    size_t off = ((size_t)nints * 4 + 15) & ~(size_t)15;
+    const int NJ = VARSIDE ? V : C;
+    T* s_g = (T*)(smem + off);                 // [CW][E]
+    T* s_agg = s_g + (size_t)CW * E;           // [CW][NJ]
+    const int* gtab = (const int*)g.edge_vc;
+    for (int i = tid; i < nints; i += GNND_BLOCK) s_tab[i] = gtab[i];
+    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
+    const int nE = nb * E;
+    const T* gg = gout + b0 * E * F;
+    for (int f = tid; f < nE; f += GNND_BLOCK) s_g[f] = gg[(size_t)f * F];
+    __syncthreads();
+    for (int f = tid; f < nb * NJ; f += GNND_BLOCK) {
+        int b = fdiv(f, dNode), j = f - b * NJ;
+        const T* sb = s_g + b * E;
+        T a = T(0);
+        if constexpr (VARSIDE) {
+            for (int k = s_vptr[j], ke = s_vptr[j + 1]; k < ke; ++k) a += sb[k];
+        } else {
+            for (int k = s_cptr[j], ke = s_cptr[j + 1]; k < ke; ++k) a += sb[s_cedge[k]];
+        }
+        s_agg[f] = a;
+    }
+    __syncthreads();
+    const T* mg = msg + b0 * E;
+    T* og = gmsg + b0 * E;
+    for (int f = tid; f < nE; f += GNND_BLOCK) {
+        int b = fdiv(f, dE), e = f - b * E;
+        uint32_t vc = s_evc[e];
+        int j = VARSIDE ? (int)(vc & 0xffffu) : (int)(vc >> 16);
+        og[f] = pre_grad<VAR, FLOW, T>(mg[f], s_agg[b * NJ + j] - s_g[f]);
+    }
+}
+
+template <int VAR, int FLOW, typename T>
+int launch_tiled_bwd(const gnnd_graph* gr, const void* msg, const void* gout, void* gmsg,
+                     int64_t B, hipStream_t st) {
+    const GraphView& g = gr->view;
+    const int NJ = FLOW == GNND_SOURCE_TO_TARGET ? g.V : g.C;
+    const size_t tab = ((size_t)graph_table_ints(g.V, g.C, g.E) * 4 + 15) & ~(size_t)15;
+    const size_t per = sizeof(T) * ((size_t)g.E + NJ);
+    if (tab + per > 160 * 1024) return GNND_ERR_UNSUPPORTED;
+    size_t cw = tab + per >= kLdsTarget ? 1 : (kLdsTarget - tab) / per;
+    if (cw > 64) cw = 64;
+    size_t lds = tab + cw * per;
+    auto kern = propagate_tiled_bwd_kernel<VAR, FLOW, T>;
+    if (lds > 64 * 1024)
+        GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int64_t blocks = (B + (int64_t)cw - 1) / (int64_t)cw;
+    if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
+    kern<<<(unsigned)blocks, GNND_BLOCK, lds, st>>>(g, (const T*)msg, (const T*)gout, (T*)gmsg, B,
+                                                     (int)cw, make_fastdiv(NJ), make_fastdiv(g.E));
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
+template <int VAR, int FLOW, typename T>
+__global__ void __launch_bounds__(GNND_BLOCK)
+gen_bwd_scatter_kernel(const int64_t* __restrict__ idx, const T* __restrict__ gout, int64_t nE,
+                       int64_t dim, T* acc) {
+    constexpr int F = out_width(VAR, FLOW);
+    int64_t e = (int64_t)blockIdx.x * GNND_BLOCK + threadIdx.x;
+    if (e >= nE) return;
+    int64_t j = idx[e];
+    if (j < 0 || j >= dim) return;
+    atomicAdd(acc + j, gout[e * F]);
+}
+
+template <int VAR, int FLOW, typename T>
+__global__ void __launch_bounds__(GNND_BLOCK)
+gen_bwd_out_kernel(const int64_t* __restrict__ idx, const T* __restrict__ msg,
+                   const T* __restrict__ gout, int64_t nE, int64_t dim, const T* acc,
+                   T* __restrict__ gmsg) {
+    constexpr int F = out_width(VAR, FLOW);
+    int64_t e = (int64_t)blockIdx.x * GNND_BLOCK + threadIdx.x;
+    if (e >= nE) return;
+    int64_t j = idx[e];
+    gmsg[e] = (j < 0 || j >= dim) ? T(NAN) : pre_grad<VAR, FLOW, T>(msg[e], acc[j] - gout[e * F]);
+}
+
+template <int VAR, int FLOW, typename T>
+int launch_generic_bwd(const int64_t* ei, int64_t stride, int64_t nE, const void* msg,
+                       const void* gout, int64_t dim, void* gmsg, void* ws, int64_t ws_bytes,
+                       hipStream_t st) {
+    if (ws_bytes < dim * (int64_t)sizeof(T)) return GNND_ERR_INVALID_ARG;
+    T* acc = (T*)ws;
+    const int64_t* idx = ei + (FLOW == GNND_SOURCE_TO_TARGET ? 0 : stride);
+    if (dim > 0) {
+        fill_kernel<T><<<(unsigned)((dim + GNND_BLOCK - 1) / GNND_BLOCK), GNND_BLOCK, 0, st>>>(acc, dim, T(0));
+        GNND_LAUNCH_CHECK();
+    }
+    if (nE == 0) return GNND_OK;
+    const unsigned gE = (unsigned)((nE + GNND_BLOCK - 1) / GNND_BLOCK);
+    gen_bwd_scatter_kernel<VAR, FLOW, T><<<gE, GNND_BLOCK, 0, st>>>(idx, (const T*)gout, nE, dim, acc);
+    gen_bwd_out_kernel<VAR, FLOW, T><<<gE, GNND_BLOCK, 0, st>>>(idx, (const T*)msg, (const T*)gout,
+                                                               nE, dim, acc, (T*)gmsg);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
+template <int VAR, typename T>
+int bwd_flow(bool tiled, int flow, const gnnd_graph* g, const int64_t* ei, int64_t stride,
+             int64_t nE, const void* msg, const void* gout, int64_t dim, void* gmsg, void* ws,
+             int64_t wb, int64_t B, hipStream_t st) {
+    if (flow == GNND_SOURCE_TO_TARGET)
+        return tiled ? launch_tiled_bwd<VAR, GNND_SOURCE_TO_TARGET, T>(g, msg, gout, gmsg, B, st)
+                     : launch_generic_bwd<VAR, GNND_SOURCE_TO_TARGET, T>(ei, stride, nE, msg, gout, dim, gmsg, ws, wb, st);
+    return tiled ? launch_tiled_bwd<VAR, GNND_TARGET_TO_SOURCE, T>(g, msg, gout, gmsg, B, st)
+                 : launch_generic_bwd<VAR, GNND_TARGET_TO_SOURCE, T>(ei, stride, nE, msg, gout, dim, gmsg, ws, wb, st);
+}
+
+template <typename T>
+int bwd_var(bool tiled, int var, int flow, const gnnd_graph* g, const int64_t* ei, int64_t stride,
+            int64_t nE, const void* msg, const void* gout, int64_t dim, void* gmsg, void* ws,
+            int64_t wb, int64_t B, hipStream_t st) {
+    switch (var) {
+        case GNND_V24: return bwd_flow<GNND_V24, T>(tiled, flow, g, ei, stride, nE, msg, gout, dim, gmsg, ws, wb, B, st);
+        case GNND_QGNNI: return bwd_flow<GNND_QGNNI, T>(tiled, flow, g, ei, stride, nE, msg, gout, dim, gmsg, ws, wb, B, st);
+        case GNND_CGNNI: return bwd_flow<GNND_CGNNI, T>(tiled, flow, g, ei, stride, nE, msg, gout, dim, gmsg, ws, wb, B, st);
+    }
+    return GNND_ERR_UNSUPPORTED;   // BP bodies have no trainable parameters upstream
+}
+
 }  // namespace
 
 extern "C" int gnnd_propagate_width(int variant, int flow) {
@@ -431,4 +588,33 @@ extern "C" int gnnd_propagate_generic(int variant, int flow, int aggr, int dtype
     if (dtype == GNND_F32)
         return gen_var<float>(variant, flow, aggr, d_ei, row_stride, nE, d_msg, d_extra, dim, d_out, d_ws, ws_bytes, st);
     return gen_var<double>(variant, flow, aggr, d_ei, row_stride, nE, d_msg, d_extra, dim, d_out, d_ws, ws_bytes, st);
+}
+
+extern "C" int gnnd_propagate_tiled_bwd(const gnnd_graph* g, int variant, int flow, int aggr,
+                                        int dtype, const void* d_msg, const void* d_grad_out,
+                                        void* d_grad_msg, int64_t batch, void* stream) {
+    if (!g || !valid_common(variant, flow, aggr, dtype) || batch < 0) return GNND_ERR_INVALID_ARG;
+    if (aggr != AG_ADD || is_bp(variant)) return GNND_ERR_UNSUPPORTED;
+    if (batch == 0) return GNND_OK;
+    if (!d_msg || !d_grad_out || !d_grad_msg) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GNND_F32)
+        return bwd_var<float>(true, variant, flow, g, nullptr, 0, 0, d_msg, d_grad_out, 0, d_grad_msg, nullptr, 0, batch, st);
+    return bwd_var<double>(true, variant, flow, g, nullptr, 0, 0, d_msg, d_grad_out, 0, d_grad_msg, nullptr, 0, batch, st);
+}
+
+extern "C" int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
+                                          const int64_t* d_ei, int64_t row_stride, int64_t nE,
+                                          const void* d_msg, const void* d_grad_out,
+                                          int64_t dim, void* d_grad_msg, void* d_ws,
+                                          int64_t ws_bytes, void* stream) {
+    if (!valid_common(variant, flow, aggr, dtype) || nE < 0 || dim < 0 || row_stride < nE)
+        return GNND_ERR_INVALID_ARG;
+    if (aggr != AG_ADD || is_bp(variant)) return GNND_ERR_UNSUPPORTED;
+    if (nE > 0 && (!d_ei || !d_msg || !d_grad_out || !d_grad_msg)) return GNND_ERR_INVALID_ARG;
+    if (!d_ws && dim > 0) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GNND_F32)
+        return bwd_var<float>(false, variant, flow, nullptr, d_ei, row_stride, nE, d_msg, d_grad_out, dim, d_grad_msg, d_ws, ws_bytes, 0, st);
+    return bwd_var<double>(false, variant, flow, nullptr, d_ei, row_stride, nE, d_msg, d_grad_out, dim, d_grad_msg, d_ws, ws_bytes, 0, st);
 }

@@ -4,7 +4,7 @@ Drop-in for the `MessagePassing.propagate()` T-iteration decode loop of
 ironmanaudi/GNN-decode.  Compute runs in hand-written HIP kernels (libgnnd.so, C ABI in
 include/gnnd.h); PyTorch provides device memory, streams and torch.distributed only.
 """
-from . import _lib, codes, data
+from . import _lib, codes, data, loss, train
 from .graph import TannerGraph
 from .nn import MessagePassing, ClassicalMessagePassing, message_passing_class
 from .models import (DecoderV24, QGNNI, QuantumBP, CGNNI, ClassicalBP, MODELS, DEFAULT_ITERS,
@@ -13,4 +13,4 @@ from . import ops
 
 __all__ = ['TannerGraph', 'MessagePassing', 'ClassicalMessagePassing', 'message_passing_class',
            'DecoderV24', 'QGNNI', 'QuantumBP', 'CGNNI', 'ClassicalBP', 'MODELS', 'DEFAULT_ITERS',
-           'init_weights', 'ops', 'codes', 'data']
+           'init_weights', 'ops', 'codes', 'data', 'loss', 'train']

@@ -36,6 +36,9 @@ SIGNATURES = {
     'gnnd_propagate_generic_workspace': (_int, [_int, _int, _int, _int, _i64, _i64, _c_i64p]),
     'gnnd_propagate_generic': (_int, [_int, _int, _int, _int, _vp, _i64, _i64, _vp, _vp, _i64,
                                       _vp, _vp, _i64, _vp]),
+    'gnnd_propagate_tiled_bwd': (_int, [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _i64, _vp]),
+    'gnnd_propagate_generic_bwd': (_int, [_int, _int, _int, _int, _vp, _i64, _i64, _vp, _vp, _i64,
+                                          _vp, _vp, _i64, _vp]),
     'gnnd_weights_count': (_int, [_int, _c_i64p]),
     'gnnd_prepare_weights': (_int, [_int, _int, _vp, _vp, _vp]),
     'gnnd_decode': (_int, [_vp, _int, _int, _vp, _vp, _vp, _i64, _i32, _vp]),

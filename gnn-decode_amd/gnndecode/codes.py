@@ -189,3 +189,59 @@ def get_code(name):
     if name.startswith('toric_'):
         return toric_code(int(name.split('_')[1]))
     return CODES[name]()
+
+
+# ---------------------------------------------------------------------------------------
+# toric logical operators (for the training loss and FER metric)
+# ---------------------------------------------------------------------------------------
+def _symplectic(a, b):
+    n = a.size // 2
+    return int(np.dot(a, np.concatenate([b[n:], b[:n]])) % 2)
+
+
+def toric_logicals(H):
+    """Logical operators [4, V] of the code with parity-check matrix H[V, C], restating the
+    reference's construction exactly (quantum/error_generate.py:145-248: `H_Prep`
+    Gauss-Jordan with its column-exchange bookkeeping, then `get_logical`'s pairing of
+    rows with symplectic product 1).  The loss (quantum/decoder_v2_4.py:314-315) sums
+    |sin(pi/2 * L (e + e_hat))| per row, so the specific basis matters, not only its span."""
+    Hc = (np.asarray(H) != 0).T.astype(np.int64)        # [C, V] as H_Prep(H.t()) receives it
+    rows, cols = Hc.shape
+    Hp = Hc.copy()
+    exchange = []
+    for i in range(rows):                                # H_Prep.Get_Identity
+        if Hp[i, i] != 1:
+            for j in range(i, cols):
+                if Hp[i, j] == 1:
+                    Hp[:, [i, j]] = Hp[:, [j, i]]
+                    exchange.append((i, j))
+        for j in range(rows):
+            if Hp[j, i] == 1 and i != j:
+                Hp[j, :] = (Hp[i, :] + Hp[j, :]) % 2
+    exchange.reverse()
+    P = np.concatenate([Hp[:, rows:cols], np.eye(cols - rows, dtype=np.int64)], axis=0)
+    for a, b in exchange:                                # H_Prep.get_H_Prep
+        P[[a, b], :] = P[[b, a], :]
+    P = np.concatenate([P[cols // 2:cols, :], P[0:cols // 2, :]], axis=0).T.copy()
+    prows = P.shape[0]
+    logical = []                                         # indices into P (rows never change
+                                                         # once chosen: they match themselves)
+
+    def is_logical(k):
+        return any((P[k] == P[l]).all() for l in logical)
+
+    for i in range(prows):                               # H_Prep.get_logical
+        if is_logical(i):
+            continue
+        for j in range(i + 1, prows):
+            if is_logical(j) or _symplectic(P[i], P[j]) != 1:
+                continue
+            logical += [i, j]
+            for k in range(j + 1, prows):
+                if not is_logical(k) and _symplectic(P[i], P[k]) == 1:
+                    P[k] = (P[k] + P[j]) % 2
+            for m in range(i + 1, prows):
+                if not is_logical(m) and _symplectic(P[j], P[m]) == 1:
+                    P[m] = (P[m] + P[i]) % 2
+            break
+    return np.stack([P[l] for l in logical]).astype(np.uint8)

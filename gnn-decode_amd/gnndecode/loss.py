@@ -1,0 +1,65 @@
+"""Training objectives and decode metrics of the reference (device tensors).
+
+* `SyndromeLoss` — quantum/decoder_v2_4.py:297-317: sum |sin(pi/2 H^T (y + p))| +
+  sum |sin(pi/2 Lambda (y + p))| over the batch (a SUM, so data-parallel gradients
+  all-reduce with SUM).  `logical_only=True` is quantum/QGNNI.py:255-290 (Lambda term only).
+* `ClassicalLoss` — classical/CGNNI.py:287-309: lambda * mean BCE + (1 - lambda) * mean
+  |sin(pi/2 H^T p)| (train) or mean BCE (test), lambda = 0.8 (classical/CGNNI.py:206).
+* `toric_failures` — hard FER rule of quantum/neural_BP.py:338-348 (non-zero residual
+  syndrome, or zero syndrome with a logical flip).
+
+The reference builds [V, B] matrices with an O(B) torch.cat loop; here the same matrices are
+views ([B*V,1] -> [B, V] -> transpose), identical values.
+"""
+import math
+
+import torch
+
+
+def _cols(t, V):
+    return t.reshape(-1, V).t()          # [V, B], column b = codeword b
+
+
+class SyndromeLoss(torch.nn.Module):
+    def __init__(self, H, logical, logical_only=False):
+        super().__init__()
+        H = torch.as_tensor(H, dtype=torch.float64)
+        self.V = H.size(0)
+        self.register_buffer('Ht', H.t().contiguous())                      # [C, V]
+        self.register_buffer('logical', torch.as_tensor(logical, dtype=torch.float64))
+        self.logical_only = logical_only
+
+    def forward(self, pred, y):
+        s = _cols(y, self.V).to(pred.dtype) + _cols(pred, self.V)
+        loss = torch.abs(torch.sin(torch.matmul(self.logical.to(pred.dtype), s) * math.pi / 2)).sum()
+        if not self.logical_only:
+            loss = torch.abs(torch.sin(torch.matmul(self.Ht.to(pred.dtype), s) * math.pi / 2)).sum() + loss
+        return loss
+
+
+class ClassicalLoss(torch.nn.Module):
+    def __init__(self, H, lambda_a=0.8):
+        super().__init__()
+        H = torch.as_tensor(H, dtype=torch.float32)
+        self.V = H.size(0)
+        self.register_buffer('Ht', H.t().contiguous())                      # [C, V]
+        self.lambda_a = lambda_a
+
+    def forward(self, pred, y, train=True):
+        loss_a = (1 - y).mul(torch.log(1 - pred)) + y.mul(torch.log(pred))
+        if not train:
+            return torch.sum(loss_a) / (-1 * torch.numel(loss_a))
+        loss_c = torch.abs(torch.sin(torch.matmul(self.Ht.to(pred.dtype), _cols(pred, self.V)) * math.pi / 2))
+        return (torch.sum(self.lambda_a * loss_a) / (-1 * torch.numel(loss_a))
+                + torch.sum((1 - self.lambda_a) * loss_c) / torch.numel(loss_c))
+
+
+def toric_failures(H, logical, y, pred):
+    """(residual-syndrome failures, logical failures) for hard decisions pred > 0.5."""
+    Ht = torch.as_tensor(H, dtype=torch.float32, device=pred.device).t()
+    lg = torch.as_tensor(logical, dtype=torch.float32, device=pred.device)
+    V = Ht.size(1)
+    e = torch.remainder(_cols(y, V).float() + (_cols(pred, V) > 0.5).float(), 2)
+    bad_syn = (torch.remainder(Ht @ e, 2) != 0).any(dim=0)
+    bad_log = (~bad_syn) & (torch.remainder(lg @ e, 2) != 0).any(dim=0)
+    return int(bad_syn.sum()), int(bad_log.sum())

@@ -15,8 +15,9 @@ passed to the constructor (`GNNI(Nc, H)`) instead of being read from module glob
 
 `forward(data)` runs the fused single-launch decoder (libgnnd `gnnd_decode`) whenever the
 batch is the tiled Tanner graph and no autograd graph is requested (eval mode or
-no_grad); otherwise it runs the reference's layer-by-layer loop on the device operator
-(`MessagePassing.propagate` -> gnnd_propagate_*).
+no_grad); otherwise (training) it runs the reference's layer-by-layer loop on the device
+operator (`MessagePassing.propagate` -> gnnd_propagate_*, with HIP backward kernels) and
+torch autograd through the MLPs.
 """
 import torch
 
@@ -188,10 +189,7 @@ class _Decoder(torch.nn.Module):
             return ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(x.dtype, x.device))
         if not x.is_cuda:
             raise RuntimeError('gnndecode runs on the GPU only (HIP/gfx950); move data to cuda')
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError('training through the device operator is not implemented '
-                                      'yet: run inference in eval mode or under torch.no_grad()')
-        self.graph(x.device)
+        self.graph(x.device)      # training: autograd through the HIP propagate kernels
         return self.forward_layers(x, edge_index)
 
     # ---- reference layer-by-layer loop on the device operator ---------------------------

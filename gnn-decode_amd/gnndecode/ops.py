@@ -27,12 +27,79 @@ def propagate_width(variant, flow):
     return _lib.get().gnnd_propagate_width(_lib.VARIANT[variant], _lib.FLOW[flow])
 
 
+def _tiled_batch(graph, edge_index, nE, dim_size, extra, aggr, chk_shift):
+    """Batch size if edge_index is `graph` tiled over codewords, else None."""
+    if graph is None or aggr == 'mean':
+        return None
+    shift = graph.V if chk_shift is None else chk_shift
+    if (dim_size == (nE // graph.E) * graph.N and (extra is None or extra.size(0) == dim_size)
+            and graph.is_tiled(edge_index, shift)):
+        return nE // graph.E
+    return None
+
+
+def _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B):
+    nE = msg.size(0)
+    F = propagate_width(variant, flow)
+    out = torch.empty(nE, F, dtype=msg.dtype, device=msg.device)
+    v, f, a = _lib.VARIANT[variant], _lib.FLOW[flow], _lib.AGGR[aggr]
+    dt = dtype_code(msg.dtype)
+    stream = current_stream(msg.device)
+    if B is not None:
+        _lib.call('gnnd_propagate_tiled', B[0].handle, v, f, a, dt, _ptr(msg), _ptr(extra),
+                  _ptr(out), B[1], stream)
+        return out
+    ei = edge_index if edge_index.stride(1) == 1 else edge_index.contiguous()
+    ws_bytes = ctypes.c_int64()
+    _lib.call('gnnd_propagate_generic_workspace', v, f, a, dt, nE, dim_size, ctypes.byref(ws_bytes))
+    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=msg.device)
+    _lib.call('gnnd_propagate_generic', v, f, a, dt, _ptr(ei), ei.stride(0), nE, _ptr(msg),
+              _ptr(extra), dim_size, _ptr(out), _ptr(ws), ws_bytes.value, stream)
+    return out
+
+
+def _propagate_bwd(variant, flow, aggr, edge_index, msg, grad_out, dim_size, B):
+    grad_out = grad_out.contiguous()
+    gmsg = torch.empty_like(msg)
+    v, f, a = _lib.VARIANT[variant], _lib.FLOW[flow], _lib.AGGR[aggr]
+    dt = dtype_code(msg.dtype)
+    stream = current_stream(msg.device)
+    if B is not None:
+        _lib.call('gnnd_propagate_tiled_bwd', B[0].handle, v, f, a, dt, _ptr(msg), _ptr(grad_out),
+                  _ptr(gmsg), B[1], stream)
+        return gmsg
+    ei = edge_index if edge_index.stride(1) == 1 else edge_index.contiguous()
+    ws = torch.empty(max(dim_size, 1), dtype=msg.dtype, device=msg.device)
+    _lib.call('gnnd_propagate_generic_bwd', v, f, a, dt, _ptr(ei), ei.stride(0), msg.size(0),
+              _ptr(msg), _ptr(grad_out), dim_size, _ptr(gmsg), _ptr(ws),
+              ws.numel() * ws.element_size(), stream)
+    return gmsg
+
+
+class _PropagateFn(torch.autograd.Function):
+    """propagate with a HIP backward w.r.t. the per-edge message (extra is data)."""
+
+    @staticmethod
+    def forward(ctx, msg, variant, flow, aggr, edge_index, extra, dim_size, B):
+        ctx.save_for_backward(msg, edge_index)
+        ctx.args = (variant, flow, aggr, dim_size, B)
+        return _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        msg, edge_index = ctx.saved_tensors
+        variant, flow, aggr, dim_size, B = ctx.args
+        gmsg = _propagate_bwd(variant, flow, aggr, edge_index, msg, grad_out, dim_size, B)
+        return gmsg, None, None, None, None, None, None, None
+
+
 def propagate(variant, flow, aggr, edge_index, msg, extra, dim_size, graph=None, chk_shift=None):
     """One reference `propagate` body on the device.
 
     msg [nE, 1] per-edge message, extra [dim_size, 1] node tensor (or None for CGNNI's
     `post=None`), edge_index int64 [2, nE].  Uses the tiled LDS kernel when `graph` matches
-    the batched edge_index, otherwise the generic (atomic) kernels.
+    the batched edge_index, otherwise the generic (atomic) kernels.  Differentiable w.r.t.
+    `msg` (aggr 'add', non-BP bodies) through HIP backward kernels.
     Returns [nE, F] with F = propagate_width(variant, flow).
     """
     _require_gpu(edge_index, msg, extra)
@@ -41,34 +108,23 @@ def propagate(variant, flow, aggr, edge_index, msg, extra, dim_size, graph=None,
     if msg.size(-1) != 1:
         raise ValueError('per-edge message must have one feature column (reference models)')
     msg = msg.contiguous()
-    dt = dtype_code(msg.dtype)
+    dtype_code(msg.dtype)
     if extra is not None:
         if extra.dim() == 1:
             extra = extra.unsqueeze(1)
-        extra = extra.to(msg.dtype).contiguous()
+        extra = extra.detach().to(msg.dtype).contiguous()
     nE = msg.size(0)
     if edge_index.size(1) != nE:
         raise ValueError('edge_index and message disagree on the number of edges')
-    F = propagate_width(variant, flow)
-    out = torch.empty(nE, F, dtype=msg.dtype, device=msg.device)
-    v, f, a = _lib.VARIANT[variant], _lib.FLOW[flow], _lib.AGGR[aggr]
-    stream = current_stream(msg.device)
     if extra is None and variant != 'cgnni':
         raise ValueError(f'{variant}: propagate needs `extra`')
-    if graph is not None and aggr != 'mean':
-        shift = graph.V if chk_shift is None else chk_shift
-        if (dim_size == (nE // graph.E) * graph.N and (extra is None or extra.size(0) == dim_size)
-                and graph.is_tiled(edge_index, shift)):
-            _lib.call('gnnd_propagate_tiled', graph.handle, v, f, a, dt, _ptr(msg), _ptr(extra),
-                      _ptr(out), nE // graph.E, stream)
-            return out
-    ei = edge_index if edge_index.stride(1) == 1 else edge_index.contiguous()
-    ws_bytes = ctypes.c_int64()
-    _lib.call('gnnd_propagate_generic_workspace', v, f, a, dt, nE, dim_size, ctypes.byref(ws_bytes))
-    ws = torch.empty(max(ws_bytes.value, 1), dtype=torch.uint8, device=msg.device)
-    _lib.call('gnnd_propagate_generic', v, f, a, dt, _ptr(ei), ei.stride(0), nE, _ptr(msg),
-              _ptr(extra), dim_size, _ptr(out), _ptr(ws), ws_bytes.value, stream)
-    return out
+    b = _tiled_batch(graph, edge_index, nE, dim_size, extra, aggr, chk_shift)
+    B = (graph, b) if b is not None else None
+    if msg.requires_grad and torch.is_grad_enabled():
+        if aggr != 'add' or variant in ('qbp', 'cbp'):
+            raise NotImplementedError(f'no backward for aggr={aggr!r} / variant {variant!r}')
+        return _PropagateFn.apply(msg, variant, flow, aggr, edge_index, extra, dim_size, B)
+    return _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B)
 
 
 def weights_count(model):

@@ -107,6 +107,18 @@ int gnnd_propagate_generic(int variant, int flow, int aggr, int dtype,
                            void* d_out, void* d_workspace, int64_t workspace_bytes,
                            void* stream);
 
+/* Backward of one propagate call w.r.t. d_msg (training; aggr ADD, non-BP variants — the BP
+ * decoders have no parameters).  d_grad_out is [B*E, F] like d_out, d_grad_msg [B*E].  The
+ * generic form needs a workspace of dim_size elements of `dtype`.                        */
+int gnnd_propagate_tiled_bwd(const gnnd_graph* g, int variant, int flow, int aggr, int dtype,
+                             const void* d_msg, const void* d_grad_out, void* d_grad_msg,
+                             int64_t batch, void* stream);
+int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
+                               const int64_t* d_edge_index, int64_t row_stride,
+                               int64_t num_edges, const void* d_msg, const void* d_grad_out,
+                               int64_t dim_size, void* d_grad_msg, void* d_workspace,
+                               int64_t workspace_bytes, void* stream);
+
 /* ---- fused T-iteration decoder --------------------------------------------------------
  * Runs the whole GNNI.forward (m0 = 0, T iterations of both half-steps, residual, readout)
  * for `batch` codewords in one launch; messages never leave the CU.

@@ -352,7 +352,98 @@ def gen_propagate(eg, H5, H4):
     save('propagate_ops', **arrays)
 
 
+def grads_of(model):
+    return {'g/' + k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()
+            if p.grad is not None}
+
+
+def gen_training():
+    """One forward + reference LossFunc + backward per trainable model: loss value and
+    parameter gradients (pins the training path)."""
+    sys.path.insert(0, os.path.join(REF, 'quantum'))
+    import error_generate as eg
+
+    def toric(L):
+        Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+        H = torch.from_numpy(Hnp).t()
+        hp = eg.H_Prep(H.t())
+        H_prep = torch.from_numpy(hp.get_H_Prep())
+        logical, _ = hp.get_logical(H_prep)
+        return H, H_prep, logical
+
+    # decoder_v2_4 at L = 5 (epoch-67 weights) and L = 7 (seeded init, config 5 shape)
+    for L, ckpt, B, T, seed in ((5, 'quantum/new_model/decoder_parameters_epoch67.pkl', 4, 15, 91),
+                                (7, None, 2, 15, 92)):
+        H, H_prep, logical = toric(L)
+        names = {'scatter_mean', 'scatter_', 'MessagePassing', 'GraphConv', 'GNNI',
+                 'init_weights', 'init_weights_2', 'LossFunc'}
+        ns = load_ref('quantum/decoder_v2_4.py', names, logical=logical)
+        x, y = toric_inputs(eg, H, L, [0.05, 0.1], B, seed)
+        V, C = H.shape
+        ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, B, H
+        set_seed(seed + 1)
+        model = ns['GNNI'](T)
+        if ckpt:
+            model.load_state_dict(torch.load(os.path.join(REF, ckpt), map_location='cpu',
+                                             weights_only=True))
+        sd = {k: v.clone() for k, v in model.state_dict().items()}
+        ei = batch_edge_index(single_edge_index(H), B, V + C)
+        data = types.SimpleNamespace(x=x, edge_index=ei, y=y)
+        pred = model(data)
+        loss = ns['LossFunc'](H, H_prep)(pred, data)
+        loss.backward()
+        save(f'train_v24_L{L}', x=x.numpy(), y=y.numpy(), loss=np.array(loss.item()),
+             pred=pred.detach().numpy(),
+             T=np.array(T), **sd_to_np(sd), **grads_of(model))
+
+    # QGNNI at L = 4 (logical-only loss)
+    H, H_prep, logical = toric(4)
+    ns = load_ref('quantum/QGNNI.py', {'MessagePassing', 'GraphConv', 'GNNI', 'LossFunc'},
+                  logical=logical)
+    B, T = 4, 25
+    x, y = toric_inputs(eg, H, 4, [0.05, 0.1], B, 93)
+    V, C = H.shape
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, B, H
+    set_seed(94)
+    model = ns['GNNI'](T)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    data = types.SimpleNamespace(x=x, edge_index=batch_edge_index(single_edge_index(H), B, V + C), y=y)
+    pred = model(data)
+    loss = ns['LossFunc'](H, H_prep)(pred, data)
+    loss.backward()
+    save('train_qgnni_L4', x=x.numpy(), y=y.numpy(), loss=np.array(loss.item()), T=np.array(T),
+         pred=pred.detach().numpy(),
+         **sd_to_np(sd), **grads_of(model))
+
+    # CGNNI on BCH(63,45) (epoch-18 weights), train-mode loss with lambda = 0.8
+    H = bch_H()
+    V, C = H.shape
+    ns = load_ref('classical/CGNNI.py', {'MessagePassing', 'GatedGraphConv', 'GNNI', 'LossFunc'},
+                  lambda_a=0.8)
+    B, T = 8, 25
+    llr, _ = awgn_llr(B, V, 1, 95)
+    x = classical_x(llr, C)
+    y = torch.ones(B * V, 1)
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, B, H
+    model = ns['GNNI'](T)
+    model.load_state_dict(torch.load(os.path.join(REF, 'classical/model/decoder_parameters_epoch18.pkl'),
+                                     map_location='cpu', weights_only=True))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    data = types.SimpleNamespace(x=x, edge_index=batch_edge_index(single_edge_index(H), B, V + C), y=y)
+    pred = model(data)
+    loss = ns['LossFunc'](H)(pred, data.y, 1)
+    loss.backward()
+    save('train_cgnni_bch', x=x.numpy(), y=y.numpy(), loss=np.array(loss.item()), T=np.array(T),
+         pred=pred.detach().numpy(),
+         **sd_to_np(sd), **grads_of(model))
+
+
 if __name__ == '__main__':
     torch.set_num_threads(1)
-    gen_classical()
-    gen_quantum()
+    which = sys.argv[1:] or ['classical', 'quantum', 'training']
+    if 'classical' in which:
+        gen_classical()
+    if 'quantum' in which:
+        gen_quantum()
+    if 'training' in which:
+        gen_training()

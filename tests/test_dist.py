@@ -1,0 +1,90 @@
+"""Multi-process data-parallel logic on CPU (gloo, world_size 2): shard bounds, the single
+flat SUM all-reduce, and that 2-rank training equals 1-process full-batch training."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from gnndecode import train
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_bounds_cover_exactly():
+    for B in (0, 1, 7, 64, 65536, 1 << 20):
+        for world in (1, 2, 3, 8):
+            spans = [train.shard_bounds(B, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == B
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [e - s for s, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+class _Toy(torch.nn.Module):
+    """Stand-in decoder with the reference's parameter structure (two MLPs, fp64)."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.mlp = torch.nn.Sequential(torch.nn.Linear(2, 16), torch.nn.Softplus(),
+                                       torch.nn.Linear(16, 1)).double()
+
+    def forward(self, x):
+        return torch.sigmoid(-self.mlp(x))
+
+
+def _sum_loss(pred, y):
+    return torch.abs(torch.sin((pred + y) * 3.14159 / 2)).sum()
+
+
+def _data(B, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(B, 2, generator=g, dtype=torch.float64), \
+        (torch.rand(B, 1, generator=g) < 0.3).double()
+
+
+def _worker(rank, world, port, B, steps, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    model = _Toy()
+    tr = train.Trainer(model, _sum_loss, lr=1e-2)
+    x, y = _data(B)
+    s, e = train.shard_bounds(B, rank, world)
+    losses = [float(tr.step(x[s:e], y[s:e])) for _ in range(steps)]
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    q.put((rank, losses, flat))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_training_equals_full_batch():
+    B, steps, world = 10, 3, 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process, full batch
+    model = _Toy()
+    tr = train.Trainer(model, _sum_loss, lr=1e-2)
+    x, y = _data(B)
+    ref_losses = [float(tr.step(x, y)) for _ in range(steps)]
+    ref_flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    for rank, losses, flat in res:
+        assert torch.allclose(flat, res[0][2], rtol=0, atol=0)     # ranks bitwise equal
+        assert torch.allclose(flat, ref_flat, rtol=1e-12, atol=1e-13)
+        assert all(abs(a - b) <= 1e-10 * max(1, abs(b)) for a, b in zip(losses, ref_losses))
