@@ -390,10 +390,11 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
         mlp_msg.load((const float*)s_w + kMlp10Msg);
 
-    // ---- per-lane resident state: item q = tid + q*256 (QMAX items; idle items of a
-    // partial last tile compute on a copy of the last real item and never store)
-    const int IC = C * G;
-    const int nItem = nb * IC;
+    // ---- per-lane resident state.  Item f = tid + q*256 -> (check c, codeword b, lane g)
+    // with g fastest and the CODEWORD next: a wave's 8 check groups are 8 codewords of one
+    // check, so their {S_v, x_v} reads and message writes land on different LDS banks
+    // (codeword strides V and E+1 are odd).  dItem divides by CW here.  Items of codewords
+    // b >= nb (partial last tile) or checks c >= C compute on clamped copies, never store.
     uint32_t ve[QMAX][R];      // v | e << 16 (padding: 0 | E << 16)
     T m[QMAX][R];
     T sc[QMAX];
@@ -402,13 +403,15 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
         const int f = tid + q * GNND_BLOCK;
-        const bool act = f < nItem;
-        const int fc = act ? f : nItem - 1;
-        const int b = fdiv(fc, dItem);
-        const int rem = fc - b * IC;
+        const int gi = f >> logG;
+        const int c = fdiv(gi, dItem);
+        const int b = gi - c * CW;
+        const bool act = c < C && b < nb;
+        const int cc = c < C ? c : C - 1, bb = b < nb ? b : nb - 1;
+        const int rem = cc * G + (f & (G - 1));
         actmask |= (act ? 1u : 0u) << q;
-        sc[q] = s_xc[b * C + (rem >> logG)];
-        cb[q] = b;
+        sc[q] = s_xc[bb * C + cc];
+        cb[q] = bb;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             ve[q][r] = g.slot_ve[rem * R + r];
@@ -448,13 +451,16 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             }
         }
         __syncthreads();
-        for (int f = tid; f < nV; f += GNND_BLOCK) {
-            const int b = fdiv(f, dV), v = f - b * V;
+        // variable sums, codeword fastest: the lanes of a wave sum the same variable (same
+        // trip count, no divergence) of consecutive codewords (odd stride E+1: no conflicts)
+        for (int f = tid; f < V * CW; f += GNND_BLOCK) {
+            const int v = fdiv(f, dItem), b = f - v * CW;
+            if (b >= nb) continue;
             const T* mb = s_m + b * E1;
             T s = T(0);
             for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[k];
-            if (it + 1 == iters) out[b0 * V + f] = M::readout(s + s_sx[f].x, s_w);
-            else s_sx[f].s = s;
+            if (it + 1 == iters) out[(b0 + b) * V + v] = M::readout(s + s_sx[b * V + v].x, s_w);
+            else s_sx[b * V + v].s = s;
         }
         __syncthreads();
     }
@@ -566,7 +572,8 @@ int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out,
     int64_t blocks = (B + p.cw - 1) / p.cw;
     if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
     const int nw = weights_count(MODEL);
-    const FastDiv dI = make_fastdiv(g.C * g.G), dV = make_fastdiv(g.V), dN = make_fastdiv(g.N);
+    const FastDiv dI = make_fastdiv(p.resident ? p.cw : g.C * g.G);
+    const FastDiv dV = make_fastdiv(g.V), dN = make_fastdiv(g.N);
     auto go = [&](auto kern) -> int {
         if (p.lds > 64 * 1024)
             GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,

@@ -21,7 +21,7 @@ def load(dirpath):
     for f in glob.glob(os.path.join(dirpath, '**', '*counter_collection.csv'), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if 'decode_kernel' not in row.get('Kernel_Name', ''):
+                if 'decode_kernel' not in row.get('Kernel_Name', '') and 'decode_resident_kernel' not in row.get('Kernel_Name', ''):
                     continue
                 key = (row['Dispatch_Id'], row['Counter_Name'])
                 vals[key].append(float(row['Counter_Value']))
