@@ -141,6 +141,17 @@ __device__ __forceinline__ float group_sum(float v, int G) {
     if (G > 32) v += __shfl_xor(v, 32);
     return v;
 }
+// compile-time group size: the butterfly is straight-line code (no uniform branches
+// splitting the caller's basic block, so independent work items interleave)
+template <int G> __device__ __forceinline__ float group_sum_c(float v) {
+    if constexpr (G > 1) v += dpp_mov<0xB1>(v);
+    if constexpr (G > 2) v += dpp_mov<0x4E>(v);
+    if constexpr (G > 4) v += dpp_mov<0x141>(v);
+    if constexpr (G > 8) v += dpp_mov<0x140>(v);
+    if constexpr (G > 16) v += __shfl_xor(v, 16);
+    if constexpr (G > 32) v += __shfl_xor(v, 32);
+    return v;
+}
 __device__ __forceinline__ double group_sum(double v, int G) {
     for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o);
     return v;
@@ -155,6 +166,13 @@ __device__ __forceinline__ float tanh_half_fast(float a) {
     return copysignf(t, a);
 }
 __device__ __forceinline__ double tanh_half_fast(double a) { return tanh(a / 2.0); }
+// tanh(a/2) from the base-2 scaled argument a2 = a * log2(e):  1 - 2 / (1 + 2^a2).
+// Saturates to +-1 (2^a2 -> inf or 0), never NaN; absolute error ~1.5e-7 near 0, i.e.
+// below the rounding of the 24-term check sums it feeds.  4 VALU ops, 2 transcendental.
+__device__ __forceinline__ float tanh_half_base2(float a2) {
+    const float r = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a2));
+    return __builtin_fmaf(-2.0f, r, 1.0f);
+}
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));

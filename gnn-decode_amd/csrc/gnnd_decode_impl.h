@@ -24,6 +24,7 @@
 #pragma once
 #include "gnnd_common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -353,15 +354,22 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 // (variable, edge) and check feature.  Step 1 therefore touches LDS only to read
 // {S_v, x_v} and to publish m_e in VARIABLE-major order (E + 1 per codeword, the extra
 // slot absorbs padding writes), and step 2 sums contiguous rows with no indirection.
-template <int MODEL, typename T, int R, int QMAX>
-__global__ void __launch_bounds__(GNND_BLOCK, 4)   // 4 waves/SIMD: <= 128 VGPRs
+#ifndef GNND_RESIDENT_WAVES
+#define GNND_RESIDENT_WAVES 4      // min waves per SIMD: 4 -> <= 128 VGPRs (tuning builds vary it)
+#endif
+template <int MODEL, typename T, int G, int R, int QMAX>
+__global__ void __launch_bounds__(GNND_BLOCK, GNND_RESIDENT_WAVES)
 decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
                        T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem,
                        FastDiv dV, FastDiv dN) {
     using M = EdgeMath<MODEL, T>;
     constexpr bool BP = ModelTraits<MODEL>::bp;
+    // fp32 GNN models keep x_v pre-scaled by log2(e) so the v->c pre-op is one FMA into
+    // the base-2 tanh (tanh_half_base2); the readout re-reads the unscaled x_v from HBM.
+    constexpr bool kBase2 = sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI);
+    constexpr int kLogG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
+    const int V = g.V, C = g.C, E = g.E, N = g.N;
     const int E1 = E + 1;
     const int tid = threadIdx.x;
 
@@ -381,7 +389,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     for (int i = tid; i < nb * N; i += GNND_BLOCK) {
         int b = fdiv(i, dN), n = i - b * N;
         T xv = xg[i];
-        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
+        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
         else s_xc[b * C + n - V] = xv;
     }
     __syncthreads();
@@ -394,32 +402,32 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     // with g fastest and the CODEWORD next: a wave's 8 check groups are 8 codewords of one
     // check, so their {S_v, x_v} reads and message writes land on different LDS banks
     // (codeword strides V and E+1 are odd).  dItem divides by CW here.  Items of codewords
-    // b >= nb (partial last tile) or checks c >= C compute on clamped copies, never store.
-    uint32_t ve[QMAX][R];      // v | e << 16 (padding: 0 | E << 16)
+    // b >= nb (partial last tile) or checks c >= C compute on clamped copies and, like
+    // padding slots, store into the spare slot E of their codeword: the item loop is
+    // straight-line code.
+    uint32_t ve[QMAX][R];      // v | e << 16 (padding and idle items: e = E)
     T m[QMAX][R];
     T sc[QMAX];
     int cb[QMAX];              // codeword of the item
-    uint32_t actmask = 0;
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
         const int f = tid + q * GNND_BLOCK;
-        const int gi = f >> logG;
+        const int gi = f >> kLogG;
         const int c = fdiv(gi, dItem);
         const int b = gi - c * CW;
         const bool act = c < C && b < nb;
         const int cc = c < C ? c : C - 1, bb = b < nb ? b : nb - 1;
         const int rem = cc * G + (f & (G - 1));
-        actmask |= (act ? 1u : 0u) << q;
         sc[q] = s_xc[bb * C + cc];
         cb[q] = bb;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            ve[q][r] = g.slot_ve[rem * R + r];
+            const uint32_t sv = g.slot_ve[rem * R + r];
+            ve[q][r] = act ? sv : ((sv & 0xffffu) | ((uint32_t)E << 16));
             m[q][r] = T(0);
         }
     }
 
-    const int nV = nb * V;
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int q = 0; q < QMAX; ++q) {
@@ -431,41 +439,52 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                 const uint32_t sv = ve[q][r];
                 const bool valid = (int)(sv >> 16) != E;
                 const SumX<T> p = sxb[sv & 0xffffu];
-                T cc;
-                T t = M::pre(p.s - m[q][r], p.x, w, cc);
+                T cc = T(0), t;
+                if constexpr (kBase2) t = tanh_half_base2(__builtin_fmaf(p.s - m[q][r], kLog2e, p.x));
+                else t = M::pre(p.s - m[q][r], p.x, w, cc);
                 tv[r] = valid ? t : T(0);
                 cf[r] = valid ? cc : T(0);
                 tsum += tv[r];
                 if constexpr (BP) csum += cf[r];
             }
-            const T Sc = group_sum(tsum, G);
+            const T Sc = group_sum_c<G>(tsum);
             T Sc2 = T(0);
-            if constexpr (BP) Sc2 = group_sum(csum, G);
+            if constexpr (BP) Sc2 = group_sum_c<G>(csum);
+            T* mb = s_m + cb[q] * E1;
 #pragma unroll
-            for (int r = 0; r < R; ++r)
+            for (int r = 0; r < R; ++r) {
                 m[q][r] = M::post(Sc - tv[r], Sc2 - cf[r], sc[q], m[q][r], mlp_msg, s_w, w);
-            if (actmask & (1u << q)) {
-                T* mb = s_m + cb[q] * E1;
-#pragma unroll
-                for (int r = 0; r < R; ++r) mb[ve[q][r] >> 16] = m[q][r];
+                mb[ve[q][r] >> 16] = m[q][r];
             }
         }
         __syncthreads();
         // variable sums, codeword fastest: the lanes of a wave sum the same variable (same
-        // trip count, no divergence) of consecutive codewords (odd stride E+1: no conflicts)
+        // trip count, no divergence) of consecutive codewords (odd stride E+1: no conflicts).
+        // Four independent LDS reads in flight per step, added in edge (index_add) order.
+        const bool last = it + 1 == iters;
         for (int f = tid; f < V * CW; f += GNND_BLOCK) {
             const int v = fdiv(f, dItem), b = f - v * CW;
             if (b >= nb) continue;
             const T* mb = s_m + b * E1;
+            const int k0 = s_vptr[v], ke = s_vptr[v + 1];
             T s = T(0);
-            for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += mb[k];
-            if (it + 1 == iters) out[(b0 + b) * V + v] = M::readout(s + s_sx[b * V + v].x, s_w);
+            for (int k = k0; k < ke; k += 4) {
+                T val[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) val[j] = mb[min(k + j, ke - 1)];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s += k + j < ke ? val[j] : T(0);
+            }
+            if (last) out[(b0 + b) * V + v] = M::readout(s + (kBase2 ? xg[b * N + v] : s_sx[b * V + v].x), s_w);
             else s_sx[b * V + v].s = s;
         }
         __syncthreads();
     }
     if (iters == 0)
-        for (int f = tid; f < nV; f += GNND_BLOCK) out[b0 * V + f] = M::readout(s_sx[f].x, s_w);
+        for (int f = tid; f < nb * V; f += GNND_BLOCK) {
+            const int b = fdiv(f, dV), v = f - b * V;
+            out[b0 * V + f] = M::readout(xg[b * N + v], s_w);
+        }
 }
 
 int weights_count(int model) {
@@ -514,7 +533,8 @@ int make_plan(int model, int dtype, const GraphView& g, Plan* p) {
     const size_t target = lds_target();
     const int IC = g.C * g.G;
     const bool light = model != GNND_V24;
-    if (light && dtype == GNND_F32 && !resident_disabled()) {
+    const bool g_ok = g.G == 4 || g.G == 8 || g.G == 16;   // instantiated group sizes
+    if (light && dtype == GNND_F32 && g_ok && !resident_disabled()) {
         // resident layout: weights, var_ptr, then [CW][E+1] messages, [CW][V] {S, x}, [CW][C].
         // Pick (CW, Q) with Q in kResidentQ maximising lane utilisation CW*IC / (Q*256),
         // ties to the larger tile.
@@ -585,11 +605,22 @@ int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out,
     };
     if constexpr (MODEL != GNND_V24 && sizeof(T) == 4) {
         if (p.resident) {
-            switch (p.q) {
-                case 3: return go(decode_resident_kernel<MODEL, T, R, 3>);
-                case 6: return go(decode_resident_kernel<MODEL, T, R, 6>);
-                case 9: return go(decode_resident_kernel<MODEL, T, R, 9>);
-                case 12: return go(decode_resident_kernel<MODEL, T, R, 12>);
+            auto by_q = [&](auto gtag) -> int {
+                constexpr int G = decltype(gtag)::value;
+                switch (p.q) {
+                    case 3: return go(decode_resident_kernel<MODEL, T, G, R, 3>);
+                    case 6: return go(decode_resident_kernel<MODEL, T, G, R, 6>);
+                    case 9: if constexpr (R <= 3) return go(decode_resident_kernel<MODEL, T, G, R, 9>);
+                            break;
+                    case 12: if constexpr (R <= 2) return go(decode_resident_kernel<MODEL, T, G, R, 12>);
+                             break;
+                }
+                return GNND_ERR_UNSUPPORTED;
+            };
+            switch (g.G) {
+                case 4: return by_q(std::integral_constant<int, 4>{});
+                case 8: return by_q(std::integral_constant<int, 8>{});
+                case 16: return by_q(std::integral_constant<int, 16>{});
             }
             return GNND_ERR_UNSUPPORTED;
         }

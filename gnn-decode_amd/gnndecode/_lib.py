@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libgnnd.so')
+LIB_PATH = os.environ.get('GNND_LIB') or os.path.join(_HERE, 'libgnnd.so')   # GNND_LIB: tuning builds
 
 # enums (include/gnnd.h)
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_GRAPH, ERR_ALLOC = range(6)

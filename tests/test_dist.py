@@ -61,7 +61,9 @@ def _worker(rank, world, port, B, steps, q):
     s, e = train.shard_bounds(B, rank, world)
     losses = [float(tr.step(x[s:e], y[s:e])) for _ in range(steps)]
     flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
-    q.put((rank, losses, flat))
+    # plain list, not a tensor: a tensor goes through fd sharing, which races the
+    # worker's exit
+    q.put((rank, losses, flat.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -85,6 +87,7 @@ def test_two_rank_training_equals_full_batch():
     ref_losses = [float(tr.step(x, y)) for _ in range(steps)]
     ref_flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
     for rank, losses, flat in res:
-        assert torch.allclose(flat, res[0][2], rtol=0, atol=0)     # ranks bitwise equal
+        flat = torch.tensor(flat, dtype=torch.float64)
+        assert flat.tolist() == res[0][2]     # ranks bitwise equal
         assert torch.allclose(flat, ref_flat, rtol=1e-12, atol=1e-13)
         assert all(abs(a - b) <= 1e-10 * max(1, abs(b)) for a, b in zip(losses, ref_losses))
