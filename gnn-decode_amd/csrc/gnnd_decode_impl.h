@@ -57,29 +57,45 @@ __device__ __forceinline__ T mlp10_relu(const T* w, T u) {
     return acc + w[30];
 }
 
-// fp32 packed form with the 31 weights held in VGPRs (two hidden units per v_pk_fma_f32)
+// fp32 form with the 31 weights held in VGPRs.  ReLU is folded into the first FMA as the
+// hardware [0, 1] output clamp: unit k is evaluated as clamp(fma(u, W1_k 2^-s_k, b1_k 2^-s_k))
+// and weighted by W2_k 2^s_k, where 2^s_k > |W1_k| umax + |b1_k| bounds the pre-activation
+// over the input range |u| <= umax.  Scaling by a power of two commutes with the rounding
+// of the FMA and of the product, so every unit's contribution is bit-identical to
+// W2_k relu(fma(u, W1_k, b1_k)); the clamp saves the separate max.  The second layer
+// accumulates two units per v_pk_fma_f32.
 struct Mlp10F32 {
     f32x2 w1[5], b1[5], w2[5];
     float b2;
-    __device__ __forceinline__ void load(const float* w) {
+    __device__ __forceinline__ void load(const float* w, float umax) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            w1[k] = f32x2{w[2 * k], w[2 * k + 1]};
-            b1[k] = f32x2{w[10 + 2 * k], w[11 + 2 * k]};
-            w2[k] = f32x2{w[20 + 2 * k], w[21 + 2 * k]};
+        for (int k = 0; k < 10; ++k) {
+            int e;
+            frexpf(fabsf(w[k]) * umax + fabsf(w[10 + k]), &e);    // 2^e > bound
+            const float a = ldexpf(w[k], -e), b = ldexpf(w[10 + k], -e), v = ldexpf(w[20 + k], e);
+            if (k & 1) { w1[k >> 1].y = a; b1[k >> 1].y = b; w2[k >> 1].y = v; }
+            else       { w1[k >> 1].x = a; b1[k >> 1].x = b; w2[k >> 1].x = v; }
         }
         b2 = w[30];
     }
     __device__ __forceinline__ float operator()(float u) const {
-        const f32x2 uu = {u, u};
-        f32x2 acc = {0.f, 0.f};
+        f32x2 acc = {b2, 0.f};                 // bias rides in the even-unit accumulator
+        f32x2 uu;                              // only the lo half is read (op_sel_hi 0)
+        uu.x = u;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            f32x2 h = __builtin_elementwise_fma(uu, w1[k], b1[k]);
-            h = __builtin_elementwise_max(h, f32x2{0.f, 0.f});
+#ifdef GNND_SCALAR_CLAMP
+            const f32x2 h = {__builtin_amdgcn_fmed3f(__builtin_fmaf(u, w1[k].x, b1[k].x), 0.f, 1.f),
+                             __builtin_amdgcn_fmed3f(__builtin_fmaf(u, w1[k].y, b1[k].y), 0.f, 1.f)};
+#else
+            // hipcc does not fold a clamp into v_pk_fma_f32: one packed FMA + clamp in asm
+            f32x2 h;
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp"
+                : "=v"(h) : "v"(uu), "v"(w1[k]), "v"(b1[k]));
+#endif
             acc = __builtin_elementwise_fma(h, w2[k], acc);
         }
-        return (acc.x + acc.y) + b2;
+        return acc.x + acc.y;
     }
 };
 
@@ -280,7 +296,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     const T* __restrict__ wv = w;
     Mlp10F32 mlp_msg;   // 10-hidden message MLP weights live in VGPRs for the whole decode
     if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
-        mlp_msg.load((const float*)s_w + kMlp10Msg);
+        mlp_msg.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
 
     const int IC = C * G;               // work items (lanes) per codeword
     const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
@@ -396,7 +412,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 
     Mlp10F32 mlp_msg;
     if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
-        mlp_msg.load((const float*)s_w + kMlp10Msg);
+        mlp_msg.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
 
     // ---- per-lane resident state.  Item f = tid + q*256 -> (check c, codeword b, lane g)
     // with g fastest and the CODEWORD next: a wave's 8 check groups are 8 codewords of one
