@@ -23,6 +23,9 @@ struct GraphView {            // passed by value to kernels
     const uint32_t* slot;     // [C*G*R]  variable of the slot's edge; GNND_SLOT_PAD if padding
     const int* vslot;         // [E]      slot of edge e (reference edge order = var-major)
     const uint32_t* slot_ve;  // [C*G*R]  v | (e << 16); padding = 0 | (E << 16) (dummy edge)
+    // variables sorted by (degree, v): {v | dv << 16, first edge}.  Consecutive entries have
+    // (nearly) equal degree, so lanes summing them run the same trip count.
+    const uint2* var_ord;     // [V]
 };
 #define GNND_SLOT_PAD 0x80000000u   // padding slot: variable 0, flag bit 31
 

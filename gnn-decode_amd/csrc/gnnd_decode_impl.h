@@ -391,14 +391,14 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 
     T* s_w = (T*)smem;
     size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
-    int* s_vptr = (int*)(smem + off);
-    off += (((size_t)V + 1) * 4 + 15) & ~(size_t)15;
+    uint2* s_vord = (uint2*)(smem + off);
+    off += ((size_t)V * 8 + 15) & ~(size_t)15;
     T* s_m = (T*)(smem + off);                             // [CW][E+1] messages, var-major
     SumX<T>* s_sx = (SumX<T>*)(s_m + (((size_t)CW * E1 + 1) & ~(size_t)1));  // [CW][V]
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
 
     for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
-    for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
+    for (int i = tid; i < V; i += GNND_BLOCK) s_vord[i] = g.var_ord[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     const T* xg = x + b0 * N;
@@ -474,23 +474,29 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             }
         }
         __syncthreads();
-        // variable sums, codeword fastest: the lanes of a wave sum the same variable (same
-        // trip count, no divergence) of consecutive codewords (odd stride E+1: no conflicts).
-        // Four independent LDS reads in flight per step, added in edge (index_add) order.
+        // variable sums, codeword fastest, variables in degree order (var_ord): a wave's
+        // lanes sum 64 / CW variables of (nearly) the same degree for consecutive codewords
+        // (odd stride E+1: no bank conflicts).  Edge (index_add) order within a variable;
+        // two-value ds_read2 loads, four values in flight per step, no masking.
         const bool last = it + 1 == iters;
         for (int f = tid; f < V * CW; f += GNND_BLOCK) {
-            const int v = fdiv(f, dItem), b = f - v * CW;
+            const int i = fdiv(f, dItem), b = f - i * CW;
             if (b >= nb) continue;
-            const T* mb = s_m + b * E1;
-            const int k0 = s_vptr[v], ke = s_vptr[v + 1];
+            const uint2 o = s_vord[i];
+            const int v = (int)(o.x & 0xffffu), dv = (int)(o.x >> 16);
+            const T* mp = s_m + b * E1 + (int)o.y;
             T s = T(0);
-            for (int k = k0; k < ke; k += 4) {
-                T val[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) val[j] = mb[min(k + j, ke - 1)];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) s += k + j < ke ? val[j] : T(0);
+            int k = 0;
+            for (; k + 4 <= dv; k += 4) {
+                const T a0 = mp[k], a1 = mp[k + 1], a2 = mp[k + 2], a3 = mp[k + 3];
+                s += a0; s += a1; s += a2; s += a3;
             }
+            if (dv & 2) {
+                const T a0 = mp[k], a1 = mp[k + 1];
+                s += a0; s += a1;
+                k += 2;
+            }
+            if (dv & 1) s += mp[k];
             if (last) out[(b0 + b) * V + v] = M::readout(s + (kBase2 ? xg[b * N + v] : s_sx[b * V + v].x), s_w);
             else s_sx[b * V + v].s = s;
         }
@@ -551,10 +557,10 @@ int make_plan(int model, int dtype, const GraphView& g, Plan* p) {
     const bool light = model != GNND_V24;
     const bool g_ok = g.G == 4 || g.G == 8 || g.G == 16;   // instantiated group sizes
     if (light && dtype == GNND_F32 && g_ok && !resident_disabled()) {
-        // resident layout: weights, var_ptr, then [CW][E+1] messages, [CW][V] {S, x}, [CW][C].
+        // resident layout: weights, var_ord, then [CW][E+1] messages, [CW][V] {S, x}, [CW][C].
         // Pick (CW, Q) with Q in kResidentQ maximising lane utilisation CW*IC / (Q*256),
         // ties to the larger tile.
-        const size_t fixed = wb + align16(((size_t)g.V + 1) * 4);
+        const size_t fixed = wb + align16((size_t)g.V * 8);
         auto lds_of = [&](int cw) {
             return fixed + esz * (((size_t)cw * (g.E + 1) + 1) & ~(size_t)1) +
                    esz * ((size_t)cw * (2 * (size_t)g.V + g.C));

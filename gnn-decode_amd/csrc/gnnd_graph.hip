@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
+#include <algorithm>
 
 static thread_local int g_last_hip_error = 0;
 
@@ -84,8 +85,15 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             vslot[e] = pos;
         }
 
+    std::vector<int> vord(V);
+    for (int v = 0; v < V; ++v) vord[v] = v;
+    std::stable_sort(vord.begin(), vord.end(), [&](int a, int b) {
+        return vptr[a + 1] - vptr[a] < vptr[b + 1] - vptr[b];
+    });
+
     const int nints = graph_table_ints(V, C, E);
-    std::vector<int> table(nints + nslot + E + nslot);
+    const int ord_off = (nints + nslot + E + nslot + 1) & ~1;     // uint2 alignment
+    std::vector<int> table(ord_off + 2 * V);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
@@ -93,6 +101,11 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     memcpy(table.data() + nints, slot.data(), sizeof(int) * nslot);
     memcpy(table.data() + nints + nslot, vslot.data(), sizeof(int) * E);
     memcpy(table.data() + nints + nslot + E, slot_ve.data(), sizeof(int) * nslot);
+    for (int i = 0; i < V; ++i) {
+        const int v = vord[i];
+        table[ord_off + 2 * i] = v | ((vptr[v + 1] - vptr[v]) << 16);
+        table[ord_off + 2 * i + 1] = vptr[v];
+    }
 
     gnnd_graph* g = (gnnd_graph*)calloc(1, sizeof(gnnd_graph));
     if (!g) return GNND_ERR_ALLOC;
@@ -115,6 +128,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     gv.slot = (const uint32_t*)(d + nints);
     gv.vslot = d + nints + nslot;
     gv.slot_ve = (const uint32_t*)(d + nints + nslot + E);
+    gv.var_ord = (const uint2*)(d + ord_off);
     *out = g;
     return GNND_OK;
 }
