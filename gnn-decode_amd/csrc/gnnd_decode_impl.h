@@ -64,6 +64,9 @@ __device__ __forceinline__ T mlp10_relu(const T* w, T u) {
 // of the FMA and of the product, so every unit's contribution is bit-identical to
 // W2_k relu(fma(u, W1_k, b1_k)); the clamp saves the separate max.  The second layer
 // accumulates two units per v_pk_fma_f32.
+__device__ __forceinline__ float uniform(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
 struct Mlp10F32 {
     f32x2 w1[5], b1[5], w2[5];
     float b2;
@@ -72,11 +75,14 @@ struct Mlp10F32 {
         for (int k = 0; k < 10; ++k) {
             int e;
             frexpf(fabsf(w[k]) * umax + fabsf(w[10 + k]), &e);    // 2^e > bound
-            const float a = ldexpf(w[k], -e), b = ldexpf(w[10 + k], -e), v = ldexpf(w[20 + k], e);
+            // wave-uniform: readfirstlane puts the weights in SGPRs (one scalar operand per
+            // packed op), leaving the VGPRs to the resident messages
+            const float a = uniform(ldexpf(w[k], -e)), b = uniform(ldexpf(w[10 + k], -e)),
+                        v = uniform(ldexpf(w[20 + k], e));
             if (k & 1) { w1[k >> 1].y = a; b1[k >> 1].y = b; w2[k >> 1].y = v; }
             else       { w1[k >> 1].x = a; b1[k >> 1].x = b; w2[k >> 1].x = v; }
         }
-        b2 = w[30];
+        b2 = uniform(w[30]);
     }
     __device__ __forceinline__ float operator()(float u) const {
         f32x2 acc = {b2, 0.f};                 // bias rides in the even-unit accumulator
@@ -91,7 +97,7 @@ struct Mlp10F32 {
             // hipcc does not fold a clamp into v_pk_fma_f32: one packed FMA + clamp in asm
             f32x2 h;
             asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp"
-                : "=v"(h) : "v"(uu), "v"(w1[k]), "v"(b1[k]));
+                : "=v"(h) : "v"(uu), "s"(w1[k]), "v"(b1[k]));
 #endif
             acc = __builtin_elementwise_fma(h, w2[k], acc);
         }
@@ -373,7 +379,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 #ifndef GNND_RESIDENT_WAVES
 #define GNND_RESIDENT_WAVES 4      // min waves per SIMD: 4 -> <= 128 VGPRs (tuning builds vary it)
 #endif
-template <int MODEL, typename T, int G, int R, int QMAX>
+template <int MODEL, typename T, int G, int R, int QMAX, bool PAD>
 __global__ void __launch_bounds__(GNND_BLOCK, GNND_RESIDENT_WAVES)
 decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
                        T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem,
@@ -453,15 +459,16 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t sv = ve[q][r];
-                const bool valid = (int)(sv >> 16) != E;
+                const bool valid = !PAD || (int)(sv >> 16) != E;   // every slot real: no mask
                 const SumX<T> p = sxb[sv & 0xffffu];
                 T cc = T(0), t;
                 if constexpr (kBase2) t = tanh_half_base2(__builtin_fmaf(p.s - m[q][r], kLog2e, p.x));
                 else t = M::pre(p.s - m[q][r], p.x, w, cc);
                 tv[r] = valid ? t : T(0);
                 cf[r] = valid ? cc : T(0);
-                tsum += tv[r];
-                if constexpr (BP) csum += cf[r];
+                // the first term starts the sum (0 + t == t: t is never -0)
+                tsum = r == 0 ? tv[0] : tsum + tv[r];
+                if constexpr (BP) csum = r == 0 ? cf[0] : csum + cf[r];
             }
             const T Sc = group_sum_c<G>(tsum);
             T Sc2 = T(0);
@@ -627,24 +634,28 @@ int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out,
     };
     if constexpr (MODEL != GNND_V24 && sizeof(T) == 4) {
         if (p.resident) {
-            auto by_q = [&](auto gtag) -> int {
+            auto by_q = [&](auto gtag, auto ptag) -> int {
                 constexpr int G = decltype(gtag)::value;
+                constexpr bool P = decltype(ptag)::value;
                 switch (p.q) {
-                    case 3: return go(decode_resident_kernel<MODEL, T, G, R, 3>);
-                    case 6: return go(decode_resident_kernel<MODEL, T, G, R, 6>);
-                    case 9: if constexpr (R <= 3) return go(decode_resident_kernel<MODEL, T, G, R, 9>);
+                    case 3: return go(decode_resident_kernel<MODEL, T, G, R, 3, P>);
+                    case 6: return go(decode_resident_kernel<MODEL, T, G, R, 6, P>);
+                    case 9: if constexpr (R <= 3) return go(decode_resident_kernel<MODEL, T, G, R, 9, P>);
                             break;
-                    case 12: if constexpr (R <= 2) return go(decode_resident_kernel<MODEL, T, G, R, 12>);
+                    case 12: if constexpr (R <= 2) return go(decode_resident_kernel<MODEL, T, G, R, 12, P>);
                              break;
                 }
                 return GNND_ERR_UNSUPPORTED;
             };
-            switch (g.G) {
-                case 4: return by_q(std::integral_constant<int, 4>{});
-                case 8: return by_q(std::integral_constant<int, 8>{});
-                case 16: return by_q(std::integral_constant<int, 16>{});
-            }
-            return GNND_ERR_UNSUPPORTED;
+            auto by_g = [&](auto ptag) -> int {
+                switch (g.G) {
+                    case 4: return by_q(std::integral_constant<int, 4>{}, ptag);
+                    case 8: return by_q(std::integral_constant<int, 8>{}, ptag);
+                    case 16: return by_q(std::integral_constant<int, 16>{}, ptag);
+                }
+                return GNND_ERR_UNSUPPORTED;
+            };
+            return g.padded ? by_g(std::true_type{}) : by_g(std::false_type{});
         }
     }
     return go(decode_kernel<MODEL, T, R>);

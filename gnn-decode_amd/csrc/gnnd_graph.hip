@@ -123,6 +123,8 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     gv.chk_ptr = d + E + V + 1;
     gv.chk_edge = d + E + V + 1 + C + 1;
     gv.G = bestG; gv.R = bestR;
+    gv.padded = 0;
+    for (int c = 0; c < C; ++c) gv.padded |= (cptr[c + 1] - cptr[c]) != bestG * bestR;
     gv.logG = 0;
     while ((1 << gv.logG) < bestG) ++gv.logG;
     gv.slot = (const uint32_t*)(d + nints);
