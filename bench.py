@@ -65,16 +65,21 @@ def parse():
     return p.parse_args()
 
 
-def load_pmc_traffic(tag):
-    """HBM bytes per launch from a committed rocprofv3 --pmc summary (profiles/), or None."""
+def load_pmc(tag):
+    """Committed rocprofv3 --pmc summary of this workload (profiles/pmc_<tag>.json) or {}."""
     path = os.path.join(ROOT, 'profiles', f'pmc_{tag}.json')
     if not os.path.exists(path):
-        return None
+        return {}
     try:
         with open(path) as f:
-            return json.load(f).get('hbm_bytes_per_launch')
+            return json.load(f)
     except Exception:
-        return None
+        return {}
+
+
+# VALU issue capacity: one wave64 VALU instruction per CU per clock (4 SIMDs x one
+# 4-cycle wave64 op); 256 CUs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md).
+VALU_ISSUE_PER_S = 256 * 2.4e9
 
 
 def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
@@ -227,9 +232,11 @@ def main():
         peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
         esz = 4 if dtype == torch.float32 else 8
         io_bytes = (g.N + g.V) * esz * a.batch
-        cw_cfg = gd.ops.decode_tile(g, a.model, dtype)
+        plan = gd.ops.decode_plan(g, a.model, dtype)
         tag = f'{a.model}_{a.code}_B{a.batch}_T{T}_{a.dtype}'
-        traffic = load_pmc_traffic(tag)
+        pmc = load_pmc(tag)
+        traffic = pmc.get('hbm_bytes_per_launch')
+        valu = (pmc.get('counters_per_dispatch_mean') or {}).get('SQ_INSTS_VALU')
         res = {
             'metric': 'codewords/sec (whole node) at matched BER, T-iter GNN decode',
             'value': world * a.batch * a.steps / elapsed,
@@ -241,11 +248,17 @@ def main():
             'config': {'workload': f'{a.code} {a.model} decode, T={T}, batch={a.batch}/GPU',
                        'code': a.code, 'model': a.model, 'iters': T, 'batch_per_gpu': a.batch,
                        'global_batch': a.batch * world, 'parallelism': f'dp{world} (codeword shards)',
-                       'codewords_per_workgroup': cw_cfg[0], 'lds_bytes_per_workgroup': cw_cfg[1],
+                       'codewords_per_workgroup': plan['cw'], 'lds_bytes_per_workgroup': plan['lds'],
+                       'items_per_lane': plan['items_per_lane'],
                        'hard_decision_error_rate': ber},
             'roofline': {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
                          'frac': achieved / peak, 'traffic': traffic,
-                         'kernel': f'decode_kernel<{a.model}, {a.dtype}>',
+                         'kernel': f"{plan['kernel']}<{a.model}, {a.dtype}>",
+                         # from the committed PMC pass of this workload: wave64 VALU
+                         # instructions per launch / issue capacity over the kernel time
+                         'valu_insts_per_launch': valu,
+                         'valu_issue_frac_at_peak_clock':
+                             valu / (kernel_s * VALU_ISSUE_PER_S) if valu else None,
                          'kernel_ms': kernel_s * 1e3,
                          'flops_per_codeword': fl, 'transcendentals_per_codeword': trans,
                          'hbm_io_bytes_per_launch': io_bytes,

@@ -80,6 +80,19 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
     return GNND_OK;
 }
 
+extern "C" int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan) {
+    if (!g || !h_plan || weights_count(model) < 0) return GNND_ERR_INVALID_ARG;
+    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
+    Plan p;
+    int rc = make_plan(model, dtype, g->view, &p);
+    if (rc != GNND_OK) return rc;
+    h_plan[0] = p.cw;
+    h_plan[1] = (int32_t)p.lds;
+    h_plan[2] = p.resident ? 1 : 0;
+    h_plan[3] = p.q;
+    return GNND_OK;
+}
+
 extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w,
                            const void* d_x, void* d_out, int64_t batch, int32_t iters,
                            void* stream) {

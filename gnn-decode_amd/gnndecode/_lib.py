@@ -43,6 +43,7 @@ SIGNATURES = {
     'gnnd_prepare_weights': (_int, [_int, _int, _vp, _vp, _vp]),
     'gnnd_decode': (_int, [_vp, _int, _int, _vp, _vp, _vp, _i64, _i32, _vp]),
     'gnnd_decode_tile': (_int, [_vp, _int, _int, _c_i32p, _c_i32p]),
+    'gnnd_decode_plan': (_int, [_vp, _int, _int, _c_i32p]),
     'gnnd_status_string': (ctypes.c_char_p, [_int]),
     'gnnd_last_hip_error': (_int, []),
     'gnnd_version': (_int, []),

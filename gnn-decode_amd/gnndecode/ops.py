@@ -167,6 +167,15 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     return out
 
 
+def decode_plan(graph, model, dtype):
+    """{'cw', 'lds', 'kernel', 'items_per_lane'} of the fused decoder's launch plan."""
+    plan = (ctypes.c_int32 * 4)()
+    _lib.call('gnnd_decode_plan', graph.handle, _lib.VARIANT[model], dtype_code(dtype), plan)
+    return {'cw': plan[0], 'lds': plan[1],
+            'kernel': 'decode_resident_kernel' if plan[2] else 'decode_kernel',
+            'items_per_lane': plan[3]}
+
+
 def decode_tile(graph, model, dtype):
     cw, lds = ctypes.c_int32(), ctypes.c_int32()
     _lib.call('gnnd_decode_tile', graph.handle, _lib.VARIANT[model], dtype_code(dtype),

@@ -144,6 +144,10 @@ int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, cons
 /* Codewords per workgroup the decoder would use (for roofline bookkeeping). */
 int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32_t* h_cw_per_block,
                      int32_t* h_lds_bytes);
+/* Full launch plan: h_plan[0] codewords per workgroup, [1] LDS bytes per workgroup,
+ * [2] kernel (0 = streaming decode_kernel, 1 = register-resident decode_resident_kernel),
+ * [3] work items per lane (resident kernel; 0 otherwise). */
+int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan);
 
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gnnd_status_string(int status);
