@@ -31,7 +31,8 @@ struct GraphView {            // passed by value to kernels
 #define GNND_SLOT_PAD 0x80000000u   // padding slot: variable 0, flag bit 31
 
 struct gnnd_graph {
-    GraphView view;
+    GraphView view;           // slot plan of the streaming kernel (ties -> smaller R)
+    GraphView rview;          // slot plan of the register-resident kernel (ties -> larger R)
     void* dev;                // single device allocation holding every table
     size_t table_bytes;       // bytes of the four CSR/CSC tables (staged to LDS)
 };

@@ -73,7 +73,7 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
     if (!g || !h_cw || !h_lds || weights_count(model) < 0) return GNND_ERR_INVALID_ARG;
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     Plan p;
-    int rc = make_plan(model, dtype, g->view, &p);
+    int rc = make_plan(model, dtype, g, &p);
     if (rc != GNND_OK) return rc;
     *h_cw = p.cw;
     *h_lds = (int32_t)p.lds;
@@ -84,7 +84,7 @@ extern "C" int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32
     if (!g || !h_plan || weights_count(model) < 0) return GNND_ERR_INVALID_ARG;
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     Plan p;
-    int rc = make_plan(model, dtype, g->view, &p);
+    int rc = make_plan(model, dtype, g, &p);
     if (rc != GNND_OK) return rc;
     h_plan[0] = p.cw;
     h_plan[1] = (int32_t)p.lds;

@@ -548,6 +548,7 @@ bool resident_disabled() {
 }
 
 struct Plan {
+    const GraphView* view;   // slot plan the chosen kernel runs on (gnnd_graph::view/rview)
     bool resident;
     int cw;       // codewords per workgroup
     int q;        // work items per lane (resident)
@@ -556,14 +557,14 @@ struct Plan {
 
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
-int make_plan(int model, int dtype, const GraphView& g, Plan* p) {
+int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p) {
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
     const size_t wb = align16((size_t)weights_count(model) * esz);
     const size_t target = lds_target();
-    const int IC = g.C * g.G;
     const bool light = model != GNND_V24;
-    const bool g_ok = g.G == 4 || g.G == 8 || g.G == 16;   // instantiated group sizes
-    if (light && dtype == GNND_F32 && g_ok && !resident_disabled()) {
+    if (light && dtype == GNND_F32 && gr->rview.G <= 16 && !resident_disabled()) {
+        const GraphView& g = gr->rview;          // instantiated group sizes 1..16
+        const int IC = g.C * g.G;
         // resident layout: weights, var_ord, then [CW][E+1] messages, [CW][V] {S, x}, [CW][C].
         // Pick (CW, Q) with Q in kResidentQ maximising lane utilisation CW*IC / (Q*256),
         // ties to the larger tile.
@@ -589,6 +590,7 @@ int make_plan(int model, int dtype, const GraphView& g, Plan* p) {
             if (u > bestu + 1e-9 || (u > bestu - 1e-9 && cw > best)) { bestu = u; best = cw; bestq = q; }
         }
         if (best > 0 && bestu >= 0.5) {
+            p->view = &g;
             p->resident = true;
             p->cw = best;
             p->q = bestq;
@@ -598,12 +600,14 @@ int make_plan(int model, int dtype, const GraphView& g, Plan* p) {
     }
     // streaming layout: weights, slot table, var_ptr, vslot, then [CW][nslot] messages,
     // [CW][V] {S, x}, [CW][C]
-    const size_t nslot = (size_t)IC * g.R;
+    const GraphView& g = gr->view;
+    const size_t nslot = (size_t)g.C * g.G * g.R;
     const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4);
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     size_t n = fixed + per >= target ? 1 : (target - fixed) / per;
     if (n > 64) n = 64;
+    p->view = &g;
     p->resident = false;
     p->cw = (int)n;
     p->q = 0;
@@ -612,12 +616,9 @@ int make_plan(int model, int dtype, const GraphView& g, Plan* p) {
 }
 
 template <int MODEL, typename T, int R>
-int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out, int64_t B,
+int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_t B,
                   int iters, hipStream_t st) {
-    const GraphView& g = gr->view;
-    Plan p;
-    int rc = make_plan(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p);
-    if (rc != GNND_OK) return rc;
+    const GraphView& g = *p.view;
     int64_t blocks = (B + p.cw - 1) / p.cw;
     if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
     const int nw = weights_count(MODEL);
@@ -649,6 +650,8 @@ int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out,
             };
             auto by_g = [&](auto ptag) -> int {
                 switch (g.G) {
+                    case 1: return by_q(std::integral_constant<int, 1>{}, ptag);
+                    case 2: return by_q(std::integral_constant<int, 2>{}, ptag);
                     case 4: return by_q(std::integral_constant<int, 4>{}, ptag);
                     case 8: return by_q(std::integral_constant<int, 8>{}, ptag);
                     case 16: return by_q(std::integral_constant<int, 16>{}, ptag);
@@ -665,11 +668,14 @@ int launch_decode(const gnnd_graph* gr, const void* w, const void* x, void* out,
 template <int MODEL, typename T>
 int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
                     int iters, hipStream_t st) {
-    switch (g->view.R) {
-        case 1: return launch_decode<MODEL, T, 1>(g, w, x, out, B, iters, st);
-        case 2: return launch_decode<MODEL, T, 2>(g, w, x, out, B, iters, st);
-        case 3: return launch_decode<MODEL, T, 3>(g, w, x, out, B, iters, st);
-        case 4: return launch_decode<MODEL, T, 4>(g, w, x, out, B, iters, st);
+    Plan p;
+    int rc = make_plan(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p);
+    if (rc != GNND_OK) return rc;
+    switch (p.view->R) {
+        case 1: return launch_decode<MODEL, T, 1>(p, w, x, out, B, iters, st);
+        case 2: return launch_decode<MODEL, T, 2>(p, w, x, out, B, iters, st);
+        case 3: return launch_decode<MODEL, T, 3>(p, w, x, out, B, iters, st);
+        case 4: return launch_decode<MODEL, T, 4>(p, w, x, out, B, iters, st);
     }
     return GNND_ERR_UNSUPPORTED;
 }

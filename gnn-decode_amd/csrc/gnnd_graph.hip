@@ -61,29 +61,53 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         std::vector<int> fill(cptr.begin(), cptr.end() - 1);
         for (int e = 0; e < E; ++e) cedge[fill[h_chk[e]]++] = e;   // increasing e per check
     }
-    // check-group plan: R slots per lane, G (power of two) lanes per check, minimal padding
-    int bestG = 0, bestR = 0;
-    long best = -1;
-    for (int R = 1; R <= 4; ++R) {
-        int need = (max_dc + R - 1) / R, G = 1;
-        while (G < need) G <<= 1;
-        if (G > 64) continue;
-        long slots = (long)C * G * R;
-        if (best < 0 || slots < best) { best = slots; bestG = G; bestR = R; }
-    }
-    if (best < 0) return GNND_ERR_UNSUPPORTED;     // check degree > 256
-    const int nslot = C * bestG * bestR;
-    std::vector<uint32_t> slot(nslot, GNND_SLOT_PAD);
-    std::vector<uint32_t> slot_ve(nslot, (uint32_t)E << 16);   // padding: v 0, dummy edge E
-    std::vector<int> vslot(E);
-    for (int c = 0; c < C; ++c)
-        for (int k = cptr[c], i = 0; k < cptr[c + 1]; ++k, ++i) {
-            int e = cedge[k];
-            int pos = c * bestG * bestR + i;
-            slot[pos] = evc[e] & 0xffffu;
-            slot_ve[pos] = (evc[e] & 0xffffu) | ((uint32_t)e << 16);
-            vslot[e] = pos;
+    // check-group plans: R slots per lane, G (power of two) lanes per check, minimal padding.
+    // Two tie-breaks between equal-slot plans: the streaming kernel prefers the smaller R
+    // (more lanes per check: V24's heavy per-edge MLPs spread over more lanes; measured
+    // toric-5 V24 fp32 5.1 vs 4.8 M cw/s), the register-resident kernel the larger R (fewer
+    // butterfly steps per edge: toric QGNNI 147 -> 159 M cw/s, LDPC CGNNI 12.7 -> 13.9 M).
+    // GNND_GROUP_R forces R in both (tuning sweeps) when it yields G <= 64.
+    static const int force_r = [] {
+        const char* e = getenv("GNND_GROUP_R");
+        return e ? atoi(e) : 0;
+    }();
+    struct SlotPlan {
+        int G = 0, R = 0, padded = 0;
+        std::vector<uint32_t> slot, slot_ve;
+        std::vector<int> vslot;
+    };
+    auto build_plan = [&](bool prefer_large_r, SlotPlan& sp) -> bool {
+        long best = -1;
+        for (int R = 1; R <= 4; ++R) {
+            int need = (max_dc + R - 1) / R, G = 1;
+            while (G < need) G <<= 1;
+            if (G > 64) continue;
+            long slots = (long)C * G * R;
+            if (force_r == R) { best = slots; sp.G = G; sp.R = R; break; }
+            if (best < 0 || slots < best || (prefer_large_r && slots == best)) {
+                best = slots; sp.G = G; sp.R = R;
+            }
         }
+        if (best < 0) return false;     // check degree > 256
+        const int ns = C * sp.G * sp.R;
+        sp.slot.assign(ns, GNND_SLOT_PAD);
+        sp.slot_ve.assign(ns, (uint32_t)E << 16);   // padding: v 0, dummy edge E
+        sp.vslot.assign(E, 0);
+        sp.padded = 0;
+        for (int c = 0; c < C; ++c) {
+            sp.padded |= (cptr[c + 1] - cptr[c]) != sp.G * sp.R;
+            for (int k = cptr[c], i = 0; k < cptr[c + 1]; ++k, ++i) {
+                int e = cedge[k];
+                int pos = c * sp.G * sp.R + i;
+                sp.slot[pos] = evc[e] & 0xffffu;
+                sp.slot_ve[pos] = (evc[e] & 0xffffu) | ((uint32_t)e << 16);
+                sp.vslot[e] = pos;
+            }
+        }
+        return true;
+    };
+    SlotPlan plans[2];
+    if (!build_plan(false, plans[0]) || !build_plan(true, plans[1])) return GNND_ERR_UNSUPPORTED;
 
     std::vector<int> vord(V);
     for (int v = 0; v < V; ++v) vord[v] = v;
@@ -92,15 +116,24 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     });
 
     const int nints = graph_table_ints(V, C, E);
-    const int ord_off = (nints + nslot + E + nslot + 1) & ~1;     // uint2 alignment
+    int plan_off[2];
+    int off = nints;
+    for (int i = 0; i < 2; ++i) {
+        plan_off[i] = off;
+        off += 2 * (int)plans[i].slot.size() + E;
+    }
+    const int ord_off = (off + 1) & ~1;     // uint2 alignment
     std::vector<int> table(ord_off + 2 * V);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
     memcpy(table.data() + E + V + 1 + C + 1, cedge.data(), sizeof(int) * E);
-    memcpy(table.data() + nints, slot.data(), sizeof(int) * nslot);
-    memcpy(table.data() + nints + nslot, vslot.data(), sizeof(int) * E);
-    memcpy(table.data() + nints + nslot + E, slot_ve.data(), sizeof(int) * nslot);
+    for (int i = 0; i < 2; ++i) {
+        const int ns = (int)plans[i].slot.size();
+        memcpy(table.data() + plan_off[i], plans[i].slot.data(), sizeof(int) * ns);
+        memcpy(table.data() + plan_off[i] + ns, plans[i].vslot.data(), sizeof(int) * E);
+        memcpy(table.data() + plan_off[i] + ns + E, plans[i].slot_ve.data(), sizeof(int) * ns);
+    }
     for (int i = 0; i < V; ++i) {
         const int v = vord[i];
         table[ord_off + 2 * i] = v | ((vptr[v + 1] - vptr[v]) << 16);
@@ -122,15 +155,19 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     gv.var_ptr = d + E;
     gv.chk_ptr = d + E + V + 1;
     gv.chk_edge = d + E + V + 1 + C + 1;
-    gv.G = bestG; gv.R = bestR;
-    gv.padded = 0;
-    for (int c = 0; c < C; ++c) gv.padded |= (cptr[c + 1] - cptr[c]) != bestG * bestR;
-    gv.logG = 0;
-    while ((1 << gv.logG) < bestG) ++gv.logG;
-    gv.slot = (const uint32_t*)(d + nints);
-    gv.vslot = d + nints + nslot;
-    gv.slot_ve = (const uint32_t*)(d + nints + nslot + E);
     gv.var_ord = (const uint2*)(d + ord_off);
+    g->rview = gv;
+    for (int i = 0; i < 2; ++i) {
+        GraphView& pv = i == 0 ? g->view : g->rview;
+        const int ns = (int)plans[i].slot.size();
+        pv.G = plans[i].G; pv.R = plans[i].R;
+        pv.padded = plans[i].padded;
+        pv.logG = 0;
+        while ((1 << pv.logG) < pv.G) ++pv.logG;
+        pv.slot = (const uint32_t*)(d + plan_off[i]);
+        pv.vslot = d + plan_off[i] + ns;
+        pv.slot_ve = (const uint32_t*)(d + plan_off[i] + ns + E);
+    }
     *out = g;
     return GNND_OK;
 }
