@@ -60,6 +60,8 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=12.0,
                    help='bounded CPU-baseline sample (0 disables)')
     p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--no-graph', action='store_true',
+                   help='train mode: eager steps instead of one captured HIP graph per step')
     p.add_argument('--mode', default='decode', choices=['decode', 'train'],
                    help='train = config 5: decoder_v2_4 training step (DP, RCCL all-reduce)')
     return p.parse_args()
@@ -130,7 +132,7 @@ def train_main(a, world, rank, dev):
     model = gd.MODELS[model_name](T, H).to(dev).to(dtype)
     lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
                               logical_only=(model_name == 'qgnni')).to(dev)
-    tr = gd.train.Trainer(model, lf)
+    tr = gd.train.Trainer(model, lf, graph=not a.no_graph, warmup=2)   # captured after 2 eager steps
     x, y = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
     data = gd.data.make_batch(x, model.graph(dev))
     for _ in range(a.warmup):
@@ -158,7 +160,8 @@ def train_main(a, world, rank, dev):
             'data': 'synthetic toric errors (on-device sampler, seeded); seeded Kaiming init',
             'config': {'workload': f'{code} {model_name} training step, T={T}, batch={a.batch}/GPU',
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
-                       'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters())},
+                       'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters()),
+                       'hip_graph': not a.no_graph},
             'roofline': None, 'cpu_baseline': None}), flush=True)
 
 

@@ -41,6 +41,45 @@ def init_weights(m):
         m.bias.data.fill_(0)
 
 
+class _SkinnyLinear(torch.autograd.Function):
+    """y = x W^T + b for the per-edge MLPs (in or out width <= 2 on one side, rows = edges
+    x batch).  Same forward as torch.nn.Linear; the backward forms the weight gradient as a
+    fused multiply + column reduction over the rows instead of a K = rows GEMM: hipBLASLt
+    runs those tall-skinny GEMMs at ~0.1 TFLOP/s (100-190 us each, 56 % of a decoder_v2_4
+    training step, profiles/r01/train_v24_kernel_stats.csv), the reduction streams the
+    operands once."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        ctx.save_for_backward(x, W)
+        return torch.addmm(b, x, W.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, W = ctx.saved_tensors
+        gx = gW = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = gy * W if W.size(0) == 1 else gy @ W          # [n,1]*[1,in] or [n,out]@[out,in]
+        if ctx.needs_input_grad[1]:
+            if W.size(1) == 1:
+                gW = (gy * x).sum(0).unsqueeze(1)                # [out, 1]
+            elif W.size(0) == 1:
+                gW = (x * gy).sum(0).unsqueeze(0)                # [1, in]
+            else:
+                gW = torch.stack([(gy * x[:, i:i + 1]).sum(0) for i in range(W.size(1))], 1)
+        if ctx.needs_input_grad[2]:
+            gb = gy.sum(0)
+        return gx, gW, gb
+
+
+def _apply_mlp(seq, u):
+    """seq = Sequential(Linear, activation, Linear) evaluated with _SkinnyLinear (training)."""
+    if not torch.is_grad_enabled():
+        return seq(u)
+    h = _SkinnyLinear.apply(u, seq[0].weight, seq[0].bias)
+    return _SkinnyLinear.apply(seq[1](h), seq[2].weight, seq[2].bias)
+
+
 def _flat_mlp(seq, split_inputs=False):
     W1 = seq[0].weight
     parts = [W1[:, k] for k in range(W1.size(1))] if split_inputs else [W1.reshape(-1)]
@@ -66,9 +105,9 @@ class GraphConvV24(_MP['v24']):
 
     def update(self, aggr_out):
         if self.flow == 'source_to_target':
-            return self.mlp(aggr_out.to(self.mlp[0].weight.dtype)).to(aggr_out.dtype)
+            return _apply_mlp(self.mlp, aggr_out.to(self.mlp[0].weight.dtype)).to(aggr_out.dtype)
         u = aggr_out[:, 0:1].to(self.mlp[0].weight.dtype)
-        return self.mlp(u).to(aggr_out.dtype) * aggr_out[:, 1:2]
+        return _apply_mlp(self.mlp, u).to(aggr_out.dtype) * aggr_out[:, 1:2]
 
 
 class GraphConvQGNNI(_MP['qgnni']):
@@ -86,7 +125,7 @@ class GraphConvQGNNI(_MP['qgnni']):
     def update(self, aggr_out):
         if self.flow == 'target_to_source':
             u = aggr_out[:, 0:1].to(self.mlp[0].weight.dtype)
-            return self.mlp(u).to(aggr_out.dtype) * aggr_out[:, 1:2]
+            return _apply_mlp(self.mlp, u).to(aggr_out.dtype) * aggr_out[:, 1:2]
         return aggr_out
 
 
@@ -123,7 +162,7 @@ class GatedGraphConvCGNNI(ClassicalMessagePassing):
 
     def update(self, aggr_out):
         if self.flow == 'target_to_source':
-            return self.mlp2(aggr_out.to(self.mlp2[0].weight.dtype)).to(aggr_out.dtype)
+            return _apply_mlp(self.mlp2, aggr_out.to(self.mlp2[0].weight.dtype)).to(aggr_out.dtype)
         return aggr_out
 
 
@@ -194,7 +233,15 @@ class _Decoder(torch.nn.Module):
 
     # ---- reference layer-by-layer loop on the device operator ---------------------------
     def _shifted(self, edge_index):
-        return torch.stack([edge_index[0], edge_index[1] + self.rows])
+        # cached per input tensor: the same shifted tensor keeps the propagate ops' tiled-
+        # structure check cached (no device round trip per step; required under graph capture)
+        c = getattr(self, '_shift_cache', None)
+        if c is not None and c[0]() is edge_index and c[1] == edge_index._version:
+            return c[2]
+        import weakref
+        out = torch.stack([edge_index[0], edge_index[1] + self.rows])
+        self._shift_cache = (weakref.ref(edge_index), edge_index._version, out)
+        return out
 
     def _var_rows(self, t, B):
         N = self.rows + self.cols
@@ -231,7 +278,7 @@ class DecoderV24(_Decoder):
             m_p = m
             m = self.ggc1(m, ei, x)
             m = self.ggc2(m, ei, x) + m_p
-        f = self.mlp(m.to(self.mlp[0].weight.dtype)).to(x.dtype)
+        f = _apply_mlp(self.mlp, m.to(self.mlp[0].weight.dtype)).to(x.dtype)
         res = self._var_rows(self._var_sum(f, ei, x.size(0)), B) + self._var_rows(x, B)
         return torch.sigmoid(-res)
 
@@ -258,7 +305,7 @@ class QGNNI(_Decoder):
             m = self.ggc1(m, ei, x)
             m = self.ggc2(m, ei, x) + m_p
         r = self._var_rows(self._var_sum(m, ei, x.size(0)) + x, B)
-        return torch.sigmoid(-self.mlp(r.to(self.mlp[0].weight.dtype)).to(x.dtype))
+        return torch.sigmoid(-_apply_mlp(self.mlp, r.to(self.mlp[0].weight.dtype)).to(x.dtype))
 
 
 class QuantumBP(_Decoder):
@@ -304,7 +351,7 @@ class CGNNI(_Decoder):
             m = self.ggc1(m, ei, x)
             m = self.ggc2(m, ei) + m_p
         r = self._var_rows(self._var_sum(m, ei, x.size(0)) + x, B)
-        res = torch.sigmoid(-self.mlp(r.to(self.mlp[0].weight.dtype)).to(x.dtype))
+        res = torch.sigmoid(-_apply_mlp(self.mlp, r.to(self.mlp[0].weight.dtype)).to(x.dtype))
         return torch.clamp(res, 1e-7, 1 - 1e-7)
 
 

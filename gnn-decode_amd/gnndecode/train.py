@@ -42,16 +42,32 @@ def allreduce_grads(params, group=None):
 
 
 class Trainer:
-    """zero_grad -> forward -> summed loss -> backward -> all_reduce(SUM) -> Adam."""
+    """zero_grad -> forward -> summed loss -> backward -> all_reduce(SUM) -> Adam.
 
-    def __init__(self, model, loss_fn, lr=3e-4, weight_decay=1e-9, group=None):
+    `graph=True` captures that whole step (the layer-by-layer decoder launches ~900 small
+    kernels per step for T = 15) in one HIP graph after a few eager warm-up steps and
+    replays it; inputs are copied into static buffers first.  Same arithmetic, same order.
+    Requires a fixed batch shape and edge_index; Adam runs in its capturable form."""
+
+    def __init__(self, model, loss_fn, lr=3e-4, weight_decay=1e-9, group=None, graph=False,
+                 warmup=3, capturable=None):
         self.model = model
         self.loss_fn = loss_fn
         self.group = group
-        self.opt = torch.optim.Adam(model.parameters(), lr, weight_decay=weight_decay)
+        self.use_graph = graph
+        self.warmup = warmup
+        # capturable Adam (device-side step count) is required under capture; its update
+        # rounds differently from the host-step form, so pass capturable=True to compare an
+        # eager run against a graphed one bit for bit
+        self.opt = torch.optim.Adam(model.parameters(), lr, weight_decay=weight_decay,
+                                    capturable=graph if capturable is None else capturable)
+        self._graph = None
+        self._eager_steps = 0
 
-    def step(self, data, y):
-        self.model.train()
+    def _dist(self):
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def _body(self, data, y):
         self.opt.zero_grad(set_to_none=False)
         pred = self.model(data)
         loss = self.loss_fn(pred, y)
@@ -59,6 +75,37 @@ class Trainer:
         allreduce_grads(self.model.parameters(), self.group)
         self.opt.step()
         total = loss.detach().clone()
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+        if self._dist():
             dist.all_reduce(total, op=dist.ReduceOp.SUM, group=self.group)
         return total
+
+    def step(self, data, y):
+        self.model.train()
+        if not self.use_graph:
+            return self._body(data, y)
+        if self._graph is None:
+            if self._eager_steps < self.warmup:
+                # eager warm-up on a side stream (allocator pools, cached graph checks)
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    out = self._body(data, y)
+                torch.cuda.current_stream().wait_stream(s)
+                self._eager_steps += 1
+                return out
+            self._sx = data.x.clone()
+            self._sy = y.clone()
+            self._sdata = _StaticBatch(self._sx, data.edge_index)
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._sloss = self._body(self._sdata, self._sy)
+        self._sx.copy_(data.x)
+        self._sy.copy_(y)
+        self._graph.replay()
+        return self._sloss
+
+
+class _StaticBatch:
+    def __init__(self, x, edge_index):
+        self.x = x
+        self.edge_index = edge_index

@@ -96,3 +96,20 @@ def test_data_parallel_step_on_one_gpu_matches_plain_step(golden):
     loss = tr.step(data, y)
     assert abs(float(loss) - float(z['loss'])) <= 1e-9 * abs(float(z['loss']))
     assert any((a != p.detach()).any() for a, p in zip(before, m.parameters()))
+
+
+def test_graph_captured_trainer_matches_eager(golden):
+    """Trainer(graph=True) replays one captured HIP graph per step: same losses and the
+    same parameters as eager steps on the same data (fp64, exact order preserved)."""
+    import gnndecode as gd
+    z, m, loss_fn, data, y = _setup(golden, 'train_v24_L5', 'v24', ('toric', 5), 'syndrome')
+    _, m2, _, _, _ = _setup(golden, 'train_v24_L5', 'v24', ('toric', 5), 'syndrome')
+    eager = gd.train.Trainer(m, loss_fn, lr=1e-3, capturable=True)
+    graphed = gd.train.Trainer(m2, loss_fn, lr=1e-3, graph=True, warmup=2)
+    for it in range(5):          # 2 eager warm-up steps, capture at step 3, replays after
+        a = float(eager.step(data, y))
+        b = float(graphed.step(data, y))
+        assert abs(a - b) <= 1e-10 * max(1.0, abs(a)), (it, a, b)
+    for (n, p), q in zip(m.named_parameters(), m2.parameters()):
+        np.testing.assert_allclose(q.detach().cpu().numpy(), p.detach().cpu().numpy(),
+                                   rtol=1e-10, atol=1e-13, err_msg=n)
