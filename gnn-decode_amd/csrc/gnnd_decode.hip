@@ -5,25 +5,25 @@
 namespace {
 
 // ---------------------------------------------------------------------------------------
-// weights: fp32 V24 gets the interleaved base-2 layout read by mlp128*_sp(float)
+// weights: fp32 V24 gets the paired-edge base-2 layout read by mlp128*_sp2 (gnnd_decode_impl.h)
 // ---------------------------------------------------------------------------------------
 __global__ void prepare_v24_f32_kernel(const float* __restrict__ in, float* __restrict__ o) {
     const int k = threadIdx.x;          // hidden unit, one block of 128 threads
-    const int j = k >> 1, h = k & 1;
-    // ggc1.mlp (plain: W1a[128], W1b[128], b1[128], W2[128], b2)
+    // ggc1.mlp (plain: W1a[128], W1b[128], b1[128], W2[128], b2) ->
+    //   {W1b'_k, b1'_k}[128] | W1a'[128] | w2'[128] | b2
     const float* a = in + kV24Ggc1;
     float* q = o + kV24Ggc1;
-    q[8 * j + h] = a[k] * kLog2e;
-    q[8 * j + 2 + h] = a[128 + k] * kLog2e;
-    q[8 * j + 4 + h] = a[256 + k] * kLog2e;
-    q[8 * j + 6 + h] = a[384 + k] * kLn2;
+    q[2 * k] = a[128 + k] * kLog2e;
+    q[2 * k + 1] = a[256 + k] * kLog2e;
+    q[256 + k] = a[k] * kLog2e;
+    q[384 + k] = a[384 + k] * kLn2;
     if (k == 0) q[512] = a[512];
-    // ggc2.mlp and mlp (plain: W1[128], b1[128], W2[128], b2)
+    // ggc2.mlp and mlp (plain: W1[128], b1[128], W2[128], b2) -> {W1'_k, b1'_k}[128] | w2' | b2
     for (int seg = 0; seg < 2; ++seg) {
         const float* s = in + (seg ? kV24Mlp : kV24Ggc2);
         float* d = o + (seg ? kV24Mlp : kV24Ggc2);
-        d[4 * j + h] = s[k] * kLog2e;
-        d[4 * j + 2 + h] = s[128 + k] * kLog2e;
+        d[2 * k] = s[k] * kLog2e;
+        d[2 * k + 1] = s[128 + k] * kLog2e;
         d[256 + k] = s[256 + k] * kLn2;
         if (k == 0) d[384] = s[384];
     }

@@ -125,45 +125,111 @@ __device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double
     return acc + w[512];
 }
 
-// fp32 forms on the prepared (interleaved, base-2 rescaled) layout of gnnd_prepare_weights:
-//   1-input:  [64] {W1[2j], W1[2j+1], b1[2j], b1[2j+1]} (x log2e), W2[128] (x ln2), b2
-//   2-input:  [64] {W1a[2j], W1a[2j+1], W1b[2j], W1b[2j+1]}, {b1[2j], b1[2j+1], W2[2j], W2[2j+1]}, b2
-__device__ __forceinline__ f32x2 softplus2_fast2(f32x2 hs) {
+// fp32 forms: TWO EDGES per call, riding the two halves of packed FMAs (the lane's
+// slots are processed in pairs).  Prepared layout (gnnd_prepare_weights; base-2 rescaled:
+// W1', b1' = W1, b1 x log2(e); w2' = W2 x ln(2)):
+//   1-input (ggc2.mlp, mlp): [0,256) {W1'_k, b1'_k} per unit k | [256,384) w2' | [384] b2
+//   2-input (ggc1.mlp):      [0,256) {W1b'_k, b1'_k}           | [256,384) W1a' |
+//                            [384,512) w2' | [512] b2
+// A unit's {W1'_k, b1'_k} is ONE scalar register pair feeding both the multiplier and the
+// addend of one v_pk_fma_f32 through op_sel (the constant bus allows one SGPR pair per
+// instruction), so layer 1 is one packed FMA per unit for two edges, with no bias moves.
+// Softplus is split as  sp(h) = h/2 + |h|/2 + ln(1 + e^-|h|)  (exact identity; for h > 20
+// it equals h to within 2e-9 relative, the reference's threshold branch).  The h/2 terms
+// are linear in the inputs: sum_k W2_k h_k / 2 collapses to one FMA per edge (V24Lin,
+// computed once per workgroup).  Per unit and edge pair:
+//   v_pk_fma (layer 1) | 2 v_exp_f32(-|hs|) | v_pk_add 1 | 2 v_log_f32 |
+//   2 v_fma_f32(|hs|, 0.5, l) | v_pk_fma (layer 2)
+// The exp argument is <= 0 (no overflow, no clamp) and -|.| / |.| are free source
+// modifiers.  tools/micro: v_exp/v_log issue at ~2x a plain VALU op; this form has 5
+// plain ops per 4 transcendentals (the max(hs, log2(1 + 2^min(hs, 28))) form had 9).
+struct V24Lin {
+    float a0, a1, b;     // lin(u0, u1) = a0 u0 + a1 u1 + b  (a1 = 0 for 1-input MLPs)
+};
+__device__ __forceinline__ f32x2 softplus_tail2(f32x2 hs) {   // |hs|/2 + log2(1 + 2^-|hs|)
     f32x2 e;
-    e.x = __builtin_amdgcn_exp2f(fminf(hs.x, 28.0f));
-    e.y = __builtin_amdgcn_exp2f(fminf(hs.y, 28.0f));
+    e.x = __builtin_amdgcn_exp2f(-fabsf(hs.x));
+    e.y = __builtin_amdgcn_exp2f(-fabsf(hs.y));
     e = e + f32x2{1.0f, 1.0f};
-    f32x2 l;
-    l.x = __builtin_amdgcn_logf(e.x);
-    l.y = __builtin_amdgcn_logf(e.y);
-    return __builtin_elementwise_max(hs, l);
+    // |hs| as a source modifier of one v_fma_f32 per value (hipcc otherwise materialises
+    // |hs| with v_and and packs the FMA: one extra VALU op per pair)
+    float tx, ty;
+    asm("v_fma_f32 %0, |%1|, 0.5, %2" : "=v"(tx) : "v"(hs.x), "v"(__builtin_amdgcn_logf(e.x)));
+    asm("v_fma_f32 %0, |%1|, 0.5, %2" : "=v"(ty) : "v"(hs.y), "v"(__builtin_amdgcn_logf(e.y)));
+    return f32x2{tx, ty};
 }
-__device__ __forceinline__ float mlp128_sp(const float* w, float u) {
-    const f32x4* q = (const f32x4*)w;
-    const f32x2* w2 = (const f32x2*)(w + 256);
-    const f32x2 uu = {u, u};
-    f32x2 acc = {0.f, 0.f};
+// {u0 wb.x + wb.y, u1 wb.x + wb.y}: one SGPR pair as multiplier (lo) and addend (hi)
+__device__ __forceinline__ f32x2 pk_fma_sb(f32x2 u, f32x2 wb) {
+    f32x2 h;
+    asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(h) : "v"(u), "s"(wb));
+    return h;
+}
+// {u0 w.x + c0, u1 w.x + c1} and {u0 w.y + c0, u1 w.y + c1}: scalar weight broadcast
+__device__ __forceinline__ f32x2 pk_fma_lo(f32x2 u, f32x2 w, f32x2 c) {
+    f32x2 h;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(h) : "v"(u), "s"(w), "v"(c));
+    return h;
+}
+__device__ __forceinline__ f32x2 pk_fma_hi(f32x2 u, f32x2 w, f32x2 c) {
+    f32x2 h;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(h) : "v"(u), "s"(w), "v"(c));
+    return h;
+}
+// wg: the MLP's prepared weights in global memory (uniform address: scalar loads)
+__device__ __forceinline__ f32x2 mlp128_sp2(const float* __restrict__ wg, const V24Lin& lin,
+                                            f32x2 u) {
+    const f32x2* wb = (const f32x2*)wg;
+    const f32x2* w2 = (const f32x2*)(wg + 256);
+    f32x2 acc0 = __builtin_elementwise_fma(u, f32x2{lin.a0, lin.a0}, f32x2{lin.b, lin.b});
+    f32x2 acc1 = {0.f, 0.f};                 // even units -> acc0, odd units -> acc1
 #pragma unroll 8
     for (int j = 0; j < 64; ++j) {
-        const f32x4 a = q[j];
-        f32x2 hs = __builtin_elementwise_fma(uu, f32x2{a.x, a.y}, f32x2{a.z, a.w});
-        acc = __builtin_elementwise_fma(softplus2_fast2(hs), w2[j], acc);
+        const f32x2 h0 = pk_fma_sb(u, wb[2 * j]), h1 = pk_fma_sb(u, wb[2 * j + 1]);
+        acc0 = pk_fma_lo(softplus_tail2(h0), w2[j], acc0);
+        acc1 = pk_fma_hi(softplus_tail2(h1), w2[j], acc1);
     }
-    return (acc.x + acc.y) + w[384];
+    return acc0 + acc1;
 }
-__device__ __forceinline__ float mlp128x2_sp(const float* w, float u0, float u1) {
-    const f32x4* q = (const f32x4*)w;
-    const f32x2 uu0 = {u0, u0}, uu1 = {u1, u1};
-    f32x2 acc = {0.f, 0.f};
+__device__ __forceinline__ f32x2 mlp128x2_sp2(const float* __restrict__ wg, const V24Lin& lin,
+                                              f32x2 u0, f32x2 u1) {
+    const f32x2* wb = (const f32x2*)wg;            // {W1b'_k, b1'_k}
+    const f32x2* wa = (const f32x2*)(wg + 256);    // W1a' pairs
+    const f32x2* w2 = (const f32x2*)(wg + 384);
+    f32x2 acc0 = __builtin_elementwise_fma(u0, f32x2{lin.a0, lin.a0},
+                     __builtin_elementwise_fma(u1, f32x2{lin.a1, lin.a1}, f32x2{lin.b, lin.b}));
+    f32x2 acc1 = {0.f, 0.f};
 #pragma unroll 8
     for (int j = 0; j < 64; ++j) {
-        const f32x4 a = q[2 * j], c = q[2 * j + 1];
-        f32x2 hs = __builtin_elementwise_fma(uu1, f32x2{a.z, a.w}, f32x2{c.x, c.y});
-        hs = __builtin_elementwise_fma(uu0, f32x2{a.x, a.y}, hs);
-        acc = __builtin_elementwise_fma(softplus2_fast2(hs), f32x2{c.z, c.w}, acc);
+        const f32x2 a = wa[j];
+        const f32x2 h0 = pk_fma_lo(u0, a, pk_fma_sb(u1, wb[2 * j]));
+        const f32x2 h1 = pk_fma_hi(u0, a, pk_fma_sb(u1, wb[2 * j + 1]));
+        acc0 = pk_fma_lo(softplus_tail2(h0), w2[j], acc0);
+        acc1 = pk_fma_hi(softplus_tail2(h1), w2[j], acc1);
     }
-    return (acc.x + acc.y) + w[512];
+    return acc0 + acc1;
 }
+// linear parts, identical in every thread (fixed summation order)
+__device__ __forceinline__ V24Lin v24_lin1(const float* __restrict__ wg) {
+    float a = 0.f, b = 0.f;
+    for (int k = 0; k < 128; ++k) {
+        a = __builtin_fmaf(wg[256 + k], wg[2 * k], a);
+        b = __builtin_fmaf(wg[256 + k], wg[2 * k + 1], b);
+    }
+    return V24Lin{0.5f * a, 0.f, __builtin_fmaf(0.5f, b, wg[384])};
+}
+__device__ __forceinline__ V24Lin v24_lin2(const float* __restrict__ wg) {
+    float a0 = 0.f, a1 = 0.f, b = 0.f;
+    for (int k = 0; k < 128; ++k) {
+        a0 = __builtin_fmaf(wg[384 + k], wg[256 + k], a0);
+        a1 = __builtin_fmaf(wg[384 + k], wg[2 * k], a1);
+        b = __builtin_fmaf(wg[384 + k], wg[2 * k + 1], b);
+    }
+    return V24Lin{0.5f * a0, 0.5f * a1, __builtin_fmaf(0.5f, b, wg[512])};
+}
+struct V24F32 {            // fp32 V24 weights of the streaming kernel
+    const float* __restrict__ g;
+    V24Lin l1, l2, l3;     // ggc1.mlp, ggc2.mlp, mlp
+};
 
 // ---------------------------------------------------------------------------------------
 // the fused kernel
@@ -200,6 +266,7 @@ __device__ __forceinline__ T var_sum(const T* mb, const int* vslot, int k0, int 
 template <int MODEL, typename T> struct EdgeMath {
     static constexpr bool BP = ModelTraits<MODEL>::bp;
     // v->c message update and c->v pre-op: a_e = (S_v - m_e) + x_v -> t_e (+ BP sign flag)
+    // (fp32 V24 runs the paired-edge path of decode_kernel instead)
     __device__ static __forceinline__ T pre(T ext, T xv, const T* __restrict__ wv, T& cc) {
         cc = T(0);
         if constexpr (MODEL == GNND_V24) {
@@ -300,6 +367,13 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     // no LDS traffic, one SGPR operand per packed FMA.  Broadcast ds_read_b128 of the same
     // weights from LDS costs 4 LDS cycles per 4 floats per wave and saturated the LDS pipe.
     const T* __restrict__ wv = w;
+    constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
+    V24F32 v24{(const float*)w, {}, {}, {}};
+    if constexpr (kV24F32) {
+        v24.l1 = v24_lin2((const float*)w + kV24Ggc1);
+        v24.l2 = v24_lin1((const float*)w + kV24Ggc2);
+        v24.l3 = v24_lin1((const float*)w + kV24Mlp);
+    }
     Mlp10F32 mlp_msg;   // 10-hidden message MLP weights live in VGPRs for the whole decode
     if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
         mlp_msg.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
@@ -320,27 +394,65 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
             const SumX<T>* sxb = s_sx + b * V;
             T mv[R], tv[R], cf[R];
             T tsum = T(0), csum = T(0);
+            if constexpr (kV24F32) {
+                // slots in pairs through the two-edge MLP (odd R: the last pair repeats)
+                float ext[R], xs[R];
+                bool val[R];
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint32_t sv = sl[r];
-                const bool valid = !(sv & GNND_SLOT_PAD);
-                mv[r] = mb[r];
-                const SumX<T> p = sxb[sv & 0xffffu];      // padding reads variable 0
-                T cc;
-                T t = M::pre(p.s - mv[r], p.x, wv, cc);
-                tv[r] = valid ? t : T(0);
-                cf[r] = valid ? cc : T(0);
-                tsum += tv[r];
-                if constexpr (BP) csum += cf[r];
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t sv = sl[r];
+                    val[r] = !(sv & GNND_SLOT_PAD);
+                    mv[r] = mb[r];
+                    const SumX<T> p = sxb[sv & 0xffffu];
+                    ext[r] = p.s - mv[r];
+                    xs[r] = p.x;
+                }
+#pragma unroll
+                for (int r = 0; r < R; r += 2) {
+                    const int r1 = r + 1 < R ? r + 1 : r;
+                    const f32x2 a = mlp128x2_sp2(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
+                                                 f32x2{xs[r], xs[r1]});
+                    tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
+                    if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    cf[r] = T(0);
+                    tsum += tv[r];
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t sv = sl[r];
+                    const bool valid = !(sv & GNND_SLOT_PAD);
+                    mv[r] = mb[r];
+                    const SumX<T> p = sxb[sv & 0xffffu];      // padding reads variable 0
+                    T cc;
+                    T t = M::pre(p.s - mv[r], p.x, wv, cc);
+                    tv[r] = valid ? t : T(0);
+                    cf[r] = valid ? cc : T(0);
+                    tsum += tv[r];
+                    if constexpr (BP) csum += cf[r];
+                }
             }
             const T Sc = group_sum(tsum, G);
             T Sc2 = T(0);
             if constexpr (BP) Sc2 = group_sum(csum, G);
             const T sc = s_xc[b * C + c];
             T mn[R];
+            if constexpr (kV24F32) {
 #pragma unroll
-            for (int r = 0; r < R; ++r)   // every slot computes; padding slots are never read
-                mn[r] = M::post(Sc - tv[r], Sc2 - cf[r], sc, mv[r], mlp_msg, s_w, wv);
+                for (int r = 0; r < R; r += 2) {
+                    const int r1 = r + 1 < R ? r + 1 : r;
+                    const f32x2 y = mlp128_sp2(v24.g + kV24Ggc2, v24.l2, f32x2{Sc - tv[r], Sc - tv[r1]});
+                    mn[r] = y.x * sc + mv[r];
+                    if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r)   // every slot computes; padding slots are never read
+                    mn[r] = M::post(Sc - tv[r], Sc2 - cf[r], sc, mv[r], mlp_msg, s_w, wv);
+            }
             if (act) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) mb[r] = mn[r];
@@ -357,7 +469,17 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 
     if constexpr (MODEL == GNND_V24) {
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
-        for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
+        if constexpr (kV24F32) {
+            const int n = nb * nslot;
+            for (int f = 2 * tid; f < n; f += 2 * GNND_BLOCK) {
+                const int f1 = f + 1 < n ? f + 1 : f;
+                const f32x2 y = mlp128_sp2(v24.g + kV24Mlp, v24.l3, f32x2{s_m[f], s_m[f1]});
+                s_m[f] = y.x;
+                if (f + 1 < n) s_m[f + 1] = y.y;
+            }
+        } else {
+            for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
+        }
         __syncthreads();
     }
     T* og = out + b0 * V;
@@ -599,14 +721,30 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p) {
         }
     }
     // streaming layout: weights, slot table, var_ptr, vslot, then [CW][nslot] messages,
-    // [CW][V] {S, x}, [CW][C]
-    const GraphView& g = gr->view;
+    // [CW][V] {S, x}, [CW][C].  fp32 V24 runs its MLPs on slot PAIRS (two edges per packed
+    // FMA): it takes the larger-R plan (toric dc = 4: G = 1, R = 4 instead of G = 4, R = 1)
+    const GraphView& g = (model == GNND_V24 && dtype == GNND_F32) ? gr->rview : gr->view;
     const size_t nslot = (size_t)g.C * g.G * g.R;
     const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4);
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     size_t n = fixed + per >= target ? 1 : (target - fixed) / per;
     if (n > 64) n = 64;
+    // step-1 lane utilisation: the tile's C*G work items run in rounds of 256 lanes; among
+    // tiles down to half the LDS-limited size take the one wasting the fewest lanes (ties:
+    // larger).  toric-5 V24 fp32 (C*G = 48): 19 -> 16 codewords (3 full rounds, and 4
+    // workgroups per CU instead of 3)
+    {
+        const size_t IC = (size_t)g.C * g.G;
+        size_t best = n;
+        double bu = 0;
+        for (size_t c = n; c >= 1 && 2 * c >= n; --c) {
+            const size_t items = c * IC, rounds = (items + GNND_BLOCK - 1) / GNND_BLOCK;
+            const double u = (double)items / (double)(rounds * GNND_BLOCK);
+            if (u > bu + 1e-9) { bu = u; best = c; }
+        }
+        n = best;
+    }
     p->view = &g;
     p->resident = false;
     p->cw = (int)n;
