@@ -38,6 +38,8 @@ int dispatch_decode(const gnnd_graph* g, int model, int dtype, const void* w, co
         case GNND_QBP: return gnnd_launch_qbp(g, dtype, w, x, out, B, iters, st);
         case GNND_CGNNI: return gnnd_launch_cgnni(g, dtype, w, x, out, B, iters, st);
         case GNND_CBP: return gnnd_launch_cbp(g, dtype, w, x, out, B, iters, st);
+        case GNND_NBP: return gnnd_launch_nbp(g, dtype, w, x, out, B, iters, st);
+        case GNND_V10: return gnnd_launch_v10(g, dtype, w, x, out, B, iters, st);
         default: return GNND_ERR_INVALID_ARG;
     }
 }
@@ -46,15 +48,24 @@ int dispatch_decode(const gnnd_graph* g, int model, int dtype, const void* w, co
 
 extern "C" int gnnd_weights_count(int model, int64_t* h_count) {
     int n = weights_count(model);
-    if (n < 0 || !h_count) return GNND_ERR_INVALID_ARG;
+    if (n == -1 || !h_count) return GNND_ERR_INVALID_ARG;
+    if (n < 0) return GNND_ERR_UNSUPPORTED;     // graph-dependent: gnnd_decode_weights_count
     *h_count = n;
+    return GNND_OK;
+}
+
+extern "C" int gnnd_decode_weights_count(const gnnd_graph* g, int model, int32_t iters,
+                                         int64_t* h_count) {
+    if (!g || !h_count || iters < 0 || weights_count(model) == -1) return GNND_ERR_INVALID_ARG;
+    *h_count = decode_weights_count(model, g->view.E, iters);
     return GNND_OK;
 }
 
 extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void* d_prepared,
                                     void* stream) {
     int n = weights_count(model);
-    if (n < 0 || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
+    if (n == -1 || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
+    if (n < 0) return GNND_ERR_UNSUPPORTED;     // NBP/V10: decode takes the packed layout as is
     if (n == 0) return GNND_OK;
     if (!d_w || !d_prepared || d_w == d_prepared) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
@@ -70,7 +81,7 @@ extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void*
 
 extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32_t* h_cw,
                                 int32_t* h_lds) {
-    if (!g || !h_cw || !h_lds || weights_count(model) < 0) return GNND_ERR_INVALID_ARG;
+    if (!g || !h_cw || !h_lds || weights_count(model) == -1) return GNND_ERR_INVALID_ARG;
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     Plan p;
     int rc = make_plan(model, dtype, g, &p);
@@ -81,7 +92,7 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
 }
 
 extern "C" int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan) {
-    if (!g || !h_plan || weights_count(model) < 0) return GNND_ERR_INVALID_ARG;
+    if (!g || !h_plan || weights_count(model) == -1) return GNND_ERR_INVALID_ARG;
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     Plan p;
     int rc = make_plan(model, dtype, g, &p);
@@ -97,10 +108,10 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
                            const void* d_x, void* d_out, int64_t batch, int32_t iters,
                            void* stream) {
     int nw = weights_count(model);
-    if (!g || nw < 0 || batch < 0 || iters < 0) return GNND_ERR_INVALID_ARG;
+    if (!g || nw == -1 || batch < 0 || iters < 0) return GNND_ERR_INVALID_ARG;
     if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
     if (batch == 0) return GNND_OK;
-    if (!d_x || !d_out || (nw > 0 && !d_w)) return GNND_ERR_INVALID_ARG;
+    if (!d_x || !d_out || ((nw > 0 || nw == -2) && !d_w)) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
     return dispatch_decode(g, model, dtype, d_w, d_x, d_out, batch, iters, st);
 }

@@ -9,6 +9,10 @@
 //   QGNNI  quantum/QGNNI.py:228-252     (fp64; c->v MLP 1->10->1 ReLU x syndrome; residual)
 //   V24    quantum/decoder_v2_4.py:272-294 (fp64 reference; v->c MLP 2->128->1 Softplus,
 //          c->v MLP 1->128->1 Softplus x syndrome, residual, per-edge readout MLP)
+//   NBP    quantum/neural_BP.py:263-314  (fp64; weighted BP: per-layer per-edge W on the
+//          v->c messages and W_p on the prior, residual alpha, weighted readout)
+//   V10    quantum/decoder_v1_0.py:282-313 (fp64; per-layer per-edge W on the c->v input,
+//          residual alpha)
 //
 // MI355X mapping.  Every codeword has the same Tanner graph, so the graph tables and the
 // weights are staged once per workgroup into LDS and each workgroup decodes a tile of CW
@@ -36,7 +40,64 @@ constexpr int kV24Ggc1 = 0, kV24Ggc2 = 513, kV24Mlp = 898;
 constexpr int kMlp10Msg = 0, kMlp10Out = 31;
 
 template <int MODEL> struct ModelTraits {
-    static constexpr bool bp = (MODEL == GNND_QBP || MODEL == GNND_CBP);
+    static constexpr bool wbp = (MODEL == GNND_NBP || MODEL == GNND_V10);   // weighted BP
+    static constexpr bool bp = (MODEL == GNND_QBP || MODEL == GNND_CBP || wbp);
+};
+
+// ---------------------------------------------------------------------------------------
+// weighted quantum BP check step (quantum/neural_BP.py:109-122 = decoder_v1_0.py:109-122):
+//   t = tanh(a/2) (no pre-clamp), c = [t < 0], L = log(clamp(|t|, 1e-20, 1e10));
+//   Lambda = S_c(L) - L, n = S_c(c) - c + (1 - s)/2,
+//   p = clamp(exp(Lambda) cos(pi n), +-(1 - 1e-15)), out = log(1 + p) - log(1 - p).
+// fp64: literally.  fp32 cannot represent the clamp (1 - 1e-15 rounds to 1, and tanh
+// saturates at |a| ~ 17 where fp64 keeps resolving 1 - t down to 1e-16): the fp32 form
+// evaluates the same function through the small quantities instead,
+//   L = log tanh(|a|/2) = log1p(-e) - log1p(e), e = exp(-|a|)  (|a| >= 1; tanhf below),
+//   1 - |p| = -expm1(Lambda) clamped at 1 - fl64(1 - 1e-15), 1 + |p| = 1 + exp(Lambda),
+// so messages track the fp64 reference instead of saturating at log(2^25).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ double wbp_L(double a, double& c) {
+    const double t = tanh(a / 2.0);
+    c = t < 0.0 ? 1.0 : 0.0;
+    return log(g_clamp(fabs(t), 1e-20, 1e10));
+}
+__device__ __forceinline__ float wbp_L(float a, float& c) {
+    c = a < 0.f ? 1.f : 0.f;                  // tanh(a/2) < 0 exactly when a < 0
+    const float y = fabsf(a);
+    float L;
+    if (y < 1.f) {
+        L = logf(fmaxf(tanhf(0.5f * y), 1e-20f));
+    } else {
+        const float e = expf(-y);
+        L = log1pf(-e) - log1pf(e);
+    }
+    return L;
+}
+__device__ __forceinline__ double wbp_out(double lam, double n, double s) {
+    n = n + (1.0 - s) / 2.0;
+    const double hi = 1 - 1e-15;
+    const double p = g_clamp(exp(lam) * cos_pi(n), -hi, hi);
+    return log(1.0 + p) - log(1.0 - p);
+}
+__device__ __forceinline__ float wbp_out(float lam, float n, float s) {
+    n = n + (1.f - s) / 2.f;
+    const float sgn = cos_pi(n);
+    const float one_m = fmaxf(-expm1f(lam), 9.992007221626409e-16f);  // 1 - fl64(1 - 1e-15)
+    const float one_p = fminf(1.f + expf(lam), 2.f - 9.992007221626409e-16f);
+    return sgn * (logf(one_p) - logf(one_m));
+}
+// per-edge weights of iteration t (reference edge order; NBP [T][2][E] + readout, V10 [T][E])
+template <int MODEL, typename T> struct WbpW {
+    const T* __restrict__ w;
+    int E, T_;
+    __device__ __forceinline__ T msg(int t, int e) const { return w[(size_t)2 * t * E + e]; }      // NBP W
+    __device__ __forceinline__ T prior(int t, int e) const { return w[(size_t)(2 * t + 1) * E + e]; }  // NBP W_p
+    __device__ __forceinline__ T chk(int t, int e) const { return w[(size_t)t * E + e]; }          // V10 W
+    __device__ __forceinline__ T out_w(int e) const { return w[(size_t)2 * T_ * E + e]; }          // NBP W
+    __device__ __forceinline__ T out_p(int e) const { return w[(size_t)(2 * T_ + 1) * E + e]; }    // NBP W_p
+    __device__ __forceinline__ T alpha() const {
+        return MODEL == GNND_NBP ? w[(size_t)2 * T_ * E + 2 * E] : w[(size_t)T_ * E];
+    }
 };
 
 // torch constants are Python doubles converted to the tensor dtype
@@ -260,6 +321,16 @@ __device__ __forceinline__ T var_sum(const T* mb, const int* vslot, int k0, int 
 }
 
 
+// S_v = sum_k fl(wk[k] * mb[vslot[k]]) in k order (NBP: the messages are weighted before
+// the variable aggregation, neural_BP.py:248)
+template <typename T>
+__device__ __forceinline__ T var_sum_w(const T* mb, const int* vslot, int k0, int ke,
+                                       const T* __restrict__ wk) {
+    T s = T(0);
+    for (int k = k0; k < ke; ++k) s += mb[vslot[k]] * wk[k];
+    return s;
+}
+
 // ---------------------------------------------------------------------------------------
 // per-edge model math shared by both kernels
 // ---------------------------------------------------------------------------------------
@@ -348,7 +419,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
 
     for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
-    for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot[i];
+    for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot_ve[i];   // v | e << 16
     for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
     for (int i = tid; i < E; i += GNND_BLOCK) s_vslot[i] = g.vslot[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
@@ -377,6 +448,10 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     Mlp10F32 mlp_msg;   // 10-hidden message MLP weights live in VGPRs for the whole decode
     if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
         mlp_msg.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
+    constexpr bool WBP = ModelTraits<MODEL>::wbp;
+    const WbpW<MODEL, T> ww{w, E, iters};
+    T alpha = T(0);
+    if constexpr (WBP) alpha = ww.alpha();
 
     const int IC = C * G;               // work items (lanes) per codeword
     const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
@@ -401,7 +476,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t sv = sl[r];
-                    val[r] = !(sv & GNND_SLOT_PAD);
+                    val[r] = (int)(sv >> 16) != E;
                     mv[r] = mb[r];
                     const SumX<T> p = sxb[sv & 0xffffu];
                     ext[r] = p.s - mv[r];
@@ -420,11 +495,33 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     cf[r] = T(0);
                     tsum += tv[r];
                 }
+            } else if constexpr (WBP) {
+                // v->c with this iteration's per-edge weights, then the BP pre-op
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t sv = sl[r];
+                    const int e = (int)(sv >> 16);
+                    const bool valid = e != E;
+                    const int ec = valid ? e : 0;
+                    mv[r] = mb[r];
+                    const SumX<T> p = sxb[sv & 0xffffu];
+                    T a;
+                    if constexpr (MODEL == GNND_NBP)   // LOO_v(W m) + x_v W_p  (neural_BP.py:248-260)
+                        a = (p.s - mv[r] * ww.msg(it, ec)) + p.x * ww.prior(it, ec);
+                    else                               // (LOO_v(m) + x_v) W  (decoder_v1_0.py:248-251)
+                        a = ((p.s - mv[r]) + p.x) * ww.chk(it, ec);
+                    T cc;
+                    const T L = wbp_L(a, cc);
+                    tv[r] = valid ? L : T(0);
+                    cf[r] = valid ? cc : T(0);
+                    tsum += tv[r];
+                    csum += cf[r];
+                }
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const uint32_t sv = sl[r];
-                    const bool valid = !(sv & GNND_SLOT_PAD);
+                    const bool valid = (int)(sv >> 16) != E;
                     mv[r] = mb[r];
                     const SumX<T> p = sxb[sv & 0xffffu];      // padding reads variable 0
                     T cc;
@@ -448,6 +545,10 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
                 }
+            } else if constexpr (WBP) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)   // m = BP(.) + m_prev @ alpha  (neural_BP.py:304)
+                    mn[r] = wbp_out(Sc - tv[r], Sc2 - cf[r], sc) + mv[r] * alpha;
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r)   // every slot computes; padding slots are never read
@@ -462,7 +563,11 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         if (it + 1 == iters) break;
         for (int f = tid; f < nV; f += GNND_BLOCK) {
             const int b = fdiv(f, dV), v = f - b * V;
-            s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
+            if constexpr (MODEL == GNND_NBP)   // S_v of the next layer's weighted messages
+                s_sx[f].s = var_sum_w(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1],
+                                      w + (size_t)2 * (it + 1) * E);
+            else
+                s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
         }
         __syncthreads();
     }
@@ -485,8 +590,18 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     T* og = out + b0 * V;
     for (int f = tid; f < nV; f += GNND_BLOCK) {
         const int b = fdiv(f, dV), v = f - b * V;
-        const T s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
-        og[f] = M::readout(s + s_sx[f].x, s_w);
+        if constexpr (MODEL == GNND_NBP) {
+            // sum_v(m W) + sum_v(x_v W_p)  (neural_BP.py:307-312), each in edge order
+            const int k0 = s_vptr[v], ke = s_vptr[v + 1];
+            const T s1 = var_sum_w(s_m + b * nslot, s_vslot, k0, ke, w + (size_t)2 * iters * E);
+            const T xv = s_sx[f].x;
+            T s2 = T(0);
+            for (int k = k0; k < ke; ++k) s2 += xv * ww.out_p(k);
+            og[f] = sigmoid_ref(-(s1 + s2));
+        } else {
+            const T s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
+            og[f] = M::readout(s + s_sx[f].x, s_w);
+        }
     }
 }
 
@@ -638,13 +753,25 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
         }
 }
 
+// graph-independent weight count (-1: unknown model, -2: depends on the graph and T)
 int weights_count(int model) {
     switch (model) {
         case GNND_CGNNI: case GNND_QGNNI: return 62;
         case GNND_V24: return 1283;
         case GNND_CBP: case GNND_QBP: return 0;
+        case GNND_NBP: case GNND_V10: return -2;
         default: return -1;
     }
+}
+int64_t decode_weights_count(int model, int E, int iters) {
+    if (model == GNND_NBP) return 2 * (int64_t)E * iters + 2 * (int64_t)E + 1;
+    if (model == GNND_V10) return (int64_t)E * iters + 1;
+    return weights_count(model);
+}
+// weights staged to LDS by the kernels (the weighted-BP tables are read through the cache)
+int lds_weights(int model) {
+    const int n = weights_count(model);
+    return n > 0 ? n : 0;
 }
 
 constexpr size_t kLdsMax = 160 * 1024;
@@ -681,9 +808,9 @@ size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
 int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p) {
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
-    const size_t wb = align16((size_t)weights_count(model) * esz);
+    const size_t wb = align16((size_t)lds_weights(model) * esz);
     const size_t target = lds_target();
-    const bool light = model != GNND_V24;
+    const bool light = model != GNND_V24 && model != GNND_NBP && model != GNND_V10;
     if (light && dtype == GNND_F32 && gr->rview.G <= 16 && !resident_disabled()) {
         const GraphView& g = gr->rview;          // instantiated group sizes 1..16
         const int IC = g.C * g.G;
@@ -759,7 +886,7 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
     const GraphView& g = *p.view;
     int64_t blocks = (B + p.cw - 1) / p.cw;
     if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
-    const int nw = weights_count(MODEL);
+    const int nw = lds_weights(MODEL);
     const FastDiv dI = make_fastdiv(p.resident ? p.cw : g.C * g.G);
     const FastDiv dV = make_fastdiv(g.V), dN = make_fastdiv(g.N);
     auto go = [&](auto kern) -> int {
@@ -833,3 +960,5 @@ int gnnd_launch_qgnni(const gnnd_graph*, int, const void*, const void*, void*, i
 int gnnd_launch_qbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_cgnni(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_cbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_nbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_v10(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

@@ -3,7 +3,8 @@
 // Restates the per-script propagate bodies (paths relative to /root/reference/GNN-decode/):
 //   V24   quantum/decoder_v2_4.py:132-144   QGNNI quantum/QGNNI.py:101-112
 //   QBP   quantum/BP.py:101-119             CGNNI classical/CGNNI.py:99-108
-//   CBP   classical/BP.py:99-119
+//   CBP   classical/BP.py:99-119            NBP   quantum/neural_BP.py:108-131
+//   V10   quantum/decoder_v1_0.py:109-131
 // i.e.  out = post( scatter_(aggr, pre(msg), idx_j, dim_size)[idx_j] - pre(msg), extra[idx_j] )
 // with idx_j = edge_index[0] for flow source_to_target and edge_index[1] for
 // target_to_source (quantum/decoder_v2_4.py:89), PyG-1.x scatter_ fill rules
@@ -26,10 +27,31 @@ template <typename T> __device__ __forceinline__ T cst(double v) { return (T)v; 
 
 constexpr int AG_ADD = GNND_AGGR_ADD, AG_MEAN = GNND_AGGR_MEAN, AG_MAX = GNND_AGGR_MAX;
 
-__host__ __device__ constexpr bool is_bp(int var) { return var == GNND_QBP || var == GNND_CBP; }
+__host__ __device__ constexpr bool is_bp(int var) {
+    return var == GNND_QBP || var == GNND_CBP || var == GNND_NBP || var == GNND_V10;
+}
+// syndrome-aware quantum BP bodies (sign term (1 - s)/2, log(1+p) - log(1-p))
+__host__ __device__ constexpr bool is_qbp(int var) {
+    return var == GNND_QBP || var == GNND_NBP || var == GNND_V10;
+}
+// the weighted-BP scripts drop the +-10 pre-clamp and clamp p at 1 - 1e-15
+__host__ __device__ constexpr bool is_nbp(int var) { return var == GNND_NBP || var == GNND_V10; }
 
 __host__ __device__ constexpr int out_width(int var, int flow) {
-    return (var == GNND_V24 || (var == GNND_QGNNI && flow == GNND_TARGET_TO_SOURCE)) ? 2 : 1;
+    return (var == GNND_V24 || (var == GNND_QGNNI && flow == GNND_TARGET_TO_SOURCE) ||
+            (var == GNND_NBP && flow == GNND_SOURCE_TO_TARGET)) ? 2 : 1;
+}
+
+template <int VAR, typename T> __device__ __forceinline__ T bp_lo() {
+    return VAR == GNND_CBP ? cst<T>(1e-7) : cst<T>(1e-20);
+}
+template <int VAR, typename T> __device__ __forceinline__ T bp_hi() {
+    return VAR == GNND_CBP ? cst<T>(1 - 1e-7) : is_nbp(VAR) ? cst<T>(1 - 1e-15) : cst<T>(1 - 1e-12);
+}
+// BP c->v input: tanh(x/2) after the +-10 clamp (QBP/CBP only)
+template <int VAR, typename T> __device__ __forceinline__ T bp_tanh(T m) {
+    if constexpr (is_nbp(VAR)) return g_tanh(m / T(2));
+    else return g_tanh(g_clamp(m, T(-10), T(10)) / T(2));
 }
 
 // c->v pre-op on the per-edge message (the BP variants also produce the sign indicator)
@@ -37,10 +59,9 @@ template <int VAR, int FLOW, typename T>
 __device__ __forceinline__ T pre_op(T m, T* coeff) {
     if constexpr (FLOW == GNND_TARGET_TO_SOURCE) {
         if constexpr (is_bp(VAR)) {
-            T t = g_tanh(g_clamp(m, T(-10), T(10)) / T(2));
+            T t = bp_tanh<VAR, T>(m);
             *coeff = t < T(0) ? T(1) : T(0);
-            const T lo = VAR == GNND_QBP ? cst<T>(1e-20) : cst<T>(1e-7);
-            return g_log(g_clamp(g_abs(t), lo, cst<T>(1e10)));
+            return g_log(g_clamp(g_abs(t), bp_lo<VAR, T>(), cst<T>(1e10)));
         } else {
             return g_tanh(m / T(2));
         }
@@ -55,10 +76,10 @@ template <int VAR, int FLOW, typename T>
 __device__ __forceinline__ void post_op(T val, T val2, T ex, bool has_extra, T* o) {
     if constexpr (is_bp(VAR) && FLOW == GNND_TARGET_TO_SOURCE) {
         T n = val2;
-        if constexpr (VAR == GNND_QBP) n = n + (T(1) - ex) / T(2);
-        const T hi = VAR == GNND_QBP ? cst<T>(1 - 1e-12) : cst<T>(1 - 1e-7);
+        if constexpr (is_qbp(VAR)) n = n + (T(1) - ex) / T(2);
+        const T hi = bp_hi<VAR, T>();
         T p = g_clamp(g_exp(val) * cos_pi(n), -hi, hi);
-        if constexpr (VAR == GNND_QBP)
+        if constexpr (is_qbp(VAR))
             o[0] = g_log(T(1) + p) - g_log(T(1) - p);
         else
             o[0] = g_log((T(1) + p) / (T(1) - p));
@@ -67,7 +88,7 @@ __device__ __forceinline__ void post_op(T val, T val2, T ex, bool has_extra, T* 
         o[1] = ex;
     } else if constexpr (VAR == GNND_CGNNI) {
         o[0] = has_extra ? val + ex : val;
-    } else {   // QGNNI / QBP / CBP source_to_target: + extra
+    } else {   // QGNNI / QBP / CBP / V10 source_to_target: + extra
         o[0] = val + ex;
     }
 }
@@ -201,6 +222,8 @@ int tiled_var(const gnnd_graph* g, int var, int flow, int aggr, const void* m, c
         case GNND_QBP: return tiled_flow<GNND_QBP, T>(g, flow, aggr, m, ex, o, B, st);
         case GNND_CGNNI: return tiled_flow<GNND_CGNNI, T>(g, flow, aggr, m, ex, o, B, st);
         case GNND_CBP: return tiled_flow<GNND_CBP, T>(g, flow, aggr, m, ex, o, B, st);
+        case GNND_NBP: return tiled_flow<GNND_NBP, T>(g, flow, aggr, m, ex, o, B, st);
+        case GNND_V10: return tiled_flow<GNND_V10, T>(g, flow, aggr, m, ex, o, B, st);
     }
     return GNND_ERR_INVALID_ARG;
 }
@@ -379,12 +402,14 @@ int gen_var(int var, int flow, int aggr, const int64_t* ei, int64_t s, int64_t n
         case GNND_QBP: return gen_flow<GNND_QBP, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
         case GNND_CGNNI: return gen_flow<GNND_CGNNI, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
         case GNND_CBP: return gen_flow<GNND_CBP, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
+        case GNND_NBP: return gen_flow<GNND_NBP, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
+        case GNND_V10: return gen_flow<GNND_V10, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
     }
     return GNND_ERR_INVALID_ARG;
 }
 
 bool valid_common(int var, int flow, int aggr, int dtype) {
-    return var >= GNND_V24 && var <= GNND_CBP &&
+    return var >= GNND_V24 && var <= GNND_V10 &&
            (flow == GNND_SOURCE_TO_TARGET || flow == GNND_TARGET_TO_SOURCE) &&
            aggr >= AG_ADD && aggr <= AG_MAX && (dtype == GNND_F32 || dtype == GNND_F64);
 }
@@ -456,6 +481,210 @@ propagate_tiled_bwd_kernel(GraphView g, const T* __restrict__ msg, const T* __re
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// backward of the c->v BP bodies (QBP, CBP, NBP, V10; flow target_to_source, aggr 'add').
+// The forward is recomputed per check:  t = tanh(x/2) (QBP/CBP: x clamped to +-10 first),
+// L = log(clamp(|t|, lo, 1e10)), Lambda = S_c(L) - L, n = S_c([t<0]) - [t<0] (+ (1-s)/2),
+// q = exp(Lambda), p = clamp(q cos(pi n), -hi, hi), out = log(1+p) - log(1-p) (CBP:
+// log((1+p)/(1-p))).  torch's autograd rules, in its order:
+//   g_p = g (1/(1+p) + 1/(1-p)) [p inside the clamp]   g_Lambda = (g_p cos) q
+//   g_L = S_c(g_Lambda) - g_Lambda                     (leave-one-out, like the forward)
+//   g_t = g_L / clamp(|t|) [|t| inside the clamp] sgn(t)
+//   g_x = (g_t (1 - t^2)) / 2 [QBP/CBP: x inside +-10]
+// ---------------------------------------------------------------------------------------
+template <int VAR, typename T> struct BpFwd {
+    T t, L, c;
+    __device__ __forceinline__ void init(T m) {
+        t = bp_tanh<VAR, T>(m);
+        c = t < T(0) ? T(1) : T(0);
+        L = g_log(g_clamp(g_abs(t), bp_lo<VAR, T>(), cst<T>(1e10)));
+    }
+    // gradient w.r.t. the input message given g_L
+    __device__ __forceinline__ T input_grad(T m, T gL) const {
+        const T u = g_abs(t);
+        const T uc = g_clamp(u, bp_lo<VAR, T>(), cst<T>(1e10));
+        T gu = (u >= bp_lo<VAR, T>() && u <= cst<T>(1e10)) ? gL / uc : T(0);
+        T gt = gu * (t > T(0) ? T(1) : (t < T(0) ? T(-1) : T(0)));
+        T gx = (gt * (T(1) - t * t)) / T(2);
+        if constexpr (!is_nbp(VAR)) gx = (m >= T(-10) && m <= T(10)) ? gx : T(0);
+        return gx;
+    }
+};
+// g_Lambda of one edge from its leave-one-out sums (lam, n) and the output gradient
+template <int VAR, typename T>
+__device__ __forceinline__ T bp_lambda_grad(T lam, T n, T ex, T g) {
+    if constexpr (is_qbp(VAR)) n = n + (T(1) - ex) / T(2);
+    const T hi = bp_hi<VAR, T>();
+    const T sgn = cos_pi(n), q = g_exp(lam);
+    const T p = q * sgn;
+    const T pc = g_clamp(p, -hi, hi);
+    T gp;
+    if constexpr (is_qbp(VAR)) gp = g / (T(1) + pc) + g / (T(1) - pc);
+    else gp = T(2) * g / ((T(1) + pc) * (T(1) - pc));
+    gp = (p >= -hi && p <= hi) ? gp : T(0);
+    return (gp * sgn) * q;
+}
+
+template <int VAR, typename T>
+__global__ void __launch_bounds__(GNND_BLOCK)
+propagate_tiled_bp_bwd_kernel(GraphView g, const T* __restrict__ msg, const T* __restrict__ extra,
+                              const T* __restrict__ gout, T* __restrict__ gmsg, int64_t B, int CW,
+                              FastDiv dNode, FastDiv dE) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int V = g.V, C = g.C, E = g.E, N = g.N;
+    const int tid = threadIdx.x;
+    int* s_tab = (int*)smem;
+    const int nints = graph_table_ints(V, C, E);
+    const uint32_t* s_evc = (const uint32_t*)s_tab;
+    const int* s_cptr = s_tab + E + V + 1;
+    const int* s_cedge = s_cptr + C + 1;
+    size_t off = ((size_t)nints * 4 + 15) & ~(size_t)15;
+    T* s_L = (T*)(smem + off);                 // [CW][E]
+    T* s_c = s_L + (size_t)CW * E;             // [CW][E]  sign indicator, then g_Lambda
+    T* s_aL = s_c + (size_t)CW * E;            // [CW][C]  S_c(L), then S_c(g_Lambda)
+    T* s_ac = s_aL + (size_t)CW * C;           // [CW][C]  S_c(sign)
+    const int* gtab = (const int*)g.edge_vc;
+    for (int i = tid; i < nints; i += GNND_BLOCK) s_tab[i] = gtab[i];
+    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
+    const int nE = nb * E;
+    const T* mg = msg + b0 * E;
+    for (int f = tid; f < nE; f += GNND_BLOCK) {
+        BpFwd<VAR, T> fw;
+        fw.init(mg[f]);
+        s_L[f] = fw.L;
+        s_c[f] = fw.c;
+    }
+    __syncthreads();
+    for (int f = tid; f < nb * C; f += GNND_BLOCK) {
+        int b = fdiv(f, dNode), j = f - b * C;
+        T a = T(0), a2 = T(0);
+        for (int k = s_cptr[j], ke = s_cptr[j + 1]; k < ke; ++k) {
+            int e = s_cedge[k];
+            a += s_L[b * E + e];
+            a2 += s_c[b * E + e];
+        }
+        s_aL[f] = a;
+        s_ac[f] = a2;
+    }
+    __syncthreads();
+    const T* gg = gout + b0 * E;
+    for (int f = tid; f < nE; f += GNND_BLOCK) {
+        int b = fdiv(f, dE), e = f - b * E;
+        int j = (int)(s_evc[e] >> 16);
+        T ex = is_qbp(VAR) ? extra[(b0 + b) * N + V + j] : T(0);
+        const T gl = bp_lambda_grad<VAR, T>(s_aL[b * C + j] - s_L[f], s_ac[b * C + j] - s_c[f], ex, gg[f]);
+        s_c[f] = gl;            // same thread read s_c[f] above: in-place is safe                           // sign indicator no longer needed
+    }
+    __syncthreads();
+    for (int f = tid; f < nb * C; f += GNND_BLOCK) {
+        int b = fdiv(f, dNode), j = f - b * C;
+        T a = T(0);
+        for (int k = s_cptr[j], ke = s_cptr[j + 1]; k < ke; ++k) a += s_c[b * E + s_cedge[k]];
+        s_aL[f] = a;
+    }
+    __syncthreads();
+    T* og = gmsg + b0 * E;
+    for (int f = tid; f < nE; f += GNND_BLOCK) {
+        int b = fdiv(f, dE), e = f - b * E;
+        int j = (int)(s_evc[e] >> 16);
+        BpFwd<VAR, T> fw;
+        fw.init(mg[f]);
+        og[f] = fw.input_grad(mg[f], s_aL[b * C + j] - s_c[f]);
+    }
+}
+
+template <int VAR, typename T>
+int launch_tiled_bp_bwd(const gnnd_graph* gr, const void* msg, const void* extra, const void* gout,
+                        void* gmsg, int64_t B, hipStream_t st) {
+    const GraphView& g = gr->view;
+    const size_t tab = ((size_t)graph_table_ints(g.V, g.C, g.E) * 4 + 15) & ~(size_t)15;
+    const size_t per = sizeof(T) * (2 * (size_t)g.E + 2 * (size_t)g.C);
+    if (tab + per > 160 * 1024) return GNND_ERR_UNSUPPORTED;
+    size_t cw = tab + per >= kLdsTarget ? 1 : (kLdsTarget - tab) / per;
+    if (cw > 64) cw = 64;
+    size_t lds = tab + cw * per;
+    auto kern = propagate_tiled_bp_bwd_kernel<VAR, T>;
+    if (lds > 64 * 1024)
+        GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int64_t blocks = (B + (int64_t)cw - 1) / (int64_t)cw;
+    if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
+    kern<<<(unsigned)blocks, GNND_BLOCK, lds, st>>>(g, (const T*)msg, (const T*)extra, (const T*)gout,
+                                                     (T*)gmsg, B, (int)cw, make_fastdiv(g.C),
+                                                     make_fastdiv(g.E));
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
+// generic (any edge_index) BP backward: three edge passes with atomic node sums.
+// workspace: L[nE], c/g_Lambda[nE], S(L)[dim], S(c)[dim], S(g_Lambda)[dim]
+template <int VAR, typename T>
+__global__ void __launch_bounds__(GNND_BLOCK)
+gen_bp_bwd_a(const int64_t* __restrict__ idx, const T* __restrict__ msg, int64_t nE, int64_t dim,
+             T* L, T* c, T* aL, T* ac) {
+    int64_t e = (int64_t)blockIdx.x * GNND_BLOCK + threadIdx.x;
+    if (e >= nE) return;
+    BpFwd<VAR, T> fw;
+    fw.init(msg[e]);
+    L[e] = fw.L;
+    c[e] = fw.c;
+    int64_t j = idx[e];
+    if (j < 0 || j >= dim) return;
+    atomicAdd(aL + j, fw.L);
+    atomicAdd(ac + j, fw.c);
+}
+template <int VAR, typename T>
+__global__ void __launch_bounds__(GNND_BLOCK)
+gen_bp_bwd_b(const int64_t* __restrict__ idx, const T* __restrict__ extra, const T* __restrict__ gout,
+             int64_t nE, int64_t dim, const T* L, T* c, const T* aL, const T* ac, T* ag) {
+    int64_t e = (int64_t)blockIdx.x * GNND_BLOCK + threadIdx.x;
+    if (e >= nE) return;
+    int64_t j = idx[e];
+    if (j < 0 || j >= dim) { c[e] = T(NAN); return; }
+    T ex = is_qbp(VAR) ? extra[j] : T(0);
+    T gl = bp_lambda_grad<VAR, T>(aL[j] - L[e], ac[j] - c[e], ex, gout[e]);
+    c[e] = gl;
+    atomicAdd(ag + j, gl);
+}
+template <int VAR, typename T>
+__global__ void __launch_bounds__(GNND_BLOCK)
+gen_bp_bwd_c(const int64_t* __restrict__ idx, const T* __restrict__ msg, int64_t nE, int64_t dim,
+             const T* gl, const T* ag, T* __restrict__ gmsg) {
+    int64_t e = (int64_t)blockIdx.x * GNND_BLOCK + threadIdx.x;
+    if (e >= nE) return;
+    int64_t j = idx[e];
+    if (j < 0 || j >= dim) { gmsg[e] = T(NAN); return; }
+    BpFwd<VAR, T> fw;
+    fw.init(msg[e]);
+    gmsg[e] = fw.input_grad(msg[e], ag[j] - gl[e]);
+}
+
+int64_t gen_bwd_ws_elems(bool bp, int64_t nE, int64_t dim) {
+    return bp ? 2 * nE + 3 * dim : dim;
+}
+
+template <int VAR, typename T>
+int launch_generic_bp_bwd(const int64_t* ei, int64_t stride, int64_t nE, const void* msg,
+                          const void* extra, const void* gout, int64_t dim, void* gmsg, void* ws,
+                          int64_t ws_bytes, hipStream_t st) {
+    if (ws_bytes < gen_bwd_ws_elems(true, nE, dim) * (int64_t)sizeof(T)) return GNND_ERR_INVALID_ARG;
+    T* w = (T*)ws;
+    T *L = w, *c = w + nE, *aL = w + 2 * nE, *ac = aL + dim, *ag = ac + dim;
+    const int64_t* idx = ei + stride;                       // target_to_source: edge_index[1]
+    if (dim > 0) {
+        fill_kernel<T><<<(unsigned)((3 * dim + GNND_BLOCK - 1) / GNND_BLOCK), GNND_BLOCK, 0, st>>>(aL, 3 * dim, T(0));
+        GNND_LAUNCH_CHECK();
+    }
+    if (nE == 0) return GNND_OK;
+    const unsigned gE = (unsigned)((nE + GNND_BLOCK - 1) / GNND_BLOCK);
+    gen_bp_bwd_a<VAR, T><<<gE, GNND_BLOCK, 0, st>>>(idx, (const T*)msg, nE, dim, L, c, aL, ac);
+    gen_bp_bwd_b<VAR, T><<<gE, GNND_BLOCK, 0, st>>>(idx, (const T*)extra, (const T*)gout, nE, dim, L, c, aL, ac, ag);
+    gen_bp_bwd_c<VAR, T><<<gE, GNND_BLOCK, 0, st>>>(idx, (const T*)msg, nE, dim, c, ag, (T*)gmsg);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
 template <int VAR, int FLOW, typename T>
 int launch_tiled_bwd(const gnnd_graph* gr, const void* msg, const void* gout, void* gmsg,
                      int64_t B, hipStream_t st) {
@@ -525,31 +754,45 @@ int launch_generic_bwd(const int64_t* ei, int64_t stride, int64_t nE, const void
 
 template <int VAR, typename T>
 int bwd_flow(bool tiled, int flow, const gnnd_graph* g, const int64_t* ei, int64_t stride,
-             int64_t nE, const void* msg, const void* gout, int64_t dim, void* gmsg, void* ws,
-             int64_t wb, int64_t B, hipStream_t st) {
+             int64_t nE, const void* msg, const void* extra, const void* gout, int64_t dim,
+             void* gmsg, void* ws, int64_t wb, int64_t B, hipStream_t st) {
     if (flow == GNND_SOURCE_TO_TARGET)
         return tiled ? launch_tiled_bwd<VAR, GNND_SOURCE_TO_TARGET, T>(g, msg, gout, gmsg, B, st)
                      : launch_generic_bwd<VAR, GNND_SOURCE_TO_TARGET, T>(ei, stride, nE, msg, gout, dim, gmsg, ws, wb, st);
+    if constexpr (is_bp(VAR))
+        return tiled ? launch_tiled_bp_bwd<VAR, T>(g, msg, extra, gout, gmsg, B, st)
+                     : launch_generic_bp_bwd<VAR, T>(ei, stride, nE, msg, extra, gout, dim, gmsg, ws, wb, st);
     return tiled ? launch_tiled_bwd<VAR, GNND_TARGET_TO_SOURCE, T>(g, msg, gout, gmsg, B, st)
                  : launch_generic_bwd<VAR, GNND_TARGET_TO_SOURCE, T>(ei, stride, nE, msg, gout, dim, gmsg, ws, wb, st);
 }
 
 template <typename T>
 int bwd_var(bool tiled, int var, int flow, const gnnd_graph* g, const int64_t* ei, int64_t stride,
-            int64_t nE, const void* msg, const void* gout, int64_t dim, void* gmsg, void* ws,
-            int64_t wb, int64_t B, hipStream_t st) {
+            int64_t nE, const void* msg, const void* extra, const void* gout, int64_t dim,
+            void* gmsg, void* ws, int64_t wb, int64_t B, hipStream_t st) {
+#define GNND_BWD_CASE(V) \
+    case V: return bwd_flow<V, T>(tiled, flow, g, ei, stride, nE, msg, extra, gout, dim, gmsg, ws, wb, B, st);
     switch (var) {
-        case GNND_V24: return bwd_flow<GNND_V24, T>(tiled, flow, g, ei, stride, nE, msg, gout, dim, gmsg, ws, wb, B, st);
-        case GNND_QGNNI: return bwd_flow<GNND_QGNNI, T>(tiled, flow, g, ei, stride, nE, msg, gout, dim, gmsg, ws, wb, B, st);
-        case GNND_CGNNI: return bwd_flow<GNND_CGNNI, T>(tiled, flow, g, ei, stride, nE, msg, gout, dim, gmsg, ws, wb, B, st);
+        GNND_BWD_CASE(GNND_V24)
+        GNND_BWD_CASE(GNND_QGNNI)
+        GNND_BWD_CASE(GNND_QBP)
+        GNND_BWD_CASE(GNND_CGNNI)
+        GNND_BWD_CASE(GNND_CBP)
+        GNND_BWD_CASE(GNND_NBP)
+        GNND_BWD_CASE(GNND_V10)
     }
-    return GNND_ERR_UNSUPPORTED;   // BP bodies have no trainable parameters upstream
+#undef GNND_BWD_CASE
+    return GNND_ERR_INVALID_ARG;
+}
+
+bool bwd_needs_extra(int variant, int flow) {
+    return is_qbp(variant) && flow == GNND_TARGET_TO_SOURCE;
 }
 
 }  // namespace
 
 extern "C" int gnnd_propagate_width(int variant, int flow) {
-    if (variant < GNND_V24 || variant > GNND_CBP) return -1;
+    if (variant < GNND_V24 || variant > GNND_V10) return -1;
     if (flow != GNND_SOURCE_TO_TARGET && flow != GNND_TARGET_TO_SOURCE) return -1;
     return out_width(variant, flow);
 }
@@ -591,30 +834,43 @@ extern "C" int gnnd_propagate_generic(int variant, int flow, int aggr, int dtype
 }
 
 extern "C" int gnnd_propagate_tiled_bwd(const gnnd_graph* g, int variant, int flow, int aggr,
-                                        int dtype, const void* d_msg, const void* d_grad_out,
-                                        void* d_grad_msg, int64_t batch, void* stream) {
+                                        int dtype, const void* d_msg, const void* d_extra,
+                                        const void* d_grad_out, void* d_grad_msg, int64_t batch,
+                                        void* stream) {
     if (!g || !valid_common(variant, flow, aggr, dtype) || batch < 0) return GNND_ERR_INVALID_ARG;
-    if (aggr != AG_ADD || is_bp(variant)) return GNND_ERR_UNSUPPORTED;
+    if (aggr != AG_ADD) return GNND_ERR_UNSUPPORTED;
     if (batch == 0) return GNND_OK;
     if (!d_msg || !d_grad_out || !d_grad_msg) return GNND_ERR_INVALID_ARG;
+    if (!d_extra && bwd_needs_extra(variant, flow)) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == GNND_F32)
-        return bwd_var<float>(true, variant, flow, g, nullptr, 0, 0, d_msg, d_grad_out, 0, d_grad_msg, nullptr, 0, batch, st);
-    return bwd_var<double>(true, variant, flow, g, nullptr, 0, 0, d_msg, d_grad_out, 0, d_grad_msg, nullptr, 0, batch, st);
+        return bwd_var<float>(true, variant, flow, g, nullptr, 0, 0, d_msg, d_extra, d_grad_out, 0, d_grad_msg, nullptr, 0, batch, st);
+    return bwd_var<double>(true, variant, flow, g, nullptr, 0, 0, d_msg, d_extra, d_grad_out, 0, d_grad_msg, nullptr, 0, batch, st);
+}
+
+extern "C" int gnnd_propagate_generic_bwd_workspace(int variant, int flow, int aggr, int dtype,
+                                                    int64_t nE, int64_t dim, int64_t* h_bytes) {
+    if (!valid_common(variant, flow, aggr, dtype) || nE < 0 || dim < 0 || !h_bytes)
+        return GNND_ERR_INVALID_ARG;
+    if (aggr != AG_ADD) return GNND_ERR_UNSUPPORTED;
+    const bool bp = is_bp(variant) && flow == GNND_TARGET_TO_SOURCE;
+    *h_bytes = gen_bwd_ws_elems(bp, nE, dim) * (dtype == GNND_F64 ? 8 : 4);
+    return GNND_OK;
 }
 
 extern "C" int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
                                           const int64_t* d_ei, int64_t row_stride, int64_t nE,
-                                          const void* d_msg, const void* d_grad_out,
-                                          int64_t dim, void* d_grad_msg, void* d_ws,
-                                          int64_t ws_bytes, void* stream) {
+                                          const void* d_msg, const void* d_extra,
+                                          const void* d_grad_out, int64_t dim, void* d_grad_msg,
+                                          void* d_ws, int64_t ws_bytes, void* stream) {
     if (!valid_common(variant, flow, aggr, dtype) || nE < 0 || dim < 0 || row_stride < nE)
         return GNND_ERR_INVALID_ARG;
-    if (aggr != AG_ADD || is_bp(variant)) return GNND_ERR_UNSUPPORTED;
+    if (aggr != AG_ADD) return GNND_ERR_UNSUPPORTED;
     if (nE > 0 && (!d_ei || !d_msg || !d_grad_out || !d_grad_msg)) return GNND_ERR_INVALID_ARG;
+    if (nE > 0 && !d_extra && bwd_needs_extra(variant, flow)) return GNND_ERR_INVALID_ARG;
     if (!d_ws && dim > 0) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
     if (dtype == GNND_F32)
-        return bwd_var<float>(false, variant, flow, nullptr, d_ei, row_stride, nE, d_msg, d_grad_out, dim, d_grad_msg, d_ws, ws_bytes, 0, st);
-    return bwd_var<double>(false, variant, flow, nullptr, d_ei, row_stride, nE, d_msg, d_grad_out, dim, d_grad_msg, d_ws, ws_bytes, 0, st);
+        return bwd_var<float>(false, variant, flow, nullptr, d_ei, row_stride, nE, d_msg, d_extra, d_grad_out, dim, d_grad_msg, d_ws, ws_bytes, 0, st);
+    return bwd_var<double>(false, variant, flow, nullptr, d_ei, row_stride, nE, d_msg, d_extra, d_grad_out, dim, d_grad_msg, d_ws, ws_bytes, 0, st);
 }

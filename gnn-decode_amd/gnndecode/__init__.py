@@ -7,10 +7,11 @@ include/gnnd.h); PyTorch provides device memory, streams and torch.distributed o
 from . import _lib, codes, data, loss, train
 from .graph import TannerGraph
 from .nn import MessagePassing, ClassicalMessagePassing, message_passing_class
-from .models import (DecoderV24, QGNNI, QuantumBP, CGNNI, ClassicalBP, MODELS, DEFAULT_ITERS,
-                     init_weights)
+from .models import (DecoderV24, QGNNI, QuantumBP, CGNNI, ClassicalBP, NeuralBP, DecoderV10,
+                     MODELS, DEFAULT_ITERS, init_weights)
 from . import ops
 
 __all__ = ['TannerGraph', 'MessagePassing', 'ClassicalMessagePassing', 'message_passing_class',
-           'DecoderV24', 'QGNNI', 'QuantumBP', 'CGNNI', 'ClassicalBP', 'MODELS', 'DEFAULT_ITERS',
+           'DecoderV24', 'QGNNI', 'QuantumBP', 'CGNNI', 'ClassicalBP', 'NeuralBP', 'DecoderV10',
+           'MODELS', 'DEFAULT_ITERS',
            'init_weights', 'ops', 'codes', 'data', 'loss', 'train']

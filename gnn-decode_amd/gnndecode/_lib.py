@@ -16,7 +16,7 @@ F32, F64 = 0, 1
 SOURCE_TO_TARGET, TARGET_TO_SOURCE = 0, 1
 AGGR = {'add': 0, 'mean': 1, 'max': 2}
 FLOW = {'source_to_target': SOURCE_TO_TARGET, 'target_to_source': TARGET_TO_SOURCE}
-VARIANT = {'v24': 0, 'qgnni': 1, 'qbp': 2, 'cgnni': 3, 'cbp': 4}
+VARIANT = {'v24': 0, 'qgnni': 1, 'qbp': 2, 'cgnni': 3, 'cbp': 4, 'nbp': 5, 'v10': 6}
 
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
 _c_i32p = ctypes.POINTER(ctypes.c_int32)
@@ -36,10 +36,13 @@ SIGNATURES = {
     'gnnd_propagate_generic_workspace': (_int, [_int, _int, _int, _int, _i64, _i64, _c_i64p]),
     'gnnd_propagate_generic': (_int, [_int, _int, _int, _int, _vp, _i64, _i64, _vp, _vp, _i64,
                                       _vp, _vp, _i64, _vp]),
-    'gnnd_propagate_tiled_bwd': (_int, [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _i64, _vp]),
-    'gnnd_propagate_generic_bwd': (_int, [_int, _int, _int, _int, _vp, _i64, _i64, _vp, _vp, _i64,
-                                          _vp, _vp, _i64, _vp]),
+    'gnnd_propagate_tiled_bwd': (_int, [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _vp, _i64,
+                                        _vp]),
+    'gnnd_propagate_generic_bwd_workspace': (_int, [_int, _int, _int, _int, _i64, _i64, _c_i64p]),
+    'gnnd_propagate_generic_bwd': (_int, [_int, _int, _int, _int, _vp, _i64, _i64, _vp, _vp, _vp,
+                                          _i64, _vp, _vp, _i64, _vp]),
     'gnnd_weights_count': (_int, [_int, _c_i64p]),
+    'gnnd_decode_weights_count': (_int, [_vp, _int, _i32, _c_i64p]),
     'gnnd_prepare_weights': (_int, [_int, _int, _vp, _vp, _vp]),
     'gnnd_decode': (_int, [_vp, _int, _int, _vp, _vp, _vp, _i64, _i32, _vp]),
     'gnnd_decode_tile': (_int, [_vp, _int, _int, _c_i32p, _c_i32p]),

@@ -8,6 +8,8 @@ Each class mirrors one reference script's `GNNI` (paths relative to
   QuantumBP    quantum/BP.py:179-219              (no parameters)
   CGNNI        classical/CGNNI.py:212-284         keys ggc{1,2}.mlp{1,2}.*, ggc{1,2}.rnn.*, mlp.*
   ClassicalBP  classical/BP.py:216-259            (no parameters)
+  NeuralBP     quantum/neural_BP.py:236-314       keys layers.{i}.W, layers.{i}.W_p, W, W_p, alpha
+  DecoderV10   quantum/decoder_v1_0.py:236-313    keys layers.{i}.W, alpha
 
 Differences from the reference, all at the call boundary: the parity-check matrix is
 passed to the constructor (`GNNI(Nc, H)`) instead of being read from module globals
@@ -25,7 +27,7 @@ from . import ops
 from .graph import TannerGraph
 from .nn import MessagePassing, ClassicalMessagePassing, message_passing_class
 
-_MP = {v: message_passing_class(v) for v in ('v24', 'qgnni', 'qbp', 'cbp')}
+_MP = {v: message_passing_class(v) for v in ('v24', 'qgnni', 'qbp', 'cbp', 'nbp', 'v10')}
 _MP['cgnni'] = ClassicalMessagePassing
 
 
@@ -164,6 +166,49 @@ class GatedGraphConvCGNNI(ClassicalMessagePassing):
         if self.flow == 'target_to_source':
             return _apply_mlp(self.mlp2, aggr_out.to(self.mlp2[0].weight.dtype)).to(aggr_out.dtype)
         return aggr_out
+
+
+def _edge_param(E, value):
+    return torch.nn.Parameter(torch.full((E, 1), float(value), dtype=torch.float64))
+
+
+class GraphConvNBP(_MP['nbp']):
+    """quantum/neural_BP.py:236-260.  Per-edge W scales the v->c input messages and W_p the
+    prior in `update`; both act in the source_to_target layer only (the target_to_source
+    layer's pair exists as unused parameters, as in the reference)."""
+
+    def __init__(self, flow, E, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        self.W = _edge_param(E, 1.0)
+        self.W_p = _edge_param(E, 1.0)
+
+    def forward(self, m, edge_index, x, prev=None, size=None):
+        x = x if x.dim() == 2 else x.unsqueeze(-1)
+        if self.flow == 'source_to_target':
+            m = m.mul(self.W.repeat(m.size(0) // self.W.size(0), 1))
+        size = size or (x.size(0), x.size(0))
+        return self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
+
+    def update(self, aggr_out):
+        if self.flow == 'source_to_target':
+            B = aggr_out.size(0) // self.W_p.size(0)
+            return aggr_out[:, 0:1] + aggr_out[:, 1:2].mul(self.W_p.repeat(B, 1))
+        return aggr_out
+
+
+class GraphConvV10(_MP['v10']):
+    """quantum/decoder_v1_0.py:236-252: per-edge W scales the c->v layer's input."""
+
+    def __init__(self, flow, E, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        self.W = _edge_param(E, 1.0)
+
+    def forward(self, m, edge_index, x, prev=None, size=None):
+        x = x if x.dim() == 2 else x.unsqueeze(-1)
+        if self.flow != 'source_to_target':
+            m = m.mul(self.W.repeat(m.size(0) // self.W.size(0), 1))
+        size = size or (x.size(0), x.size(0))
+        return self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
 
 
 # ---------------------------------------------------------------------------------------
@@ -376,5 +421,78 @@ class ClassicalBP(_Decoder):
         return torch.clamp(torch.sigmoid(-res), 1e-7, 1 - 1e-7)
 
 
-MODELS = {'v24': DecoderV24, 'qgnni': QGNNI, 'qbp': QuantumBP, 'cgnni': CGNNI, 'cbp': ClassicalBP}
-DEFAULT_ITERS = {'v24': 15, 'qgnni': 25, 'qbp': 10, 'cgnni': 25, 'cbp': 25}
+class _WeightedBP(_Decoder):
+    """Shared plumbing of the weighted ("neural") BP decoders: Nc pairs of layers with
+    per-edge weight tables, residual m = c2v + m_prev @ alpha."""
+    layer_cls = None
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.E = int(self.H.sum())
+        layers = []
+        for _ in range(Nc):
+            layers.append(self.layer_cls('source_to_target', self.E))
+            layers.append(self.layer_cls('target_to_source', self.E))
+        self.layers = torch.nn.Sequential(*layers)
+        self.alpha = torch.nn.Parameter(torch.zeros(1, 1, dtype=torch.float64))
+
+    def prepared_weights(self, dtype, device):
+        flat = self.packed_weights()
+        return ops.prepare_weights(self.kind, flat.detach().to(device=device, dtype=dtype))
+
+    def _messages(self, x, ei):
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        alpha = self.alpha.to(x.dtype)
+        for i in range(0, len(self.layers), 2):
+            m_p = m
+            m = self.layers[i](m, ei, x)
+            m = self.layers[i + 1](m, ei, x) + torch.matmul(m_p, alpha)
+        return m
+
+
+class NeuralBP(_WeightedBP):
+    """quantum/neural_BP.py:263-314 (Nc = 15, toric L = 4 in the reference)."""
+    kind = 'nbp'
+    layer_cls = GraphConvNBP
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.W = _edge_param(self.E, 1.0)
+        self.W_p = _edge_param(self.E, 0.5)
+
+    def packed_weights(self):
+        per = [torch.cat([self.layers[2 * t].W.reshape(-1), self.layers[2 * t].W_p.reshape(-1)])
+               for t in range(self.Nc)]
+        return torch.cat(per + [self.W.reshape(-1), self.W_p.reshape(-1), self.alpha.reshape(-1)])
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        m = self._messages(x, ei)
+        m = m.mul(self.W.repeat(B, 1).to(x.dtype))
+        prior = x[ei[0]].mul(self.W_p.repeat(B, 1).to(x.dtype))
+        res = (self._var_rows(self._var_sum(m, ei, x.size(0)), B)
+               + self._var_rows(self._var_sum(prior, ei, x.size(0)), B))
+        return torch.sigmoid(-res)
+
+
+class DecoderV10(_WeightedBP):
+    """quantum/decoder_v1_0.py:263-313 (Nc = 15, toric L = 4 in the reference)."""
+    kind = 'v10'
+    layer_cls = GraphConvV10
+
+    def packed_weights(self):
+        return torch.cat([self.layers[2 * t + 1].W.reshape(-1) for t in range(self.Nc)]
+                         + [self.alpha.reshape(-1)])
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        m = self._messages(x, ei)
+        res = self._var_rows(self._var_sum(m, ei, x.size(0)), B) + self._var_rows(x, B)
+        return torch.sigmoid(-res)
+
+
+MODELS = {'v24': DecoderV24, 'qgnni': QGNNI, 'qbp': QuantumBP, 'cgnni': CGNNI, 'cbp': ClassicalBP,
+          'nbp': NeuralBP, 'v10': DecoderV10}
+DEFAULT_ITERS = {'v24': 15, 'qgnni': 25, 'qbp': 10, 'cgnni': 25, 'cbp': 25, 'nbp': 15, 'v10': 15}

@@ -10,7 +10,8 @@ import torch
 from . import _lib
 from .graph import TannerGraph, current_stream, dtype_code
 
-MODELS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp')
+MODELS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10')
+WEIGHTED_BP = ('nbp', 'v10')      # per-edge weight tables: count depends on the graph and T
 
 
 def _ptr(t):
@@ -58,21 +59,24 @@ def _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B):
     return out
 
 
-def _propagate_bwd(variant, flow, aggr, edge_index, msg, grad_out, dim_size, B):
+def _propagate_bwd(variant, flow, aggr, edge_index, msg, extra, grad_out, dim_size, B):
     grad_out = grad_out.contiguous()
     gmsg = torch.empty_like(msg)
     v, f, a = _lib.VARIANT[variant], _lib.FLOW[flow], _lib.AGGR[aggr]
     dt = dtype_code(msg.dtype)
     stream = current_stream(msg.device)
     if B is not None:
-        _lib.call('gnnd_propagate_tiled_bwd', B[0].handle, v, f, a, dt, _ptr(msg), _ptr(grad_out),
-                  _ptr(gmsg), B[1], stream)
+        _lib.call('gnnd_propagate_tiled_bwd', B[0].handle, v, f, a, dt, _ptr(msg), _ptr(extra),
+                  _ptr(grad_out), _ptr(gmsg), B[1], stream)
         return gmsg
     ei = edge_index if edge_index.stride(1) == 1 else edge_index.contiguous()
-    ws = torch.empty(max(dim_size, 1), dtype=msg.dtype, device=msg.device)
+    nb = ctypes.c_int64()
+    _lib.call('gnnd_propagate_generic_bwd_workspace', v, f, a, dt, msg.size(0), dim_size,
+              ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=msg.device)
     _lib.call('gnnd_propagate_generic_bwd', v, f, a, dt, _ptr(ei), ei.stride(0), msg.size(0),
-              _ptr(msg), _ptr(grad_out), dim_size, _ptr(gmsg), _ptr(ws),
-              ws.numel() * ws.element_size(), stream)
+              _ptr(msg), _ptr(extra), _ptr(grad_out), dim_size, _ptr(gmsg), _ptr(ws),
+              nb.value, stream)
     return gmsg
 
 
@@ -81,15 +85,15 @@ class _PropagateFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, msg, variant, flow, aggr, edge_index, extra, dim_size, B):
-        ctx.save_for_backward(msg, edge_index)
+        ctx.save_for_backward(msg, edge_index, extra)
         ctx.args = (variant, flow, aggr, dim_size, B)
         return _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B)
 
     @staticmethod
     def backward(ctx, grad_out):
-        msg, edge_index = ctx.saved_tensors
+        msg, edge_index, extra = ctx.saved_tensors
         variant, flow, aggr, dim_size, B = ctx.args
-        gmsg = _propagate_bwd(variant, flow, aggr, edge_index, msg, grad_out, dim_size, B)
+        gmsg = _propagate_bwd(variant, flow, aggr, edge_index, msg, extra, grad_out, dim_size, B)
         return gmsg, None, None, None, None, None, None, None
 
 
@@ -121,25 +125,36 @@ def propagate(variant, flow, aggr, edge_index, msg, extra, dim_size, graph=None,
     b = _tiled_batch(graph, edge_index, nE, dim_size, extra, aggr, chk_shift)
     B = (graph, b) if b is not None else None
     if msg.requires_grad and torch.is_grad_enabled():
-        if aggr != 'add' or variant in ('qbp', 'cbp'):
-            raise NotImplementedError(f'no backward for aggr={aggr!r} / variant {variant!r}')
+        if aggr != 'add':
+            raise NotImplementedError(f'no backward for aggr={aggr!r}')
         return _PropagateFn.apply(msg, variant, flow, aggr, edge_index, extra, dim_size, B)
     return _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B)
 
 
-def weights_count(model):
+def weights_count(model, graph=None, iters=None):
+    """Packed weight count of a fused decoder (gnnd.h); the weighted-BP models need the
+    graph and the iteration count."""
     n = ctypes.c_int64()
-    _lib.call('gnnd_weights_count', _lib.VARIANT[model], ctypes.byref(n))
+    if model in WEIGHTED_BP:
+        if graph is None or iters is None:
+            raise ValueError(f'{model}: the weight count depends on the graph and T')
+        _lib.call('gnnd_decode_weights_count', graph.handle, _lib.VARIANT[model], int(iters),
+                  ctypes.byref(n))
+    else:
+        _lib.call('gnnd_weights_count', _lib.VARIANT[model], ctypes.byref(n))
     return n.value
 
 
 def prepare_weights(model, flat):
-    """Kernel-layout copy of a packed weight vector (gnnd_prepare_weights)."""
+    """Kernel-layout copy of a packed weight vector (gnnd_prepare_weights).  The weighted-BP
+    tables are used as packed."""
+    _require_gpu(flat)
+    flat = flat.contiguous()
+    if model in WEIGHTED_BP:
+        return flat
     n = weights_count(model)
     if n == 0:
         return None
-    _require_gpu(flat)
-    flat = flat.contiguous()
     if flat.numel() != n:
         raise ValueError(f'{model}: expected {n} packed weights, got {flat.numel()}')
     out = torch.empty_like(flat)
@@ -155,7 +170,7 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     if x.numel() % graph.N:
         raise ValueError(f'x has {x.numel()} rows, not a multiple of N={graph.N}')
     B = x.numel() // graph.N
-    nw = weights_count(model)
+    nw = weights_count(model, graph, iters)
     if nw and (prepared_weights is None or prepared_weights.numel() != nw):
         raise ValueError(f'{model}: needs {nw} prepared weights')
     if prepared_weights is not None and prepared_weights.dtype != x.dtype:

@@ -58,9 +58,13 @@ typedef enum gnnd_aggr { GNND_AGGR_ADD = 0, GNND_AGGR_MEAN = 1, GNND_AGGR_MAX = 
  *   QGNNI  quantum/QGNNI.py:101-112         c->v tanh(x/2), cat (F=2); v->c + extra (F=1)
  *   QBP    quantum/BP.py:101-119            c->v log-domain BP with syndrome; v->c + extra
  *   CGNNI  classical/CGNNI.py:99-108        c->v tanh(x/2); + post (if non-NULL) (F=1)
- *   CBP    classical/BP.py:99-119           c->v log-domain BP; v->c + extra (F=1)        */
+ *   CBP    classical/BP.py:99-119           c->v log-domain BP; v->c + extra (F=1)
+ *   NBP    quantum/neural_BP.py:108-131     c->v log-domain BP with syndrome, no +-10
+ *                                           pre-clamp, p clamp 1 - 1e-15; v->c cat (F=2)
+ *   V10    quantum/decoder_v1_0.py:109-131  c->v as NBP; v->c + extra (F=1)              */
 typedef enum gnnd_variant {
-    GNND_V24 = 0, GNND_QGNNI = 1, GNND_QBP = 2, GNND_CGNNI = 3, GNND_CBP = 4
+    GNND_V24 = 0, GNND_QGNNI = 1, GNND_QBP = 2, GNND_CGNNI = 3, GNND_CBP = 4,
+    GNND_NBP = 5, GNND_V10 = 6
 } gnnd_variant;
 
 /* Whole-decoder models for gnnd_decode (same enumerators as gnnd_variant). */
@@ -107,17 +111,23 @@ int gnnd_propagate_generic(int variant, int flow, int aggr, int dtype,
                            void* d_out, void* d_workspace, int64_t workspace_bytes,
                            void* stream);
 
-/* Backward of one propagate call w.r.t. d_msg (training; aggr ADD, non-BP variants — the BP
- * decoders have no parameters).  d_grad_out is [B*E, F] like d_out, d_grad_msg [B*E].  The
- * generic form needs a workspace of dim_size elements of `dtype`.                        */
+/* Backward of one propagate call w.r.t. d_msg (training; aggr ADD, every variant).
+ * d_grad_out is [B*E, F] like d_out, d_grad_msg [B*E].  d_extra is the forward's `extra`
+ * (the syndrome sets the sign of the BP check step; may be NULL except for the quantum BP
+ * bodies QBP/NBP/V10 with flow TARGET_TO_SOURCE).  The c->v BP bodies recompute their
+ * forward and apply torch's autograd rules (clamp passes the gradient on [lo, hi], abs
+ * uses sign(t), tanh 1 - t^2).  The generic form needs a workspace of
+ * gnnd_propagate_generic_bwd_workspace() bytes.                                           */
 int gnnd_propagate_tiled_bwd(const gnnd_graph* g, int variant, int flow, int aggr, int dtype,
-                             const void* d_msg, const void* d_grad_out, void* d_grad_msg,
-                             int64_t batch, void* stream);
+                             const void* d_msg, const void* d_extra, const void* d_grad_out,
+                             void* d_grad_msg, int64_t batch, void* stream);
+int gnnd_propagate_generic_bwd_workspace(int variant, int flow, int aggr, int dtype,
+                                         int64_t num_edges, int64_t dim_size, int64_t* h_bytes);
 int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
                                const int64_t* d_edge_index, int64_t row_stride,
-                               int64_t num_edges, const void* d_msg, const void* d_grad_out,
-                               int64_t dim_size, void* d_grad_msg, void* d_workspace,
-                               int64_t workspace_bytes, void* stream);
+                               int64_t num_edges, const void* d_msg, const void* d_extra,
+                               const void* d_grad_out, int64_t dim_size, void* d_grad_msg,
+                               void* d_workspace, int64_t workspace_bytes, void* stream);
 
 /* ---- fused T-iteration decoder --------------------------------------------------------
  * Runs the whole GNNI.forward (m0 = 0, T iterations of both half-steps, residual, readout)
@@ -132,10 +142,18 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  *            ggc2.mlp  {W1[128], b1[128], W2[128], b2}, mlp {W1[128], b1[128], W2[128], b2}
  *                                                                                    = 1283
  *     CBP, QBP: none (d_w may be NULL)
+ *     NBP (quantum/neural_BP.py, per-edge weights in reference edge order, T = iters):
+ *            for t < T {layers[2t].W[E], layers[2t].W_p[E]}, then W[E], W_p[E], alpha
+ *                                                                          = 2 E T + 2 E + 1
+ *     V10 (quantum/decoder_v1_0.py): for t < T {layers[2t+1].W[E]}, then alpha  = E T + 1
  * gnnd_prepare_weights converts that layout into the kernel layout (for the fp32 V24
  * kernel the softplus layers are rescaled to base 2: layer-1 rows * log2(e), layer-2
- * weights * ln(2); every other model/dtype is a plain copy).  Call it once per weights. */
+ * weights * ln(2); every other model/dtype is a plain copy).  Call it once per weights.
+ * gnnd_weights_count is the graph-independent count (GNND_ERR_UNSUPPORTED for NBP/V10,
+ * whose packed layout is passed to gnnd_decode as is, without preparation);
+ * gnnd_decode_weights_count covers every model for a graph and iteration count.         */
 int gnnd_weights_count(int model, int64_t* h_count);
+int gnnd_decode_weights_count(const gnnd_graph* g, int model, int32_t iters, int64_t* h_count);
 int gnnd_prepare_weights(int model, int dtype, const void* d_w, void* d_prepared,
                          void* stream);
 int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,

@@ -16,6 +16,8 @@ ironmanaudi/GNN-decode (paths relative to /root/reference/GNN-decode/):
                           quantum/decoder_v2_4.py:272-294
 * `update()` MLPs         classical/CGNNI.py:238-242, quantum/QGNNI.py:207-214,
                           quantum/decoder_v2_4.py:253-257
+* weighted ("neural") BP  quantum/neural_BP.py:59-143 (propagate), :236-314 (layers, GNNI);
+                          quantum/decoder_v1_0.py:60-133, :236-313
 
 Parity pinning: every function here is checked against golden vectors produced by running the
 reference's own class definitions (tests/golden/make_golden.py) in tests/test_oracle_golden.py.
@@ -28,7 +30,7 @@ Batch layout (A10): graph-major.  `x` is [B*N, 1] with N = V + C
 """
 import numpy as np
 
-SCRIPTS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp')
+SCRIPTS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10')
 
 
 def tanner_edges(H):
@@ -93,12 +95,22 @@ def propagate(script, flow, aggr, edge_index, msg, extra, dim_size):
     * qbp   quantum/BP.py:101-121            (c->v log-domain BP with syndrome; v->c + extra)
     * cgnni classical/CGNNI.py:99-110        (c->v tanh(x/2); `post` added if not None)
     * cbp   classical/BP.py:99-121           (c->v log-domain BP; v->c + extra)
+    * nbp   quantum/neural_BP.py:108-131     (c->v BP without the +-10 pre-clamp, p clamp
+                                              1 - 1e-15; v->c cat extra[idx_j])
+    * v10   quantum/decoder_v1_0.py:109-131  (c->v as nbp; v->c + extra)
     """
     ei = np.asarray(edge_index)
     i, j = (0, 1) if flow == 'target_to_source' else (1, 0)
     idx = ei[j]
     out = np.asarray(msg)
     dt = out.dtype.type
+    if script in ('nbp', 'v10'):
+        if flow == 'target_to_source':
+            return _nbp_check_literal(aggr, out, extra[idx], idx, dim_size)
+        out = _extrinsic(aggr, out, idx, dim_size)
+        if script == 'v10':
+            return out + extra[idx]
+        return np.concatenate([out, extra[idx]], axis=1)
     if script in ('qbp', 'cbp') and flow == 'target_to_source':
         lo = 1e-20 if script == 'qbp' else 1e-7
         hi = 1 - 1e-12 if script == 'qbp' else 1 - 1e-7
@@ -131,6 +143,22 @@ def propagate(script, flow, aggr, edge_index, msg, extra, dim_size):
     if script == 'qgnni' and flow == 'source_to_target':
         return out + extra[idx]
     return np.concatenate([out, extra[idx]], axis=1)  # v24 both flows, qgnni c->v
+
+
+def _nbp_check_literal(aggr, a, s_e, idx, dim_size):
+    """c->v step of quantum/neural_BP.py:109-122 / quantum/decoder_v1_0.py:109-122 (same
+    text): tanh(a/2) with NO pre-clamp, sign count, log|t| clamped to [1e-20, 1e10],
+    leave-one-out sums at the check, cos(pi (n + (1 - s)/2)), p clamped to +-(1 - 1e-15),
+    log(1 + p) - log(1 - p).  s_e = extra[idx_j] (syndrome +-1 at the edge's check)."""
+    dt = a.dtype.type
+    t = np.tanh(a / dt(2))
+    coeff = np.where(t < 0, dt(1), dt(0))
+    mag = np.log(np.clip(np.abs(t), dt(1e-20), dt(1e10)))
+    lam = _extrinsic(aggr, mag, idx, dim_size)
+    n = _extrinsic(aggr, coeff, idx, dim_size)
+    p = np.exp(lam) * np.cos(dt(np.pi) * (n + (dt(1) - s_e) / dt(2)))
+    p = np.clip(p, dt(-1 + 1e-15), dt(1 - 1e-15))
+    return np.log(dt(1) + p) - np.log(dt(1) - p)
 
 
 # ---------------------------------------------------------------------------------------
@@ -276,6 +304,59 @@ def decode_v24(H, w, x, T):
     return sigmoid(-r).reshape(-1, 1)
 
 
+def _nbp_check(g, a, s):
+    """_nbp_check_literal on the single-graph structure: a [B, E], s [B, C]."""
+    dt = a.dtype.type
+    t = np.tanh(a / dt(2))
+    coeff = np.where(t < 0, dt(1), dt(0))
+    mag = np.log(np.clip(np.abs(t), dt(1e-20), dt(1e10)))
+    lam = g.sum_chk(mag)[:, g.c] - mag
+    n = g.sum_chk(coeff)[:, g.c] - coeff
+    p = np.exp(lam) * np.cos(dt(np.pi) * (n + (dt(1) - s[:, g.c]) / dt(2)))
+    p = np.clip(p, dt(-1 + 1e-15), dt(1 - 1e-15))
+    return np.log(dt(1) + p) - np.log(dt(1) - p)
+
+
+def _edge_w(w, key, dt):
+    return np.asarray(w[key], dt).reshape(-1)
+
+
+def decode_nbp(H, w, x, T):
+    """quantum/neural_BP.py:263-314 (fp64, Nc = 15).  Layer 2t (source_to_target,
+    :245-260): m <- m * W (per edge), a = LOO_v(m) + x_v * W_p; layer 2t+1 (c->v, its W/W_p
+    unused): BP check step; residual m = c2v + m_prev @ alpha.  Readout: sigmoid(-(sum_v
+    m * W + sum_v x_v * W_p)) with the GNNI-level W, W_p."""
+    g = _Graph(H)
+    xv, xc = _split_x(g, x)
+    dt = xv.dtype.type
+    m = np.zeros((xv.shape[0], g.E), xv.dtype)
+    alpha = dt(np.asarray(w['alpha'], dt).reshape(()))
+    for t in range(T):
+        m_p = m
+        mw = m * _edge_w(w, f'layers.{2 * t}.W', dt)
+        a = (g.sum_var(mw)[:, g.v] - mw) + xv[:, g.v] * _edge_w(w, f'layers.{2 * t}.W_p', dt)
+        m = _nbp_check(g, a, xc) + m_p * alpha
+    r = g.sum_var(m * _edge_w(w, 'W', dt)) + g.sum_var(xv[:, g.v] * _edge_w(w, 'W_p', dt))
+    return sigmoid(-r).reshape(-1, 1)
+
+
+def decode_v10(H, w, x, T):
+    """quantum/decoder_v1_0.py:282-313 (fp64, Nc = 15).  Layer 2t (source_to_target,
+    :245-252): a = LOO_v(m) + x_v; layer 2t+1: a * W (per edge), BP check step; residual
+    m = c2v + m_prev @ alpha.  Readout sigmoid(-(sum_v m + x_v))."""
+    g = _Graph(H)
+    xv, xc = _split_x(g, x)
+    dt = xv.dtype.type
+    m = np.zeros((xv.shape[0], g.E), xv.dtype)
+    alpha = dt(np.asarray(w['alpha'], dt).reshape(()))
+    for t in range(T):
+        m_p = m
+        a = g.sum_var(m)[:, g.v] - m + xv[:, g.v]
+        m = _nbp_check(g, a * _edge_w(w, f'layers.{2 * t + 1}.W', dt), xc) + m_p * alpha
+    r = g.sum_var(m) + xv
+    return sigmoid(-r).reshape(-1, 1)
+
+
 def decode(model, H, x, T, w=None):
     if model == 'cgnni':
         return decode_cgnni(H, w, x, T)
@@ -287,6 +368,10 @@ def decode(model, H, x, T, w=None):
         return decode_qgnni(H, w, x, T)
     if model == 'v24':
         return decode_v24(H, w, x, T)
+    if model == 'nbp':
+        return decode_nbp(H, w, x, T)
+    if model == 'v10':
+        return decode_v10(H, w, x, T)
     raise ValueError(model)
 
 

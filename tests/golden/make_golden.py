@@ -438,12 +438,96 @@ def gen_training():
          **sd_to_np(sd), **grads_of(model))
 
 
+def gen_neural_bp():
+    """Weighted ("neural") BP decoders on the same operator:
+    quantum/neural_BP.py (per-layer per-edge W, W_p on the v->c step; readout W, W_p;
+    residual alpha) and quantum/decoder_v1_0.py (per-layer per-edge W on the c->v input;
+    residual alpha).  Toric L = 4, T = 15 (the scripts' Nc), fp64.  The scripts initialise
+    every weight to 1 (0.5 for the readout W_p, 0 for alpha): the fixtures perturb them
+    (seeded) so that every weight path is exercised.  The shipped checkpoints under
+    quantum/neural_BP/ belong to an orphaned revision (ggc1/ggc2, 4 edge types, per-variable
+    W_p) that matches neither script and are not used.  Also: a bare propagate() per flow,
+    and one training step (reference LossFunc, train=1) with parameter gradients."""
+    sys.path.insert(0, os.path.join(REF, 'quantum'))
+    import error_generate as eg
+    L = 4
+    Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+    H = torch.from_numpy(Hnp).t()
+    hp = eg.H_Prep(H.t())
+    H_prep = torch.from_numpy(hp.get_H_Prep())
+    logical, _ = hp.get_logical(H_prep)
+    V, C = H.shape
+    N = V + C
+    specs = (('nbp', 'quantum/neural_BP.py', 201), ('v10', 'quantum/decoder_v1_0.py', 301))
+    prop = {}
+    for tag, script, seed in specs:
+        ns = load_ref(script, {'MessagePassing', 'GraphConv', 'GNNI', 'LossFunc'},
+                      logical=logical)
+        ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, 1, H
+        set_seed(seed)
+        model = ns['GNNI'](15)
+        with torch.no_grad():
+            for k, p in model.named_parameters():
+                if k == 'alpha':
+                    p.fill_(0.3)
+                else:
+                    p.mul_(1 + 0.25 * torch.randn(p.shape, dtype=p.dtype))
+        sd = {k: v.clone() for k, v in model.state_dict().items()}
+        arrays = dict(sd_to_np(sd))
+        for B, xs in ((1, seed + 1), (32, seed + 2)):
+            x, y = toric_inputs(eg, H, L, [0.05, 0.1], B, xs)
+            arrays[f'x_B{B}'], arrays[f'y_B{B}'] = x.numpy(), y.numpy()
+            for T in (1, 2, 15):
+                out, _ = run_model(ns, H, x, B, T, {k: v for k, v in sd.items()
+                                                    if not k.startswith('layers.') or
+                                                    int(k.split('.')[1]) < 2 * T})
+                arrays[f'out_B{B}_T{T}'] = out.numpy()
+        save(f'{tag}_toric4', **arrays)
+
+        # one training step at B = 4 (reference LossFunc, train=1: sum-of-|sin| syndrome +
+        # logical loss), gradients of every parameter
+        B = 4
+        x, y = toric_inputs(eg, H, L, [0.05, 0.1], B, seed + 3)
+        ns['BATCH_SIZE'] = B
+        model = ns['GNNI'](15)
+        model.load_state_dict(sd)
+        data = types.SimpleNamespace(x=x, edge_index=batch_edge_index(single_edge_index(H), B, N), y=y)
+        pred = model(data)
+        loss = ns['LossFunc'](H, H_prep)(pred, data, 1)
+        loss.backward()
+        save(f'train_{tag}_L4', x=x.numpy(), y=y.numpy(), loss=np.array(loss.item()),
+             pred=pred.detach().numpy(), T=np.array(15), **sd_to_np(sd), **grads_of(model))
+
+        # bare propagate() per flow on random messages (identity message/update)
+        B = 3
+        ei = batch_edge_index(single_edge_index(H), B, N)
+        ei = torch.stack([ei[0], ei[1] + V])
+        g = torch.Generator().manual_seed(seed + 4)
+        E = ei.size(1)
+        m = (torch.randn(E, 1, generator=g) * 3).double()
+        m[::7] *= 8                                   # saturate some tanh(x/2) below 1e-15
+        xv = torch.randn(B, V, generator=g) * 2
+        xc = torch.where(torch.rand(B, C, generator=g) < 0.3, -1.0, 1.0)
+        extra = torch.cat([xv, xc], dim=1).reshape(B * N, 1).double()
+        prop[f'{tag}/edge_index'] = ei.numpy()
+        prop[f'{tag}/msg'] = m.numpy()
+        prop[f'{tag}/extra'] = extra.numpy()
+        for flow in ('source_to_target', 'target_to_source'):
+            mp = ns['MessagePassing']('add', flow)
+            with torch.no_grad():
+                out = mp.propagate(edge_index=ei, size=(N * B, N * B), x=m, extra=extra)
+            prop[f'{tag}/{flow}/add'] = out.numpy()
+    save('propagate_ops_nbp', **prop)
+
+
 if __name__ == '__main__':
     torch.set_num_threads(1)
-    which = sys.argv[1:] or ['classical', 'quantum', 'training']
+    which = sys.argv[1:] or ['classical', 'quantum', 'training', 'neural_bp']
     if 'classical' in which:
         gen_classical()
     if 'quantum' in which:
         gen_quantum()
     if 'training' in which:
         gen_training()
+    if 'neural_bp' in which:
+        gen_neural_bp()

@@ -46,12 +46,16 @@ def test_weights_count_and_width():
     for name, cnt in expect.items():
         assert lib.gnnd_weights_count(_lib.VARIANT[name], ctypes.byref(n)) == _lib.OK
         assert n.value == cnt
-    assert lib.gnnd_weights_count(7, ctypes.byref(n)) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_weights_count(9, ctypes.byref(n)) == _lib.ERR_INVALID_ARG
+    for name in ('nbp', 'v10'):   # per-edge tables: gnnd_decode_weights_count (needs a graph)
+        assert lib.gnnd_weights_count(_lib.VARIANT[name], ctypes.byref(n)) == _lib.ERR_UNSUPPORTED
+        assert lib.gnnd_decode_weights_count(None, _lib.VARIANT[name], 15, ctypes.byref(n)) == _lib.ERR_INVALID_ARG
     w = lib.gnnd_propagate_width
     assert w(_lib.VARIANT['v24'], 0) == 2 and w(_lib.VARIANT['v24'], 1) == 2
     assert w(_lib.VARIANT['qgnni'], 0) == 1 and w(_lib.VARIANT['qgnni'], 1) == 2
-    for v in ('qbp', 'cgnni', 'cbp'):
+    for v in ('qbp', 'cgnni', 'cbp', 'v10'):
         assert w(_lib.VARIANT[v], 0) == 1 and w(_lib.VARIANT[v], 1) == 1
+    assert w(_lib.VARIANT['nbp'], 0) == 2 and w(_lib.VARIANT['nbp'], 1) == 1
     assert w(9, 0) == -1 and w(0, 5) == -1
 
 
@@ -96,3 +100,11 @@ def test_null_argument_checks():
     assert lib.gnnd_propagate_generic_workspace(2, 1, 1, 1, 100, 40, ctypes.byref(b)) == _lib.OK
     assert b.value == (100 * 2 + 40 * 3 + 200) * 8      # BP c->v mean: src, src2, agg, agg2, cnt, lm x2
     assert lib.gnnd_propagate_generic_workspace(0, 1, 3, 0, 100, 40, ctypes.byref(b)) == _lib.ERR_INVALID_ARG
+    # backward workspace: node accumulator; the BP check steps recompute L, sign, g_Lambda
+    assert lib.gnnd_propagate_generic_bwd_workspace(0, 1, 0, 1, 100, 40, ctypes.byref(b)) == _lib.OK
+    assert b.value == 40 * 8
+    assert lib.gnnd_propagate_generic_bwd_workspace(5, 1, 0, 1, 100, 40, ctypes.byref(b)) == _lib.OK
+    assert b.value == (2 * 100 + 3 * 40) * 8
+    assert lib.gnnd_propagate_generic_bwd_workspace(5, 0, 0, 0, 100, 40, ctypes.byref(b)) == _lib.OK
+    assert b.value == 40 * 4
+    assert lib.gnnd_propagate_generic_bwd_workspace(0, 1, 1, 0, 100, 40, ctypes.byref(b)) == _lib.ERR_UNSUPPORTED

@@ -26,6 +26,8 @@ DECODERS = [
     ('qgnni_toric4', 'qgnni', 'toric_L4_graph'),
     ('v24_toric5', 'v24', 'toric_L5_graph'),
     ('v24_toric7', 'v24', 'toric_L7_graph'),
+    ('nbp_toric4', 'nbp', 'toric_L4_graph'),
+    ('v10_toric4', 'v10', 'toric_L4_graph'),
 ]
 
 
@@ -42,6 +44,8 @@ def build_model(model, H, T, z):
     import gnndecode as gd
     m = gd.MODELS[model](T, H)
     w = weights_of(z)
+    if model in ('nbp', 'v10'):      # fixtures hold 15 layer pairs; a T-layer model uses the first T
+        w = {k: v for k, v in w.items() if not k.startswith('layers.') or int(k.split('.')[1]) < 2 * T}
     if w:
         m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in w.items()})
     return m.to(DEV).eval()
@@ -81,7 +85,8 @@ def test_fused_decode_native_dtype(golden, fx, model, gfx, B, T):
     assert ((out > 0.5) == (ref > 0.5))[~near].all()
 
 
-@pytest.mark.parametrize('fx,model,gfx,B,T', [c for c in _cases() if c.values[1] in ('qbp', 'qgnni', 'v24')])
+@pytest.mark.parametrize('fx,model,gfx,B,T', [c for c in _cases()
+                                              if c.values[1] in ('qbp', 'qgnni', 'v24', 'nbp', 'v10')])
 def test_fused_decode_fp32_on_quantum_models(golden, fx, model, gfx, B, T):
     z = golden(fx)
     H = golden(gfx)['H']
@@ -111,17 +116,18 @@ def test_layerwise_operator_path(golden, fx, model, gfx, B, T):
 
 
 def _prop_cases():
-    z = np.load('tests/golden/propagate_ops.npz')
-    for k in z.files:
-        if len(k.split('/')) >= 3:
-            yield pytest.param(k, id=k)
+    for fx in ('propagate_ops', 'propagate_ops_nbp'):
+        z = np.load(f'tests/golden/{fx}.npz')
+        for k in z.files:
+            if len(k.split('/')) >= 3:
+                yield pytest.param(fx, k, id=f'{fx}:{k}')
 
 
 @pytest.mark.parametrize('path', ['tiled', 'generic'])
-@pytest.mark.parametrize('key', list(_prop_cases()))
-def test_propagate_operator(golden, key, path):
+@pytest.mark.parametrize('fx,key', list(_prop_cases()))
+def test_propagate_operator(golden, fx, key, path):
     import gnndecode as gd
-    z = golden('propagate_ops')
+    z = golden(fx)
     tag, flow, aggr = key.split('/')[:3]
     ei = torch.from_numpy(z[f'{tag}/edge_index']).to(DEV)
     msg = torch.from_numpy(z[f'{tag}/msg']).to(DEV)
@@ -130,7 +136,8 @@ def test_propagate_operator(golden, key, path):
     graph = None
     if path == 'tiled':
         gfx = {'v24': 'toric_L5_graph', 'qgnni': 'toric_L4_graph', 'qbp': 'toric_L4_graph',
-               'cgnni': 'bch_63_45_graph', 'cbp': 'bch_63_45_graph'}[tag]
+               'cgnni': 'bch_63_45_graph', 'cbp': 'bch_63_45_graph',
+               'nbp': 'toric_L4_graph', 'v10': 'toric_L4_graph'}[tag]
         graph = gd.TannerGraph(golden(gfx)['H'], device=DEV)
         assert graph.is_tiled(ei, graph.V) or aggr == 'mean'
     out = gd.ops.propagate(tag, flow, aggr, ei, msg, extra, extra_np.shape[0], graph=graph)

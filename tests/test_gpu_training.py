@@ -14,6 +14,8 @@ CASES = [  # fixture, model, code, loss kind, dtype tolerance
     ('train_v24_L7', 'v24', ('toric', 7), 'syndrome'),
     ('train_qgnni_L4', 'qgnni', ('toric', 4), 'logical'),
     ('train_cgnni_bch', 'cgnni', ('bch', None), 'classical'),
+    ('train_nbp_L4', 'nbp', ('toric', 4), 'syndrome'),
+    ('train_v10_L4', 'v10', ('toric', 4), 'syndrome'),
 ]
 
 
@@ -113,3 +115,49 @@ def test_graph_captured_trainer_matches_eager(golden):
     for (n, p), q in zip(m.named_parameters(), m2.parameters()):
         np.testing.assert_allclose(q.detach().cpu().numpy(), p.detach().cpu().numpy(),
                                    rtol=1e-10, atol=1e-13, err_msg=n)
+
+
+@pytest.mark.parametrize('variant', ['qbp', 'cbp', 'nbp', 'v10'])
+def test_bp_check_step_backward_matches_torch_autograd(variant):
+    """d propagate / d msg of the c->v BP bodies (tiled and generic kernels) vs torch
+    autograd of the literal reference formula (quantum/BP.py:102-117, classical/BP.py:
+    100-116, quantum/neural_BP.py:109-122), including saturated and clamped messages."""
+    import math
+    import gnndecode as gd
+    H = gd.codes.toric_code(4) if variant != 'cbp' else gd.codes.bch_63_45()
+    g = gd.TannerGraph(H, device=DEV)
+    B = 3
+    ei = g.batched_edge_index(B, chk_shift=g.V)
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    dt = torch.float64
+    msg = torch.randn(ei.size(1), 1, generator=gen, device=DEV, dtype=dt) * 4
+    msg[::9] *= 10                                   # beyond +-10 and into tanh saturation
+    xc = torch.where(torch.rand(B, g.C, generator=gen, device=DEV) < 0.3, -1.0, 1.0)
+    xv = torch.randn(B, g.V, generator=gen, device=DEV)
+    extra = torch.cat([xv, xc], 1).reshape(-1, 1).to(dt)
+    w = torch.randn(ei.size(1), 1, generator=gen, device=DEV, dtype=dt)
+    quantum = variant != 'cbp'
+    lo = 1e-7 if variant == 'cbp' else 1e-20
+    hi = {'cbp': 1 - 1e-7, 'qbp': 1 - 1e-12}.get(variant, 1 - 1e-15)
+    m0 = msg.clone().requires_grad_(True)
+    out = m0 if variant in ('nbp', 'v10') else torch.clamp(m0, -10, 10)
+    out = torch.tanh(out / 2)
+    coeff = torch.where(out < 0, torch.ones_like(out), torch.zeros_like(out))
+    out = torch.log(torch.clamp(abs(out), lo, 1e10))
+    j = ei[1]
+    n = extra.size(0)
+    out = torch.zeros(n, 1, dtype=dt, device=DEV).index_add(0, j, out)[j] - out
+    coeff = torch.zeros(n, 1, dtype=dt, device=DEV).index_add(0, j, coeff)[j] - coeff
+    if quantum:
+        coeff = coeff + (1 - extra[j]) / 2
+    out = torch.clamp(torch.exp(out) * torch.cos(math.pi * coeff), -hi, hi)
+    out = torch.log(1 + out) - torch.log(1 - out) if quantum else torch.log((1 + out) / (1 - out))
+    (out * w).sum().backward()
+    for graph in (g, None):
+        m1 = msg.clone().requires_grad_(True)
+        got = gd.ops.propagate(variant, 'target_to_source', 'add', ei, m1, extra, n, graph=graph)
+        np.testing.assert_allclose(got.detach().cpu().numpy(), out.detach().cpu().numpy(),
+                                   rtol=1e-12, atol=1e-12)
+        (got * w).sum().backward()
+        np.testing.assert_allclose(m1.grad.cpu().numpy(), m0.grad.cpu().numpy(),
+                                   rtol=1e-9, atol=1e-12 * float(m0.grad.abs().max()))

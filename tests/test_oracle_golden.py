@@ -15,6 +15,8 @@ DECODERS = [
     ('qgnni_toric4', 'qgnni', 'toric_L4_graph'),
     ('v24_toric5', 'v24', 'toric_L5_graph'),
     ('v24_toric7', 'v24', 'toric_L7_graph'),
+    ('nbp_toric4', 'nbp', 'toric_L4_graph'),
+    ('v10_toric4', 'v10', 'toric_L4_graph'),
 ]
 
 
@@ -42,16 +44,17 @@ def test_oracle_decoder_matches_reference(golden, fx, model, gfx, B, T):
 
 
 def _prop_cases():
-    z = np.load('tests/golden/propagate_ops.npz')
-    for k in z.files:
-        parts = k.split('/')
-        if len(parts) >= 3:
-            yield pytest.param(k, id=k)
+    for fx in ('propagate_ops', 'propagate_ops_nbp'):
+        z = np.load(f'tests/golden/{fx}.npz')
+        for k in z.files:
+            parts = k.split('/')
+            if len(parts) >= 3:
+                yield pytest.param(fx, k, id=f'{fx}:{k}')
 
 
-@pytest.mark.parametrize('key', list(_prop_cases()))
-def test_oracle_propagate_matches_reference(golden, key):
-    z = golden('propagate_ops')
+@pytest.mark.parametrize('fx,key', list(_prop_cases()))
+def test_oracle_propagate_matches_reference(golden, fx, key):
+    z = golden(fx)
     tag, flow, aggr = key.split('/')[:3]
     extra = None if key.endswith('nopost') else z[f'{tag}/extra']
     out = O.propagate(tag, flow, aggr, z[f'{tag}/edge_index'], z[f'{tag}/msg'], extra,
