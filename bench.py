@@ -31,12 +31,20 @@ import gnndecode as gd  # noqa: E402
 # costs 3 (variable sum, leave-one-out, + x) and the c->v side 55 (/2, check sum,
 # leave-one-out, MLP 1->10->1 = 51, residual); readout 55 per variable.  Transcendentals
 # (tanh, softplus) are counted separately and not included in FLOPs.
+# Weighted BP (NBP/V10) adds the per-edge weight products and the residual to BP's 17.
+# Second value: transcendental FUNCTIONS per codeword (tanh, softplus, exp, log); each needs
+# at least two hardware transcendental ops (exp + log / rcp), which is what the
+# transcendental roofline below prices.
 def flops_per_codeword(model, g, T):
     E, V = g.E, g.V
     if model in ('cgnni', 'qgnni'):
         return 58 * E * T + 55 * V, E * T
     if model in ('cbp', 'qbp'):
         return 17 * E * T + 4 * V, 6 * E * T
+    if model == 'nbp':
+        return 22 * E * T + 4 * E + 4 * V, 6 * E * T
+    if model == 'v10':
+        return 20 * E * T + 4 * V, 6 * E * T
     if model == 'v24':
         return 1417 * E * T + 514 * E + 2 * V, 256 * E * T + 128 * E
     raise ValueError(model)
@@ -63,7 +71,8 @@ def parse():
     p.add_argument('--no-graph', action='store_true',
                    help='train mode: eager steps instead of one captured HIP graph per step')
     p.add_argument('--mode', default='decode', choices=['decode', 'train'],
-                   help='train = config 5: decoder_v2_4 training step (DP, RCCL all-reduce)')
+                   help='train = config 5: decoder_v2_4 (or --model qgnni/nbp/v10) training '
+                        'step (DP, RCCL all-reduce)')
     return p.parse_args()
 
 
@@ -82,6 +91,10 @@ def load_pmc(tag):
 # VALU issue capacity: one wave64 VALU instruction per CU per clock (4 SIMDs x one
 # 4-cycle wave64 op); 256 CUs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md).
 VALU_ISSUE_PER_S = 256 * 2.4e9
+# Transcendental ops (v_exp/v_log/v_rcp_f32): 8 issue cycles per wave64 op per SIMD
+# (MI355X_MICROARCH.md constants; measured 3.5 ns per op per SIMD-wave in
+# tools/micro/issue_mix.hip = 18.7 T/s): 1024 SIMDs x 64 lanes / 8 cycles x 2.4 GHz.
+TRANS_OPS_PER_S = 1024 * 64 / 8 * 2.4e9
 
 
 def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
@@ -99,7 +112,11 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
     chunk = 512
     x_all = x_dev.view(-1, g.N)
     o_all = out_dev.view(-1, g.V)
+    # fp32 classical BP is ill-conditioned near its clamps: also decode the first chunks in
+    # fp64 and count how often EACH fp32 implementation (GPU, numpy oracle) disagrees with it
+    cond = model == 'cbp' and x_dev.dtype == torch.float32
     done, t_total, max_err, mism = 0, 0.0, 0.0, 0
+    c_bits = c_gpu = c_orc = 0
     while t_total < seconds and done + chunk <= x_all.size(0):
         xs = x_all[done:done + chunk].cpu().numpy().reshape(-1, 1)
         t0 = time.perf_counter()
@@ -109,22 +126,31 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
         ref = ref.astype(np.float64)
         max_err = max(max_err, float(np.abs(got - ref).max()))
         mism += int(((got > 0.5) != (ref > 0.5)).sum())
+        if cond and c_bits < 8 * chunk * g.V:
+            r64 = gnn_oracle.decode(model, H, xs.astype(np.float64), T, w)
+            c_bits += r64.size
+            c_gpu += int(((got > 0.5) != (r64 > 0.5)).sum())
+            c_orc += int(((ref > 0.5) != (r64 > 0.5)).sum())
         done += chunk
     if limiter is not None:
         limiter.unregister() if hasattr(limiter, 'unregister') else None
-    return {'value': done / t_total if t_total > 0 else None, 'unit': 'codewords/s',
-            'cores': 1, 'kind': 'port',
-            'sample': f'{done} codewords of the same batch (chunks of {chunk}), oracle/gnn_oracle.py '
-                      f'numpy restatement, 1 thread, {t_total:.1f} s',
-            'parity_max_abs_err': max_err, 'parity_hard_decision_mismatches': mism,
-            'parity_bits_compared': done * g.V}
+    res = {'value': done / t_total if t_total > 0 else None, 'unit': 'codewords/s',
+           'cores': 1, 'kind': 'port',
+           'sample': f'{done} codewords of the same batch (chunks of {chunk}), oracle/gnn_oracle.py '
+                     f'numpy restatement, 1 thread, {t_total:.1f} s',
+           'parity_max_abs_err': max_err, 'parity_hard_decision_mismatches': mism,
+           'parity_bits_compared': done * g.V}
+    if cond:
+        res['conditioning_vs_f64_oracle'] = {'bits': c_bits, 'gpu_f32_mismatches': c_gpu,
+                                             'oracle_f32_mismatches': c_orc}
+    return res
 
 
 def train_main(a, world, rank, dev):
     """Config 5: decoder_v2_4 training on the toric code (default L=7), each rank a shard of
     size --batch, one flat all_reduce(SUM) of the gradient per step (gnndecode.train)."""
     code = a.code if a.code.startswith('toric') else 'toric_7'
-    model_name = a.model if a.model in ('v24', 'qgnni') else 'v24'
+    model_name = a.model if a.model in ('v24', 'qgnni', 'nbp', 'v10') else 'v24'
     T = a.iters or gd.DEFAULT_ITERS[model_name]
     dtype = torch.float64 if a.dtype == 'f64' else torch.float32
     H = gd.codes.get_code(code)
@@ -153,11 +179,11 @@ def train_main(a, world, rank, dev):
     elapsed = float(t.item())
     if rank == 0:
         print(json.dumps({
-            'metric': 'training samples/sec (whole node), decoder_v2_4 step with RCCL grad all-reduce',
+            'metric': f'training samples/sec (whole node), {model_name} step with RCCL grad all-reduce',
             'value': world * a.batch * a.steps / elapsed, 'unit': 'samples/s', 'n_gpus': world,
             'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': a.dtype,
-            'data': 'synthetic toric errors (on-device sampler, seeded); seeded Kaiming init',
+            'data': 'synthetic toric errors (on-device sampler, seeded); seeded reference init',
             'config': {'workload': f'{code} {model_name} training step, T={T}, batch={a.batch}/GPU',
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
                        'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters()),
@@ -233,6 +259,7 @@ def main():
         fl, trans = flops_per_codeword(a.model, g, T)
         achieved = fl * a.batch / kernel_s / 1e12
         peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
+        trans_frac = 2 * trans * a.batch / kernel_s / TRANS_OPS_PER_S
         esz = 4 if dtype == torch.float32 else 8
         io_bytes = (g.N + g.V) * esz * a.batch
         plan = gd.ops.decode_plan(g, a.model, dtype)
@@ -264,6 +291,9 @@ def main():
                              valu / (kernel_s * VALU_ISSUE_PER_S) if valu else None,
                          'kernel_ms': kernel_s * 1e3,
                          'flops_per_codeword': fl, 'transcendentals_per_codeword': trans,
+                         # >= 2 hardware transcendental ops per function vs the 8-cycle issue
+                         # rate (fp32; fp64 has no hardware transcendentals)
+                         'transcendental_op_frac': trans_frac if dtype == torch.float32 else None,
                          'hbm_io_bytes_per_launch': io_bytes,
                          'hbm_io_frac': io_bytes / kernel_s / 1e9 / PEAK_HBM_GBS},
         }

@@ -334,14 +334,53 @@ __device__ __forceinline__ T var_sum_w(const T* mb, const int* vslot, int k0, in
 // ---------------------------------------------------------------------------------------
 // per-edge model math shared by both kernels
 // ---------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------
+// fp32 BP check-node math (classical/BP.py:101-116, quantum/BP.py:103-117) on the native
+// v_exp_f32 / v_log_f32 / v_rcp_f32, in the BASE-2 log domain: the check sums carry
+// log2|t| instead of ln|t| (exp2 of the base-2 sum is the same exp of the natural sum), so
+// no ln2 rescaling sits between the transcendental ops.
+//   tanh(z), z = min(|a|, 10)/2:  odd Taylor polynomial to z^9 for z < 0.3 (error < 2e-8
+//   relative), (1 - e)/(1 + e) with e = 2^(-2 z log2 e) above (1 - e >= 0.45: ~2 ulp).
+// Accuracy is a few ulp of the libm forms; classical BP in fp32 is ill-conditioned near
+// its clamps (tests/test_gpu_parity.py conditioning test) for any two fp32
+// implementations alike.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float bp_log2tanh_f32(float a, float lo) {
+    const float z = 0.5f * fminf(fabsf(a), 10.f);
+    const float z2 = z * z;
+    float tp = __builtin_fmaf(z2, 62.f / 2835.f, -17.f / 315.f);
+    tp = __builtin_fmaf(z2, tp, 2.f / 15.f);
+    tp = __builtin_fmaf(z2, tp, -1.f / 3.f);
+    tp = __builtin_fmaf(z2 * z, tp, z);
+    const float e = __builtin_amdgcn_exp2f(z * (-2.f * kLog2e));
+    const float te = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
+    const float t = z < 0.3f ? tp : te;
+    return __builtin_amdgcn_logf(fmaxf(t, lo));
+}
+// m from the base-2 leave-one-out sum lam2 and the sign count n (CBP: log((1+p)/(1-p)),
+// QBP: log(1+p) - log(1-p)), p = clamp(2^lam2 cos(pi n), +-hi)
+template <bool QUANTUM>
+__device__ __forceinline__ float bp_msg_f32(float lam2, float n, float hi) {
+    const float p = g_clamp(__builtin_amdgcn_exp2f(lam2) * cos_pi(n), -hi, hi);
+    if constexpr (QUANTUM)
+        return kLn2 * (__builtin_amdgcn_logf(1.f + p) - __builtin_amdgcn_logf(1.f - p));
+    else
+        return kLn2 * __builtin_amdgcn_logf((1.f + p) * __builtin_amdgcn_rcpf(1.f - p));
+}
+
 template <int MODEL, typename T> struct EdgeMath {
     static constexpr bool BP = ModelTraits<MODEL>::bp;
+    static constexpr bool kFastBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP);
     // v->c message update and c->v pre-op: a_e = (S_v - m_e) + x_v -> t_e (+ BP sign flag)
     // (fp32 V24 runs the paired-edge path of decode_kernel instead)
     __device__ static __forceinline__ T pre(T ext, T xv, const T* __restrict__ wv, T& cc) {
         cc = T(0);
         if constexpr (MODEL == GNND_V24) {
             return tanh_half_fast(mlp128x2_sp(wv + kV24Ggc1, ext, xv));
+        } else if constexpr (kFastBP) {
+            const float a = ext + xv;
+            cc = a < 0.f ? 1.f : 0.f;          // tanh(clamp(a)/2) < 0 exactly when a < 0
+            return bp_log2tanh_f32(a, MODEL == GNND_QBP ? 1e-20f : 1e-7f);
         } else if constexpr (BP) {
             T a = ext + xv;
             T th = g_tanh(g_clamp(a, T(-10), T(10)) / T(2));
@@ -362,6 +401,11 @@ template <int MODEL, typename T> struct EdgeMath {
             if constexpr (sizeof(T) == 4) y = mlp(u);
             else y = mlp10_relu(s_w + kMlp10Msg, u);
             return (MODEL == GNND_QGNNI ? y * sc : y) + mprev;
+        } else if constexpr (kFastBP) {
+            if constexpr (MODEL == GNND_QBP)
+                return bp_msg_f32<true>(u, n2 + (1.f - sc) / 2.f, cst<float>(1 - 1e-12));
+            else
+                return bp_msg_f32<false>(u, n2, cst<float>(1 - 1e-7));
         } else {
             T n = n2;
             if constexpr (MODEL == GNND_QBP) n = n + (T(1) - sc) / T(2);

@@ -23,7 +23,11 @@ run c3_v24_toric5_f32 600 --model v24 --code toric_5 --steps 50
 run c3_v24_toric5_f64 900 --model v24 --code toric_5 --dtype f64 --steps 10 --warmup 2 --cpu-seconds 20
 # config 4: LDPC(648,324) per-GPU shard of the 1M-codeword job (131072 per GPU), CGNNI and BP
 run c4_cgnni_ldpc 600 --code ldpc_648_324 --batch 131072 --steps 50
-run c4_cbp_ldpc 600 --model cbp --code ldpc_648_324 --batch 131072 --steps 20
+run c4_cbp_ldpc 600 --model cbp --code ldpc_648_324 --batch 131072 --steps 50
+# weighted (neural) BP, quantum/neural_BP.py at the reference L = 4 and at L = 5
+run nbp_toric4_f32 600 --model nbp --code toric_4 --steps 50
+run nbp_toric5_f64 600 --model nbp --code toric_5 --dtype f64 --steps 20 --cpu-seconds 5
 # config 5: toric d=7 decoder_v2_4 training step (1 GPU shard)
 run c5_train_v24_toric7 600 --mode train --batch 128 --steps 20 --warmup 3
+run train_nbp_toric4 600 --mode train --model nbp --code toric_4 --batch 128 --steps 20 --warmup 3
 echo "=== configs done"
