@@ -70,6 +70,9 @@ def parse():
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--no-graph', action='store_true',
                    help='train mode: eager steps instead of one captured HIP graph per step')
+    p.add_argument('--layerwise', action='store_true',
+                   help='train mode: the layer-by-layer operator path instead of the fused '
+                        'decoder_v2_4 training kernels')
     p.add_argument('--mode', default='decode', choices=['decode', 'train'],
                    help='train = config 5: decoder_v2_4 (or --model qgnni/nbp/v10) training '
                         'step (DP, RCCL all-reduce)')
@@ -156,6 +159,9 @@ def train_main(a, world, rank, dev):
     H = gd.codes.get_code(code)
     torch.manual_seed(a.seed)
     model = gd.MODELS[model_name](T, H).to(dev).to(dtype)
+    fused = model_name == 'v24' and not a.layerwise
+    if model_name == 'v24':
+        model.fused_train = fused
     lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
                               logical_only=(model_name == 'qgnni')).to(dev)
     tr = gd.train.Trainer(model, lf, graph=not a.no_graph, warmup=2)   # captured after 2 eager steps
@@ -187,7 +193,8 @@ def train_main(a, world, rank, dev):
             'config': {'workload': f'{code} {model_name} training step, T={T}, batch={a.batch}/GPU',
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
                        'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters()),
-                       'hip_graph': not a.no_graph},
+                       'hip_graph': not a.no_graph,
+                       'path': 'fused gnnd_train_fwd/bwd' if fused else 'layer-by-layer propagate ops'},
             'roofline': None, 'cpu_baseline': None}), flush=True)
 
 

@@ -33,6 +33,7 @@ struct GraphView {            // passed by value to kernels
 struct gnnd_graph {
     GraphView view;           // slot plan of the streaming kernel (ties -> smaller R)
     GraphView rview;          // slot plan of the register-resident kernel (ties -> larger R)
+    GraphView pview;          // ties -> R = 2: paired-edge fp32 V24 streaming at small batch
     void* dev;                // single device allocation holding every table
     size_t table_bytes;       // bytes of the four CSR/CSC tables (staged to LDS)
 };
@@ -102,18 +103,6 @@ template <typename T> __device__ __forceinline__ T g_clamp(T x, T lo, T hi) {
 __device__ __forceinline__ double softplus_ref(double x) {
     return x > 20.0 ? x : log1p(exp(x));
 }
-// fp32 fast form on the native v_exp_f32 / v_log_f32 (base 2).  The caller passes
-// hs = h * log2(e) (folded into the layer-1 weights) and folds ln(2) into the layer-2
-// weights:  softplus(h) = ln2 * log2(1 + 2^hs).  The max() restates the threshold
-// branch (for hs > 28 the log term equals hs to within one ulp) and the min() keeps
-// 2^hs finite.  Absolute error vs log1p(exp(h)) <= ~1e-7 (1 + 2^hs rounds to 1 once
-// 2^hs < 2^-24).
-__device__ __forceinline__ float softplus2_fast(float hs) {
-    float e = __builtin_amdgcn_exp2f(fminf(hs, 28.0f));
-    float l = __builtin_amdgcn_logf(1.0f + e);
-    return fmaxf(hs, l);
-}
-
 template <typename T> __device__ __forceinline__ T sigmoid_ref(T x) {
     return T(1) / (T(1) + g_exp(-x));
 }

@@ -440,11 +440,21 @@ template <int MODEL, typename T> struct EdgeMath {
 //          Messages are stored in SLOT order (check-major, lane-contiguous).
 //  step 2  threads = (codeword, variable): S_v = sum of m over the variable's edges in
 //          the reference's index_add order (gathered through vslot).
-template <int MODEL, typename T, int R>
+// Training tape of the streaming kernel (decoder_v2_4, TAPE = true): per iteration and edge
+// (reference edge order) the v->c MLP input ext = S_v - m, the tanh output t and the c->v
+// MLP input u = S_c - t; and the final messages m^T.  Everything gnnd_train_bwd needs.
+template <typename T> struct TapeView {
+    T* ext;   // [iters][B][E]
+    T* u;     // [iters][B][E]
+    T* t;     // [iters][B][E]
+    T* mT;    // [B][E]
+};
+
+template <int MODEL, typename T, int R, bool TAPE = false>
 __global__ void __launch_bounds__(GNND_BLOCK)
 decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
               T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
-              FastDiv dN) {
+              FastDiv dN, TapeView<T> tape) {
     using M = EdgeMath<MODEL, T>;
     constexpr bool BP = ModelTraits<MODEL>::bp;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -534,6 +544,17 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
                     if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
                 }
+                if constexpr (TAPE) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const int e = (int)(sl[r] >> 16);
+                        if (act && e != E) {
+                            const size_t row = ((size_t)it * B + b0 + b) * E + e;
+                            tape.ext[row] = ext[r];
+                            tape.t[row] = tv[r];
+                        }
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     cf[r] = T(0);
@@ -574,6 +595,13 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     cf[r] = valid ? cc : T(0);
                     tsum += tv[r];
                     if constexpr (BP) csum += cf[r];
+                    if constexpr (TAPE) {
+                        if (act && valid) {
+                            const size_t row = ((size_t)it * B + b0 + b) * E + (int)(sv >> 16);
+                            tape.ext[row] = p.s - mv[r];
+                            tape.t[row] = t;
+                        }
+                    }
                 }
             }
             const T Sc = group_sum(tsum, G);
@@ -581,6 +609,13 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
             if constexpr (BP) Sc2 = group_sum(csum, G);
             const T sc = s_xc[b * C + c];
             T mn[R];
+            if constexpr (TAPE) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int e = (int)(sl[r] >> 16);
+                    if (act && e != E) tape.u[((size_t)it * B + b0 + b) * E + e] = Sc - tv[r];
+                }
+            }
             if constexpr (kV24F32) {
 #pragma unroll
                 for (int r = 0; r < R; r += 2) {
@@ -616,6 +651,13 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         __syncthreads();
     }
 
+    if constexpr (TAPE) {
+        for (int f = tid; f < nb * nslot; f += GNND_BLOCK) {
+            const int b = f / nslot, sl = f - b * nslot;
+            const int e = (int)(s_slot[sl] >> 16);
+            if (e != E) tape.mT[(size_t)(b0 + b) * E + e] = s_m[f];
+        }
+    }
     if constexpr (MODEL == GNND_V24) {
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
         if constexpr (kV24F32) {
@@ -664,7 +706,7 @@ template <int MODEL, typename T, int G, int R, int QMAX, bool PAD>
 __global__ void __launch_bounds__(GNND_BLOCK, GNND_RESIDENT_WAVES)
 decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
                        T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem,
-                       FastDiv dV, FastDiv dN) {
+                       FastDiv dV, FastDiv dN, TapeView<T>) {
     using M = EdgeMath<MODEL, T>;
     constexpr bool BP = ModelTraits<MODEL>::bp;
     // fp32 GNN models keep x_v pre-scaled by log2(e) so the v->c pre-op is one FMA into
@@ -850,7 +892,8 @@ struct Plan {
 
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
-int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p) {
+// B = batch of the launch (plan queries without one assume a large batch)
+int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = INT64_MAX) {
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
     const size_t wb = align16((size_t)lds_weights(model) * esz);
     const size_t target = lds_target();
@@ -894,7 +937,11 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p) {
     // streaming layout: weights, slot table, var_ptr, vslot, then [CW][nslot] messages,
     // [CW][V] {S, x}, [CW][C].  fp32 V24 runs its MLPs on slot PAIRS (two edges per packed
     // FMA): it takes the larger-R plan (toric dc = 4: G = 1, R = 4 instead of G = 4, R = 1)
-    const GraphView& g = (model == GNND_V24 && dtype == GNND_F32) ? gr->rview : gr->view;
+    // (small batches: the R = 2 plan puts one edge pair per lane and the most lanes on a
+    // codeword — the training step's latency-bound forward)
+    const bool v24f32 = model == GNND_V24 && dtype == GNND_F32;
+    const GraphView& g = !v24f32 ? gr->view
+                         : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
     const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4);
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
@@ -916,6 +963,9 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p) {
         }
         n = best;
     }
+    // small batches (training steps, latency-bound decodes): at least ~2 workgroups per CU
+    // before grouping codewords (B = 128 -> one codeword per workgroup, 128 workgroups)
+    if ((int64_t)n * 512 > B) n = (size_t)(B / 512 > 1 ? B / 512 : 1);
     p->view = &g;
     p->resident = false;
     p->cw = (int)n;
@@ -926,7 +976,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p) {
 
 template <int MODEL, typename T, int R>
 int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_t B,
-                  int iters, hipStream_t st) {
+                  int iters, hipStream_t st, TapeView<T> tape = {}) {
     const GraphView& g = *p.view;
     int64_t blocks = (B + p.cw - 1) / p.cw;
     if (blocks > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
@@ -938,7 +988,7 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
             GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
         kern<<<(unsigned)blocks, GNND_BLOCK, p.lds, st>>>(g, (const T*)w, nw, (const T*)x, (T*)out,
-                                                          B, iters, p.cw, dI, dV, dN);
+                                                          B, iters, p.cw, dI, dV, dN, tape);
         GNND_LAUNCH_CHECK();
         return GNND_OK;
     };
@@ -970,21 +1020,30 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
             return g.padded ? by_g(std::true_type{}) : by_g(std::false_type{});
         }
     }
+    if constexpr (MODEL == GNND_V24)
+        if (tape.ext) return go(decode_kernel<MODEL, T, R, true>);
     return go(decode_kernel<MODEL, T, R>);
 }
 
 
 template <int MODEL, typename T>
 int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
-                    int iters, hipStream_t st) {
+                    int iters, hipStream_t st, void* tape_base = nullptr) {
     Plan p;
-    int rc = make_plan(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p);
+    int rc = make_plan(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p, B);
     if (rc != GNND_OK) return rc;
+    TapeView<T> tape{};
+    if (tape_base) {                        // [ext | u | t] x [iters][B][E], then mT [B][E]
+        if (p.resident) return GNND_ERR_UNSUPPORTED;
+        const size_t n = (size_t)iters * B * g->view.E;
+        T* base = (T*)tape_base;
+        tape = TapeView<T>{base, base + n, base + 2 * n, base + 3 * n};
+    }
     switch (p.view->R) {
-        case 1: return launch_decode<MODEL, T, 1>(p, w, x, out, B, iters, st);
-        case 2: return launch_decode<MODEL, T, 2>(p, w, x, out, B, iters, st);
-        case 3: return launch_decode<MODEL, T, 3>(p, w, x, out, B, iters, st);
-        case 4: return launch_decode<MODEL, T, 4>(p, w, x, out, B, iters, st);
+        case 1: return launch_decode<MODEL, T, 1>(p, w, x, out, B, iters, st, tape);
+        case 2: return launch_decode<MODEL, T, 2>(p, w, x, out, B, iters, st, tape);
+        case 3: return launch_decode<MODEL, T, 3>(p, w, x, out, B, iters, st, tape);
+        case 4: return launch_decode<MODEL, T, 4>(p, w, x, out, B, iters, st, tape);
     }
     return GNND_ERR_UNSUPPORTED;
 }
@@ -1000,6 +1059,9 @@ int launch_model(const gnnd_graph* g, int dtype, const void* w, const void* x, v
 
 // per-model launchers (one translation unit each, compiled in parallel)
 int gnnd_launch_v24(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+// forward with the training tape (gnnd_train.hip)
+int gnnd_launch_v24_tape(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int,
+                         void*, hipStream_t);
 int gnnd_launch_qgnni(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_qbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_cgnni(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

@@ -5,3 +5,9 @@ int gnnd_launch_v24(const gnnd_graph* g, int dtype, const void* w, const void* x
                        int64_t B, int iters, hipStream_t st) {
     return launch_model<GNND_V24>(g, dtype, w, x, out, B, iters, st);
 }
+
+int gnnd_launch_v24_tape(const gnnd_graph* g, int dtype, const void* w, const void* x, void* out,
+                         int64_t B, int iters, void* tape, hipStream_t st) {
+    if (dtype == GNND_F32) return launch_decode_r<GNND_V24, float>(g, w, x, out, B, iters, st, tape);
+    return launch_decode_r<GNND_V24, double>(g, w, x, out, B, iters, st, tape);
+}

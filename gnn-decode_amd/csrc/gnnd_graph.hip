@@ -76,7 +76,9 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         std::vector<uint32_t> slot, slot_ve;
         std::vector<int> vslot;
     };
-    auto build_plan = [&](bool prefer_large_r, SlotPlan& sp) -> bool {
+    // tie preference: 0 = smaller R, 1 = larger R, 2 = R = 2 (the paired-edge fp32 V24
+    // path at small batches: one edge pair per lane, most lanes per codeword)
+    auto build_plan = [&](int pref, SlotPlan& sp) -> bool {
         long best = -1;
         for (int R = 1; R <= 4; ++R) {
             int need = (max_dc + R - 1) / R, G = 1;
@@ -84,7 +86,8 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             if (G > 64) continue;
             long slots = (long)C * G * R;
             if (force_r == R) { best = slots; sp.G = G; sp.R = R; break; }
-            if (best < 0 || slots < best || (prefer_large_r && slots == best)) {
+            const bool tie_wins = pref == 1 || (pref == 2 && R == 2);
+            if (best < 0 || slots < best || (tie_wins && slots == best)) {
                 best = slots; sp.G = G; sp.R = R;
             }
         }
@@ -106,8 +109,9 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         }
         return true;
     };
-    SlotPlan plans[2];
-    if (!build_plan(false, plans[0]) || !build_plan(true, plans[1])) return GNND_ERR_UNSUPPORTED;
+    SlotPlan plans[3];
+    for (int i = 0; i < 3; ++i)
+        if (!build_plan(i, plans[i])) return GNND_ERR_UNSUPPORTED;
 
     std::vector<int> vord(V);
     for (int v = 0; v < V; ++v) vord[v] = v;
@@ -116,9 +120,9 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     });
 
     const int nints = graph_table_ints(V, C, E);
-    int plan_off[2];
+    int plan_off[3];
     int off = nints;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         plan_off[i] = off;
         off += 2 * (int)plans[i].slot.size() + E;
     }
@@ -128,7 +132,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
     memcpy(table.data() + E + V + 1 + C + 1, cedge.data(), sizeof(int) * E);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         const int ns = (int)plans[i].slot.size();
         memcpy(table.data() + plan_off[i], plans[i].slot.data(), sizeof(int) * ns);
         memcpy(table.data() + plan_off[i] + ns, plans[i].vslot.data(), sizeof(int) * E);
@@ -157,8 +161,9 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     gv.chk_edge = d + E + V + 1 + C + 1;
     gv.var_ord = (const uint2*)(d + ord_off);
     g->rview = gv;
-    for (int i = 0; i < 2; ++i) {
-        GraphView& pv = i == 0 ? g->view : g->rview;
+    g->pview = gv;
+    for (int i = 0; i < 3; ++i) {
+        GraphView& pv = i == 0 ? g->view : i == 1 ? g->rview : g->pview;
         const int ns = (int)plans[i].slot.size();
         pv.G = plans[i].G; pv.R = plans[i].R;
         pv.padded = plans[i].padded;

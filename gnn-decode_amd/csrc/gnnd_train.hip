@@ -1,0 +1,368 @@
+// gnnd_train.hip — fused training step of decoder_v2_4.
+//
+// Forward: the streaming decode kernel with its TAPE instantiation (gnnd_decode_impl.h) runs
+// GNNI.forward (quantum/decoder_v2_4.py:272-294) and records, per iteration and edge, the
+// v->c MLP input ext = S_v - m, the tanh output t and the c->v MLP input u = S_c - t, plus
+// the final messages m^T.  The loss (quantum/decoder_v2_4.py:297-317) stays in torch.
+// Backward (this file): reverse-mode through the whole T-iteration loop in ONE launch, one
+// workgroup per codeword tile, replacing the reference's autograd graph of ~60 small ops
+// per iteration:
+//   readout  dr_v = -(g_v (1 - p_v)) p_v,  MLP_o backward at m^T  -> dm
+//   t = T-1 .. 0:
+//     A  MLP_c backward at u with dy = dm s_c                      -> du, grads ggc2.mlp
+//     B  dt = LOO_c(du), da = (dt (1 - t^2)) / 2                   (check leave-one-out)
+//     C  MLP_v backward at (ext, x_v) with dy = da                  -> dext, grads ggc1.mlp
+//     D  dm += LOO_v(dext)                                         (residual keeps dm)
+// The MLP phases are UNIT-parallel: a wave walks its share of the tile's edges while each
+// lane owns two of the 128 hidden units (weights in VGPRs), so every weight gradient
+// accumulates in the lane's registers over all edges and iterations with no cross-lane
+// traffic; only d(input) of an edge needs a wave reduction (DPP + two swizzles).  The
+// edge phases B/D are edge-parallel leave-one-out sums in LDS.  Per-workgroup gradient
+// partials are summed over the workgroups in a fixed order by a second kernel
+// (deterministic, run-to-run identical).
+// torch's autograd rules are followed: Softplus(beta 1, threshold 20) backward
+// g z / (z + 1), z = e^h (g above the threshold), tanh backward g (1 - t^2), division by 2.
+#include "gnnd_decode_impl.h"
+#include <type_traits>
+
+namespace {
+
+// threads per workgroup: 16 waves (4 per SIMD) in fp32 (88 VGPRs), 8 in fp64 (187 VGPRs)
+template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
+constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
+
+// softplus and its derivative at h (natural units)
+__device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg) {
+    if (h > 20.0) { sp = h; sg = 1.0; return; }
+    const double z = exp(h);
+    sp = log1p(z);
+    sg = z / (z + 1.0);
+}
+__device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg) {
+    if (h > 20.f) { sp = h; sg = 1.f; return; }
+    const float z = __builtin_amdgcn_exp2f(h * kLog2e);
+    const float z1 = 1.f + z;
+    sp = kLn2 * __builtin_amdgcn_logf(z1);
+    sg = z * __builtin_amdgcn_rcpf(z1);
+}
+
+__device__ __forceinline__ float wave_sum(float v) { return group_sum_c<64>(v); }
+__device__ __forceinline__ double wave_sum(double v) { return group_sum(v, 64); }
+
+// two hidden units of one MLP owned by this lane: k0 = lane, k1 = lane + 64
+template <typename T> struct Units {
+    T w1a[2], w1b[2], b1[2], w2[2];         // w1b only for the 2-input MLP
+    T gw1a[2], gw1b[2], gb1[2], gw2[2], gb2;
+    __device__ void load1(const T* __restrict__ w, int lane) {    // {W1, b1, W2, b2}
+        for (int j = 0; j < 2; ++j) {
+            const int k = lane + 64 * j;
+            w1a[j] = w[k]; w1b[j] = T(0); b1[j] = w[128 + k]; w2[j] = w[256 + k];
+            gw1a[j] = gw1b[j] = gb1[j] = gw2[j] = T(0);
+        }
+        gb2 = T(0);
+    }
+    __device__ void load2(const T* __restrict__ w, int lane) {    // {W1a, W1b, b1, W2, b2}
+        for (int j = 0; j < 2; ++j) {
+            const int k = lane + 64 * j;
+            w1a[j] = w[k]; w1b[j] = w[128 + k]; b1[j] = w[256 + k]; w2[j] = w[384 + k];
+            gw1a[j] = gw1b[j] = gb1[j] = gw2[j] = T(0);
+        }
+        gb2 = T(0);
+    }
+    // backward of y = sum_k W2_k sp(W1a_k u0 (+ W1b_k u1) + b1_k) + b2 for upstream dy;
+    // returns d y / d u0 (wave-reduced, uniform)
+    template <bool TWO>
+    __device__ __forceinline__ T bwd(T u0, T u1, T dy) {
+        T part = T(0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            T h = u0 * w1a[j];
+            if constexpr (TWO) h = h + u1 * w1b[j];
+            h = h + b1[j];
+            T sp, sg;
+            sp_and_grad(h, sp, sg);
+            gw2[j] += dy * sp;
+            const T dh = (dy * w2[j]) * sg;
+            gw1a[j] += dh * u0;
+            if constexpr (TWO) gw1b[j] += dh * u1;
+            gb1[j] += dh;
+            part += dh * w1a[j];
+        }
+        gb2 += dy;
+        return wave_sum(part);
+    }
+    // two edges at once (independent chains for the scheduler); an edge with dy = 0
+    // contributes nothing (masked tail)
+    template <bool TWO>
+    __device__ __forceinline__ void bwd2(T xa0, T xa1, T dya, T xb0, T xb1, T dyb, T& ra, T& rb) {
+        T pa = T(0), pb = T(0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            T ha = xa0 * w1a[j], hb = xb0 * w1a[j];
+            if constexpr (TWO) { ha = ha + xa1 * w1b[j]; hb = hb + xb1 * w1b[j]; }
+            ha = ha + b1[j];
+            hb = hb + b1[j];
+            T spa, sga, spb, sgb;
+            sp_and_grad(ha, spa, sga);
+            sp_and_grad(hb, spb, sgb);
+            gw2[j] += dya * spa;
+            gw2[j] += dyb * spb;
+            const T dha = (dya * w2[j]) * sga, dhb = (dyb * w2[j]) * sgb;
+            gw1a[j] += dha * xa0;
+            gw1a[j] += dhb * xb0;
+            if constexpr (TWO) { gw1b[j] += dha * xa1; gw1b[j] += dhb * xb1; }
+            gb1[j] += dha;
+            gb1[j] += dhb;
+            pa += dha * w1a[j];
+            pb += dhb * w1a[j];
+        }
+        gb2 += dya;
+        gb2 += dyb;
+        ra = wave_sum(pa);
+        rb = wave_sum(pb);
+    }
+    // add this wave's gradients into the workgroup accumulator (packed plain layout)
+    template <bool TWO>
+    __device__ void flush(T* acc, int lane) const {
+        for (int j = 0; j < 2; ++j) {
+            const int k = lane + 64 * j;
+            if constexpr (TWO) {
+                acc[k] += gw1a[j]; acc[128 + k] += gw1b[j]; acc[256 + k] += gb1[j]; acc[384 + k] += gw2[j];
+            } else {
+                acc[k] += gw1a[j]; acc[128 + k] += gb1[j]; acc[256 + k] += gw2[j];
+            }
+        }
+        if (lane == 0) acc[TWO ? 512 : 384] += gb2;
+    }
+};
+
+template <typename T, int kTrainThreads = train_threads<T>()>
+__global__ void __launch_bounds__(kTrainThreads)
+v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
+               const T* __restrict__ p, const T* __restrict__ gp, TapeView<T> tape,
+               T* __restrict__ gpart, int64_t B, int iters, int CW) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int V = g.V, C = g.C, E = g.E, N = g.N;
+    constexpr int kTrainWaves = kTrainThreads / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int* s_tab = (int*)smem;
+    const int nints = graph_table_ints(V, C, E);
+    const uint32_t* s_evc = (const uint32_t*)s_tab;
+    const int* s_vptr = s_tab + E;
+    const int* s_cptr = s_vptr + V + 1;
+    const int* s_cedge = s_cptr + C + 1;
+    size_t off = ((size_t)nints * 4 + 15) & ~(size_t)15;
+    const size_t TE = (size_t)CW * E;
+    T* s_dm = (T*)(smem + off);              // [CW][E] d loss / d m (current iteration)
+    T* s_g = s_dm + TE;                      // [CW][E] du, then dext
+    T* s_da = s_g + TE;                      // [CW][E] d a
+    T* s_u = s_da + TE;                      // [CW][E] tape of the iteration: u, t, ext
+    T* s_t = s_u + TE;
+    T* s_ext = s_t + TE;
+    T* s_x = s_ext + TE;                     // [CW][N] node features
+    T* s_acc = s_x + (size_t)CW * N;         // [1283] workgroup gradient accumulator
+
+    const int* gtab = (const int*)g.edge_vc;
+    for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
+    for (int i = tid; i < kV24W; i += kTrainThreads) s_acc[i] = T(0);
+    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
+    const int nE = nb * E;
+    for (int i = tid; i < nb * N; i += kTrainThreads) s_x[i] = x[(size_t)b0 * N + i];
+    // readout inputs: m^T into s_u, d loss / d r per edge into s_da
+    for (int f = tid; f < nE; f += kTrainThreads) {
+        const int b = f / E, e = f - b * E;
+        const size_t bv = (size_t)(b0 + b) * V + (int)(s_evc[e] & 0xffffu);
+        const T pv = p[bv];
+        s_u[f] = tape.mT[(size_t)b0 * E + f];
+        s_da[f] = -((gp[bv] * (T(1) - pv)) * pv);     // p = sigmoid(-r)
+    }
+
+    Units<T> uv, uc, uo;                     // ggc1.mlp, ggc2.mlp, mlp
+    uv.load2(w + kV24Ggc1, lane);
+    uc.load1(w + kV24Ggc2, lane);
+    uo.load1(w + kV24Mlp, lane);
+    __syncthreads();
+
+    // unit-parallel pass over the tile's edges, two per wave step:
+    // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
+    auto unit_pass = [&](auto& U, auto two_tag, const T* in0, auto in1_of, auto dy_of, T* outp) {
+        constexpr bool TWO = decltype(two_tag)::value;
+        for (int f = wave; f < nE; f += 2 * kTrainWaves) {
+            const int f2 = f + kTrainWaves;
+            const bool has2 = f2 < nE;
+            const int fb = has2 ? f2 : f;
+            T ra, rb;
+            U.template bwd2<TWO>(in0[f], in1_of(f), dy_of(f), in0[fb], in1_of(fb),
+                                 has2 ? dy_of(fb) : T(0), ra, rb);
+            if (lane == 0) {
+                outp[f] = ra;
+                if (has2) outp[f2] = rb;
+            }
+        }
+    };
+    auto zero = [](int) { return T(0); };
+
+    // readout: r_v = sum_e MLP_o(m^T_e) + x_v  ->  dm
+    unit_pass(uo, std::false_type{}, s_u, zero, [&](int f) { return s_da[f]; }, s_dm);
+    __syncthreads();
+
+    for (int it = iters - 1; it >= 0; --it) {
+        const size_t trow = ((size_t)it * B + b0) * E;
+        for (int f = tid; f < nE; f += kTrainThreads) {
+            s_u[f] = tape.u[trow + f];
+            s_t[f] = tape.t[trow + f];
+            s_ext[f] = tape.ext[trow + f];
+        }
+        __syncthreads();
+        // A: m^{t+1} = MLP_c(u) s_c + m^t
+        unit_pass(uc, std::false_type{}, s_u, zero, [&](int f) {
+            const int b = f / E, e = f - b * E;
+            return s_dm[f] * s_x[b * N + V + (int)(s_evc[e] >> 16)];
+        }, s_g);
+        __syncthreads();
+        // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
+        for (int f = tid; f < nE; f += kTrainThreads) {
+            const int b = f / E, e = f - b * E;
+            const int c = (int)(s_evc[e] >> 16);
+            const T* gb = s_g + (size_t)b * E;
+            T s = T(0);
+            for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += gb[s_cedge[k]];
+            const T t = s_t[f];
+            s_da[f] = ((s - s_g[f]) * (T(1) - t * t)) / T(2);
+        }
+        __syncthreads();
+        // C: a = MLP_v(ext, x_v)
+        unit_pass(uv, std::true_type{}, s_ext, [&](int f) {
+            const int b = f / E, e = f - b * E;
+            return s_x[b * N + (int)(s_evc[e] & 0xffffu)];
+        }, [&](int f) { return s_da[f]; }, s_g);
+        __syncthreads();
+        // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
+        for (int f = tid; f < nE; f += kTrainThreads) {
+            const int b = f / E, e = f - b * E;
+            const int v = (int)(s_evc[e] & 0xffffu);
+            const T* gb = s_g + (size_t)b * E;
+            T s = T(0);
+            for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += gb[k];
+            s_dm[f] += s - s_g[f];
+        }
+        __syncthreads();
+    }
+
+    // workgroup gradient: waves add in order (deterministic), then one row per workgroup
+    for (int wv = 0; wv < kTrainWaves; ++wv) {
+        if (wave == wv) {
+            uv.template flush<true>(s_acc + kV24Ggc1, lane);
+            uc.template flush<false>(s_acc + kV24Ggc2, lane);
+            uo.template flush<false>(s_acc + kV24Mlp, lane);
+        }
+        __syncthreads();
+    }
+    T* row = gpart + (size_t)blockIdx.x * kV24W;
+    for (int i = tid; i < kV24W; i += kTrainThreads) row[i] = s_acc[i];
+}
+
+// sum of the per-workgroup rows, fixed order (8 interleaved partial chains, then combined)
+template <typename T>
+__global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __restrict__ gw) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kV24W) return;
+    T s[8] = {};
+    int r = 0;
+    for (; r + 8 <= rows; r += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += gpart[(size_t)(r + j) * kV24W + i];
+    for (int j = 0; r < rows; ++r, ++j) s[j] += gpart[(size_t)r * kV24W + i];
+    gw[i] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+int train_tile(const gnnd_graph* g, int64_t B) {
+    (void)g;
+    // one codeword per workgroup up to 1024 codewords (>= 4 workgroups per CU's worth of
+    // waves at 8 waves each); larger batches group codewords to bound the partial rows
+    return B <= 1024 ? 1 : (int)((B + 1023) / 1024);
+}
+size_t train_lds(const gnnd_graph* g, int esz, int cw) {
+    const GraphView& v = g->view;
+    return (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
+           (size_t)esz * (6 * (size_t)cw * v.E + (size_t)cw * v.N + kV24W);
+}
+
+template <typename T>
+int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* out,
+               const void* gout, const void* tape, void* gw, void* ws, int64_t ws_bytes,
+               int64_t B, int iters, hipStream_t st) {
+    const int cw = train_tile(g, B);
+    const int64_t blocks = (B + cw - 1) / cw;
+    if ((int64_t)blocks * kV24W * (int64_t)sizeof(T) > ws_bytes) return GNND_ERR_INVALID_ARG;
+    const size_t lds = train_lds(g, sizeof(T), cw);
+    if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
+    auto kern = v24_bwd_kernel<T>;
+    if (lds > 64 * 1024)
+        GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const size_t n = (size_t)iters * B * g->view.E;
+    T* base = (T*)tape;
+    TapeView<T> tv{base, base + n, base + 2 * n, base + 3 * n};
+    kern<<<(unsigned)blocks, train_threads<T>(), lds, st>>>(g->view, (const T*)w, (const T*)x,
+                                                      (const T*)out, (const T*)gout, tv, (T*)ws,
+                                                      B, iters, cw);
+    GNND_LAUNCH_CHECK();
+    grad_reduce_kernel<T><<<(kV24W + 255) / 256, 256, 0, st>>>((const T*)ws, (int)blocks, (T*)gw);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
+bool train_args_ok(const gnnd_graph* g, int model, int dtype, int64_t B, int32_t iters) {
+    return g && model == GNND_V24 && (dtype == GNND_F32 || dtype == GNND_F64) && B >= 0 &&
+           iters >= 0;
+}
+
+}  // namespace
+
+extern "C" int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, int64_t batch,
+                                     int32_t iters, int64_t* h_bytes) {
+    if (!train_args_ok(g, model, dtype, batch, iters) || !h_bytes) return GNND_ERR_INVALID_ARG;
+    const int64_t esz = dtype == GNND_F64 ? 8 : 4;
+    *h_bytes = esz * batch * g->view.E * (3 * (int64_t)iters + 1);
+    return GNND_OK;
+}
+
+extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const void* d_w,
+                              const void* d_x, void* d_out, void* d_tape, int64_t batch,
+                              int32_t iters, void* stream) {
+    if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
+    if (batch == 0) return GNND_OK;
+    if (!d_w || !d_x || !d_out || !d_tape) return GNND_ERR_INVALID_ARG;
+    return gnnd_launch_v24_tape(g, dtype, d_w, d_x, d_out, batch, iters, d_tape,
+                                (hipStream_t)stream);
+}
+
+extern "C" int gnnd_train_bwd_workspace(const gnnd_graph* g, int model, int dtype,
+                                        int64_t batch, int64_t* h_bytes) {
+    if (!train_args_ok(g, model, dtype, batch, 0) || !h_bytes) return GNND_ERR_INVALID_ARG;
+    const int cw = train_tile(g, batch);
+    *h_bytes = ((batch + cw - 1) / cw) * (int64_t)kV24W * (dtype == GNND_F64 ? 8 : 4);
+    return GNND_OK;
+}
+
+extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const void* d_w,
+                              const void* d_x, const void* d_out, const void* d_grad_out,
+                              const void* d_tape, void* d_grad_w, void* d_workspace,
+                              int64_t workspace_bytes, int64_t batch, int32_t iters,
+                              void* stream) {
+    if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
+    if (!d_w || !d_grad_w) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (batch == 0) {
+        GNND_HIP_CHECK(hipMemsetAsync(d_grad_w, 0, (size_t)kV24W * (dtype == GNND_F64 ? 8 : 4), st));
+        return GNND_OK;
+    }
+    if (!d_x || !d_out || !d_grad_out || !d_tape || !d_workspace) return GNND_ERR_INVALID_ARG;
+    if (dtype == GNND_F32)
+        return launch_bwd<float>(g, d_w, d_x, d_out, d_grad_out, d_tape, d_grad_w, d_workspace,
+                                 workspace_bytes, batch, iters, st);
+    return launch_bwd<double>(g, d_w, d_x, d_out, d_grad_out, d_tape, d_grad_w, d_workspace,
+                              workspace_bytes, batch, iters, st);
+}

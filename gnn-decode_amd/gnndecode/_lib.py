@@ -47,6 +47,11 @@ SIGNATURES = {
     'gnnd_decode': (_int, [_vp, _int, _int, _vp, _vp, _vp, _i64, _i32, _vp]),
     'gnnd_decode_tile': (_int, [_vp, _int, _int, _c_i32p, _c_i32p]),
     'gnnd_decode_plan': (_int, [_vp, _int, _int, _c_i32p]),
+    'gnnd_train_tape_bytes': (_int, [_vp, _int, _int, _i64, _i32, _c_i64p]),
+    'gnnd_train_fwd': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _i64, _i32, _vp]),
+    'gnnd_train_bwd_workspace': (_int, [_vp, _int, _int, _i64, _c_i64p]),
+    'gnnd_train_bwd': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32,
+                              _vp]),
     'gnnd_status_string': (ctypes.c_char_p, [_int]),
     'gnnd_last_hip_error': (_int, []),
     'gnnd_version': (_int, []),

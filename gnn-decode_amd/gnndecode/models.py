@@ -301,8 +301,26 @@ class _Decoder(torch.nn.Module):
 
 
 class DecoderV24(_Decoder):
-    """quantum/decoder_v2_4.py:260-294 (T = Nc = 15 in the reference)."""
+    """quantum/decoder_v2_4.py:260-294 (T = Nc = 15 in the reference).
+
+    Training (grad enabled, tiled batch) runs the fused HIP step (ops.FusedTrainFn:
+    gnnd_train_fwd + gnnd_train_bwd, two launches per step) unless `fused_train` is False,
+    which selects the reference's layer-by-layer loop on the propagate kernels."""
     kind = 'v24'
+    fused_train = True
+
+    def forward(self, data):
+        x, edge_index = data.x, data.edge_index
+        if x.dim() == 1:
+            x = x.unsqueeze(1)
+        if (self.fused_train and x.is_cuda and torch.is_grad_enabled() and self.training
+                and any(p.requires_grad for p in self.parameters())
+                and x.dtype in (torch.float32, torch.float64)):
+            g = self.graph(x.device)
+            if (x.numel() % g.N == 0 and edge_index.size(1) == (x.numel() // g.N) * g.E
+                    and g.is_tiled(edge_index, 0)):
+                return ops.FusedTrainFn.apply(self.packed_weights(), x, g, self.kind, self.Nc)
+        return super().forward(data)
 
     def __init__(self, Nc, H):
         super().__init__(Nc, H)

@@ -196,3 +196,56 @@ def decode_tile(graph, model, dtype):
     _lib.call('gnnd_decode_tile', graph.handle, _lib.VARIANT[model], dtype_code(dtype),
               ctypes.byref(cw), ctypes.byref(lds))
     return cw.value, lds.value
+
+
+# ---------------------------------------------------------------------------------------
+# fused training step (decoder_v2_4): forward with tape + one-launch reverse pass
+# ---------------------------------------------------------------------------------------
+def train_forward(graph, model, x, prepared_weights, iters):
+    """gnnd_train_fwd: the fused decode plus the training tape.  Returns (out, tape)."""
+    _require_gpu(x, prepared_weights)
+    x = x.contiguous()
+    B = x.numel() // graph.N
+    dt = dtype_code(x.dtype)
+    nb = ctypes.c_int64()
+    _lib.call('gnnd_train_tape_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
+              ctypes.byref(nb))
+    tape = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
+    out = torch.empty(B * graph.V, 1, dtype=x.dtype, device=x.device)
+    _lib.call('gnnd_train_fwd', graph.handle, _lib.VARIANT[model], dt, _ptr(prepared_weights),
+              _ptr(x), _ptr(out), _ptr(tape), B, int(iters), current_stream(x.device))
+    return out, tape
+
+
+def train_backward(graph, model, plain_weights, x, out, grad_out, tape, iters):
+    """gnnd_train_bwd: d loss / d (plain packed weights) from d loss / d out."""
+    B = x.numel() // graph.N
+    dt = dtype_code(x.dtype)
+    nb = ctypes.c_int64()
+    _lib.call('gnnd_train_bwd_workspace', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
+    gw = torch.empty_like(plain_weights)
+    grad_out = grad_out.contiguous()
+    _lib.call('gnnd_train_bwd', graph.handle, _lib.VARIANT[model], dt, _ptr(plain_weights), _ptr(x),
+              _ptr(out), _ptr(grad_out), _ptr(tape), _ptr(gw), _ptr(ws), nb.value, B, int(iters),
+              current_stream(x.device))
+    return gw
+
+
+class FusedTrainFn(torch.autograd.Function):
+    """out = decode(weights, x) with a one-launch HIP backward to the packed weights."""
+
+    @staticmethod
+    def forward(ctx, flat_w, x, graph, model, iters):
+        w = flat_w.detach().to(x.dtype).contiguous()
+        out, tape = train_forward(graph, model, x, prepare_weights(model, w), iters)
+        ctx.save_for_backward(w, x, out, tape)
+        ctx.args = (graph, model, iters, flat_w.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        w, x, out, tape = ctx.saved_tensors
+        graph, model, iters, wdt = ctx.args
+        gw = train_backward(graph, model, w, x, out, grad_out.to(x.dtype), tape, iters)
+        return gw.to(wdt), None, None, None, None

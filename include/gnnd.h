@@ -167,6 +167,27 @@ int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32_t* h_cw_pe
  * [3] work items per lane (resident kernel; 0 otherwise). */
 int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan);
 
+/* ---- fused training step (decoder_v2_4) ------------------
+ * gnnd_train_fwd = gnnd_decode (same prepared weights, same output) that also writes the
+ * training tape (gnnd_train_tape_bytes bytes of d_tape): per iteration and edge the
+ * v->c MLP input, the tanh output and the c->v MLP input, plus the final messages.
+ * gnnd_train_bwd turns d loss / d out [B*V] into d loss / d weights [1283] in the PLAIN
+ * packed layout of gnnd_weights_count (d_w is that plain layout, not the prepared one):
+ * reverse mode through all T iterations and the readout in one launch (+ a fixed-order
+ * reduction of per-workgroup partials in d_workspace, gnnd_train_bwd_workspace bytes).
+ * Only model V24 (quantum/decoder_v2_4.py:260-294); the other models train through
+ * gnnd_propagate_*_bwd.                                                                 */
+int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, int64_t batch,
+                          int32_t iters, int64_t* h_bytes);
+int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
+                   void* d_out, void* d_tape, int64_t batch, int32_t iters, void* stream);
+int gnnd_train_bwd_workspace(const gnnd_graph* g, int model, int dtype, int64_t batch,
+                             int64_t* h_bytes);
+int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
+                   const void* d_out, const void* d_grad_out, const void* d_tape,
+                   void* d_grad_w, void* d_workspace, int64_t workspace_bytes, int64_t batch,
+                   int32_t iters, void* stream);
+
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gnnd_status_string(int status);
 int gnnd_last_hip_error(void);          /* hipError_t of the last GNND_ERR_HIP, per thread */

@@ -90,6 +90,11 @@ def test_null_argument_checks():
     assert lib.gnnd_graph_destroy(None) == _lib.ERR_INVALID_ARG
     assert lib.gnnd_graph_dims(None, None) == _lib.ERR_INVALID_ARG
     assert lib.gnnd_decode(None, 0, 0, None, None, None, 1, 1, None) == _lib.ERR_INVALID_ARG
+    b0 = ctypes.c_int64()
+    assert lib.gnnd_train_tape_bytes(None, 0, 0, 1, 1, ctypes.byref(b0)) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_train_fwd(None, 0, 0, None, None, None, None, 1, 1, None) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_train_bwd(None, 0, 0, None, None, None, None, None, None, None, 0, 1, 1,
+                              None) == _lib.ERR_INVALID_ARG
     assert lib.gnnd_propagate_tiled(None, 0, 0, 0, 0, None, None, None, 1, None) == _lib.ERR_INVALID_ARG
     cw, lds = ctypes.c_int32(), ctypes.c_int32()
     assert lib.gnnd_decode_tile(None, 0, 0, ctypes.byref(cw), ctypes.byref(lds)) == _lib.ERR_INVALID_ARG

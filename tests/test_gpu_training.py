@@ -37,9 +37,18 @@ def _setup(golden, fx, model, code, kind):
     return z, m, loss_fn, gd.data.make_batch(x, m.graph(x.device)), y
 
 
-@pytest.mark.parametrize('fx,model,code,kind', CASES, ids=[c[0] for c in CASES])
-def test_training_step_gradients_match_reference(golden, fx, model, code, kind):
+def _cases_with_path():
+    for c in CASES:
+        yield pytest.param(*c, True, id=c[0])
+        if c[1] == 'v24':    # decoder_v2_4 also through the layer-by-layer operator path
+            yield pytest.param(*c, False, id=c[0] + '-layerwise')
+
+
+@pytest.mark.parametrize('fx,model,code,kind,fused', list(_cases_with_path()))
+def test_training_step_gradients_match_reference(golden, fx, model, code, kind, fused):
     z, m, loss_fn, data, y = _setup(golden, fx, model, code, kind)
+    if model == 'v24':
+        m.fused_train = fused
     pred = m(data)
     assert pred.requires_grad, 'training forward must build an autograd graph'
     loss = loss_fn(pred, y)
@@ -87,6 +96,38 @@ def test_propagate_backward_generic_and_tiled_match_autograd_restatement(golden)
                                        rtol=1e-12, atol=1e-12)
             np.testing.assert_allclose(m1.grad.cpu().numpy(), m0.grad.cpu().numpy(),
                                        rtol=1e-11, atol=1e-12)
+
+
+@pytest.mark.parametrize('fx,L', [('train_v24_L5', 5), ('train_v24_L7', 7)])
+def test_fused_training_step_matches_layerwise_fp32(golden, fx, L):
+    """fp32: the fused HIP training step (gnnd_train_fwd/bwd) and the layer-by-layer
+    operator path give the same loss and gradients (different fp32 rounding orders)."""
+    grads = []
+    for fused in (True, False):
+        z, m, loss_fn, data, y = _setup(golden, fx, 'v24', ('toric', L), 'syndrome')
+        m = m.float()
+        m.fused_train = fused
+        data.x = data.x.float()
+        pred = m(data)
+        loss = loss_fn(pred, y.float())
+        loss.backward()
+        grads.append((loss.item(), {n: p.grad.detach().double().cpu().numpy()
+                                    for n, p in m.named_parameters()}))
+    (la, ga), (lb, gb) = grads
+    assert abs(la - lb) <= 1e-4 * abs(lb)
+    for n in gb:
+        scale = max(np.abs(gb[n]).max(), 1e-30)
+        assert np.abs(ga[n] - gb[n]).max() <= 2e-3 * scale, n
+
+
+def test_fused_training_step_is_deterministic(golden):
+    z, m, loss_fn, data, y = _setup(golden, 'train_v24_L7', 'v24', ('toric', 7), 'syndrome')
+    out = []
+    for _ in range(2):
+        m.zero_grad()
+        loss_fn(m(data), y).backward()
+        out.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]).clone())
+    assert torch.equal(out[0], out[1])
 
 
 def test_data_parallel_step_on_one_gpu_matches_plain_step(golden):
