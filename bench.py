@@ -118,10 +118,15 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
     # fp32 classical BP is ill-conditioned near its clamps: also decode the first chunks in
     # fp64 and count how often EACH fp32 implementation (GPU, numpy oracle) disagrees with it
     cond = model == 'cbp' and x_dev.dtype == torch.float32
+    # the quantum scripts compute in fp64: their oracle (the reference's arithmetic) runs in
+    # fp64 whatever the GPU dtype
+    ref_dt = np.float64 if model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10') else None
     done, t_total, max_err, mism = 0, 0.0, 0.0, 0
     c_bits = c_gpu = c_orc = 0
     while t_total < seconds and done + chunk <= x_all.size(0):
         xs = x_all[done:done + chunk].cpu().numpy().reshape(-1, 1)
+        if ref_dt is not None:
+            xs = xs.astype(ref_dt)
         t0 = time.perf_counter()
         ref = gnn_oracle.decode(model, H, xs, T, w)
         t_total += time.perf_counter() - t0
@@ -140,7 +145,8 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
     res = {'value': done / t_total if t_total > 0 else None, 'unit': 'codewords/s',
            'cores': 1, 'kind': 'port',
            'sample': f'{done} codewords of the same batch (chunks of {chunk}), oracle/gnn_oracle.py '
-                     f'numpy restatement, 1 thread, {t_total:.1f} s',
+                     f'numpy restatement ({"fp64" if ref_dt is not None else str(x_dev.dtype)[6:]}), '
+                     f'1 thread, {t_total:.1f} s',
            'parity_max_abs_err': max_err, 'parity_hard_decision_mismatches': mism,
            'parity_bits_compared': done * g.V}
     if cond:

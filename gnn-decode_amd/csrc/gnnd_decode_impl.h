@@ -51,27 +51,37 @@ template <int MODEL> struct ModelTraits {
 //   p = clamp(exp(Lambda) cos(pi n), +-(1 - 1e-15)), out = log(1 + p) - log(1 - p).
 // fp64: literally.  fp32 cannot represent the clamp (1 - 1e-15 rounds to 1, and tanh
 // saturates at |a| ~ 17 where fp64 keeps resolving 1 - t down to 1e-16): the fp32 form
-// evaluates the same function through the small quantities instead,
-//   L = log tanh(|a|/2) = log1p(-e) - log1p(e), e = exp(-|a|)  (|a| >= 1; tanhf below),
-//   1 - |p| = -expm1(Lambda) clamped at 1 - fl64(1 - 1e-15), 1 + |p| = 1 + exp(Lambda),
-// so messages track the fp64 reference instead of saturating at log(2^25).
+// evaluates the same function through the small quantities instead (base-2 log domain,
+// native transcendentals):  log2 tanh(|a|/2) via -2 atanh(e)/ln2, e = exp(-|a|), for
+// small e;  1 - |p| = -expm1(Lambda) clamped at 1 - fl64(1 - 1e-15);  so messages track
+// the fp64 reference instead of saturating at log(2^25).
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ double wbp_L(double a, double& c) {
     const double t = tanh(a / 2.0);
     c = t < 0.0 ? 1.0 : 0.0;
     return log(g_clamp(fabs(t), 1e-20, 1e10));
 }
+// fp32: BASE-2 log magnitude log2|tanh(a/2)| on the native v_exp/v_log/v_rcp, resolving
+// 1 - |t| down to fp32's range (fp64 resolves it down to 1e-16; fp32 tanh itself would
+// round to 1 from |a| ~ 17):  z = |a|/2 < 0.3: odd Taylor polynomial of tanh (5e-8 rel);
+// e = exp(-|a|) >= 1/16: log2((1 - e) / (1 + e)) (1 - e >= 0.45: ~2 ulp);
+// e < 1/16: -2 atanh(e) / ln2 by its series to e^7 (~1e-9 relative to the result).
 __device__ __forceinline__ float wbp_L(float a, float& c) {
     c = a < 0.f ? 1.f : 0.f;                  // tanh(a/2) < 0 exactly when a < 0
-    const float y = fabsf(a);
-    float L;
-    if (y < 1.f) {
-        L = logf(fmaxf(tanhf(0.5f * y), 1e-20f));
-    } else {
-        const float e = expf(-y);
-        L = log1pf(-e) - log1pf(e);
-    }
-    return L;
+    const float y = fabsf(a), z = 0.5f * y, z2 = z * z;
+    float tp = __builtin_fmaf(z2, 62.f / 2835.f, -17.f / 315.f);
+    tp = __builtin_fmaf(z2, tp, 2.f / 15.f);
+    tp = __builtin_fmaf(z2, tp, -1.f / 3.f);
+    tp = __builtin_fmaf(z2 * z, tp, z);
+    const float e = __builtin_amdgcn_exp2f(-y * kLog2e);
+    const float lmid = __builtin_amdgcn_logf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e));
+    const float e2 = e * e;
+    float at = __builtin_fmaf(e2, 1.f / 7.f, 1.f / 5.f);
+    at = __builtin_fmaf(e2, at, 1.f / 3.f);
+    at = __builtin_fmaf(e2 * e, at, e);                       // atanh(e)
+    const float lsmall = at * (-2.f * kLog2e);
+    const float lt = __builtin_amdgcn_logf(fmaxf(tp, 1e-20f));
+    return z < 0.3f ? lt : (e >= 0.0625f ? lmid : lsmall);
 }
 __device__ __forceinline__ double wbp_out(double lam, double n, double s) {
     n = n + (1.0 - s) / 2.0;
@@ -79,12 +89,25 @@ __device__ __forceinline__ double wbp_out(double lam, double n, double s) {
     const double p = g_clamp(exp(lam) * cos_pi(n), -hi, hi);
     return log(1.0 + p) - log(1.0 - p);
 }
-__device__ __forceinline__ float wbp_out(float lam, float n, float s) {
+// fp32: lam2 = base-2 leave-one-out log magnitude (<= 0), |p| = 2^lam2.  1 - |p| through
+// expm1 (degree-8 Taylor for |lam| < 0.35) so it stays accurate as |p| -> 1, clamped at
+// 1 - fl64(1 - 1e-15) like the fp64 reference's p clamp.
+__device__ __forceinline__ float wbp_out(float lam2, float n, float s) {
     n = n + (1.f - s) / 2.f;
     const float sgn = cos_pi(n);
-    const float one_m = fmaxf(-expm1f(lam), 9.992007221626409e-16f);  // 1 - fl64(1 - 1e-15)
-    const float one_p = fminf(1.f + expf(lam), 2.f - 9.992007221626409e-16f);
-    return sgn * (logf(one_p) - logf(one_m));
+    const float q = __builtin_amdgcn_exp2f(lam2);
+    const float x = lam2 * kLn2;                              // natural log of |p|, <= 0
+    float em = __builtin_fmaf(x, 1.f / 40320.f, 1.f / 5040.f);
+    em = __builtin_fmaf(x, em, 1.f / 720.f);
+    em = __builtin_fmaf(x, em, 1.f / 120.f);
+    em = __builtin_fmaf(x, em, 1.f / 24.f);
+    em = __builtin_fmaf(x, em, 1.f / 6.f);
+    em = __builtin_fmaf(x, em, 0.5f);
+    em = __builtin_fmaf(x * x, em, x);                        // expm1(x)
+    float one_m = x > -0.35f ? -em : 1.f - q;
+    one_m = fmaxf(one_m, 9.992007221626409e-16f);
+    const float one_p = fminf(1.f + q, 2.f - 9.992007221626409e-16f);
+    return sgn * (kLn2 * (__builtin_amdgcn_logf(one_p) - __builtin_amdgcn_logf(one_m)));
 }
 // per-edge weights of iteration t (reference edge order; NBP [T][2][E] + readout, V10 [T][E])
 template <int MODEL, typename T> struct WbpW {
@@ -742,6 +765,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     Mlp10F32 mlp_msg;
     if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
         mlp_msg.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
+    // weighted BP: per-edge tables read through the cache; LDS carries the messages the
+    // variable sums need (NBP: already weighted by the next layer's W, or the readout W)
+    constexpr bool WBP = ModelTraits<MODEL>::wbp;
+    const WbpW<MODEL, T> ww{w, E, iters};
+    T alpha = T(0);
+    if constexpr (WBP) alpha = ww.alpha();
 
     // ---- per-lane resident state.  Item f = tid + q*256 -> (check c, codeword b, lane g)
     // with g fastest and the CODEWORD next: a wave's 8 check groups are 8 codewords of one
@@ -786,6 +815,15 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                 const SumX<T> p = sxb[sv & 0xffffu];
                 T cc = T(0), t;
                 if constexpr (kBase2) t = tanh_half_base2(__builtin_fmaf(p.s - m[q][r], kLog2e, p.x));
+                else if constexpr (WBP) {
+                    const int e = (int)(sv >> 16), ec = e < E ? e : 0;
+                    T a;
+                    if constexpr (MODEL == GNND_NBP)
+                        a = (p.s - m[q][r] * ww.msg(it, ec)) + p.x * ww.prior(it, ec);
+                    else
+                        a = ((p.s - m[q][r]) + p.x) * ww.chk(it, ec);
+                    t = wbp_L(a, cc);
+                }
                 else t = M::pre(p.s - m[q][r], p.x, w, cc);
                 tv[r] = valid ? t : T(0);
                 cf[r] = valid ? cc : T(0);
@@ -799,8 +837,19 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             T* mb = s_m + cb[q] * E1;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                m[q][r] = M::post(Sc - tv[r], Sc2 - cf[r], sc[q], m[q][r], mlp_msg, s_w, w);
-                mb[ve[q][r] >> 16] = m[q][r];
+                const int e = (int)(ve[q][r] >> 16);
+                if constexpr (WBP) {
+                    m[q][r] = wbp_out(Sc - tv[r], Sc2 - cf[r], sc[q]) + m[q][r] * alpha;
+                    if constexpr (MODEL == GNND_NBP) {
+                        const int ec = e < E ? e : 0;
+                        mb[e] = m[q][r] * (it + 1 < iters ? ww.msg(it + 1, ec) : ww.out_w(ec));
+                    } else {
+                        mb[e] = m[q][r];
+                    }
+                } else {
+                    m[q][r] = M::post(Sc - tv[r], Sc2 - cf[r], sc[q], m[q][r], mlp_msg, s_w, w);
+                    mb[e] = m[q][r];
+                }
             }
         }
         __syncthreads();
@@ -827,15 +876,31 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                 k += 2;
             }
             if (dv & 1) s += mp[k];
-            if (last) out[(b0 + b) * V + v] = M::readout(s + (kBase2 ? xg[b * N + v] : s_sx[b * V + v].x), s_w);
-            else s_sx[b * V + v].s = s;
+            if (last) {
+                if constexpr (MODEL == GNND_NBP) {   // + sum_v(x_v W_p)  (neural_BP.py:307-312)
+                    const T xv = s_sx[b * V + v].x;
+                    T s2 = T(0);
+                    for (int j = 0; j < dv; ++j) s2 += xv * ww.out_p((int)o.y + j);
+                    out[(b0 + b) * V + v] = sigmoid_ref(-(s + s2));
+                } else {
+                    out[(b0 + b) * V + v] = M::readout(s + (kBase2 ? xg[b * N + v] : s_sx[b * V + v].x), s_w);
+                }
+            } else {
+                s_sx[b * V + v].s = s;
+            }
         }
         __syncthreads();
     }
     if (iters == 0)
         for (int f = tid; f < nb * V; f += GNND_BLOCK) {
             const int b = fdiv(f, dV), v = f - b * V;
-            out[b0 * V + f] = M::readout(xg[b * N + v], s_w);
+            if constexpr (MODEL == GNND_NBP) {
+                T s2 = T(0);
+                for (int k = g.var_ptr[v]; k < g.var_ptr[v + 1]; ++k) s2 += xg[b * N + v] * ww.out_p(k);
+                out[b0 * V + f] = sigmoid_ref(-s2);
+            } else {
+                out[b0 * V + f] = M::readout(xg[b * N + v], s_w);
+            }
         }
 }
 
@@ -897,7 +962,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
     const size_t wb = align16((size_t)lds_weights(model) * esz);
     const size_t target = lds_target();
-    const bool light = model != GNND_V24 && model != GNND_NBP && model != GNND_V10;
+    const bool light = model != GNND_V24;
     if (light && dtype == GNND_F32 && gr->rview.G <= 16 && !resident_disabled()) {
         const GraphView& g = gr->rview;          // instantiated group sizes 1..16
         const int IC = g.C * g.G;
