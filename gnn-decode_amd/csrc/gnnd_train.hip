@@ -16,7 +16,7 @@
 // The MLP phases are UNIT-parallel: a wave walks its share of the tile's edges while each
 // lane owns two of the 128 hidden units (weights in VGPRs), so every weight gradient
 // accumulates in the lane's registers over all edges and iterations with no cross-lane
-// traffic; only d(input) of an edge needs a wave reduction (DPP + two swizzles).  The
+// traffic; only d(input) of an edge needs a wave reduction (DPP only, result in lane 63).  The
 // edge phases B/D are edge-parallel leave-one-out sums in LDS.  Per-workgroup gradient
 // partials are summed over the workgroups in a fixed order by a second kernel
 // (deterministic, run-to-run identical).
@@ -46,8 +46,38 @@ __device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg) {
     sg = z * __builtin_amdgcn_rcpf(z1);
 }
 
-__device__ __forceinline__ float wave_sum(float v) { return group_sum_c<64>(v); }
-__device__ __forceinline__ double wave_sum(double v) { return group_sum(v, 64); }
+// total of a wave64 value, uniform (SGPR) result: DPP row reduction (quad_perm x2, half /
+// full row mirror), then row_bcast:15 / row_bcast:31 carry the row sums into lane 63 —
+// all on the VALU, no LDS round trip (the __shfl_xor form costs two ds_bpermute
+// latencies on every edge's critical path).
+template <int CTRL, int ROWS> __device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    v += __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x140, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x142, 0xa>(__float_as_int(v)));   // row_bcast:15 -> rows 1, 3
+    v += __int_as_float(dpp_i<0x143, 0xc>(__float_as_int(v)));   // row_bcast:31 -> rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+template <int CTRL, int ROWS> __device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_i<CTRL, ROWS>((int)b), hi = dpp_i<CTRL, ROWS>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum(double v) {
+    v += dpp_d<0xB1, 0xf>(v);
+    v += dpp_d<0x4E, 0xf>(v);
+    v += dpp_d<0x141, 0xf>(v);
+    v += dpp_d<0x140, 0xf>(v);
+    v += dpp_d<0x142, 0xa>(v);
+    v += dpp_d<0x143, 0xc>(v);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 // two hidden units of one MLP owned by this lane: k0 = lane, k1 = lane + 64
 template <typename T> struct Units {
@@ -144,7 +174,8 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N;
     constexpr int kTrainWaves = kTrainThreads / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: edge loops on SALU
     int* s_tab = (int*)smem;
     const int nints = graph_table_ints(V, C, E);
     const uint32_t* s_evc = (const uint32_t*)s_tab;
@@ -161,6 +192,9 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     T* s_ext = s_t + TE;
     T* s_x = s_ext + TE;                     // [CW][N] node features
     T* s_acc = s_x + (size_t)CW * N;         // [1283] workgroup gradient accumulator
+    int* s_eb = (int*)(s_acc + kV24W);       // [CW][E] b*E of the edge's codeword
+    int* s_nv = s_eb + TE;                   // [CW][E] b*N + v  (index into s_x)
+    int* s_nc = s_nv + TE;                   // [CW][E] b*N + V + c
 
     const int* gtab = (const int*)g.edge_vc;
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
@@ -169,10 +203,14 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     const int nE = nb * E;
     for (int i = tid; i < nb * N; i += kTrainThreads) s_x[i] = x[(size_t)b0 * N + i];
-    // readout inputs: m^T into s_u, d loss / d r per edge into s_da
+    // readout inputs: m^T into s_u, d loss / d r per edge into s_da; per-edge index tables
     for (int f = tid; f < nE; f += kTrainThreads) {
         const int b = f / E, e = f - b * E;
-        const size_t bv = (size_t)(b0 + b) * V + (int)(s_evc[e] & 0xffffu);
+        const uint32_t vc = s_evc[e];
+        s_eb[f] = b * E;
+        s_nv[f] = b * N + (int)(vc & 0xffffu);
+        s_nc[f] = b * N + V + (int)(vc >> 16);
+        const size_t bv = (size_t)(b0 + b) * V + (int)(vc & 0xffffu);
         const T pv = p[bv];
         s_u[f] = tape.mT[(size_t)b0 * E + f];
         s_da[f] = -((gp[bv] * (T(1) - pv)) * pv);     // p = sigmoid(-r)
@@ -216,16 +254,14 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
         }
         __syncthreads();
         // A: m^{t+1} = MLP_c(u) s_c + m^t
-        unit_pass(uc, std::false_type{}, s_u, zero, [&](int f) {
-            const int b = f / E, e = f - b * E;
-            return s_dm[f] * s_x[b * N + V + (int)(s_evc[e] >> 16)];
-        }, s_g);
+        unit_pass(uc, std::false_type{}, s_u, zero, [&](int f) { return s_dm[f] * s_x[s_nc[f]]; },
+                  s_g);
         __syncthreads();
         // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
         for (int f = tid; f < nE; f += kTrainThreads) {
-            const int b = f / E, e = f - b * E;
-            const int c = (int)(s_evc[e] >> 16);
-            const T* gb = s_g + (size_t)b * E;
+            const int eb = s_eb[f];
+            const int c = (int)(s_evc[f - eb] >> 16);
+            const T* gb = s_g + eb;
             T s = T(0);
             for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += gb[s_cedge[k]];
             const T t = s_t[f];
@@ -233,16 +269,14 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
         }
         __syncthreads();
         // C: a = MLP_v(ext, x_v)
-        unit_pass(uv, std::true_type{}, s_ext, [&](int f) {
-            const int b = f / E, e = f - b * E;
-            return s_x[b * N + (int)(s_evc[e] & 0xffffu)];
-        }, [&](int f) { return s_da[f]; }, s_g);
+        unit_pass(uv, std::true_type{}, s_ext, [&](int f) { return s_x[s_nv[f]]; },
+                  [&](int f) { return s_da[f]; }, s_g);
         __syncthreads();
         // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
         for (int f = tid; f < nE; f += kTrainThreads) {
-            const int b = f / E, e = f - b * E;
-            const int v = (int)(s_evc[e] & 0xffffu);
-            const T* gb = s_g + (size_t)b * E;
+            const int eb = s_eb[f];
+            const int v = (int)(s_evc[f - eb] & 0xffffu);
+            const T* gb = s_g + eb;
             T s = T(0);
             for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += gb[k];
             s_dm[f] += s - s_g[f];
@@ -286,7 +320,8 @@ int train_tile(const gnnd_graph* g, int64_t B) {
 size_t train_lds(const gnnd_graph* g, int esz, int cw) {
     const GraphView& v = g->view;
     return (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
-           (size_t)esz * (6 * (size_t)cw * v.E + (size_t)cw * v.N + kV24W);
+           (size_t)esz * (6 * (size_t)cw * v.E + (size_t)cw * v.N + kV24W) +
+           4 * 3 * (size_t)cw * v.E;
 }
 
 template <typename T>
