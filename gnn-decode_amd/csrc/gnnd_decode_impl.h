@@ -802,6 +802,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
         }
     }
 
+    // variable-sum step mapping (see below): lane-invariant when CW divides the block
+    const bool vfixed = GNND_BLOCK % CW == 0;
+    const int vb = tid % CW, vi0 = tid / CW, vstep = GNND_BLOCK / CW;
+    const bool vact = vb < nb;
+    const int vmbase = vb * E1, vsbase = vb * V;
+
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int q = 0; q < QMAX; ++q) {
@@ -858,12 +864,11 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
         // (odd stride E+1: no bank conflicts).  Edge (index_add) order within a variable;
         // two-value ds_read2 loads, four values in flight per step, no masking.
         const bool last = it + 1 == iters;
-        for (int f = tid; f < V * CW; f += GNND_BLOCK) {
-            const int i = fdiv(f, dItem), b = f - i * CW;
-            if (b >= nb) continue;
+        // one variable-item (codeword b, degree-order index i); mbase = b (E+1), sbase = b V
+        auto var_item = [&](int b, int i, int mbase, int sbase) {
             const uint2 o = s_vord[i];
             const int v = (int)(o.x & 0xffffu), dv = (int)(o.x >> 16);
-            const T* mp = s_m + b * E1 + (int)o.y;
+            const T* mp = s_m + mbase + (int)o.y;
             T s = T(0);
             int k = 0;
             for (; k + 4 <= dv; k += 4) {
@@ -878,15 +883,28 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             if (dv & 1) s += mp[k];
             if (last) {
                 if constexpr (MODEL == GNND_NBP) {   // + sum_v(x_v W_p)  (neural_BP.py:307-312)
-                    const T xv = s_sx[b * V + v].x;
+                    const T xv = s_sx[sbase + v].x;
                     T s2 = T(0);
                     for (int j = 0; j < dv; ++j) s2 += xv * ww.out_p((int)o.y + j);
-                    out[(b0 + b) * V + v] = sigmoid_ref(-(s + s2));
+                    out[b0 * V + sbase + v] = sigmoid_ref(-(s + s2));
                 } else {
-                    out[(b0 + b) * V + v] = M::readout(s + (kBase2 ? xg[b * N + v] : s_sx[b * V + v].x), s_w);
+                    out[b0 * V + sbase + v] = M::readout(s + (kBase2 ? xg[b * N + v] : s_sx[sbase + v].x), s_w);
                 }
             } else {
-                s_sx[b * V + v].s = s;
+                s_sx[sbase + v].s = s;
+            }
+        };
+        if (vfixed) {
+            // CW divides 256: f = tid + k 256 keeps f mod CW, so the lane's codeword and its
+            // LDS bases are loop-invariant (no per-item division or 32-bit multiplies: those
+            // are quarter-rate and cost as much as the sums themselves)
+            if (vact)
+                for (int i = vi0; i < V; i += vstep) var_item(vb, i, vmbase, vsbase);
+        } else {
+            for (int f = tid; f < V * CW; f += GNND_BLOCK) {
+                const int i = fdiv(f, dItem), b = f - i * CW;
+                if (b >= nb) continue;
+                var_item(b, i, b * E1, b * V);
             }
         }
         __syncthreads();
