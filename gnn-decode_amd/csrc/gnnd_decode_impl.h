@@ -168,6 +168,10 @@ struct Mlp10F32 {
         }
         b2 = uniform(w[30]);
     }
+    // The two accumulator halves are combined by one scalar add in asm: hipcc otherwise
+    // SLP-packs the combines of neighbouring edges into v_mov shuffles + v_pk_add (2 ops per
+    // edge instead of 1).  (Folding CGNNI's residual into the accumulator as well saves one
+    // more op but spills VGPRs in the 128-register resident kernel: measured slower.)
     __device__ __forceinline__ float operator()(float u) const {
         f32x2 acc = {b2, 0.f};                 // bias rides in the even-unit accumulator
         f32x2 uu;                              // only the lo half is read (op_sel_hi 0)
@@ -185,7 +189,9 @@ struct Mlp10F32 {
 #endif
             acc = __builtin_elementwise_fma(h, w2[k], acc);
         }
-        return acc.x + acc.y;
+        float r;
+        asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(acc.x), "v"(acc.y));
+        return r;
     }
 };
 
