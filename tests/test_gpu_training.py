@@ -202,3 +202,63 @@ def test_bp_check_step_backward_matches_torch_autograd(variant):
         (got * w).sum().backward()
         np.testing.assert_allclose(m1.grad.cpu().numpy(), m0.grad.cpu().numpy(),
                                    rtol=1e-9, atol=1e-12 * float(m0.grad.abs().max()))
+
+
+def _dp_worker(rank, world, port, steps, q):
+    """One rank of a 2-process data-parallel run on the single GPU (gloo all-reduce of the
+    flat gradient; the fused HIP training kernels on cuda:0)."""
+    import os
+    import torch.distributed as dist
+    import gnndecode as gd
+    from conftest import GOLDEN
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    z = np.load(os.path.join(GOLDEN, 'train_v24_L5.npz'))
+    H = gd.codes.toric_code(5)
+    m = gd.DecoderV24(int(z['T']), H)
+    m.load_state_dict({k: torch.from_numpy(np.array(v)) for k, v in weights_of(z).items()})
+    m = m.to(DEV).train()
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+    x = torch.from_numpy(z['x']).to(DEV).view(-1, H.shape[0] + H.shape[1])
+    y = torch.from_numpy(z['y']).to(DEV).view(-1, H.shape[0])
+    s, e = gd.train.shard_bounds(x.size(0), rank, world)
+    xs, ys = x[s:e].reshape(-1, 1).contiguous(), y[s:e].reshape(-1, 1).contiguous()
+    tr = gd.train.Trainer(m, lf, lr=1e-3)
+    data = gd.data.make_batch(xs, m.graph(xs.device))
+    losses = [float(tr.step(data, ys)) for _ in range(steps)]
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()
+    q.put((rank, losses, flat.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_fused_training_equals_full_batch(golden):
+    """Config 5's data-parallel step with the fused HIP kernels: 2 ranks (gloo, both on the
+    one GPU), each a shard of the batch, SUM all-reduce -> same parameters and losses as a
+    single full-batch process (the reference loss is a sum)."""
+    import socket
+    import torch.multiprocessing as mp
+    import gnndecode as gd
+    sock = socket.socket()
+    sock.bind(('127.0.0.1', 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    steps, world = 2, 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    z, m, loss_fn, data, y = _setup(golden, 'train_v24_L5', 'v24', ('toric', 5), 'syndrome')
+    tr = gd.train.Trainer(m, loss_fn, lr=1e-3)
+    ref_losses = [float(tr.step(data, y)) for _ in range(steps)]
+    ref = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()
+    for rank, losses, flat in res:
+        flat = torch.tensor(flat, dtype=torch.float64)
+        assert flat.tolist() == res[0][2]                 # ranks bitwise equal
+        assert torch.allclose(flat, ref, rtol=1e-10, atol=1e-12)
+        assert all(abs(a - b) <= 1e-9 * max(1, abs(b)) for a, b in zip(losses, ref_losses))
