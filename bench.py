@@ -209,10 +209,11 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        dist.init_process_group('nccl')
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    if world > 1:
+        # bind the RCCL communicator to this rank's GPU (barriers then never touch GPU 0)
+        dist.init_process_group('nccl', device_id=dev)
     if a.mode == 'train':
         train_main(a, world, rank, dev)
         if world > 1:

@@ -27,6 +27,16 @@ struct GraphView {            // passed by value to kernels
     // variables sorted by (degree, v): {v | dv << 16, first edge}.  Consecutive entries have
     // (nearly) equal degree, so lanes summing them run the same trip count.
     const uint2* var_ord;     // [V]
+    // register-resident kernel's LDS message layout (gnnd_graph::rlay): variable-major
+    // positions, each variable's edges padded with never-written zero slots to the largest
+    // degree among the `vgroup` consecutive var_ord entries one wave sums together, so a
+    // wave's variable sums run one uniform trip count with no masks.  vlay[i] = {v | dpad
+    // << 16, first position} in var_ord order; slot_ve of the resident plans carries the
+    // POSITION (not the edge id) in its high half; `spare` = the position padding slots and
+    // idle items write; P1 = per-codeword stride (odd: bank-conflict-free codeword strides).
+    // The identity layout (vgroup 1) is var_ord with positions = edge ids, spare = E.
+    const uint2* vlay;        // [V]
+    int vgroup, spare, P1;
 };
 #define GNND_SLOT_PAD 0x80000000u   // padding slot: variable 0, flag bit 31
 
@@ -34,6 +44,8 @@ struct gnnd_graph {
     GraphView view;           // slot plan of the streaming kernel (ties -> smaller R)
     GraphView rview;          // slot plan of the register-resident kernel (ties -> larger R)
     GraphView pview;          // ties -> R = 2: paired-edge fp32 V24 streaming at small batch
+    GraphView rlay[7];        // rview with the padded message layout for vgroup 2^i (i = 0:
+                              // identity); rlay[i].vlay == nullptr if it does not fit 16 bits
     void* dev;                // single device allocation holding every table
     size_t table_bytes;       // bytes of the four CSR/CSC tables (staged to LDS)
 };

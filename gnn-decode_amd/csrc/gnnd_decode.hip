@@ -101,6 +101,7 @@ extern "C" int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32
     h_plan[1] = (int32_t)p.lds;
     h_plan[2] = p.resident ? 1 : 0;
     h_plan[3] = p.q;
+    h_plan[4] = p.resident ? p.view->vgroup : 0;
     return GNND_OK;
 }
 

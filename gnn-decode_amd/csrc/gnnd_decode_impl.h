@@ -720,6 +720,24 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     }
 }
 
+// sum of dp >= 1 consecutive LDS values in order; dp wave-uniform, so the trip counts and
+// remainder tests are scalar branches and every lane runs unmasked
+template <typename T> __device__ __forceinline__ T var_sum_uniform(const T* mp, int dp) {
+    T s = mp[0];
+    int k = 1;
+    for (; k + 4 <= dp; k += 4) {
+        const T a0 = mp[k], a1 = mp[k + 1], a2 = mp[k + 2], a3 = mp[k + 3];
+        s += a0; s += a1; s += a2; s += a3;
+    }
+    if (k + 2 <= dp) {
+        const T a0 = mp[k], a1 = mp[k + 1];
+        s += a0; s += a1;
+        k += 2;
+    }
+    if (k < dp) s += mp[k];
+    return s;
+}
+
 // ---------------------------------------------------------------------------------------
 // resident kernel (light models: CGNNI, QGNNI, CBP, QBP)
 // ---------------------------------------------------------------------------------------
@@ -744,7 +762,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     constexpr int kLogG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N;
-    const int E1 = E + 1;
+    const int E1 = g.P1;                  // message positions per codeword (layout stride)
+    const int spare = g.spare;            // position padding slots and idle items write
     const int tid = threadIdx.x;
 
     T* s_w = (T*)smem;
@@ -756,7 +775,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
 
     for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
-    for (int i = tid; i < V; i += GNND_BLOCK) s_vord[i] = g.var_ord[i];
+    for (int i = tid; i < V; i += GNND_BLOCK) s_vord[i] = g.vlay[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     const T* xg = x + b0 * N;
@@ -766,6 +785,10 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
         if (n < V) s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
         else s_xc[b * C + n - V] = xv;
     }
+    // padded layouts: the positions past a variable's degree are read by the variable sums
+    // and never written, so they must hold 0 (s + 0 == s)
+    if (g.vgroup > 1)
+        for (int i = tid; i < CW * E1; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
 
     Mlp10F32 mlp_msg;
@@ -803,7 +826,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t sv = g.slot_ve[rem * R + r];
-            ve[q][r] = act ? sv : ((sv & 0xffffu) | ((uint32_t)E << 16));
+            ve[q][r] = act ? sv : ((sv & 0xffffu) | ((uint32_t)spare << 16));
             m[q][r] = T(0);
         }
     }
@@ -813,6 +836,10 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     const int vb = tid % CW, vi0 = tid / CW, vstep = GNND_BLOCK / CW;
     const bool vact = vb < nb;
     const int vmbase = vb * E1, vsbase = vb * V;
+    // a wave covers 64 / CW consecutive var_ord entries per step: uniform when the layout
+    // pads each such group to one degree (weighted BP keeps the identity layout: its
+    // per-edge weight tables are indexed by edge id)
+    const bool vuni = !WBP && vfixed && g.vgroup * CW >= 64;
 
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
@@ -823,7 +850,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t sv = ve[q][r];
-                const bool valid = !PAD || (int)(sv >> 16) != E;   // every slot real: no mask
+                const bool valid = !PAD || (int)(sv >> 16) != spare;   // every slot real: no mask
                 const SumX<T> p = sxb[sv & 0xffffu];
                 T cc = T(0), t;
                 if constexpr (kBase2) t = tanh_half_base2(__builtin_fmaf(p.s - m[q][r], kLog2e, p.x));
@@ -900,7 +927,21 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                 s_sx[sbase + v].s = s;
             }
         };
-        if (vfixed) {
+        if (vuni) {
+            // padded layout (GraphView::vlay): the wave's vgroup variables share one padded
+            // degree, so the sum is straight-line code selected by a wave-uniform switch —
+            // no masks, no per-edge address or loop arithmetic.  Reference (index_add) order;
+            // the padding zeros come last (s + 0 == s).
+            if (vact)
+                for (int i = vi0; i < V; i += vstep) {
+                    const uint2 o = s_vord[i];
+                    const int dp = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));
+                    const int v = (int)(o.x & 0xffffu);
+                    const T s = var_sum_uniform(s_m + vmbase + (int)o.y, dp);
+                    if (last) out[b0 * V + vsbase + v] = M::readout(s + (kBase2 ? xg[vb * N + v] : s_sx[vsbase + v].x), s_w);
+                    else s_sx[vsbase + v].s = s;
+                }
+        } else if (vfixed) {
             // CW divides 256: f = tid + k 256 keeps f mod CW, so the lane's codeword and its
             // LDS bases are loop-invariant (no per-item division or 32-bit multiplies: those
             // are quarter-rate and cost as much as the sums themselves)
@@ -971,6 +1012,15 @@ bool resident_disabled() {
     return v;
 }
 
+// GNND_NO_VLAYOUT=1: resident kernel on the identity message layout (A/B measurements)
+bool vlayout_disabled() {
+    static bool v = [] {
+        const char* e = getenv("GNND_NO_VLAYOUT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 struct Plan {
     const GraphView* view;   // slot plan the chosen kernel runs on (gnnd_graph::view/rview)
     bool resident;
@@ -990,12 +1040,25 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     if (light && dtype == GNND_F32 && gr->rview.G <= 16 && !resident_disabled()) {
         const GraphView& g = gr->rview;          // instantiated group sizes 1..16
         const int IC = g.C * g.G;
-        // resident layout: weights, var_ord, then [CW][E+1] messages, [CW][V] {S, x}, [CW][C].
-        // Pick (CW, Q) with Q in kResidentQ maximising lane utilisation CW*IC / (Q*256),
-        // ties to the larger tile.
+        // message layout for a tile of cw codewords: with cw | 256 a wave sums 64 / cw
+        // consecutive var_ord entries per step, so the layout padded for that group size
+        // makes its variable sums uniform (GraphView::vlay); weighted BP indexes per-edge
+        // weights by edge id and keeps the identity layout
+        const bool wbp = model == GNND_NBP || model == GNND_V10;
+        auto lay_of = [&](int cw) -> const GraphView* {
+            if (!wbp && !vlayout_disabled() && GNND_BLOCK % cw == 0 && cw < 64) {
+                int i = 0;
+                while ((cw << i) < 64) ++i;
+                if (gr->rlay[i].vlay) return &gr->rlay[i];
+            }
+            return &gr->rlay[0];
+        };
+        // resident layout: weights, var order, then [CW][P1] messages, [CW][V] {S, x},
+        // [CW][C].  Pick (CW, Q) with Q in kResidentQ maximising lane utilisation
+        // CW*IC / (Q*256), ties to the larger tile.
         const size_t fixed = wb + align16((size_t)g.V * 8);
         auto lds_of = [&](int cw) {
-            return fixed + esz * (((size_t)cw * (g.E + 1) + 1) & ~(size_t)1) +
+            return fixed + esz * (((size_t)cw * lay_of(cw)->P1 + 1) & ~(size_t)1) +
                    esz * ((size_t)cw * (2 * (size_t)g.V + g.C));
         };
         int best = 0, bestq = 0;
@@ -1015,7 +1078,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
             if (u > bestu + 1e-9 || (u > bestu - 1e-9 && cw > best)) { bestu = u; best = cw; bestq = q; }
         }
         if (best > 0 && bestu >= 0.5) {
-            p->view = &g;
+            p->view = lay_of(best);
             p->resident = true;
             p->cw = best;
             p->q = bestq;

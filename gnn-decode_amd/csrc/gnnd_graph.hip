@@ -127,7 +127,49 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         off += 2 * (int)plans[i].slot.size() + E;
     }
     const int ord_off = (off + 1) & ~1;     // uint2 alignment
-    std::vector<int> table(ord_off + 2 * V);
+    // padded variable-major message layouts of the resident kernel (GraphView::vlay), one per
+    // wave group size 2^i, i = 1..6: groups of 2^i consecutive var_ord entries share the
+    // group's largest degree; positions run in var_ord order
+    const int nsr = (int)plans[1].slot.size();
+    struct Layout {
+        bool ok = false;
+        int P = 0;
+        std::vector<int> vlay, slot;     // [2V] {v | dpad << 16, pos}, [nsr] v | pos << 16
+    };
+    Layout lays[7];
+    int lay_off[7] = {0};
+    off = ord_off + 2 * V;
+    for (int i = 1; i < 7; ++i) {
+        const int gs = 1 << i;
+        Layout& L = lays[i];
+        std::vector<int> epos(E);
+        L.vlay.assign(2 * V, 0);
+        int pos = 0;
+        for (int j0 = 0; j0 < V; j0 += gs) {
+            const int j1 = std::min(V, j0 + gs);
+            int dpad = 0;
+            for (int j = j0; j < j1; ++j) dpad = std::max(dpad, vptr[vord[j] + 1] - vptr[vord[j]]);
+            for (int j = j0; j < j1; ++j) {
+                const int v = vord[j];
+                L.vlay[2 * j] = v | (dpad << 16);
+                L.vlay[2 * j + 1] = pos;
+                for (int e = vptr[v]; e < vptr[v + 1]; ++e) epos[e] = pos + (e - vptr[v]);
+                pos += dpad;
+            }
+        }
+        L.P = pos;
+        if (pos >= 65535) continue;          // positions travel in 16 bits
+        L.ok = true;
+        L.slot.assign(nsr, pos << 16);       // padding: variable 0, the spare position P
+        for (int k = 0; k < nsr; ++k) {
+            const uint32_t sv = plans[1].slot_ve[k];
+            const int e = (int)(sv >> 16);
+            if (e < E) L.slot[k] = (int)(sv & 0xffffu) | (epos[e] << 16);
+        }
+        lay_off[i] = off;
+        off = (off + 2 * V + nsr + 1) & ~1;  // uint2 alignment of the next layout
+    }
+    std::vector<int> table(off);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
@@ -143,6 +185,11 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         table[ord_off + 2 * i] = v | ((vptr[v + 1] - vptr[v]) << 16);
         table[ord_off + 2 * i + 1] = vptr[v];
     }
+    for (int i = 1; i < 7; ++i)
+        if (lays[i].ok) {
+            memcpy(table.data() + lay_off[i], lays[i].vlay.data(), sizeof(int) * 2 * V);
+            memcpy(table.data() + lay_off[i] + 2 * V, lays[i].slot.data(), sizeof(int) * nsr);
+        }
 
     gnnd_graph* g = (gnnd_graph*)calloc(1, sizeof(gnnd_graph));
     if (!g) return GNND_ERR_ALLOC;
@@ -172,6 +219,19 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         pv.slot = (const uint32_t*)(d + plan_off[i]);
         pv.vslot = d + plan_off[i] + ns;
         pv.slot_ve = (const uint32_t*)(d + plan_off[i] + ns + E);
+        pv.vlay = gv.var_ord;               // identity layout: positions = edge ids
+        pv.vgroup = 1; pv.spare = E; pv.P1 = E + 1;
+    }
+    for (int i = 0; i < 7; ++i) {
+        GraphView& lv = g->rlay[i];
+        lv = g->rview;
+        if (i == 0) continue;
+        lv.vgroup = 1 << i;
+        if (!lays[i].ok) { lv.vlay = nullptr; continue; }
+        lv.vlay = (const uint2*)(d + lay_off[i]);
+        lv.slot_ve = (const uint32_t*)(d + lay_off[i] + 2 * V);
+        lv.spare = lays[i].P;
+        lv.P1 = (lays[i].P + 1) | 1;        // odd codeword stride, spare slot included
     }
     *out = g;
     return GNND_OK;

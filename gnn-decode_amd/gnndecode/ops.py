@@ -184,11 +184,11 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
 
 def decode_plan(graph, model, dtype):
     """{'cw', 'lds', 'kernel', 'items_per_lane'} of the fused decoder's launch plan."""
-    plan = (ctypes.c_int32 * 4)()
+    plan = (ctypes.c_int32 * 5)()
     _lib.call('gnnd_decode_plan', graph.handle, _lib.VARIANT[model], dtype_code(dtype), plan)
     return {'cw': plan[0], 'lds': plan[1],
             'kernel': 'decode_resident_kernel' if plan[2] else 'decode_kernel',
-            'items_per_lane': plan[3]}
+            'items_per_lane': plan[3], 'var_group': plan[4]}
 
 
 def decode_tile(graph, model, dtype):

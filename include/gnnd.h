@@ -164,7 +164,9 @@ int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32_t* h_cw_pe
                      int32_t* h_lds_bytes);
 /* Full launch plan: h_plan[0] codewords per workgroup, [1] LDS bytes per workgroup,
  * [2] kernel (0 = streaming decode_kernel, 1 = register-resident decode_resident_kernel),
- * [3] work items per lane (resident kernel; 0 otherwise). */
+ * [3] work items per lane (resident kernel; 0 otherwise), [4] variable-sum group of the
+ * resident kernel's message layout (vars per wave step padded to one degree; 1 = identity
+ * layout; 0 for the streaming kernel).  h_plan holds 5 ints. */
 int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan);
 
 /* ---- fused training step (decoder_v2_4) ------------------
