@@ -21,6 +21,7 @@ struct GraphView {            // passed by value to kernels
     // slot (c, lane g, r) = c*G*R + g*R + r holds its edges in increasing order, padded.
     int G, logG, R;
     int padded;               // 1 if some check has fewer than G*R edges (padding slots exist)
+    int padr;                 // most padding slots in one lane (trailing: lanes fill in order)
     const uint32_t* slot;     // [C*G*R]  variable of the slot's edge; GNND_SLOT_PAD if padding
     const int* vslot;         // [E]      slot of edge e (reference edge order = var-major)
     const uint32_t* slot_ve;  // [C*G*R]  v | (e << 16); padding = 0 | (E << 16) (dummy edge)

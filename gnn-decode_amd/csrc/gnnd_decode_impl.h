@@ -265,6 +265,44 @@ __device__ __forceinline__ f32x2 pk_fma_hi(f32x2 u, f32x2 w, f32x2 c) {
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(h) : "v"(u), "s"(w), "v"(c));
     return h;
 }
+// TWO EDGES per call (the paired check step of the resident kernel): the edges ride the
+// two halves of every packed FMA, one hidden unit per instruction.  Layer 1 + ReLU is one
+// clamped v_pk_fma_f32 per unit whose multiplier and addend are the two halves of ONE
+// SGPR pair {W1'_k, b1'_k} (op_sel; the constant bus takes one SGPR pair per instruction),
+// layer 2 one v_pk_fma_f32 per unit with the weight broadcast from an SGPR pair half; the
+// first unit's pair is {w2'_0, b2} (bias as its addend).  Units accumulate in order
+// 0..9 from b2 (no accumulator halves to combine): 20 packed ops per edge PAIR.  Same
+// power-of-two scaling as Mlp10F32 (bit-identical unit contributions).
+struct Mlp10Pair {
+    f32x2 w1b[10];     // {W1_k 2^-s_k, b1_k 2^-s_k}
+    f32x2 w20b;        // {W2_0 2^s_0, b2}
+    f32x2 w2[5];       // {W2_{2i} 2^s, W2_{2i+1} 2^s}  (w2[0].x unused)
+    __device__ __forceinline__ void load(const float* w, float umax) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            int e;
+            frexpf(fabsf(w[k]) * umax + fabsf(w[10 + k]), &e);
+            w1b[k] = f32x2{uniform(ldexpf(w[k], -e)), uniform(ldexpf(w[10 + k], -e))};
+            const float v = uniform(ldexpf(w[20 + k], e));
+            if (k & 1) w2[k >> 1].y = v; else w2[k >> 1].x = v;
+            if (k == 0) w20b = f32x2{v, uniform(w[30])};
+        }
+    }
+    __device__ __forceinline__ f32x2 operator()(f32x2 u) const {
+        f32x2 h, acc;
+        asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
+            : "=v"(h) : "v"(u), "s"(w1b[0]));
+        acc = pk_fma_sb(h, w20b);
+#pragma unroll
+        for (int k = 1; k < 10; ++k) {
+            asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
+                : "=v"(h) : "v"(u), "s"(w1b[k]));
+            acc = (k & 1) ? pk_fma_hi(h, w2[k >> 1], acc) : pk_fma_lo(h, w2[k >> 1], acc);
+        }
+        return acc;
+    }
+};
+
 // wg: the MLP's prepared weights in global memory (uniform address: scalar loads)
 __device__ __forceinline__ f32x2 mlp128_sp2(const float* __restrict__ wg, const V24Lin& lin,
                                             f32x2 u) {
@@ -749,7 +787,9 @@ template <typename T> __device__ __forceinline__ T var_sum_uniform(const T* mp, 
 #ifndef GNND_RESIDENT_WAVES
 #define GNND_RESIDENT_WAVES 4      // min waves per SIMD: 4 -> <= 128 VGPRs (tuning builds vary it)
 #endif
-template <int MODEL, typename T, int G, int R, int QMAX, bool PAD>
+// PADR: trailing slots per lane that may be padding (0: none, 1: only the last, R: any;
+// gnnd_graph fills each check's lanes in order, so padding is always trailing)
+template <int MODEL, typename T, int G, int R, int QMAX, int PADR>
 __global__ void __launch_bounds__(GNND_BLOCK, GNND_RESIDENT_WAVES)
 decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
                        T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem,
@@ -759,6 +799,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     // fp32 GNN models keep x_v pre-scaled by log2(e) so the v->c pre-op is one FMA into
     // the base-2 tanh (tanh_half_base2); the readout re-reads the unscaled x_v from HBM.
     constexpr bool kBase2 = sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI);
+    // fp32 GNN models run the check step on edge PAIRS (packed VALU, see below)
+    constexpr bool kPair = kBase2;
     constexpr int kLogG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N;
@@ -782,8 +824,11 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     for (int i = tid; i < nb * N; i += GNND_BLOCK) {
         int b = fdiv(i, dN), n = i - b * N;
         T xv = xg[i];
-        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
-        else s_xc[b * C + n - V] = xv;
+        if (n < V) {
+            s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
+        } else {
+            s_xc[b * C + n - V] = xv;
+        }
     }
     // padded layouts: the positions past a variable's degree are read by the variable sums
     // and never written, so they must hold 0 (s + 0 == s)
@@ -812,6 +857,18 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     T m[QMAX][R];
     T sc[QMAX];
     int cb[QMAX];              // codeword of the item
+    // fp32 GNN models run the check step on item PAIRS (2j, 2j+1): slot r of both items
+    // rides the two halves of packed VALU ops (v_pk_add/fma_f32), so every non-
+    // transcendental op covers two edges.  An odd last item pairs with itself (identical
+    // arithmetic in every position: batch-independent bits).  m2 holds the pairs' messages.
+    constexpr int QP = kPair ? QMAX / 2 : 1;              // item pairs
+    constexpr bool kSolo = kPair && (QMAX & 1);           // odd last item: slot pairs
+    constexpr int RP = (R + 1) / 2;
+    f32x2 m2[QP][R];           // m2[j][r] = {m of item 2j, m of item 2j+1} at slot r
+    f32x2 ms[RP];              // solo item: {slot 2i, slot 2i+1} (odd R: last pairs itself)
+    f32x2 sc2[QP];
+    Mlp10Pair mlp2;
+    if constexpr (kPair) mlp2.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
         const int f = tid + q * GNND_BLOCK;
@@ -830,6 +887,16 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             m[q][r] = T(0);
         }
     }
+    if constexpr (kPair) {
+#pragma unroll
+        for (int j = 0; j < QP; ++j) {
+            sc2[j] = f32x2{(float)sc[2 * j], (float)sc[2 * j + 1]};
+#pragma unroll
+            for (int r = 0; r < R; ++r) m2[j][r] = f32x2{0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < RP; ++i) ms[i] = f32x2{0.f, 0.f};
+    }
 
     // variable-sum step mapping (see below): lane-invariant when CW divides the block
     const bool vfixed = GNND_BLOCK % CW == 0;
@@ -842,6 +909,73 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     const bool vuni = !WBP && vfixed && g.vgroup * CW >= 64;
 
     for (int it = 0; it < iters; ++it) {
+        if constexpr (kPair) {
+            // tanh(a/2) of two edges, base 2: 1 - 2 / (1 + 2^a'), a' = (S - m) log2e + x'.
+            // {S_v, x_v} arrive as one ds_read_b64 per edge; a' is formed by scalar ops
+            // (packing it would need moves into {S_a, S_b} / {x_a, x_b} pairs), the rest of
+            // the chain is packed
+            auto tanh2 = [&](uint32_t sa, uint32_t sb, int ca, int cbb, f32x2 mprev, int ra, int rb) {
+                const SumX<T> pa = s_sx[ca * V + (int)(sa & 0xffffu)];
+                const SumX<T> pb = s_sx[cbb * V + (int)(sb & 0xffffu)];
+                const f32x2 a = {__builtin_fmaf(pa.s - mprev.x, kLog2e, pa.x),
+                                 __builtin_fmaf(pb.s - mprev.y, kLog2e, pb.x)};
+                f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+                e = e + f32x2{1.f, 1.f};
+                const f32x2 rc = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+                f32x2 t = __builtin_elementwise_fma(rc, f32x2{-2.f, -2.f}, f32x2{1.f, 1.f});
+                if constexpr (PADR > 0) {   // padding slot: position == spare
+                    if (ra >= R - PADR && sa >= ((uint32_t)spare << 16)) t.x = 0.f;
+                    if (rb >= R - PADR && sb >= ((uint32_t)spare << 16)) t.y = 0.f;
+                }
+                return t;
+            };
+            auto update2 = [&](f32x2 u, f32x2 scp, f32x2 mprev) {
+                const f32x2 y = mlp2(u);
+                if constexpr (MODEL == GNND_QGNNI) return __builtin_elementwise_fma(y, scp, mprev);
+                else return y + mprev;
+            };
+#pragma unroll
+            for (int j = 0; j < QP; ++j) {
+                const int qa = 2 * j, qb = 2 * j + 1;
+                f32x2 tv[R], tsum;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    tv[r] = tanh2(ve[qa][r], ve[qb][r], cb[qa], cb[qb], m2[j][r], r, r);
+                    tsum = r == 0 ? tv[0] : tsum + tv[r];
+                }
+                const f32x2 Sc = {group_sum_c<G>(tsum.x), group_sum_c<G>(tsum.y)};
+                T* mba = s_m + cb[qa] * E1;
+                T* mbb = s_m + cb[qb] * E1;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    m2[j][r] = update2(Sc - tv[r], sc2[j], m2[j][r]);
+                    mba[ve[qa][r] >> 16] = m2[j][r].x;
+                    mbb[ve[qb][r] >> 16] = m2[j][r].y;
+                }
+            }
+            if constexpr (kSolo) {
+                // the odd last item: its slots in pairs, the same per-edge arithmetic
+                constexpr int q = QMAX - 1;
+                f32x2 tv[RP];
+                float tsum = 0.f;
+#pragma unroll
+                for (int i = 0; i < RP; ++i) {
+                    const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
+                    tv[i] = tanh2(ve[q][r0], ve[q][r1], cb[q], cb[q], ms[i], r0, r1);
+                    tsum = i == 0 ? tv[0].x : tsum + tv[i].x;
+                    if (2 * i + 1 < R) tsum = tsum + tv[i].y;
+                }
+                const float Sc = group_sum_c<G>(tsum);
+                T* mb = s_m + cb[q] * E1;
+#pragma unroll
+                for (int i = 0; i < RP; ++i) {
+                    const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
+                    ms[i] = update2(f32x2{Sc, Sc} - tv[i], f32x2{(float)sc[q], (float)sc[q]}, ms[i]);
+                    mb[ve[q][r0] >> 16] = ms[i].x;
+                    if (r1 != r0) mb[ve[q][r1] >> 16] = ms[i].y;
+                }
+            }
+        } else
 #pragma unroll
         for (int q = 0; q < QMAX; ++q) {
             T tv[R], cf[R];
@@ -850,7 +984,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t sv = ve[q][r];
-                const bool valid = !PAD || (int)(sv >> 16) != spare;   // every slot real: no mask
+                const bool valid = !(PADR > 0 && r >= R - PADR) || (int)(sv >> 16) != spare;
                 const SumX<T> p = sxb[sv & 0xffffu];
                 T cc = T(0), t;
                 if constexpr (kBase2) t = tanh_half_base2(__builtin_fmaf(p.s - m[q][r], kLog2e, p.x));
@@ -1148,7 +1282,7 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         if (p.resident) {
             auto by_q = [&](auto gtag, auto ptag) -> int {
                 constexpr int G = decltype(gtag)::value;
-                constexpr bool P = decltype(ptag)::value;
+                constexpr int P = decltype(ptag)::value;
                 switch (p.q) {
                     case 3: return go(decode_resident_kernel<MODEL, T, G, R, 3, P>);
                     case 6: return go(decode_resident_kernel<MODEL, T, G, R, 6, P>);
@@ -1169,7 +1303,9 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
                 }
                 return GNND_ERR_UNSUPPORTED;
             };
-            return g.padded ? by_g(std::true_type{}) : by_g(std::false_type{});
+            if (!g.padded) return by_g(std::integral_constant<int, 0>{});
+            if (g.padr == 1) return by_g(std::integral_constant<int, 1>{});
+            return by_g(std::integral_constant<int, R>{});
         }
     }
     if constexpr (MODEL == GNND_V24)

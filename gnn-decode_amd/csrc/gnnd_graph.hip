@@ -72,7 +72,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         return e ? atoi(e) : 0;
     }();
     struct SlotPlan {
-        int G = 0, R = 0, padded = 0;
+        int G = 0, R = 0, padded = 0, padr = 0;
         std::vector<uint32_t> slot, slot_ve;
         std::vector<int> vslot;
     };
@@ -99,6 +99,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         sp.padded = 0;
         for (int c = 0; c < C; ++c) {
             sp.padded |= (cptr[c + 1] - cptr[c]) != sp.G * sp.R;
+            sp.padr = std::max(sp.padr, std::min(sp.R, sp.G * sp.R - (cptr[c + 1] - cptr[c])));
             for (int k = cptr[c], i = 0; k < cptr[c + 1]; ++k, ++i) {
                 int e = cedge[k];
                 int pos = c * sp.G * sp.R + i;
@@ -214,6 +215,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         const int ns = (int)plans[i].slot.size();
         pv.G = plans[i].G; pv.R = plans[i].R;
         pv.padded = plans[i].padded;
+        pv.padr = plans[i].padr;
         pv.logG = 0;
         while ((1 << pv.logG) < pv.G) ++pv.logG;
         pv.slot = (const uint32_t*)(d + plan_off[i]);
