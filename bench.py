@@ -100,7 +100,7 @@ VALU_ISSUE_PER_S = 256 * 2.4e9
 TRANS_OPS_PER_S = 1024 * 64 / 8 * 2.4e9
 
 
-def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
+def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
     """Time the oracle (numpy restatement, 1 thread) on a bounded sample of this workload
     and compare its outputs with the GPU outputs for the same codewords."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
@@ -122,6 +122,7 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
     # fp64 whatever the GPU dtype
     ref_dt = np.float64 if model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10') else None
     done, t_total, max_err, mism = 0, 0.0, 0.0, 0
+    err_gpu = err_orc = 0
     c_bits = c_gpu = c_orc = 0
     while t_total < seconds and done + chunk <= x_all.size(0):
         xs = x_all[done:done + chunk].cpu().numpy().reshape(-1, 1)
@@ -134,6 +135,9 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
         ref = ref.astype(np.float64)
         max_err = max(max_err, float(np.abs(got - ref).max()))
         mism += int(((got > 0.5) != (ref > 0.5)).sum())
+        lab = labels.view(-1, g.V)[done:done + chunk].double().cpu().numpy().reshape(-1, 1) > 0.5
+        err_gpu += int(((got > 0.5) != lab).sum())
+        err_orc += int(((ref > 0.5) != lab).sum())
         if cond and c_bits < 8 * chunk * g.V:
             r64 = gnn_oracle.decode(model, H, xs.astype(np.float64), T, w)
             c_bits += r64.size
@@ -148,7 +152,10 @@ def cpu_baseline(model, H, state, x_dev, out_dev, g, T, seconds):
                      f'numpy restatement ({"fp64" if ref_dt is not None else str(x_dev.dtype)[6:]}), '
                      f'1 thread, {t_total:.1f} s',
            'parity_max_abs_err': max_err, 'parity_hard_decision_mismatches': mism,
-           'parity_bits_compared': done * g.V}
+           'parity_bits_compared': done * g.V,
+           # "matched BER": bit error rate of the GPU and of the oracle on the same sample
+           'sample_ber_gpu': err_gpu / max(1, done * g.V),
+           'sample_ber_oracle': err_orc / max(1, done * g.V)}
     if cond:
         res['conditioning_vs_f64_oracle'] = {'bits': c_bits, 'gpu_f32_mismatches': c_gpu,
                                              'oracle_f32_mismatches': c_orc}
@@ -267,7 +274,13 @@ def main():
         errs = ((out > 0.5).to(labels.dtype) != labels).sum()
         if world > 1:
             dist.all_reduce(errs)
+        # uncoded reference point: hard decision on the channel LLR alone (classical codes)
+        ch_errs = ((x.view(a.batch, g.N)[:, :g.V] < 0).reshape(-1, 1).to(labels.dtype) != labels).sum() \
+            if classical else torch.zeros((), device=dev)
+        if world > 1:
+            dist.all_reduce(ch_errs)
     ber = float(errs.item()) / (a.batch * g.V * world)
+    ch_ber = float(ch_errs.item()) / (a.batch * g.V * world) if classical else None
 
     if rank == 0:
         fl, trans = flops_per_codeword(a.model, g, T)
@@ -294,7 +307,10 @@ def main():
                        'global_batch': a.batch * world, 'parallelism': f'dp{world} (codeword shards)',
                        'codewords_per_workgroup': plan['cw'], 'lds_bytes_per_workgroup': plan['lds'],
                        'items_per_lane': plan['items_per_lane'],
-                       'hard_decision_error_rate': ber},
+                       'hard_decision_error_rate': ber,
+                       'channel_hard_decision_error_rate': ch_ber,
+                       'weights': 'random init (seeded): compute cost is weight-independent; '
+                                  'BER parity vs the oracle is in cpu_baseline'},
             'roofline': {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
                          'frac': achieved / peak, 'traffic': traffic,
                          'kernel': f"{plan['kernel']}<{a.model}, {a.dtype}>",
@@ -312,7 +328,7 @@ def main():
                          'hbm_io_frac': io_bytes / kernel_s / 1e9 / PEAK_HBM_GBS},
         }
         if a.cpu_seconds > 0 and world == 1:
-            res['cpu_baseline'] = cpu_baseline(a.model, H, state, x, out, g, T, a.cpu_seconds)
+            res['cpu_baseline'] = cpu_baseline(a.model, H, state, x, out, labels, g, T, a.cpu_seconds)
         else:
             res['cpu_baseline'] = None
         print(json.dumps(res), flush=True)
