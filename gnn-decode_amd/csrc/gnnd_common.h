@@ -113,8 +113,59 @@ template <typename T> __device__ __forceinline__ T g_clamp(T x, T lo, T hi) {
 }
 
 // torch.nn.Softplus(beta=1, threshold=20): x > 20 ? x : log1p(exp(x))
+// torch.nn.Softplus (beta 1, threshold 20): x > 20 ? x : log1p(exp(x)) — fp64, evaluated as
+// max(x, 0) + log1p(exp(-|x|)) without libm (libm's exp + double-double log1p cost 177 VALU
+// ops on gfx950; this form 54).  exp: k = rint(a log2e), r = a - k ln2 (two-part ln2),
+// degree-13 Taylor on |r| <= 0.347 (truncation < 2e-16), ldexp.  log1p(u), u in (0, 1]:
+// m = 1 + u with its exact rounding error c = u - (m - 1); m' = m or m/2 in [0.707, 1.414];
+// log m' = 2 atanh(s), s = (m' - 1) / (m' + 1) (one Newton-refined v_rcp_f64), odd series
+// to s^21 (|s| <= 0.172: truncation < 1e-16 relative); + j ln2 + c/m.  A few ulp of
+// libm, far inside the fp64 parity tolerance (1e-10 relative on decoder outputs).
+// polynomial coefficients in constant memory: uniform scalar loads keep them in SGPRs
+// (a 64-bit literal cannot feed a VOP3 v_fma_f64; as literals every Horner step costs a
+// v_mov_b64 into the v_fmac accumulator)
+__constant__ static const double kSpCoef[23] = {
+    1.0 / 6227020800.0, 1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0,   // exp: 1/13!..
+    1.0 / 362880.0, 1.0 / 40320.0, 1.0 / 5040.0, 1.0 / 720.0, 1.0 / 120.0, 1.0 / 24.0,
+    1.0 / 6.0, 0.5, 1.0,
+    1.0 / 21.0, 1.0 / 19.0, 1.0 / 17.0, 1.0 / 15.0, 1.0 / 13.0, 1.0 / 11.0,      // atanh
+    1.0 / 9.0, 1.0 / 7.0, 1.0 / 5.0, 1.0 / 3.0};
+__device__ __forceinline__ double exp_nonpos_f64(double a) {          // a <= 0
+    a = a > -750.0 ? a : -750.0;                                       // exp(-750) == 0
+    const double k = __builtin_rint(a * 1.4426950408889634);
+    double r = __builtin_fma(-k, 6.93147180369123816490e-01, a);       // ln2 hi
+    r = __builtin_fma(-k, 1.90821492927058770002e-10, r);              // ln2 lo
+    double p = kSpCoef[0];
+#pragma unroll
+    for (int i = 1; i < 13; ++i) p = __builtin_fma(p, r, kSpCoef[i]);
+    p = __builtin_fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)k);
+}
+__device__ __forceinline__ double log1p_unit_f64(double u) {          // u in [0, 1]
+    const double m = 1.0 + u;
+    const double c = u - (m - 1.0);                                    // exact
+    const bool hi = m > 1.4142135623730951;
+    const double mp = hi ? 0.5 * m : m;
+    const double f = mp - 1.0;                                         // exact (Sterbenz)
+    const double d = 2.0 + f;
+    double rc = __builtin_amdgcn_rcp(d);
+    rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
+    double s = f * rc;
+    s = __builtin_fma(__builtin_fma(-s, d, f), rc, s);                 // f / d, ~0.5 ulp
+    const double z = s * s;
+    double q = kSpCoef[13];
+#pragma unroll
+    for (int i = 14; i < 23; ++i) q = __builtin_fma(q, z, kSpCoef[i]);
+    const double s2 = s + s;
+    double l = __builtin_fma(s2 * z, q, s2);                           // log m'
+    l = hi ? l + 6.93147180559945309417e-01 : l;
+    return __builtin_fma(c, __builtin_amdgcn_rcp(m), l);               // + c / m
+}
+// branch-free: both sides evaluated, selected at the end
 __device__ __forceinline__ double softplus_ref(double x) {
-    return x > 20.0 ? x : log1p(exp(x));
+    const double r = log1p_unit_f64(exp_nonpos_f64(-__builtin_fabs(x)));
+    const double y = x > 0.0 ? x + r : r;
+    return x > 20.0 ? x : y;
 }
 template <typename T> __device__ __forceinline__ T sigmoid_ref(T x) {
     return T(1) / (T(1) + g_exp(-x));
