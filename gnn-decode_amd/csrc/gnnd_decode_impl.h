@@ -435,6 +435,43 @@ __device__ __forceinline__ float bp_msg_f32(float lam2, float n, float hi) {
         return kLn2 * __builtin_amdgcn_logf((1.f + p) * __builtin_amdgcn_rcpf(1.f - p));
 }
 
+// the same two functions on TWO edges (the paired check step of the resident kernel):
+// every non-transcendental op is one packed VALU op for both; per half the arithmetic is
+// identical to the scalar forms above.  The sign (-1)^n of an integer-valued count n is
+// 1 - 2 (n - 2 floor(n / 2)) (torch.cos(pi n) rounds to exactly +-1 there too).
+__device__ __forceinline__ f32x2 bp_log2tanh_f32x2(f32x2 a, float lo) {
+    const f32x2 z = f32x2{fminf(fabsf(a.x), 10.f), fminf(fabsf(a.y), 10.f)} * 0.5f;
+    const f32x2 z2 = z * z;
+    f32x2 tp = __builtin_elementwise_fma(z2, f32x2{62.f / 2835.f, 62.f / 2835.f},
+                                         f32x2{-17.f / 315.f, -17.f / 315.f});
+    tp = __builtin_elementwise_fma(z2, tp, f32x2{2.f / 15.f, 2.f / 15.f});
+    tp = __builtin_elementwise_fma(z2, tp, f32x2{-1.f / 3.f, -1.f / 3.f});
+    tp = __builtin_elementwise_fma(z2 * z, tp, z);
+    const f32x2 ea = z * (-2.f * kLog2e);
+    const f32x2 e = {__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+    const f32x2 d = f32x2{1.f, 1.f} + e;
+    const f32x2 te = (f32x2{1.f, 1.f} - e) * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    const f32x2 t = {z.x < 0.3f ? tp.x : te.x, z.y < 0.3f ? tp.y : te.y};
+    return f32x2{__builtin_amdgcn_logf(fmaxf(t.x, lo)), __builtin_amdgcn_logf(fmaxf(t.y, lo))};
+}
+template <bool QUANTUM>
+__device__ __forceinline__ f32x2 bp_msg_f32x2(f32x2 lam2, f32x2 n, float hi) {
+    const f32x2 h = n * 0.5f;
+    const f32x2 par = __builtin_elementwise_fma(f32x2{__builtin_floorf(h.x), __builtin_floorf(h.y)},
+                                                f32x2{-2.f, -2.f}, n);
+    const f32x2 sgn = __builtin_elementwise_fma(par, f32x2{-2.f, -2.f}, f32x2{1.f, 1.f});
+    f32x2 p = f32x2{__builtin_amdgcn_exp2f(lam2.x), __builtin_amdgcn_exp2f(lam2.y)} * sgn;
+    p = f32x2{__builtin_amdgcn_fmed3f(p.x, -hi, hi), __builtin_amdgcn_fmed3f(p.y, -hi, hi)};
+    const f32x2 up = f32x2{1.f, 1.f} + p, dn = f32x2{1.f, 1.f} - p;
+    if constexpr (QUANTUM)
+        return (f32x2{__builtin_amdgcn_logf(up.x), __builtin_amdgcn_logf(up.y)} -
+                f32x2{__builtin_amdgcn_logf(dn.x), __builtin_amdgcn_logf(dn.y)}) * kLn2;
+    else {
+        const f32x2 q = up * f32x2{__builtin_amdgcn_rcpf(dn.x), __builtin_amdgcn_rcpf(dn.y)};
+        return f32x2{__builtin_amdgcn_logf(q.x), __builtin_amdgcn_logf(q.y)} * kLn2;
+    }
+}
+
 template <int MODEL, typename T> struct EdgeMath {
     static constexpr bool BP = ModelTraits<MODEL>::bp;
     static constexpr bool kFastBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP);
@@ -799,8 +836,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     // fp32 GNN models keep x_v pre-scaled by log2(e) so the v->c pre-op is one FMA into
     // the base-2 tanh (tanh_half_base2); the readout re-reads the unscaled x_v from HBM.
     constexpr bool kBase2 = sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI);
-    // fp32 GNN models run the check step on edge PAIRS (packed VALU, see below)
-    constexpr bool kPair = kBase2;
+    // fp32 GNN and BP models run the check step on edge PAIRS (packed VALU, see below)
+    constexpr bool kPairBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP);
+    constexpr bool kPair = kBase2 || kPairBP;
     constexpr int kLogG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N;
@@ -868,7 +906,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     f32x2 ms[RP];              // solo item: {slot 2i, slot 2i+1} (odd R: last pairs itself)
     f32x2 sc2[QP];
     Mlp10Pair mlp2;
-    if constexpr (kPair) mlp2.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
+    if constexpr (kBase2) mlp2.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
         const int f = tid + q * GNND_BLOCK;
@@ -910,45 +948,66 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 
     for (int it = 0; it < iters; ++it) {
         if constexpr (kPair) {
-            // tanh(a/2) of two edges, base 2: 1 - 2 / (1 + 2^a'), a' = (S - m) log2e + x'.
-            // {S_v, x_v} arrive as one ds_read_b64 per edge; a' is formed by scalar ops
-            // (packing it would need moves into {S_a, S_b} / {x_a, x_b} pairs), the rest of
-            // the chain is packed
-            auto tanh2 = [&](uint32_t sa, uint32_t sb, int ca, int cbb, f32x2 mprev, int ra, int rb) {
+            // check-node pre-op of two edges.  GNN: tanh(a/2) in base 2, 1 - 2 / (1 + 2^a'),
+            // a' = (S - m) log2e + x'.  BP: {log2|tanh(a/2)|, [a < 0]}, a = (S - m) + x.
+            // {S_v, x_v} arrive as one ds_read_b64 per edge; the leave-one-out and the
+            // prior are added by scalar ops (packing them would need moves into {S_a, S_b}
+            // / {x_a, x_b} pairs), the rest of the chain is packed
+            auto pre2 = [&](uint32_t sa, uint32_t sb, int ca, int cbb, f32x2 mprev, int ra, int rb,
+                            f32x2& cc) {
                 const SumX<T> pa = s_sx[ca * V + (int)(sa & 0xffffu)];
                 const SumX<T> pb = s_sx[cbb * V + (int)(sb & 0xffffu)];
-                const f32x2 a = {__builtin_fmaf(pa.s - mprev.x, kLog2e, pa.x),
-                                 __builtin_fmaf(pb.s - mprev.y, kLog2e, pb.x)};
-                f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-                e = e + f32x2{1.f, 1.f};
-                const f32x2 rc = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
-                f32x2 t = __builtin_elementwise_fma(rc, f32x2{-2.f, -2.f}, f32x2{1.f, 1.f});
+                f32x2 t;
+                if constexpr (kBase2) {
+                    const f32x2 a = {__builtin_fmaf(pa.s - mprev.x, kLog2e, pa.x),
+                                     __builtin_fmaf(pb.s - mprev.y, kLog2e, pb.x)};
+                    f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+                    e = e + f32x2{1.f, 1.f};
+                    const f32x2 rc = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+                    t = __builtin_elementwise_fma(rc, f32x2{-2.f, -2.f}, f32x2{1.f, 1.f});
+                    cc = f32x2{0.f, 0.f};
+                } else {
+                    const f32x2 a = {(pa.s - mprev.x) + pa.x, (pb.s - mprev.y) + pb.x};
+                    cc = f32x2{a.x < 0.f ? 1.f : 0.f, a.y < 0.f ? 1.f : 0.f};
+                    t = bp_log2tanh_f32x2(a, MODEL == GNND_QBP ? 1e-20f : 1e-7f);
+                }
                 if constexpr (PADR > 0) {   // padding slot: position == spare
-                    if (ra >= R - PADR && sa >= ((uint32_t)spare << 16)) t.x = 0.f;
-                    if (rb >= R - PADR && sb >= ((uint32_t)spare << 16)) t.y = 0.f;
+                    if (ra >= R - PADR && sa >= ((uint32_t)spare << 16)) { t.x = 0.f; cc.x = 0.f; }
+                    if (rb >= R - PADR && sb >= ((uint32_t)spare << 16)) { t.y = 0.f; cc.y = 0.f; }
                 }
                 return t;
             };
-            auto update2 = [&](f32x2 u, f32x2 scp, f32x2 mprev) {
-                const f32x2 y = mlp2(u);
-                if constexpr (MODEL == GNND_QGNNI) return __builtin_elementwise_fma(y, scp, mprev);
-                else return y + mprev;
+            // c->v update of two edges from the leave-one-out sums u (and sign counts n)
+            auto post2 = [&](f32x2 u, f32x2 n, f32x2 scp, f32x2 mprev) {
+                if constexpr (kBase2) {
+                    const f32x2 y = mlp2(u);
+                    if constexpr (MODEL == GNND_QGNNI) return __builtin_elementwise_fma(y, scp, mprev);
+                    else return y + mprev;
+                } else if constexpr (MODEL == GNND_QBP) {
+                    return bp_msg_f32x2<true>(u, __builtin_elementwise_fma(f32x2{1.f, 1.f} - scp,
+                                                  f32x2{0.5f, 0.5f}, n), cst<float>(1 - 1e-12));
+                } else {
+                    return bp_msg_f32x2<false>(u, n, cst<float>(1 - 1e-7));
+                }
             };
 #pragma unroll
             for (int j = 0; j < QP; ++j) {
                 const int qa = 2 * j, qb = 2 * j + 1;
-                f32x2 tv[R], tsum;
+                f32x2 tv[R], cv[R], tsum, csum;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    tv[r] = tanh2(ve[qa][r], ve[qb][r], cb[qa], cb[qb], m2[j][r], r, r);
+                    tv[r] = pre2(ve[qa][r], ve[qb][r], cb[qa], cb[qb], m2[j][r], r, r, cv[r]);
                     tsum = r == 0 ? tv[0] : tsum + tv[r];
+                    if constexpr (kPairBP) csum = r == 0 ? cv[0] : csum + cv[r];
                 }
                 const f32x2 Sc = {group_sum_c<G>(tsum.x), group_sum_c<G>(tsum.y)};
+                f32x2 Sc2 = {0.f, 0.f};
+                if constexpr (kPairBP) Sc2 = f32x2{group_sum_c<G>(csum.x), group_sum_c<G>(csum.y)};
                 T* mba = s_m + cb[qa] * E1;
                 T* mbb = s_m + cb[qb] * E1;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    m2[j][r] = update2(Sc - tv[r], sc2[j], m2[j][r]);
+                    m2[j][r] = post2(Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
                     mba[ve[qa][r] >> 16] = m2[j][r].x;
                     mbb[ve[qb][r] >> 16] = m2[j][r].y;
                 }
@@ -956,21 +1015,28 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             if constexpr (kSolo) {
                 // the odd last item: its slots in pairs, the same per-edge arithmetic
                 constexpr int q = QMAX - 1;
-                f32x2 tv[RP];
-                float tsum = 0.f;
+                f32x2 tv[RP], cv[RP];
+                float tsum = 0.f, csum = 0.f;
 #pragma unroll
                 for (int i = 0; i < RP; ++i) {
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
-                    tv[i] = tanh2(ve[q][r0], ve[q][r1], cb[q], cb[q], ms[i], r0, r1);
+                    tv[i] = pre2(ve[q][r0], ve[q][r1], cb[q], cb[q], ms[i], r0, r1, cv[i]);
                     tsum = i == 0 ? tv[0].x : tsum + tv[i].x;
                     if (2 * i + 1 < R) tsum = tsum + tv[i].y;
+                    if constexpr (kPairBP) {
+                        csum = i == 0 ? cv[0].x : csum + cv[i].x;
+                        if (2 * i + 1 < R) csum = csum + cv[i].y;
+                    }
                 }
                 const float Sc = group_sum_c<G>(tsum);
+                float Sc2 = 0.f;
+                if constexpr (kPairBP) Sc2 = group_sum_c<G>(csum);
                 T* mb = s_m + cb[q] * E1;
 #pragma unroll
                 for (int i = 0; i < RP; ++i) {
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
-                    ms[i] = update2(f32x2{Sc, Sc} - tv[i], f32x2{(float)sc[q], (float)sc[q]}, ms[i]);
+                    ms[i] = post2(f32x2{Sc, Sc} - tv[i], f32x2{Sc2, Sc2} - cv[i],
+                                  f32x2{(float)sc[q], (float)sc[q]}, ms[i]);
                     mb[ve[q][r0] >> 16] = ms[i].x;
                     if (r1 != r0) mb[ve[q][r1] >> 16] = ms[i].y;
                 }
