@@ -93,11 +93,8 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 // scalar math with reference (torch CPU) semantics, float and double overloads
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ float g_tanh(float x) { return tanhf(x); }
-__device__ __forceinline__ double g_tanh(double x) { return tanh(x); }
 __device__ __forceinline__ float g_log(float x) { return logf(x); }
-__device__ __forceinline__ double g_log(double x) { return log(x); }
 __device__ __forceinline__ float g_exp(float x) { return expf(x); }
-__device__ __forceinline__ double g_exp(double x) { return exp(x); }
 __device__ __forceinline__ float g_log1p(float x) { return log1pf(x); }
 __device__ __forceinline__ double g_log1p(double x) { return log1p(x); }
 __device__ __forceinline__ float g_cos(float x) { return cosf(x); }
@@ -112,7 +109,6 @@ template <typename T> __device__ __forceinline__ T g_clamp(T x, T lo, T hi) {
     return x < lo ? lo : (x > hi ? hi : x);
 }
 
-// torch.nn.Softplus(beta=1, threshold=20): x > 20 ? x : log1p(exp(x))
 // torch.nn.Softplus (beta 1, threshold 20): x > 20 ? x : log1p(exp(x)) — fp64, evaluated as
 // max(x, 0) + log1p(exp(-|x|)) without libm (libm's exp + double-double log1p cost 177 VALU
 // ops on gfx950; this form 54).  exp: k = rint(a log2e), r = a - k ln2 (two-part ln2),
@@ -166,6 +162,66 @@ __device__ __forceinline__ double softplus_ref(double x) {
     const double r = log1p_unit_f64(exp_nonpos_f64(-__builtin_fabs(x)));
     const double y = x > 0.0 ? x + r : r;
     return x > 20.0 ? x : y;
+}
+// fp64 exp / log / tanh for the decoders' fp64 (reference-dtype) paths, same scheme as the
+// Softplus above: no libm branches or double-double tails, a few ulp.
+__device__ __forceinline__ double exp_poly_f64(double r) {           // e^r, |r| <= 0.347
+    double p = kSpCoef[0];
+#pragma unroll
+    for (int i = 1; i < 13; ++i) p = __builtin_fma(p, r, kSpCoef[i]);
+    return __builtin_fma(p, r, 1.0);
+}
+__device__ __forceinline__ double g_exp(double x) {
+    x = __builtin_fmin(__builtin_fmax(x, -750.0), 710.0);
+    const double k = __builtin_rint(x * 1.4426950408889634);
+    double r = __builtin_fma(-k, 6.93147180369123816490e-01, x);
+    r = __builtin_fma(-k, 1.90821492927058770002e-10, r);
+    return __builtin_ldexp(exp_poly_f64(r), (int)k);
+}
+// expm1 without cancellation: 2^k (e^r - 1) + (2^k - 1), e^r - 1 = r P(r) by the Taylor
+// series (no leading 1); exact path at k = 0
+__device__ __forceinline__ double expm1_f64(double x) {
+    x = __builtin_fmin(__builtin_fmax(x, -750.0), 710.0);
+    const double k = __builtin_rint(x * 1.4426950408889634);
+    double r = __builtin_fma(-k, 6.93147180369123816490e-01, x);
+    r = __builtin_fma(-k, 1.90821492927058770002e-10, r);
+    double p = kSpCoef[0];
+#pragma unroll
+    for (int i = 1; i < 13; ++i) p = __builtin_fma(p, r, kSpCoef[i]);
+    const double em = r * p;                                           // e^r - 1 = r (1 + r/2 + ...)
+    const double tk = __builtin_ldexp(1.0, (int)k);
+    return __builtin_fma(tk, em, tk - 1.0);
+}
+__device__ __forceinline__ double g_log(double x) {                   // x > 0, normal
+    int e = __builtin_amdgcn_frexp_exp(x);
+    double m = __builtin_amdgcn_frexp_mant(x);                         // [0.5, 1)
+    const bool lo = m < 0.7071067811865476;
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double f = m - 1.0;                                          // exact
+    const double d = 2.0 + f;
+    double rc = __builtin_amdgcn_rcp(d);
+    rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
+    double s = f * rc;
+    s = __builtin_fma(__builtin_fma(-s, d, f), rc, s);
+    const double z = s * s;
+    double q = kSpCoef[13];
+#pragma unroll
+    for (int i = 14; i < 23; ++i) q = __builtin_fma(q, z, kSpCoef[i]);
+    const double s2 = s + s;
+    const double l = __builtin_fma(s2 * z, q, s2);
+    const double de = (double)e;
+    return __builtin_fma(de, 6.93147180369123816490e-01, __builtin_fma(de, 1.90821492927058770002e-10, l));
+}
+// tanh(x) = -expm1(-2|x|) / (2 + expm1(-2|x|)), sign restored
+__device__ __forceinline__ double g_tanh(double x) {
+    const double em = expm1_f64(-2.0 * __builtin_fabs(x));
+    const double d = 2.0 + em;                                         // (1, 2]
+    double rc = __builtin_amdgcn_rcp(d);
+    rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
+    double t = -em * rc;
+    t = __builtin_fma(__builtin_fma(t, d, em), -rc, t);                // -em / d, ~0.5 ulp
+    return __builtin_copysign(t, x);
 }
 template <typename T> __device__ __forceinline__ T sigmoid_ref(T x) {
     return T(1) / (T(1) + g_exp(-x));
@@ -223,7 +279,7 @@ __device__ __forceinline__ float tanh_half_fast(float a) {
     float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
     return copysignf(t, a);
 }
-__device__ __forceinline__ double tanh_half_fast(double a) { return tanh(a / 2.0); }
+__device__ __forceinline__ double tanh_half_fast(double a) { return g_tanh(a / 2.0); }
 // tanh(a/2) from the base-2 scaled argument a2 = a * log2(e):  1 - 2 / (1 + 2^a2).
 // Saturates to +-1 (2^a2 -> inf or 0), never NaN; absolute error ~1.5e-7 near 0, i.e.
 // below the rounding of the 24-term check sums it feeds.  4 VALU ops, 2 transcendental.

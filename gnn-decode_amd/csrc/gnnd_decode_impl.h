@@ -57,9 +57,9 @@ template <int MODEL> struct ModelTraits {
 // the fp64 reference instead of saturating at log(2^25).
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ double wbp_L(double a, double& c) {
-    const double t = tanh(a / 2.0);
+    const double t = g_tanh(a / 2.0);
     c = t < 0.0 ? 1.0 : 0.0;
-    return log(g_clamp(fabs(t), 1e-20, 1e10));
+    return g_log(g_clamp(fabs(t), 1e-20, 1e10));
 }
 // fp32: BASE-2 log magnitude log2|tanh(a/2)| on the native v_exp/v_log/v_rcp, resolving
 // 1 - |t| down to fp32's range (fp64 resolves it down to 1e-16; fp32 tanh itself would
@@ -86,8 +86,8 @@ __device__ __forceinline__ float wbp_L(float a, float& c) {
 __device__ __forceinline__ double wbp_out(double lam, double n, double s) {
     n = n + (1.0 - s) / 2.0;
     const double hi = 1 - 1e-15;
-    const double p = g_clamp(exp(lam) * cos_pi(n), -hi, hi);
-    return log(1.0 + p) - log(1.0 - p);
+    const double p = g_clamp(g_exp(lam) * cos_pi(n), -hi, hi);
+    return g_log(1.0 + p) - g_log(1.0 - p);
 }
 // fp32: lam2 = base-2 leave-one-out log magnitude (<= 0), |p| = 2^lam2.  1 - |p| through
 // expm1 (degree-8 Taylor for |lam| < 0.35) so it stays accurate as |p| -> 1, clamped at
