@@ -266,6 +266,22 @@ template <int G> __device__ __forceinline__ float group_sum_c(float v) {
     if constexpr (G > 32) v += __shfl_xor(v, 32);
     return v;
 }
+// fp64: the same butterfly, each step moving the two 32-bit halves with DPP
+template <int CTRL> __device__ __forceinline__ double dpp_mov(double v) {
+    const int2 h = __builtin_bit_cast(int2, v);
+    const int2 r = {__builtin_amdgcn_update_dpp(0, h.x, CTRL, 0xf, 0xf, false),
+                    __builtin_amdgcn_update_dpp(0, h.y, CTRL, 0xf, 0xf, false)};
+    return __builtin_bit_cast(double, r);
+}
+template <int G> __device__ __forceinline__ double group_sum_c(double v) {
+    if constexpr (G > 1) v += dpp_mov<0xB1>(v);
+    if constexpr (G > 2) v += dpp_mov<0x4E>(v);
+    if constexpr (G > 4) v += dpp_mov<0x141>(v);
+    if constexpr (G > 8) v += dpp_mov<0x140>(v);
+    if constexpr (G > 16) v += __shfl_xor(v, 16);
+    if constexpr (G > 32) v += __shfl_xor(v, 32);
+    return v;
+}
 __device__ __forceinline__ double group_sum(double v, int G) {
     for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o);
     return v;

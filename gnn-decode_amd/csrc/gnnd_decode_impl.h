@@ -1204,6 +1204,14 @@ size_t lds_target() {
     }();
     return v;
 }
+// GNND_NO_F64_RESIDENT=1: fp64 light models on the streaming kernel (A/B)
+bool f64_resident_disabled() {
+    static bool v = [] {
+        const char* e = getenv("GNND_NO_F64_RESIDENT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
 bool resident_disabled() {
     static bool v = [] {
         const char* e = getenv("GNND_NO_RESIDENT");
@@ -1237,8 +1245,16 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const size_t wb = align16((size_t)lds_weights(model) * esz);
     const size_t target = lds_target();
     const bool light = model != GNND_V24;
-    if (light && dtype == GNND_F32 && gr->rview.G <= 16 && !resident_disabled()) {
+    // fp64 (the quantum scripts' dtype): the same kernel with scalar math, fewer items per
+    // lane (a double message takes two VGPRs) and twice the LDS budget (2 workgroups/CU).
+    // Measured faster for the quantum models on the toric code (Q/BP +24 %, QGNNI +35 %,
+    // decoder_v1_0 +11 %) and slower for the classical ones on BCH (-8..-10 %, whose
+    // reference dtype is fp32 anyway): quantum models only.
+    const bool quantum = model == GNND_QBP || model == GNND_QGNNI || model == GNND_NBP || model == GNND_V10;
+    const bool f64res = dtype == GNND_F64 && quantum && !f64_resident_disabled();
+    if (light && (dtype == GNND_F32 || f64res) && gr->rview.G <= 16 && !resident_disabled()) {
         const GraphView& g = gr->rview;          // instantiated group sizes 1..16
+        const size_t target = dtype == GNND_F64 ? 2 * lds_target() : lds_target();
         const int IC = g.C * g.G;
         // message layout for a tile of cw codewords: with cw | 256 a wave sums 64 / cw
         // consecutive var_ord entries per step, so the layout padded for that group size
@@ -1268,7 +1284,8 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
             return e ? atoi(e) : 0;
         }();
         for (int q : kResidentQ) {
-            if (q * (2 * g.R + 2) > kResidentRegBudget) continue;
+            if (dtype == GNND_F32 ? q * (2 * g.R + 2) > kResidentRegBudget
+                                  : (q > 6 || q * (3 * g.R + 3) > kResidentRegBudget)) continue;
             if (force_q && q != force_q) continue;
             int cw = q * GNND_BLOCK / IC;               // largest tile that fits q items/lane
             if (cw > 64) cw = 64;
@@ -1344,7 +1361,7 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         GNND_LAUNCH_CHECK();
         return GNND_OK;
     };
-    if constexpr (MODEL != GNND_V24 && sizeof(T) == 4) {
+    if constexpr (MODEL != GNND_V24) {
         if (p.resident) {
             auto by_q = [&](auto gtag, auto ptag) -> int {
                 constexpr int G = decltype(gtag)::value;
@@ -1352,9 +1369,9 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
                 switch (p.q) {
                     case 3: return go(decode_resident_kernel<MODEL, T, G, R, 3, P>);
                     case 6: return go(decode_resident_kernel<MODEL, T, G, R, 6, P>);
-                    case 9: if constexpr (R <= 3) return go(decode_resident_kernel<MODEL, T, G, R, 9, P>);
+                    case 9: if constexpr (R <= 3 && sizeof(T) == 4) return go(decode_resident_kernel<MODEL, T, G, R, 9, P>);
                             break;
-                    case 12: if constexpr (R <= 2) return go(decode_resident_kernel<MODEL, T, G, R, 12, P>);
+                    case 12: if constexpr (R <= 2 && sizeof(T) == 4) return go(decode_resident_kernel<MODEL, T, G, R, 12, P>);
                              break;
                 }
                 return GNND_ERR_UNSUPPORTED;

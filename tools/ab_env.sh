@@ -17,10 +17,16 @@ run() {  # tag args...
     grep '^{' "$OUT/$tag.$mode.log" | sed "s/^{/{\"ab\": \"$tag.$mode\", /" >> "$OUT/ab.jsonl"
   done
 }
-run cgnni_bch --steps 100
-run cbp_bch --model cbp --steps 100
-run cgnni_ldpc --code ldpc_648_324 --batch 131072 --steps 30
-run cbp_ldpc --model cbp --code ldpc_648_324 --batch 131072 --steps 30
-run qbp_toric5 --model qbp --code toric_5 --steps 100
-run qgnni_toric5 --model qgnni --code toric_5 --steps 100
+if [ "${3:-f32}" = f64 ]; then
+  for m in qbp qgnni nbp v10; do run ${m}_toric5_f64 --model $m --code toric_5 --dtype f64 --steps 10 --warmup 2; done
+  run cbp_bch_f64 --model cbp --dtype f64 --steps 10 --warmup 2
+  run cgnni_bch_f64 --dtype f64 --steps 10 --warmup 2
+else
+  run cgnni_bch --steps 100
+  run cbp_bch --model cbp --steps 100
+  run cgnni_ldpc --code ldpc_648_324 --batch 131072 --steps 30
+  run cbp_ldpc --model cbp --code ldpc_648_324 --batch 131072 --steps 30
+  run qbp_toric5 --model qbp --code toric_5 --steps 100
+  run qgnni_toric5 --model qgnni --code toric_5 --steps 100
+fi
 echo done
