@@ -24,6 +24,11 @@ run c3_v24_toric5_f64 900 --model v24 --code toric_5 --dtype f64 --steps 10 --wa
 # config 4: LDPC(648,324) per-GPU shard of the 1M-codeword job (131072 per GPU), CGNNI and BP
 run c4_cgnni_ldpc 600 --code ldpc_648_324 --batch 131072 --steps 50
 run c4_cbp_ldpc 600 --model cbp --code ldpc_648_324 --batch 131072 --steps 50
+# quantum BP / QGNNI (quantum/BP.py, quantum/QGNNI.py) on toric d=5: fp32 and the reference fp64
+run qbp_toric5_f32 600 --model qbp --code toric_5 --steps 100
+run qbp_toric5_f64 600 --model qbp --code toric_5 --dtype f64 --steps 20 --cpu-seconds 5
+run qgnni_toric5_f32 600 --model qgnni --code toric_5 --steps 100
+run qgnni_toric5_f64 600 --model qgnni --code toric_5 --dtype f64 --steps 20 --cpu-seconds 5
 # weighted (neural) BP, quantum/neural_BP.py at the reference L = 4 and at L = 5
 run nbp_toric4_f32 600 --model nbp --code toric_4 --steps 50
 run nbp_toric5_f64 600 --model nbp --code toric_5 --dtype f64 --steps 20 --cpu-seconds 5
