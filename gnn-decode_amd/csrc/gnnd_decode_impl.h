@@ -74,14 +74,38 @@ __device__ __forceinline__ float wbp_L(float a, float& c) {
     tp = __builtin_fmaf(z2, tp, -1.f / 3.f);
     tp = __builtin_fmaf(z2 * z, tp, z);
     const float e = __builtin_amdgcn_exp2f(-y * kLog2e);
-    const float lmid = __builtin_amdgcn_logf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e));
+    const float te = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
     const float e2 = e * e;
     float at = __builtin_fmaf(e2, 1.f / 7.f, 1.f / 5.f);
     at = __builtin_fmaf(e2, at, 1.f / 3.f);
     at = __builtin_fmaf(e2 * e, at, e);                       // atanh(e)
     const float lsmall = at * (-2.f * kLog2e);
-    const float lt = __builtin_amdgcn_logf(fmaxf(tp, 1e-20f));
-    return z < 0.3f ? lt : (e >= 0.0625f ? lmid : lsmall);
+    // one log: of the polynomial (z < 0.3) or of (1 - e)/(1 + e); e < 1/16 implies z > 1.38
+    const float l = __builtin_amdgcn_logf(z < 0.3f ? fmaxf(tp, 1e-20f) : te);
+    return e >= 0.0625f ? l : lsmall;
+}
+// the same on two edges, non-transcendental ops packed (paired check step)
+__device__ __forceinline__ f32x2 wbp_L2(f32x2 a, f32x2& c) {
+    c = f32x2{a.x < 0.f ? 1.f : 0.f, a.y < 0.f ? 1.f : 0.f};
+    const f32x2 y = {fabsf(a.x), fabsf(a.y)};
+    const f32x2 z = y * 0.5f, z2 = z * z;
+    f32x2 tp = __builtin_elementwise_fma(z2, f32x2{62.f / 2835.f, 62.f / 2835.f},
+                                         f32x2{-17.f / 315.f, -17.f / 315.f});
+    tp = __builtin_elementwise_fma(z2, tp, f32x2{2.f / 15.f, 2.f / 15.f});
+    tp = __builtin_elementwise_fma(z2, tp, f32x2{-1.f / 3.f, -1.f / 3.f});
+    tp = __builtin_elementwise_fma(z2 * z, tp, z);
+    const f32x2 ya = y * (-kLog2e);
+    const f32x2 e = {__builtin_amdgcn_exp2f(ya.x), __builtin_amdgcn_exp2f(ya.y)};
+    const f32x2 d = f32x2{1.f, 1.f} + e;
+    const f32x2 te = (f32x2{1.f, 1.f} - e) * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    const f32x2 e2 = e * e;
+    f32x2 at = __builtin_elementwise_fma(e2, f32x2{1.f / 7.f, 1.f / 7.f}, f32x2{1.f / 5.f, 1.f / 5.f});
+    at = __builtin_elementwise_fma(e2, at, f32x2{1.f / 3.f, 1.f / 3.f});
+    at = __builtin_elementwise_fma(e2 * e, at, e);
+    const f32x2 lsmall = at * (-2.f * kLog2e);
+    const f32x2 l = {__builtin_amdgcn_logf(z.x < 0.3f ? fmaxf(tp.x, 1e-20f) : te.x),
+                     __builtin_amdgcn_logf(z.y < 0.3f ? fmaxf(tp.y, 1e-20f) : te.y)};
+    return f32x2{e.x >= 0.0625f ? l.x : lsmall.x, e.y >= 0.0625f ? l.y : lsmall.y};
 }
 __device__ __forceinline__ double wbp_out(double lam, double n, double s) {
     n = n + (1.0 - s) / 2.0;
@@ -108,6 +132,29 @@ __device__ __forceinline__ float wbp_out(float lam2, float n, float s) {
     one_m = fmaxf(one_m, 9.992007221626409e-16f);
     const float one_p = fminf(1.f + q, 2.f - 9.992007221626409e-16f);
     return sgn * (kLn2 * (__builtin_amdgcn_logf(one_p) - __builtin_amdgcn_logf(one_m)));
+}
+__device__ __forceinline__ f32x2 wbp_out2(f32x2 lam2, f32x2 n, f32x2 s) {
+    n = __builtin_elementwise_fma(f32x2{1.f, 1.f} - s, f32x2{0.5f, 0.5f}, n);
+    const f32x2 h = n * 0.5f;                                 // (-1)^n, n integer-valued
+    const f32x2 par = __builtin_elementwise_fma(f32x2{__builtin_floorf(h.x), __builtin_floorf(h.y)},
+                                                f32x2{-2.f, -2.f}, n);
+    const f32x2 sgn = __builtin_elementwise_fma(par, f32x2{-2.f, -2.f}, f32x2{1.f, 1.f});
+    const f32x2 q = {__builtin_amdgcn_exp2f(lam2.x), __builtin_amdgcn_exp2f(lam2.y)};
+    const f32x2 x = lam2 * kLn2;
+    f32x2 em = __builtin_elementwise_fma(x, f32x2{1.f / 40320.f, 1.f / 40320.f}, f32x2{1.f / 5040.f, 1.f / 5040.f});
+    em = __builtin_elementwise_fma(x, em, f32x2{1.f / 720.f, 1.f / 720.f});
+    em = __builtin_elementwise_fma(x, em, f32x2{1.f / 120.f, 1.f / 120.f});
+    em = __builtin_elementwise_fma(x, em, f32x2{1.f / 24.f, 1.f / 24.f});
+    em = __builtin_elementwise_fma(x, em, f32x2{1.f / 6.f, 1.f / 6.f});
+    em = __builtin_elementwise_fma(x, em, f32x2{0.5f, 0.5f});
+    em = __builtin_elementwise_fma(x * x, em, x);
+    const f32x2 qm = f32x2{1.f, 1.f} - q, qp = f32x2{1.f, 1.f} + q;
+    const float lo = 9.992007221626409e-16f, hi = 2.f - 9.992007221626409e-16f;
+    const f32x2 one_m = {fmaxf(x.x > -0.35f ? -em.x : qm.x, lo), fmaxf(x.y > -0.35f ? -em.y : qm.y, lo)};
+    const f32x2 one_p = {fminf(qp.x, hi), fminf(qp.y, hi)};
+    const f32x2 l = f32x2{__builtin_amdgcn_logf(one_p.x), __builtin_amdgcn_logf(one_p.y)} -
+                    f32x2{__builtin_amdgcn_logf(one_m.x), __builtin_amdgcn_logf(one_m.y)};
+    return sgn * (l * kLn2);
 }
 // per-edge weights of iteration t (reference edge order; NBP [T][2][E] + readout, V10 [T][E])
 template <int MODEL, typename T> struct WbpW {
@@ -837,7 +884,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     // the base-2 tanh (tanh_half_base2); the readout re-reads the unscaled x_v from HBM.
     constexpr bool kBase2 = sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI);
     // fp32 GNN and BP models run the check step on edge PAIRS (packed VALU, see below)
-    constexpr bool kPairBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP);
+    constexpr bool kPairBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP ||
+                                                MODEL == GNND_NBP || MODEL == GNND_V10);
     constexpr bool kPair = kBase2 || kPairBP;
     constexpr int kLogG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -874,8 +922,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
         for (int i = tid; i < CW * E1; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
 
-    Mlp10F32 mlp_msg;
-    if constexpr (sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
+    Mlp10F32 mlp_msg;   // scalar-path form (unused: fp32 GNN models run the paired step)
+    if constexpr (sizeof(T) == 4 && !kPair && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
         mlp_msg.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
     // weighted BP: per-edge tables read through the cache; LDS carries the messages the
     // variable sums need (NBP: already weighted by the next layer's W, or the readout W)
@@ -966,6 +1014,19 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     const f32x2 rc = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
                     t = __builtin_elementwise_fma(rc, f32x2{-2.f, -2.f}, f32x2{1.f, 1.f});
                     cc = f32x2{0.f, 0.f};
+                } else if constexpr (WBP) {
+                    // weighted BP: the edge's iteration weights (identity layout: position =
+                    // reference edge id) read through the cache
+                    const int ea = (int)(sa >> 16), eb = (int)(sb >> 16);
+                    const int xa = ea < E ? ea : 0, xb = eb < E ? eb : 0;
+                    f32x2 a;
+                    if constexpr (MODEL == GNND_NBP)
+                        a = f32x2{(pa.s - mprev.x * ww.msg(it, xa)) + pa.x * ww.prior(it, xa),
+                                  (pb.s - mprev.y * ww.msg(it, xb)) + pb.x * ww.prior(it, xb)};
+                    else
+                        a = f32x2{((pa.s - mprev.x) + pa.x) * ww.chk(it, xa),
+                                  ((pb.s - mprev.y) + pb.x) * ww.chk(it, xb)};
+                    t = wbp_L2(a, cc);
                 } else {
                     const f32x2 a = {(pa.s - mprev.x) + pa.x, (pb.s - mprev.y) + pb.x};
                     cc = f32x2{a.x < 0.f ? 1.f : 0.f, a.y < 0.f ? 1.f : 0.f};
@@ -983,11 +1044,24 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     const f32x2 y = mlp2(u);
                     if constexpr (MODEL == GNND_QGNNI) return __builtin_elementwise_fma(y, scp, mprev);
                     else return y + mprev;
+                } else if constexpr (WBP) {
+                    return __builtin_elementwise_fma(mprev, f32x2{(float)alpha, (float)alpha},
+                                                     wbp_out2(u, n, scp));
                 } else if constexpr (MODEL == GNND_QBP) {
                     return bp_msg_f32x2<true>(u, __builtin_elementwise_fma(f32x2{1.f, 1.f} - scp,
                                                   f32x2{0.5f, 0.5f}, n), cst<float>(1 - 1e-12));
                 } else {
                     return bp_msg_f32x2<false>(u, n, cst<float>(1 - 1e-7));
+                }
+            };
+            // NBP publishes m already weighted by the next layer's W (or the readout W) for
+            // the variable sums (neural_BP.py:248); 1 otherwise (x 1.0 is exact)
+            auto wnext = [&](uint32_t sv) -> float {
+                if constexpr (MODEL == GNND_NBP) {
+                    const int e = (int)(sv >> 16), ec = e < E ? e : 0;
+                    return it + 1 < iters ? ww.msg(it + 1, ec) : ww.out_w(ec);
+                } else {
+                    return 1.f;
                 }
             };
 #pragma unroll
@@ -1008,8 +1082,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     m2[j][r] = post2(Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
-                    mba[ve[qa][r] >> 16] = m2[j][r].x;
-                    mbb[ve[qb][r] >> 16] = m2[j][r].y;
+                    mba[ve[qa][r] >> 16] = m2[j][r].x * wnext(ve[qa][r]);
+                    mbb[ve[qb][r] >> 16] = m2[j][r].y * wnext(ve[qb][r]);
                 }
             }
             if constexpr (kSolo) {
@@ -1037,8 +1111,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
                     ms[i] = post2(f32x2{Sc, Sc} - tv[i], f32x2{Sc2, Sc2} - cv[i],
                                   f32x2{(float)sc[q], (float)sc[q]}, ms[i]);
-                    mb[ve[q][r0] >> 16] = ms[i].x;
-                    if (r1 != r0) mb[ve[q][r1] >> 16] = ms[i].y;
+                    mb[ve[q][r0] >> 16] = ms[i].x * wnext(ve[q][r0]);
+                    if (r1 != r0) mb[ve[q][r1] >> 16] = ms[i].y * wnext(ve[q][r1]);
                 }
             }
         } else
