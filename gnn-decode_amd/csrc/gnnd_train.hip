@@ -354,6 +354,84 @@ bool train_args_ok(const gnnd_graph* g, int model, int dtype, int64_t B, int32_t
            iters >= 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// syndrome loss of the quantum training scripts with its gradient
+// ---------------------------------------------------------------------------------------
+// quantum/decoder_v2_4.py:297-317 (QGNNI.py:255-290 with logical_only): per codeword
+//   s = y + p;  loss = sum_c |sin(pi/2 (H^T s)_c)| + sum_l |sin(pi/2 (Lambda s)_l)|
+//   d loss / d p_v = sum_{rows r containing v} (pi/2) cos(x_r) sign(sin(x_r)),  x_r = (s_r pi) / 2
+// (torch: d|u|/du = sign(u), sign(0) = 0).  One wave per codeword: lanes over variables
+// (s into LDS), lanes over rows (check rows from the graph CSR, logical rows from the dense
+// 0/1 table) -> |sin| terms and row gradients in LDS, wave-reduced loss, lanes over
+// variables for the gradient (variable CSR).  Replaces ~30 small torch kernels per step.
+template <typename T>
+__global__ void __launch_bounds__(256)
+syndrome_loss_kernel(GraphView g, const int32_t* __restrict__ lg, int nl, int logical_only,
+                     const T* __restrict__ pred, const T* __restrict__ y, T* __restrict__ loss_b,
+                     T* __restrict__ dpred, int64_t B) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int V = g.V, C = g.C;
+    const int nr = C + nl;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    T* s_s = (T*)smem + (size_t)wave * (V + nr);
+    T* s_g = s_s + V;
+    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+    if (b >= B) return;                          // whole wave exits (no block barrier below)
+    const T* pb = pred + b * V;
+    const T* yb = y + b * V;
+    for (int v = lane; v < V; v += 64) s_s[v] = yb[v] + pb[v];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    T term = T(0);
+    const T kPi = T(M_PI);
+    for (int r = lane; r < nr; r += 64) {
+        T sr = T(0);
+        bool on = true;
+        if (r < C) {
+            on = !logical_only;
+            for (int k = g.chk_ptr[r]; k < g.chk_ptr[r + 1]; ++k)
+                sr += s_s[g.edge_vc[g.chk_edge[k]] & 0xffffu];
+        } else {
+            const int32_t* row = lg + (size_t)(r - C) * V;
+            for (int v = 0; v < V; ++v)
+                if (row[v]) sr += s_s[v];
+        }
+        const T xr = sr * kPi / T(2);
+        const T sn = sin(xr);
+        const T gr = (sn > T(0) ? T(1) : sn < T(0) ? T(-1) : T(0)) * cos(xr) * (kPi / T(2));
+        s_g[r] = on ? gr : T(0);
+        if (on) term += sn < T(0) ? -sn : sn;
+    }
+    // wave sum of the row terms, fixed butterfly order
+    for (int o = 32; o >= 1; o >>= 1) term += __shfl_xor(term, o);
+    if (lane == 0) loss_b[b] = term;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int v = lane; v < V; v += 64) {
+        T d = T(0);
+        for (int k = g.var_ptr[v]; k < g.var_ptr[v + 1]; ++k) d += s_g[g.edge_vc[k] >> 16];
+        for (int l = 0; l < nl; ++l)
+            if (lg[(size_t)l * V + v]) d += s_g[C + l];
+        dpred[b * V + v] = d;
+    }
+}
+
+template <typename T>
+int launch_syndrome_loss(const gnnd_graph* g, const int32_t* lg, int nl, int logical_only,
+                         const void* pred, const void* y, void* loss_b, void* dpred, int64_t B,
+                         hipStream_t st) {
+    const GraphView& v = g->view;
+    const size_t lds = 4 * (size_t)(v.V + v.C + nl) * sizeof(T);
+    if (lds > 64 * 1024) return GNND_ERR_UNSUPPORTED;
+    const int64_t blocks = (B + 3) / 4;
+    syndrome_loss_kernel<T><<<(unsigned)blocks, 256, lds, st>>>(
+        v, lg, nl, logical_only, (const T*)pred, (const T*)y, (T*)loss_b, (T*)dpred, B);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
 }  // namespace
 
 extern "C" int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, int64_t batch,
@@ -400,4 +478,20 @@ extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const v
                                  workspace_bytes, batch, iters, st);
     return launch_bwd<double>(g, d_w, d_x, d_out, d_grad_out, d_tape, d_grad_w, d_workspace,
                               workspace_bytes, batch, iters, st);
+}
+
+extern "C" int gnnd_syndrome_loss(const gnnd_graph* g, const int32_t* d_logical, int32_t n_logical,
+                                  int32_t logical_only, int dtype, const void* d_pred,
+                                  const void* d_y, void* d_loss_b, void* d_dpred, int64_t batch,
+                                  void* stream) {
+    if (!g || n_logical < 0 || (n_logical > 0 && !d_logical) || batch < 0) return GNND_ERR_INVALID_ARG;
+    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
+    if (batch == 0) return GNND_OK;
+    if (!d_pred || !d_y || !d_loss_b || !d_dpred) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GNND_F32)
+        return launch_syndrome_loss<float>(g, d_logical, n_logical, logical_only, d_pred, d_y,
+                                           d_loss_b, d_dpred, batch, st);
+    return launch_syndrome_loss<double>(g, d_logical, n_logical, logical_only, d_pred, d_y,
+                                        d_loss_b, d_dpred, batch, st);
 }

@@ -52,6 +52,7 @@ SIGNATURES = {
     'gnnd_train_bwd_workspace': (_int, [_vp, _int, _int, _i64, _c_i64p]),
     'gnnd_train_bwd': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32,
                               _vp]),
+    'gnnd_syndrome_loss': (_int, [_vp, _vp, _i32, _i32, _int, _vp, _vp, _vp, _vp, _i64, _vp]),
     'gnnd_status_string': (ctypes.c_char_p, [_int]),
     'gnnd_last_hip_error': (_int, []),
     'gnnd_version': (_int, []),

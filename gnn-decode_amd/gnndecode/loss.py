@@ -21,20 +21,50 @@ def _cols(t, V):
 
 
 class SyndromeLoss(torch.nn.Module):
-    def __init__(self, H, logical, logical_only=False):
+    """On GPU tensors (fp32/fp64) the loss and its gradient come from ONE HIP launch
+    (`gnnd_syndrome_loss`, ops.SyndromeLossFn); `reference_forward` is the reference's
+    formula in torch ops (CPU tensors and the tests' cross-check)."""
+
+    def __init__(self, H, logical, logical_only=False, fused=True):
         super().__init__()
+        self.H_np = H.detach().cpu().numpy() if isinstance(H, torch.Tensor) else H
         H = torch.as_tensor(H, dtype=torch.float64)
         self.V = H.size(0)
         self.register_buffer('Ht', H.t().contiguous())                      # [C, V]
         self.register_buffer('logical', torch.as_tensor(logical, dtype=torch.float64))
+        self.register_buffer('logical_rows', (torch.as_tensor(logical) != 0).to(torch.int32))
         self.logical_only = logical_only
+        self.fused = fused
+        self._graphs = {}
+        self._casts = {}
+
+    def _graph(self, device):
+        g = self._graphs.get(device)
+        if g is None:
+            from .graph import TannerGraph
+            g = self._graphs[device] = TannerGraph(self.H_np, device)
+        return g
+
+    def _cast(self, t, dtype):      # cached dtype copies of the constant matrices
+        key = (id(t), dtype, t.device)
+        c = self._casts.get(key)
+        if c is None:
+            c = self._casts[key] = t.to(dtype)
+        return c
+
+    def reference_forward(self, pred, y):
+        s = _cols(y, self.V).to(pred.dtype) + _cols(pred, self.V)
+        loss = torch.abs(torch.sin(torch.matmul(self._cast(self.logical, pred.dtype), s) * math.pi / 2)).sum()
+        if not self.logical_only:
+            loss = torch.abs(torch.sin(torch.matmul(self._cast(self.Ht, pred.dtype), s) * math.pi / 2)).sum() + loss
+        return loss
 
     def forward(self, pred, y):
-        s = _cols(y, self.V).to(pred.dtype) + _cols(pred, self.V)
-        loss = torch.abs(torch.sin(torch.matmul(self.logical.to(pred.dtype), s) * math.pi / 2)).sum()
-        if not self.logical_only:
-            loss = torch.abs(torch.sin(torch.matmul(self.Ht.to(pred.dtype), s) * math.pi / 2)).sum() + loss
-        return loss
+        if self.fused and pred.is_cuda and pred.dtype in (torch.float32, torch.float64):
+            from .ops import SyndromeLossFn
+            return SyndromeLossFn.apply(pred, y, self._graph(pred.device), self.logical_rows,
+                                        self.logical_only)
+        return self.reference_forward(pred, y)
 
 
 class ClassicalLoss(torch.nn.Module):

@@ -249,3 +249,40 @@ class FusedTrainFn(torch.autograd.Function):
         graph, model, iters, wdt = ctx.args
         gw = train_backward(graph, model, w, x, out, grad_out.to(x.dtype), tape, iters)
         return gw.to(wdt), None, None, None, None
+
+
+# ---------------------------------------------------------------------------------------
+# training objective: syndrome loss + gradient in one launch (gnnd_syndrome_loss)
+# ---------------------------------------------------------------------------------------
+def syndrome_loss(graph, logical_rows, logical_only, pred, y):
+    """(per-codeword losses [B], d loss / d pred [B*V, 1]) of quantum/decoder_v2_4.py:297-317
+    (logical_only: quantum/QGNNI.py:255-290).  logical_rows: int32 [n_l, V] on the device."""
+    _require_gpu(pred, y)
+    V = graph.V
+    pred = pred.contiguous()
+    y = y.to(pred.dtype).contiguous()
+    B = pred.numel() // V
+    if pred.numel() != B * V or y.numel() != pred.numel():
+        raise ValueError(f'pred/y must hold B*V values (V = {V})')
+    loss_b = torch.empty(B, dtype=pred.dtype, device=pred.device)
+    dpred = torch.empty_like(pred)
+    lg = logical_rows.contiguous()
+    _lib.call('gnnd_syndrome_loss', graph.handle, _ptr(lg), int(lg.size(0)), int(bool(logical_only)),
+              dtype_code(pred.dtype), _ptr(pred), _ptr(y), _ptr(loss_b), _ptr(dpred), B,
+              current_stream(pred.device))
+    return loss_b, dpred
+
+
+class SyndromeLossFn(torch.autograd.Function):
+    """Batch-summed syndrome loss; backward scales the kernel's d loss / d pred."""
+
+    @staticmethod
+    def forward(ctx, pred, y, graph, logical_rows, logical_only):
+        loss_b, dpred = syndrome_loss(graph, logical_rows, logical_only, pred, y)
+        ctx.save_for_backward(dpred)
+        return loss_b.sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dpred,) = ctx.saved_tensors
+        return dpred * g, None, None, None, None

@@ -190,6 +190,18 @@ int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const void* d_w, c
                    void* d_grad_w, void* d_workspace, int64_t workspace_bytes, int64_t batch,
                    int32_t iters, void* stream);
 
+/* ---- training objective ------------------------------------------------
+ * Syndrome loss of quantum/decoder_v2_4.py:297-317 (logical_only != 0: the Lambda term of
+ * quantum/QGNNI.py:255-290 only) and its gradient, per codeword b of the batch:
+ *   d_loss_b[b] = sum_c |sin(pi/2 (H^T (y+p))_c)| + sum_l |sin(pi/2 (Lambda (y+p))_l)|
+ *   d_dpred[b*V+v] = d loss_b / d p_v  (torch's |.| rule: sign(0) = 0)
+ * d_pred, d_y: [B*V] in dtype; d_logical: int32 [n_logical][V] 0/1 rows of Lambda.  The
+ * batch loss of the reference is sum_b d_loss_b[b].  Replaces the reference's LossFunc
+ * (its O(B) torch.cat reshape loop and ~30 small autograd kernels per step).            */
+int gnnd_syndrome_loss(const gnnd_graph* g, const int32_t* d_logical, int32_t n_logical,
+                       int32_t logical_only, int dtype, const void* d_pred, const void* d_y,
+                       void* d_loss_b, void* d_dpred, int64_t batch, void* stream);
+
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gnnd_status_string(int status);
 int gnnd_last_hip_error(void);          /* hipError_t of the last GNND_ERR_HIP, per thread */

@@ -262,3 +262,28 @@ def test_two_rank_fused_training_equals_full_batch(golden):
         assert flat.tolist() == res[0][2]                 # ranks bitwise equal
         assert torch.allclose(flat, ref, rtol=1e-10, atol=1e-12)
         assert all(abs(a - b) <= 1e-9 * max(1, abs(b)) for a, b in zip(losses, ref_losses))
+
+
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+@pytest.mark.parametrize('logical_only', [False, True])
+@pytest.mark.parametrize('Ld', [5, 7])
+def test_fused_syndrome_loss_matches_reference_formula(dtype, logical_only, Ld):
+    """gnnd_syndrome_loss (one launch: loss and d loss / d pred) equals the reference's
+    LossFunc formula (quantum/decoder_v2_4.py:297-317) under torch autograd."""
+    import gnndecode as gd
+    H = gd.codes.toric_code(Ld)
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H), logical_only=logical_only).to(DEV)
+    B, V = 37, H.shape[0]
+    g = torch.Generator(device='cpu').manual_seed(Ld)
+    pred = torch.rand(B * V, 1, generator=g, dtype=torch.float64).to(dtype).to(DEV)
+    y = (torch.rand(B * V, 1, generator=g) < 0.1).to(dtype).to(DEV)
+    pred[:V] = 0.0                      # integer-valued rows: sin(k pi / 2) edge cases
+    p1 = pred.clone().requires_grad_(True)
+    p2 = pred.clone().requires_grad_(True)
+    l1 = lf(p1, y)
+    l1.backward()
+    l2 = lf.reference_forward(p2, y)
+    l2.backward()
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    assert abs(l1.item() - l2.item()) <= tol * max(1.0, abs(l2.item()))
+    torch.testing.assert_close(p1.grad, p2.grad, rtol=tol, atol=tol)
