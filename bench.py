@@ -73,6 +73,9 @@ def parse():
     p.add_argument('--layerwise', action='store_true',
                    help='train mode: the layer-by-layer operator path instead of the fused '
                         'decoder_v2_4 training kernels')
+    p.add_argument('--torch-trainer', action='store_true',
+                   help='train mode: torch autograd/optimizer Trainer around the fused kernels '
+                        'instead of FusedV24Trainer')
     p.add_argument('--mode', default='decode', choices=['decode', 'train'],
                    help='train = config 5: decoder_v2_4 (or --model qgnni/nbp/v10) training '
                         'step (DP, RCCL all-reduce)')
@@ -177,7 +180,11 @@ def train_main(a, world, rank, dev):
         model.fused_train = fused
     lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
                               logical_only=(model_name == 'qgnni')).to(dev)
-    tr = gd.train.Trainer(model, lf, graph=not a.no_graph, warmup=2)   # captured after 2 eager steps
+    if fused and not a.torch_trainer:
+        # prepare -> fwd+tape -> syndrome loss -> reverse pass -> [all_reduce] -> Adam, one HIP graph
+        tr = gd.train.FusedV24Trainer(model, lf, graph=not a.no_graph, warmup=2)
+    else:
+        tr = gd.train.Trainer(model, lf, graph=not a.no_graph, warmup=2)   # captured after 2 eager steps
     x, y = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
     data = gd.data.make_batch(x, model.graph(dev))
     for _ in range(a.warmup):
@@ -207,7 +214,10 @@ def train_main(a, world, rank, dev):
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
                        'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters()),
                        'hip_graph': not a.no_graph,
-                       'path': 'fused gnnd_train_fwd/bwd' if fused else 'layer-by-layer propagate ops'},
+                       'path': ('FusedV24Trainer: gnnd_train_fwd/bwd + gnnd_syndrome_loss + gnnd_adam_step'
+                                if fused and not a.torch_trainer else
+                                'fused gnnd_train_fwd/bwd, torch loss/optimizer' if fused
+                                else 'layer-by-layer propagate ops')},
             'roofline': None, 'cpu_baseline': None}), flush=True)
 
 

@@ -385,23 +385,26 @@ syndrome_loss_kernel(GraphView g, const int32_t* __restrict__ lg, int nl, int lo
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     T term = T(0);
     const T kPi = T(M_PI);
-    for (int r = lane; r < nr; r += 64) {
-        T sr = T(0);
-        bool on = true;
-        if (r < C) {
-            on = !logical_only;
-            for (int k = g.chk_ptr[r]; k < g.chk_ptr[r + 1]; ++k)
-                sr += s_s[g.edge_vc[g.chk_edge[k]] & 0xffffu];
-        } else {
-            const int32_t* row = lg + (size_t)(r - C) * V;
-            for (int v = 0; v < V; ++v)
-                if (row[v]) sr += s_s[v];
-        }
+    auto row_grad = [&](T sr, int r, bool on) {     // |sin| term and d|sin(x_r)|/ds_r
         const T xr = sr * kPi / T(2);
         const T sn = sin(xr);
         const T gr = (sn > T(0) ? T(1) : sn < T(0) ? T(-1) : T(0)) * cos(xr) * (kPi / T(2));
         s_g[r] = on ? gr : T(0);
         if (on) term += sn < T(0) ? -sn : sn;
+    };
+    for (int r = lane; r < C; r += 64) {            // check rows: lanes over checks
+        T sr = T(0);
+        for (int k = g.chk_ptr[r]; k < g.chk_ptr[r + 1]; ++k)
+            sr += s_s[g.edge_vc[g.chk_edge[k]] & 0xffffu];
+        row_grad(sr, r, !logical_only);
+    }
+    for (int l = 0; l < nl; ++l) {                  // logical rows: the wave sums each one
+        const int32_t* row = lg + (size_t)l * V;
+        T part = T(0);
+        for (int v = lane; v < V; v += 64)
+            if (row[v]) part += s_s[v];
+        for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+        if (lane == l % 64) row_grad(part, C + l, true);
     }
     // wave sum of the row terms, fixed butterfly order
     for (int o = 32; o >= 1; o >>= 1) term += __shfl_xor(term, o);
@@ -430,6 +433,39 @@ int launch_syndrome_loss(const gnnd_graph* g, const int32_t* lg, int nl, int log
         v, lg, nl, logical_only, (const T*)pred, (const T*)y, (T*)loss_b, (T*)dpred, B);
     GNND_LAUNCH_CHECK();
     return GNND_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Adam on one flat parameter buffer (torch.optim.Adam, amsgrad/maximize off, the
+// non-capturable update order), device-resident step counter: graph-capturable
+// ---------------------------------------------------------------------------------------
+// g' = g + wd p;  m = m + (1 - b1)(g' - m)  (lerp, weight < 0.5);  v = v b2; v += ((1 - b2) g') g';
+// t = step + 1;  p += -(lr / (1 - b1^t)) * (m / (sqrt(v) / sqrt(1 - b2^t) + eps)).
+// Bias corrections in double (torch computes them as Python floats).  ONE workgroup: the
+// counter is read by every thread and written back after a barrier.
+template <typename T>
+__global__ void __launch_bounds__(1024)
+adam_kernel(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ m, T* __restrict__ v,
+            double* __restrict__ step, int64_t n, double lr, double b1, double b2, double eps,
+            double wd) {
+    const double t = step[0] + 1.0;
+    const T step_size = (T)(lr / (1.0 - pow(b1, t)));
+    const T bc2s = (T)sqrt(1.0 - pow(b2, t));
+    const T w1 = (T)(1.0 - b1), tb2 = (T)b2, w2 = (T)(1.0 - b2), te = (T)eps, twd = (T)wd;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const T pi = p[i];
+        T gi = g[i];
+        if (wd != 0.0) gi = gi + twd * pi;
+        const T mi = m[i] + w1 * (gi - m[i]);
+        T vi = v[i] * tb2;
+        vi = vi + (w2 * gi) * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const T denom = sqrt(vi) / bc2s + te;
+        p[i] = pi + (-step_size) * (mi / denom);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) step[0] = t;
 }
 
 }  // namespace
@@ -494,4 +530,24 @@ extern "C" int gnnd_syndrome_loss(const gnnd_graph* g, const int32_t* d_logical,
                                            d_loss_b, d_dpred, batch, st);
     return launch_syndrome_loss<double>(g, d_logical, n_logical, logical_only, d_pred, d_y,
                                         d_loss_b, d_dpred, batch, st);
+}
+
+extern "C" int gnnd_adam_step(int dtype, void* d_param, const void* d_grad, void* d_exp_avg,
+                              void* d_exp_avg_sq, double* d_step, int64_t n, double lr,
+                              double beta1, double beta2, double eps, double weight_decay,
+                              void* stream) {
+    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
+    if (n < 0 || !d_step) return GNND_ERR_INVALID_ARG;
+    if (n > 0 && (!d_param || !d_grad || !d_exp_avg || !d_exp_avg_sq)) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GNND_F32)
+        adam_kernel<float><<<1, 1024, 0, st>>>((float*)d_param, (const float*)d_grad,
+                                               (float*)d_exp_avg, (float*)d_exp_avg_sq, d_step, n,
+                                               lr, beta1, beta2, eps, weight_decay);
+    else
+        adam_kernel<double><<<1, 1024, 0, st>>>((double*)d_param, (const double*)d_grad,
+                                                (double*)d_exp_avg, (double*)d_exp_avg_sq, d_step,
+                                                n, lr, beta1, beta2, eps, weight_decay);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
 }

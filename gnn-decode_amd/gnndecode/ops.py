@@ -286,3 +286,18 @@ class SyndromeLossFn(torch.autograd.Function):
     def backward(ctx, g):
         (dpred,) = ctx.saved_tensors
         return dpred * g, None, None, None, None
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, betas=(0.9, 0.999), eps=1e-8,
+              weight_decay=0.0):
+    """In-place torch.optim.Adam update of one flat parameter buffer (gnnd_adam_step);
+    `step` is a float64 device scalar tensor incremented by the call."""
+    _require_gpu(param, grad, exp_avg, exp_avg_sq, step)
+    for t in (grad, exp_avg, exp_avg_sq):
+        if t.dtype != param.dtype or t.numel() != param.numel() or not t.is_contiguous():
+            raise ValueError('adam_step: buffers must match the parameter (dtype, size, contiguous)')
+    if step.dtype != torch.float64 or step.numel() != 1:
+        raise ValueError('adam_step: step must be a float64 scalar tensor')
+    _lib.call('gnnd_adam_step', dtype_code(param.dtype), _ptr(param), _ptr(grad), _ptr(exp_avg),
+              _ptr(exp_avg_sq), _ptr(step), param.numel(), float(lr), float(betas[0]),
+              float(betas[1]), float(eps), float(weight_decay), current_stream(param.device))

@@ -12,6 +12,8 @@ single-process full-batch gradient.  Then every rank applies the same Adam step
 import torch
 import torch.distributed as dist
 
+from . import ops
+
 
 def shard_bounds(global_batch, rank, world):
     """Contiguous codeword shard [start, end) of rank r (sizes differ by at most one)."""
@@ -109,3 +111,93 @@ class _StaticBatch:
     def __init__(self, x, edge_index):
         self.x = x
         self.edge_index = edge_index
+
+
+class FusedV24Trainer:
+    """decoder_v2_4 training step (quantum/decoder_v2_4.py:320-348) as a handful of HIP
+    launches, the whole step captured in one HIP graph:
+
+        prepare weights -> forward with tape (gnnd_train_fwd) -> syndrome loss and
+        d loss / d out (gnnd_syndrome_loss) -> reverse pass to the flat gradient
+        (gnnd_train_bwd) -> [one RCCL all_reduce(SUM) of that gradient] -> Adam on the
+        flat parameter buffer (gnnd_adam_step)
+
+    The model's parameters are re-bound as VIEWS of one flat buffer in the gnnd.h packed
+    layout, so nothing is packed, split, zeroed or accumulated per parameter (the torch
+    path, `Trainer`, spends ~80 small kernels per step on that, the loss graph and Adam).
+    state_dict / load_state_dict keep working on the views.  Same update as `Trainer`
+    (torch.optim.Adam's order; lr 3e-4, weight decay 1e-9 of the reference)."""
+
+    def __init__(self, model, loss_fn, lr=3e-4, weight_decay=1e-9, betas=(0.9, 0.999), eps=1e-8,
+                 group=None, graph=True, warmup=2):
+        from .models import DecoderV24
+        if not isinstance(model, DecoderV24):
+            raise TypeError('FusedV24Trainer trains decoder_v2_4 (DecoderV24) models')
+        self.model, self.loss_fn, self.group = model, loss_fn, group
+        self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
+        self.use_graph, self.warmup = graph, warmup
+        flat = model.packed_weights().detach().clone().contiguous()
+        off = 0
+        for seq, split in ((model.ggc1.mlp, True), (model.ggc2.mlp, False), (model.mlp, False)):
+            W1, b1, W2, b2 = seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias
+            hidden, fan_in = W1.shape
+            n = hidden * fan_in
+            W1.data = (flat[off:off + n].view(fan_in, hidden).t() if split
+                       else flat[off:off + n].view(hidden, fan_in))
+            off += n
+            b1.data = flat[off:off + hidden]
+            off += hidden
+            W2.data = flat[off:off + hidden].view(1, hidden)
+            off += hidden
+            b2.data = flat[off:off + 1]
+            off += 1
+        assert off == flat.numel()
+        self.flat = flat
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.step_count = torch.zeros(1, dtype=torch.float64, device=flat.device)
+        self._graph = None
+        self._eager_steps = 0
+
+    def _dist(self):
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def _body(self, x, y):
+        m = self.model
+        g = m.graph(x.device)
+        w = self.flat if self.flat.dtype == x.dtype else self.flat.to(x.dtype)
+        out, tape = ops.train_forward(g, m.kind, x, ops.prepare_weights(m.kind, w), m.Nc)
+        lf = self.loss_fn
+        loss_b, dpred = ops.syndrome_loss(lf._graph(x.device), lf.logical_rows, lf.logical_only,
+                                          out, y)
+        gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
+        total = loss_b.sum()
+        if self._dist():
+            dist.all_reduce(gw, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(total, op=dist.ReduceOp.SUM, group=self.group)
+        ops.adam_step(self.flat, gw, self.exp_avg, self.exp_avg_sq, self.step_count, self.lr,
+                      self.betas, self.eps, self.wd)
+        return total
+
+    def step(self, data, y):
+        self.model.train()
+        x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
+        if not self.use_graph:
+            return self._body(x, y)
+        if self._graph is None:
+            if self._eager_steps < self.warmup:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    out = self._body(x, y)
+                torch.cuda.current_stream().wait_stream(s)
+                self._eager_steps += 1
+                return out
+            self._sx, self._sy = x.clone(), y.clone()
+            self._graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._graph):
+                self._sloss = self._body(self._sx, self._sy)
+        self._sx.copy_(x)
+        self._sy.copy_(y)
+        self._graph.replay()
+        return self._sloss

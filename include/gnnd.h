@@ -202,6 +202,14 @@ int gnnd_syndrome_loss(const gnnd_graph* g, const int32_t* d_logical, int32_t n_
                        int32_t logical_only, int dtype, const void* d_pred, const void* d_y,
                        void* d_loss_b, void* d_dpred, int64_t batch, void* stream);
 
+/* Adam (torch.optim.Adam update order, amsgrad/maximize off) on one flat parameter buffer of
+ * n values with its two moment buffers; *d_step is the device-resident step count (double,
+ * incremented by the call), so a whole training step with the update can be captured in one
+ * HIP graph.  Single-workgroup kernel (sized for the decoders' ~10^3 parameters).          */
+int gnnd_adam_step(int dtype, void* d_param, const void* d_grad, void* d_exp_avg,
+                   void* d_exp_avg_sq, double* d_step, int64_t n, double lr, double beta1,
+                   double beta2, double eps, double weight_decay, void* stream);
+
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gnnd_status_string(int status);
 int gnnd_last_hip_error(void);          /* hipError_t of the last GNND_ERR_HIP, per thread */

@@ -287,3 +287,46 @@ def test_fused_syndrome_loss_matches_reference_formula(dtype, logical_only, Ld):
     tol = 1e-12 if dtype == torch.float64 else 2e-5
     assert abs(l1.item() - l2.item()) <= tol * max(1.0, abs(l2.item()))
     torch.testing.assert_close(p1.grad, p2.grad, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+def test_fused_adam_matches_torch_adam(dtype):
+    import gnndecode as gd
+    g = torch.Generator(device='cpu').manual_seed(3)
+    p0 = torch.randn(1283, generator=g, dtype=torch.float64).to(dtype)
+    ref = torch.nn.Parameter(p0.clone().to(DEV))
+    opt = torch.optim.Adam([ref], lr=3e-4, weight_decay=1e-9, foreach=False)
+    flat = p0.clone().to(DEV)
+    m, v = torch.zeros_like(flat), torch.zeros_like(flat)
+    step = torch.zeros(1, dtype=torch.float64, device=DEV)
+    tol = 1e-13 if dtype == torch.float64 else 2e-6
+    for _ in range(6):
+        gr = torch.randn(1283, generator=g, dtype=torch.float64).to(dtype).to(DEV)
+        ref.grad = gr.clone()
+        opt.step()
+        gd.ops.adam_step(flat, gr, m, v, step, 3e-4, (0.9, 0.999), 1e-8, 1e-9)
+        torch.testing.assert_close(flat, ref.detach(), rtol=tol, atol=tol * 1e-3)
+    assert step.item() == 6.0
+
+
+def test_fused_v24_trainer_matches_torch_trainer():
+    """FusedV24Trainer (flat parameter views, one-launch loss, HIP Adam, HIP-graph step)
+    follows the torch-optimizer Trainer on the same seeded data (fp64, toric d=5)."""
+    import gnndecode as gd
+    H = gd.codes.toric_code(5)
+    lg = gd.codes.toric_logicals(H)
+    torch.manual_seed(0)
+    a = gd.MODELS['v24'](15, H).to(DEV)
+    b = gd.MODELS['v24'](15, H).to(DEV)
+    b.load_state_dict(a.state_dict())
+    ta = gd.train.Trainer(a, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=False)
+    tb = gd.train.FusedV24Trainer(b, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1)
+    keys = sorted(a.state_dict())
+    assert sorted(b.state_dict()) == keys
+    for s in range(4):
+        x, y = gd.data.toric_batch(H, 24, seed=100 + s, device=DEV)
+        la = ta.step(gd.data.make_batch(x, a.graph(x.device)), y)
+        lb = tb.step(gd.data.make_batch(x, b.graph(x.device)), y)
+        assert abs(la.item() - lb.item()) <= 1e-9 * max(1.0, abs(la.item()))
+    for k in keys:
+        torch.testing.assert_close(b.state_dict()[k], a.state_dict()[k], rtol=1e-9, atol=1e-12)
