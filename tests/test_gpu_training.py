@@ -204,7 +204,7 @@ def test_bp_check_step_backward_matches_torch_autograd(variant):
                                    rtol=1e-9, atol=1e-12 * float(m0.grad.abs().max()))
 
 
-def _dp_worker(rank, world, port, steps, q):
+def _dp_worker(rank, world, port, steps, q, fused_trainer=False):
     """One rank of a 2-process data-parallel run on the single GPU (gloo all-reduce of the
     flat gradient; the fused HIP training kernels on cuda:0)."""
     import os
@@ -223,7 +223,10 @@ def _dp_worker(rank, world, port, steps, q):
     y = torch.from_numpy(z['y']).to(DEV).view(-1, H.shape[0])
     s, e = gd.train.shard_bounds(x.size(0), rank, world)
     xs, ys = x[s:e].reshape(-1, 1).contiguous(), y[s:e].reshape(-1, 1).contiguous()
-    tr = gd.train.Trainer(m, lf, lr=1e-3)
+    if fused_trainer:      # eager steps: the gloo all-reduce is not graph-capturable
+        tr = gd.train.FusedV24Trainer(m, lf, lr=1e-3, graph=False)
+    else:
+        tr = gd.train.Trainer(m, lf, lr=1e-3)
     data = gd.data.make_batch(xs, m.graph(xs.device))
     losses = [float(tr.step(data, ys)) for _ in range(steps)]
     flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()
@@ -232,7 +235,8 @@ def _dp_worker(rank, world, port, steps, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_fused_training_equals_full_batch(golden):
+@pytest.mark.parametrize('fused_trainer', [False, True], ids=['torch-trainer', 'fused-trainer'])
+def test_two_rank_fused_training_equals_full_batch(golden, fused_trainer):
     """Config 5's data-parallel step with the fused HIP kernels: 2 ranks (gloo, both on the
     one GPU), each a shard of the batch, SUM all-reduce -> same parameters and losses as a
     single full-batch process (the reference loss is a sum)."""
@@ -246,7 +250,8 @@ def test_two_rank_fused_training_equals_full_batch(golden):
     steps, world = 2, 2
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, steps, q, fused_trainer))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)])
