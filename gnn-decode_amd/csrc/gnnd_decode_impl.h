@@ -519,6 +519,14 @@ __device__ __forceinline__ f32x2 bp_msg_f32x2(f32x2 lam2, f32x2 n, float hi) {
     }
 }
 
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
+template <int N, typename F, int I = 0> __device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, F, I + 1>(static_cast<F&&>(f));
+    }
+}
+
 template <int MODEL, typename T> struct EdgeMath {
     static constexpr bool BP = ModelTraits<MODEL>::bp;
     static constexpr bool kFastBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP);
@@ -1064,8 +1072,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     return 1.f;
                 }
             };
-#pragma unroll
-            for (int j = 0; j < QP; ++j) {
+            // item pair (2j, 2j + 1)
+            auto pair_step = [&](auto jc) {
+                constexpr int j = decltype(jc)::value;
                 const int qa = 2 * j, qb = 2 * j + 1;
                 f32x2 tv[R], cv[R], tsum, csum;
 #pragma unroll
@@ -1085,16 +1094,17 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     mba[ve[qa][r] >> 16] = m2[j][r].x * wnext(ve[qa][r]);
                     mbb[ve[qb][r] >> 16] = m2[j][r].y * wnext(ve[qb][r]);
                 }
-            }
-            if constexpr (kSolo) {
-                // the odd last item: its slots in pairs, the same per-edge arithmetic
-                constexpr int q = QMAX - 1;
+            };
+            // one item with its slots in pairs (the same per-edge arithmetic as pair_step:
+            // bitwise-identical messages)
+            auto solo_step = [&](auto qc, f32x2* msp) {
+                constexpr int q = decltype(qc)::value;
                 f32x2 tv[RP], cv[RP];
                 float tsum = 0.f, csum = 0.f;
 #pragma unroll
                 for (int i = 0; i < RP; ++i) {
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
-                    tv[i] = pre2(ve[q][r0], ve[q][r1], cb[q], cb[q], ms[i], r0, r1, cv[i]);
+                    tv[i] = pre2(ve[q][r0], ve[q][r1], cb[q], cb[q], msp[i], r0, r1, cv[i]);
                     tsum = i == 0 ? tv[0].x : tsum + tv[i].x;
                     if (2 * i + 1 < R) tsum = tsum + tv[i].y;
                     if constexpr (kPairBP) {
@@ -1109,12 +1119,38 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
                 for (int i = 0; i < RP; ++i) {
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
-                    ms[i] = post2(f32x2{Sc, Sc} - tv[i], f32x2{Sc2, Sc2} - cv[i],
-                                  f32x2{(float)sc[q], (float)sc[q]}, ms[i]);
-                    mb[ve[q][r0] >> 16] = ms[i].x * wnext(ve[q][r0]);
-                    if (r1 != r0) mb[ve[q][r1] >> 16] = ms[i].y * wnext(ve[q][r1]);
+                    msp[i] = post2(f32x2{Sc, Sc} - tv[i], f32x2{Sc2, Sc2} - cv[i],
+                                  f32x2{(float)sc[q], (float)sc[q]}, msp[i]);
+                    mb[ve[q][r0] >> 16] = msp[i].x * wnext(ve[q][r0]);
+                    if (r1 != r0) mb[ve[q][r1] >> 16] = msp[i].y * wnext(ve[q][r1]);
                 }
-            }
+            };
+            // waves whose last work item is idle (tile rounds not filled: LDPC 1 296 items
+            // in 6 rounds) run the last item pair as the first item alone
+            const bool last_item_live = (int)(__builtin_amdgcn_readfirstlane(tid) & ~63) +
+                                        (QMAX - 1) * GNND_BLOCK < C * G * CW;
+            static_for<QP>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                if constexpr (!kSolo && j == QP - 1) {
+                    if (!last_item_live) {
+                        f32x2 tmp[RP];
+#pragma unroll
+                        for (int i = 0; i < RP; ++i) {
+                            const int r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
+                            tmp[i] = f32x2{m2[j][2 * i].x, m2[j][r1].x};
+                        }
+                        solo_step(std::integral_constant<int, 2 * j>{}, tmp);
+#pragma unroll
+                        for (int i = 0; i < RP; ++i) {
+                            m2[j][2 * i].x = tmp[i].x;
+                            if (2 * i + 1 < R) m2[j][2 * i + 1].x = tmp[i].y;
+                        }
+                        return;
+                    }
+                }
+                pair_step(jc);
+            });
+            if constexpr (kSolo) solo_step(std::integral_constant<int, QMAX - 1>{}, ms);
         } else
 #pragma unroll
         for (int q = 0; q < QMAX; ++q) {
