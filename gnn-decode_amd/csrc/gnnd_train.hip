@@ -62,6 +62,22 @@ __device__ __forceinline__ float wave_sum(float v) {
     v += __int_as_float(dpp_i<0x143, 0xc>(__float_as_int(v)));   // row_bcast:31 -> rows 2, 3
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
+// totals of two wave64 values at once (gfx950 lane swaps): v_permlane32_swap folds the upper
+// half of a onto its lower half and the lower half of b onto its upper half, so lanes 0-31
+// carry a and lanes 32-63 carry b; v_permlane16_swap folds row pairs, four row DPP steps
+// finish each row.  One chain for both (vs two six-step DPP chains with their wait states).
+__device__ __forceinline__ void wave_sum2(float a, float b, float& ra, float& rb) {
+    const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_int(a), __float_as_int(b), false, false);
+    float v = __int_as_float(s32[0]) + __int_as_float(s32[1]);
+    const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+    v = __int_as_float(s16[0]) + __int_as_float(s16[1]);
+    v += __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x140, 0xf>(__float_as_int(v)));
+    ra = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    rb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+}
 template <int CTRL, int ROWS> __device__ __forceinline__ double dpp_d(double v) {
     const long long b = __double_as_longlong(v);
     const int lo = dpp_i<CTRL, ROWS>((int)b), hi = dpp_i<CTRL, ROWS>((int)(b >> 32));
@@ -83,6 +99,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 template <typename T> struct Units {
     T w1a[2], w1b[2], b1[2], w2[2];         // w1b only for the 2-input MLP
     T gw1a[2], gw1b[2], gb1[2], gw2[2], gb2;
+    f32x2 pgw1a[2], pgw1b[2], pgb1[2], pgw2[2];  // fp32 packed path: per-edge-half partials
+    __device__ void zero_packed() {
+        for (int j = 0; j < 2; ++j) pgw1a[j] = pgw1b[j] = pgb1[j] = pgw2[j] = f32x2{0.f, 0.f};
+    }
     __device__ void load1(const T* __restrict__ w, int lane) {    // {W1, b1, W2, b2}
         for (int j = 0; j < 2; ++j) {
             const int k = lane + 64 * j;
@@ -90,6 +110,7 @@ template <typename T> struct Units {
             gw1a[j] = gw1b[j] = gb1[j] = gw2[j] = T(0);
         }
         gb2 = T(0);
+        zero_packed();
     }
     __device__ void load2(const T* __restrict__ w, int lane) {    // {W1a, W1b, b1, W2, b2}
         for (int j = 0; j < 2; ++j) {
@@ -98,33 +119,17 @@ template <typename T> struct Units {
             gw1a[j] = gw1b[j] = gb1[j] = gw2[j] = T(0);
         }
         gb2 = T(0);
+        zero_packed();
     }
-    // backward of y = sum_k W2_k sp(W1a_k u0 (+ W1b_k u1) + b1_k) + b2 for upstream dy;
-    // returns d y / d u0 (wave-reduced, uniform)
-    template <bool TWO>
-    __device__ __forceinline__ T bwd(T u0, T u1, T dy) {
-        T part = T(0);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            T h = u0 * w1a[j];
-            if constexpr (TWO) h = h + u1 * w1b[j];
-            h = h + b1[j];
-            T sp, sg;
-            sp_and_grad(h, sp, sg);
-            gw2[j] += dy * sp;
-            const T dh = (dy * w2[j]) * sg;
-            gw1a[j] += dh * u0;
-            if constexpr (TWO) gw1b[j] += dh * u1;
-            gb1[j] += dh;
-            part += dh * w1a[j];
-        }
-        gb2 += dy;
-        return wave_sum(part);
-    }
-    // two edges at once (independent chains for the scheduler); an edge with dy = 0
-    // contributes nothing (masked tail)
+    // backward of y = sum_k W2_k sp(W1a_k u0 (+ W1b_k u1) + b1_k) + b2 at two edges a, b
+    // (independent chains for the scheduler); returns d y / d u0 per edge (wave-reduced,
+    // uniform).  An edge with dy = 0 contributes nothing (masked tail).
     template <bool TWO>
     __device__ __forceinline__ void bwd2(T xa0, T xa1, T dya, T xb0, T xb1, T dyb, T& ra, T& rb) {
+        if constexpr (sizeof(T) == 4) {
+            bwd2_f32<TWO>(xa0, xa1, dya, xb0, xb1, dyb, ra, rb);
+            return;
+        }
         T pa = T(0), pb = T(0);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -151,9 +156,48 @@ template <typename T> struct Units {
         ra = wave_sum(pa);
         rb = wave_sum(pb);
     }
+    // fp32: edges a and b ride the two halves of every packed op (v_pk_fma/mul/add_f32 with
+    // the lane's weights broadcast); the weight gradients accumulate per half (pg*) and are
+    // folded at flush.  Softplus(beta 1, threshold 20): the argument of exp is capped at 20
+    // (no overflow; e^20 / (1 + e^20) rounds to 1 = the threshold branch's derivative) and
+    // sp = max(h, log1p(e^min(h, 20))), which is h above the threshold.
+    template <bool TWO>
+    __device__ __forceinline__ void bwd2_f32(float xa0, float xa1, float dya, float xb0, float xb1,
+                                             float dyb, float& ra, float& rb) {
+        const f32x2 x0 = {xa0, xb0}, x1 = {xa1, xb1}, dy = {dya, dyb};
+        f32x2 p = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            f32x2 h = x0 * (float)w1a[j] + (float)b1[j];
+            if constexpr (TWO) h = x1 * (float)w1b[j] + h;
+            const f32x2 hc = {__builtin_fminf(h.x, 20.f), __builtin_fminf(h.y, 20.f)};
+            const f32x2 hl = hc * kLog2e;
+            const f32x2 z = {__builtin_amdgcn_exp2f(hl.x), __builtin_amdgcn_exp2f(hl.y)};
+            const f32x2 z1 = z + 1.f;
+            const f32x2 l = f32x2{__builtin_amdgcn_logf(z1.x), __builtin_amdgcn_logf(z1.y)} * kLn2;
+            const f32x2 sp = {__builtin_fmaxf(h.x, l.x), __builtin_fmaxf(h.y, l.y)};
+            const f32x2 sg = z * f32x2{__builtin_amdgcn_rcpf(z1.x), __builtin_amdgcn_rcpf(z1.y)};
+            pgw2[j] = dy * sp + pgw2[j];
+            const f32x2 dh = (dy * (float)w2[j]) * sg;
+            pgw1a[j] = dh * x0 + pgw1a[j];
+            if constexpr (TWO) pgw1b[j] = dh * x1 + pgw1b[j];
+            pgb1[j] = pgb1[j] + dh;
+            p = dh * (float)w1a[j] + p;
+        }
+        gb2 += dya;
+        gb2 += dyb;
+        wave_sum2(p.x, p.y, ra, rb);
+    }
     // add this wave's gradients into the workgroup accumulator (packed plain layout)
     template <bool TWO>
-    __device__ void flush(T* acc, int lane) const {
+    __device__ void flush(T* acc, int lane) {
+        if constexpr (sizeof(T) == 4)
+            for (int j = 0; j < 2; ++j) {
+                gw1a[j] += pgw1a[j].x + pgw1a[j].y;
+                gw1b[j] += pgw1b[j].x + pgw1b[j].y;
+                gb1[j] += pgb1[j].x + pgb1[j].y;
+                gw2[j] += pgw2[j].x + pgw2[j].y;
+            }
         for (int j = 0; j < 2; ++j) {
             const int k = lane + 64 * j;
             if constexpr (TWO) {
@@ -241,18 +285,42 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     };
     auto zero = [](int) { return T(0); };
 
+    // the iteration's tape rows: the first kPF per thread are loaded into registers one
+    // iteration ahead (their HBM latency hides behind the previous iteration's phases),
+    // the rest (tiles of several codewords) load when staged
+    constexpr int kPF = 2;
+    T pu[kPF], pt[kPF], pe[kPF];
+    auto prefetch = [&](int it) {
+        const size_t trow = ((size_t)it * B + b0) * E;
+#pragma unroll
+        for (int i = 0; i < kPF; ++i) {
+            const int f = tid + i * kTrainThreads;
+            if (f < nE) { pu[i] = tape.u[trow + f]; pt[i] = tape.t[trow + f]; pe[i] = tape.ext[trow + f]; }
+        }
+    };
+    auto stage = [&](int it) {
+#pragma unroll
+        for (int i = 0; i < kPF; ++i) {
+            const int f = tid + i * kTrainThreads;
+            if (f < nE) { s_u[f] = pu[i]; s_t[f] = pt[i]; s_ext[f] = pe[i]; }
+        }
+        const size_t trow = ((size_t)it * B + b0) * E;
+        for (int f = tid + kPF * kTrainThreads; f < nE; f += kTrainThreads) {
+            s_u[f] = tape.u[trow + f];
+            s_t[f] = tape.t[trow + f];
+            s_ext[f] = tape.ext[trow + f];
+        }
+    };
+    if (iters > 0) prefetch(iters - 1);
+
     // readout: r_v = sum_e MLP_o(m^T_e) + x_v  ->  dm
     unit_pass(uo, std::false_type{}, s_u, zero, [&](int f) { return s_da[f]; }, s_dm);
     __syncthreads();
 
     for (int it = iters - 1; it >= 0; --it) {
-        const size_t trow = ((size_t)it * B + b0) * E;
-        for (int f = tid; f < nE; f += kTrainThreads) {
-            s_u[f] = tape.u[trow + f];
-            s_t[f] = tape.t[trow + f];
-            s_ext[f] = tape.ext[trow + f];
-        }
+        stage(it);
         __syncthreads();
+        if (it > 0) prefetch(it - 1);
         // A: m^{t+1} = MLP_c(u) s_c + m^t
         unit_pass(uc, std::false_type{}, s_u, zero, [&](int f) { return s_dm[f] * s_x[s_nc[f]]; },
                   s_g);
