@@ -100,8 +100,14 @@ template <typename T> struct Units {
     T w1a[2], w1b[2], b1[2], w2[2];         // w1b only for the 2-input MLP
     T gw1a[2], gw1b[2], gb1[2], gw2[2], gb2;
     f32x2 pgw1a[2], pgw1b[2], pgb1[2], pgw2[2];  // fp32 packed path: per-edge-half partials
+    float s1a[2], s1b[2], sb1[2];                // fp32: layer 1 in log2 units (x log2 e)
     __device__ void zero_packed() {
-        for (int j = 0; j < 2; ++j) pgw1a[j] = pgw1b[j] = pgb1[j] = pgw2[j] = f32x2{0.f, 0.f};
+        for (int j = 0; j < 2; ++j) {
+            pgw1a[j] = pgw1b[j] = pgb1[j] = pgw2[j] = f32x2{0.f, 0.f};
+            s1a[j] = (float)w1a[j] * kLog2e;
+            s1b[j] = (float)w1b[j] * kLog2e;
+            sb1[j] = (float)b1[j] * kLog2e;
+        }
     }
     __device__ void load1(const T* __restrict__ w, int lane) {    // {W1, b1, W2, b2}
         for (int j = 0; j < 2; ++j) {
@@ -158,9 +164,11 @@ template <typename T> struct Units {
     }
     // fp32: edges a and b ride the two halves of every packed op (v_pk_fma/mul/add_f32 with
     // the lane's weights broadcast); the weight gradients accumulate per half (pg*) and are
-    // folded at flush.  Softplus(beta 1, threshold 20): the argument of exp is capped at 20
-    // (no overflow; e^20 / (1 + e^20) rounds to 1 = the threshold branch's derivative) and
-    // sp = max(h, log1p(e^min(h, 20))), which is h above the threshold.
+    // folded at flush.  Layer 1 runs on log2(e)-scaled weights, so hs = h log2 e feeds exp2
+    // directly and sp log2 e = max(hs, log2(1 + 2^min(hs, 20 log2 e))) accumulates into gW2
+    // (times ln 2 at flush).  Softplus(beta 1, threshold 20): the capped exp argument cannot
+    // overflow, e^20 / (1 + e^20) rounds to 1 (the threshold branch's derivative) and the max
+    // is h above the threshold.
     template <bool TWO>
     __device__ __forceinline__ void bwd2_f32(float xa0, float xa1, float dya, float xb0, float xb1,
                                              float dyb, float& ra, float& rb) {
@@ -168,14 +176,17 @@ template <typename T> struct Units {
         f32x2 p = {0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            f32x2 h = x0 * (float)w1a[j] + (float)b1[j];
-            if constexpr (TWO) h = x1 * (float)w1b[j] + h;
-            const f32x2 hc = {__builtin_fminf(h.x, 20.f), __builtin_fminf(h.y, 20.f)};
-            const f32x2 hl = hc * kLog2e;
-            const f32x2 z = {__builtin_amdgcn_exp2f(hl.x), __builtin_amdgcn_exp2f(hl.y)};
+            f32x2 h = x0 * s1a[j] + sb1[j];
+            if constexpr (TWO) h = x1 * s1b[j] + h;
+            constexpr float kCap = 20.f * kLog2e;
+            const f32x2 hc = {__builtin_fminf(h.x, kCap), __builtin_fminf(h.y, kCap)};
+            const f32x2 z = {__builtin_amdgcn_exp2f(hc.x), __builtin_amdgcn_exp2f(hc.y)};
             const f32x2 z1 = z + 1.f;
-            const f32x2 l = f32x2{__builtin_amdgcn_logf(z1.x), __builtin_amdgcn_logf(z1.y)} * kLn2;
-            const f32x2 sp = {__builtin_fmaxf(h.x, l.x), __builtin_fmaxf(h.y, l.y)};
+            const f32x2 l = {__builtin_amdgcn_logf(z1.x), __builtin_amdgcn_logf(z1.y)};
+            // max as med3(h, l, +inf): fmaxf adds NaN-quieting maxes of h in IEEE mode (and
+            // inline asm would hide the v_log -> use wait state from the hazard recognizer)
+            const f32x2 sp = {__builtin_amdgcn_fmed3f(h.x, l.x, __builtin_inff()),
+                              __builtin_amdgcn_fmed3f(h.y, l.y, __builtin_inff())};
             const f32x2 sg = z * f32x2{__builtin_amdgcn_rcpf(z1.x), __builtin_amdgcn_rcpf(z1.y)};
             pgw2[j] = dy * sp + pgw2[j];
             const f32x2 dh = (dy * (float)w2[j]) * sg;
@@ -196,7 +207,7 @@ template <typename T> struct Units {
                 gw1a[j] += pgw1a[j].x + pgw1a[j].y;
                 gw1b[j] += pgw1b[j].x + pgw1b[j].y;
                 gb1[j] += pgb1[j].x + pgb1[j].y;
-                gw2[j] += pgw2[j].x + pgw2[j].y;
+                gw2[j] += (pgw2[j].x + pgw2[j].y) * kLn2;
             }
         for (int j = 0; j < 2; ++j) {
             const int k = lane + 64 * j;
