@@ -193,11 +193,13 @@ template <typename T> struct Units {
             pgw1a[j] = dh * x0 + pgw1a[j];
             if constexpr (TWO) pgw1b[j] = dh * x1 + pgw1b[j];
             pgb1[j] = pgb1[j] + dh;
-            p = dh * (float)w1a[j] + p;
+            p = dh * s1a[j] + p;             // d input in log2 units (ln 2 below)
         }
         gb2 += dya;
         gb2 += dyb;
         wave_sum2(p.x, p.y, ra, rb);
+        ra *= kLn2;
+        rb *= kLn2;
     }
     // add this wave's gradients into the workgroup accumulator (packed plain layout)
     template <bool TWO>
@@ -225,7 +227,7 @@ template <typename T, int kTrainThreads = train_threads<T>()>
 __global__ void __launch_bounds__(kTrainThreads)
 v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
                const T* __restrict__ p, const T* __restrict__ gp, TapeView<T> tape,
-               T* __restrict__ gpart, int64_t B, int iters, int CW) {
+               T* __restrict__ gpart, int64_t B, int iters) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N;
     constexpr int kTrainWaves = kTrainThreads / 64;
@@ -238,129 +240,118 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     const int* s_cptr = s_vptr + V + 1;
     const int* s_cedge = s_cptr + C + 1;
     size_t off = ((size_t)nints * 4 + 15) & ~(size_t)15;
-    const size_t TE = (size_t)CW * E;
-    T* s_dm = (T*)(smem + off);              // [CW][E] d loss / d m (current iteration)
-    T* s_g = s_dm + TE;                      // [CW][E] du, then dext
-    T* s_da = s_g + TE;                      // [CW][E] d a
-    T* s_u = s_da + TE;                      // [CW][E] tape of the iteration: u, t, ext
-    T* s_t = s_u + TE;
-    T* s_ext = s_t + TE;
-    T* s_x = s_ext + TE;                     // [CW][N] node features
-    T* s_acc = s_x + (size_t)CW * N;         // [1283] workgroup gradient accumulator
-    int* s_eb = (int*)(s_acc + kV24W);       // [CW][E] b*E of the edge's codeword
-    int* s_nv = s_eb + TE;                   // [CW][E] b*N + v  (index into s_x)
-    int* s_nc = s_nv + TE;                   // [CW][E] b*N + V + c
+    T* s_dm = (T*)(smem + off);              // [E] d loss / d m (current iteration)
+    T* s_g = s_dm + E;                       // [E] du, then dext
+    T* s_da = s_g + E;                       // [E] d a
+    T* s_u = s_da + E;                       // [E] tape of the iteration: u, t, ext
+    T* s_t = s_u + E;
+    T* s_ext = s_t + E;
+    T* s_xv = s_ext + E;                     // [E] x_{v(e)}  (prior of the edge's variable)
+    T* s_sc = s_xv + E;                      // [E] s_{c(e)}  (syndrome of the edge's check)
+    T* s_acc = s_sc + E;                     // [1283] workgroup gradient accumulator
 
     const int* gtab = (const int*)g.edge_vc;
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     for (int i = tid; i < kV24W; i += kTrainThreads) s_acc[i] = T(0);
-    const int64_t b0 = (int64_t)blockIdx.x * CW;
-    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
-    const int nE = nb * E;
-    for (int i = tid; i < nb * N; i += kTrainThreads) s_x[i] = x[(size_t)b0 * N + i];
-    // readout inputs: m^T into s_u, d loss / d r per edge into s_da; per-edge index tables
-    for (int f = tid; f < nE; f += kTrainThreads) {
-        const int b = f / E, e = f - b * E;
-        const uint32_t vc = s_evc[e];
-        s_eb[f] = b * E;
-        s_nv[f] = b * N + (int)(vc & 0xffffu);
-        s_nc[f] = b * N + V + (int)(vc >> 16);
-        const size_t bv = (size_t)(b0 + b) * V + (int)(vc & 0xffffu);
-        const T pv = p[bv];
-        s_u[f] = tape.mT[(size_t)b0 * E + f];
-        s_da[f] = -((gp[bv] * (T(1) - pv)) * pv);     // p = sigmoid(-r)
-    }
-
     Units<T> uv, uc, uo;                     // ggc1.mlp, ggc2.mlp, mlp
     uv.load2(w + kV24Ggc1, lane);
     uc.load1(w + kV24Ggc2, lane);
     uo.load1(w + kV24Mlp, lane);
     __syncthreads();
 
-    // unit-parallel pass over the tile's edges, two per wave step:
+    // unit-parallel pass over the codeword's edges, two per wave step:
     // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
-    auto unit_pass = [&](auto& U, auto two_tag, const T* in0, auto in1_of, auto dy_of, T* outp) {
+    auto unit_pass = [&](auto& U, auto two_tag, const T* in0, const T* in1, auto dy_of, T* outp) {
         constexpr bool TWO = decltype(two_tag)::value;
-        for (int f = wave; f < nE; f += 2 * kTrainWaves) {
+        for (int f = wave; f < E; f += 2 * kTrainWaves) {
             const int f2 = f + kTrainWaves;
-            const bool has2 = f2 < nE;
+            const bool has2 = f2 < E;
             const int fb = has2 ? f2 : f;
             T ra, rb;
-            U.template bwd2<TWO>(in0[f], in1_of(f), dy_of(f), in0[fb], in1_of(fb),
-                                 has2 ? dy_of(fb) : T(0), ra, rb);
+            U.template bwd2<TWO>(in0[f], TWO ? in1[f] : T(0), dy_of(f), in0[fb],
+                                 TWO ? in1[fb] : T(0), has2 ? dy_of(fb) : T(0), ra, rb);
             if (lane == 0) {
                 outp[f] = ra;
                 if (has2) outp[f2] = rb;
             }
         }
     };
-    auto zero = [](int) { return T(0); };
 
     // the iteration's tape rows: the first kPF per thread are loaded into registers one
-    // iteration ahead (their HBM latency hides behind the previous iteration's phases),
-    // the rest (tiles of several codewords) load when staged
-    constexpr int kPF = 2;
+    // iteration ahead (their HBM latency hides behind the previous iteration's phases)
+    constexpr int kPF = 1;
     T pu[kPF], pt[kPF], pe[kPF];
-    auto prefetch = [&](int it) {
-        const size_t trow = ((size_t)it * B + b0) * E;
+    // persistent over codewords b = blockIdx.x, blockIdx.x + gridDim.x, ...: the lanes'
+    // gradient registers accumulate across all of them (one partial row per workgroup, any
+    // batch size, LDS independent of B)
+    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+        auto prefetch = [&](int it) {
+            const size_t trow = ((size_t)it * B + b) * E;
 #pragma unroll
-        for (int i = 0; i < kPF; ++i) {
-            const int f = tid + i * kTrainThreads;
-            if (f < nE) { pu[i] = tape.u[trow + f]; pt[i] = tape.t[trow + f]; pe[i] = tape.ext[trow + f]; }
-        }
-    };
-    auto stage = [&](int it) {
+            for (int i = 0; i < kPF; ++i) {
+                const int f = tid + i * kTrainThreads;
+                if (f < E) { pu[i] = tape.u[trow + f]; pt[i] = tape.t[trow + f]; pe[i] = tape.ext[trow + f]; }
+            }
+        };
+        auto stage = [&](int it) {
 #pragma unroll
-        for (int i = 0; i < kPF; ++i) {
-            const int f = tid + i * kTrainThreads;
-            if (f < nE) { s_u[f] = pu[i]; s_t[f] = pt[i]; s_ext[f] = pe[i]; }
+            for (int i = 0; i < kPF; ++i) {
+                const int f = tid + i * kTrainThreads;
+                if (f < E) { s_u[f] = pu[i]; s_t[f] = pt[i]; s_ext[f] = pe[i]; }
+            }
+            const size_t trow = ((size_t)it * B + b) * E;
+            for (int f = tid + kPF * kTrainThreads; f < E; f += kTrainThreads) {
+                s_u[f] = tape.u[trow + f];
+                s_t[f] = tape.t[trow + f];
+                s_ext[f] = tape.ext[trow + f];
+            }
+        };
+        if (iters > 0) prefetch(iters - 1);
+        // readout inputs: m^T into s_u, d loss / d r per edge into s_da; per-edge x_v, s_c
+        const T* xb = x + (size_t)b * N;
+        for (int f = tid; f < E; f += kTrainThreads) {
+            const uint32_t vc = s_evc[f];
+            const size_t bv = (size_t)b * V + (int)(vc & 0xffffu);
+            const T pv = p[bv];
+            s_xv[f] = xb[vc & 0xffffu];
+            s_sc[f] = xb[V + (int)(vc >> 16)];
+            s_u[f] = tape.mT[(size_t)b * E + f];
+            s_da[f] = -((gp[bv] * (T(1) - pv)) * pv);     // p = sigmoid(-r)
         }
-        const size_t trow = ((size_t)it * B + b0) * E;
-        for (int f = tid + kPF * kTrainThreads; f < nE; f += kTrainThreads) {
-            s_u[f] = tape.u[trow + f];
-            s_t[f] = tape.t[trow + f];
-            s_ext[f] = tape.ext[trow + f];
-        }
-    };
-    if (iters > 0) prefetch(iters - 1);
+        __syncthreads();
 
-    // readout: r_v = sum_e MLP_o(m^T_e) + x_v  ->  dm
-    unit_pass(uo, std::false_type{}, s_u, zero, [&](int f) { return s_da[f]; }, s_dm);
-    __syncthreads();
+        // readout: r_v = sum_e MLP_o(m^T_e) + x_v  ->  dm
+        unit_pass(uo, std::false_type{}, s_u, nullptr, [&](int f) { return s_da[f]; }, s_dm);
+        __syncthreads();
 
-    for (int it = iters - 1; it >= 0; --it) {
-        stage(it);
-        __syncthreads();
-        if (it > 0) prefetch(it - 1);
-        // A: m^{t+1} = MLP_c(u) s_c + m^t
-        unit_pass(uc, std::false_type{}, s_u, zero, [&](int f) { return s_dm[f] * s_x[s_nc[f]]; },
-                  s_g);
-        __syncthreads();
-        // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
-        for (int f = tid; f < nE; f += kTrainThreads) {
-            const int eb = s_eb[f];
-            const int c = (int)(s_evc[f - eb] >> 16);
-            const T* gb = s_g + eb;
-            T s = T(0);
-            for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += gb[s_cedge[k]];
-            const T t = s_t[f];
-            s_da[f] = ((s - s_g[f]) * (T(1) - t * t)) / T(2);
+        for (int it = iters - 1; it >= 0; --it) {
+            stage(it);
+            __syncthreads();
+            if (it > 0) prefetch(it - 1);
+            // A: m^{t+1} = MLP_c(u) s_c + m^t
+            unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; }, s_g);
+            __syncthreads();
+            // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
+            for (int f = tid; f < E; f += kTrainThreads) {
+                const int c = (int)(s_evc[f] >> 16);
+                T s = T(0);
+                for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += s_g[s_cedge[k]];
+                const T t = s_t[f];
+                s_da[f] = ((s - s_g[f]) * (T(1) - t * t)) / T(2);
+            }
+            __syncthreads();
+            // C: a = MLP_v(ext, x_v)
+            unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; }, s_g);
+            __syncthreads();
+            // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
+            for (int f = tid; f < E; f += kTrainThreads) {
+                const int v = (int)(s_evc[f] & 0xffffu);
+                T s = T(0);
+                for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += s_g[k];
+                s_dm[f] += s - s_g[f];
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        // C: a = MLP_v(ext, x_v)
-        unit_pass(uv, std::true_type{}, s_ext, [&](int f) { return s_x[s_nv[f]]; },
-                  [&](int f) { return s_da[f]; }, s_g);
-        __syncthreads();
-        // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
-        for (int f = tid; f < nE; f += kTrainThreads) {
-            const int eb = s_eb[f];
-            const int v = (int)(s_evc[f - eb] & 0xffffu);
-            const T* gb = s_g + eb;
-            T s = T(0);
-            for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += gb[k];
-            s_dm[f] += s - s_g[f];
-        }
-        __syncthreads();
     }
 
     // workgroup gradient: waves add in order (deterministic), then one row per workgroup
@@ -390,27 +381,23 @@ __global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __r
     gw[i] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
-int train_tile(const gnnd_graph* g, int64_t B) {
-    (void)g;
-    // one codeword per workgroup up to 1024 codewords (>= 4 workgroups per CU's worth of
-    // waves at 8 waves each); larger batches group codewords to bound the partial rows
-    return B <= 1024 ? 1 : (int)((B + 1023) / 1024);
-}
-size_t train_lds(const gnnd_graph* g, int esz, int cw) {
+// workgroups of the reverse pass: one codeword each up to 1024 (the partial-row count),
+// larger batches loop (each workgroup a fixed, strided set of codewords: deterministic)
+constexpr int64_t kTrainMaxBlocks = 1024;
+int64_t train_blocks(int64_t B) { return B < kTrainMaxBlocks ? B : kTrainMaxBlocks; }
+size_t train_lds(const gnnd_graph* g, int esz) {
     const GraphView& v = g->view;
     return (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
-           (size_t)esz * (6 * (size_t)cw * v.E + (size_t)cw * v.N + kV24W) +
-           4 * 3 * (size_t)cw * v.E;
+           (size_t)esz * (8 * (size_t)v.E + kV24W);
 }
 
 template <typename T>
 int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* out,
                const void* gout, const void* tape, void* gw, void* ws, int64_t ws_bytes,
                int64_t B, int iters, hipStream_t st) {
-    const int cw = train_tile(g, B);
-    const int64_t blocks = (B + cw - 1) / cw;
+    const int64_t blocks = train_blocks(B);
     if ((int64_t)blocks * kV24W * (int64_t)sizeof(T) > ws_bytes) return GNND_ERR_INVALID_ARG;
-    const size_t lds = train_lds(g, sizeof(T), cw);
+    const size_t lds = train_lds(g, sizeof(T));
     if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     auto kern = v24_bwd_kernel<T>;
     if (lds > 64 * 1024)
@@ -421,7 +408,7 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     TapeView<T> tv{base, base + n, base + 2 * n, base + 3 * n};
     kern<<<(unsigned)blocks, train_threads<T>(), lds, st>>>(g->view, (const T*)w, (const T*)x,
                                                       (const T*)out, (const T*)gout, tv, (T*)ws,
-                                                      B, iters, cw);
+                                                      B, iters);
     GNND_LAUNCH_CHECK();
     grad_reduce_kernel<T><<<(kV24W + 255) / 256, 256, 0, st>>>((const T*)ws, (int)blocks, (T*)gw);
     GNND_LAUNCH_CHECK();
@@ -570,8 +557,7 @@ extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const v
 extern "C" int gnnd_train_bwd_workspace(const gnnd_graph* g, int model, int dtype,
                                         int64_t batch, int64_t* h_bytes) {
     if (!train_args_ok(g, model, dtype, batch, 0) || !h_bytes) return GNND_ERR_INVALID_ARG;
-    const int cw = train_tile(g, batch);
-    *h_bytes = ((batch + cw - 1) / cw) * (int64_t)kV24W * (dtype == GNND_F64 ? 8 : 4);
+    *h_bytes = train_blocks(batch) * (int64_t)kV24W * (dtype == GNND_F64 ? 8 : 4);
     return GNND_OK;
 }
 

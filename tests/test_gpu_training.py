@@ -335,3 +335,35 @@ def test_fused_v24_trainer_matches_torch_trainer():
         assert abs(la.item() - lb.item()) <= 1e-9 * max(1.0, abs(la.item()))
     for k in keys:
         torch.testing.assert_close(b.state_dict()[k], a.state_dict()[k], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize('dtype', [torch.float64, torch.float32])
+def test_fused_training_large_batch_equals_sum_of_chunks(dtype):
+    """B > 1024: the reverse pass loops each workgroup over a strided set of codewords (one
+    gradient row per workgroup).  The reference loss is a sum, so the full-batch gradient
+    equals the sum of the gradients of chunks that each take the one-codeword-per-workgroup
+    path."""
+    import gnndecode as gd
+    H = gd.codes.toric_code(5)
+    torch.manual_seed(3)
+    m = gd.MODELS['v24'](4, H).to(DEV).to(dtype).train()
+    m.fused_train = True
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+    x, y = gd.data.toric_batch(H, 2500, seed=11, device=DEV, dtype=dtype)
+    V, N = H.shape[0], H.shape[0] + H.shape[1]
+
+    def grads(xs, ys):
+        m.zero_grad()
+        loss = lf(m(gd.data.make_batch(xs, m.graph(xs.device))), ys)
+        loss.backward()
+        return loss.item(), torch.cat([p.grad.reshape(-1) for p in m.parameters()]).double()
+
+    lf_full, g_full = grads(x, y)
+    lsum, gsum = 0.0, torch.zeros_like(g_full)
+    for b0, b1 in ((0, 1000), (1000, 2000), (2000, 2500)):
+        l, gc = grads(x[b0 * N:b1 * N], y[b0 * V:b1 * V])
+        lsum += l
+        gsum += gc
+    tol = 1e-10 if dtype == torch.float64 else 2e-4
+    assert abs(lf_full - lsum) <= tol * abs(lsum)
+    assert (g_full - gsum).abs().max().item() <= tol * gsum.abs().max().item()
