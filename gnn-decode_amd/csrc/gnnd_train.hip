@@ -95,6 +95,11 @@ __device__ __forceinline__ double wave_sum(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// v with lane k replaced by the uniform value x (compare + select)
+template <typename T> __device__ __forceinline__ T put_lane(T v, T x, int k, int lane) {
+    return lane == k ? x : v;
+}
+
 // two hidden units of one MLP owned by this lane: k0 = lane, k1 = lane + 64
 template <typename T> struct Units {
     T w1a[2], w1b[2], b1[2], w2[2];         // w1b only for the 2-input MLP
@@ -167,8 +172,8 @@ template <typename T> struct Units {
     // folded at flush.  Layer 1 runs on log2(e)-scaled weights, so hs = h log2 e feeds exp2
     // directly and sp log2 e = max(hs, log2(1 + 2^min(hs, 20 log2 e))) accumulates into gW2
     // (times ln 2 at flush).  Softplus(beta 1, threshold 20): the capped exp argument cannot
-    // overflow, e^20 / (1 + e^20) rounds to 1 (the threshold branch's derivative) and the max
-    // is h above the threshold.
+    // overflow, e^20 / (1 + e^20) rounds to 1 (the threshold branch's derivative) and the
+    // value is h above the threshold.
     template <bool TWO>
     __device__ __forceinline__ void bwd2_f32(float xa0, float xa1, float dya, float xb0, float xb1,
                                              float dyb, float& ra, float& rb) {
@@ -183,10 +188,9 @@ template <typename T> struct Units {
             const f32x2 z = {__builtin_amdgcn_exp2f(hc.x), __builtin_amdgcn_exp2f(hc.y)};
             const f32x2 z1 = z + 1.f;
             const f32x2 l = {__builtin_amdgcn_logf(z1.x), __builtin_amdgcn_logf(z1.y)};
-            // max as med3(h, l, +inf): fmaxf adds NaN-quieting maxes of h in IEEE mode (and
-            // inline asm would hide the v_log -> use wait state from the hazard recognizer)
-            const f32x2 sp = {__builtin_amdgcn_fmed3f(h.x, l.x, __builtin_inff()),
-                              __builtin_amdgcn_fmed3f(h.y, l.y, __builtin_inff())};
+            // l + (h - hc): l below the cap, h (to within an ulp) above it; two packed adds
+            // instead of max(h, l) (whose fmaxf form adds NaN-quieting maxes in IEEE mode)
+            const f32x2 sp = l + (h - hc);
             const f32x2 sg = z * f32x2{__builtin_amdgcn_rcpf(z1.x), __builtin_amdgcn_rcpf(z1.y)};
             pgw2[j] = dy * sp + pgw2[j];
             const f32x2 dh = (dy * (float)w2[j]) * sg;
@@ -261,18 +265,28 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
 
     // unit-parallel pass over the codeword's edges, two per wave step:
     // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
+    // The uniform results of step k go to lane k of two VGPRs (compare + select), stored by the
+    // lanes after every 64 steps (no per-step exec-masked lane-0 stores).
     auto unit_pass = [&](auto& U, auto two_tag, const T* in0, const T* in1, auto dy_of, T* outp) {
         constexpr bool TWO = decltype(two_tag)::value;
-        for (int f = wave; f < E; f += 2 * kTrainWaves) {
-            const int f2 = f + kTrainWaves;
-            const bool has2 = f2 < E;
-            const int fb = has2 ? f2 : f;
-            T ra, rb;
-            U.template bwd2<TWO>(in0[f], TWO ? in1[f] : T(0), dy_of(f), in0[fb],
-                                 TWO ? in1[fb] : T(0), has2 ? dy_of(fb) : T(0), ra, rb);
-            if (lane == 0) {
-                outp[f] = ra;
-                if (has2) outp[f2] = rb;
+        constexpr int kStride = 2 * kTrainWaves;
+        for (int f0 = wave; f0 < E; f0 += 64 * kStride) {
+            T resa = T(0), resb = T(0);
+            int k = 0;
+            for (int f = f0; f < E && k < 64; f += kStride, ++k) {
+                const int f2 = f + kTrainWaves;
+                const bool has2 = f2 < E;
+                const int fb = has2 ? f2 : f;
+                T ra, rb;
+                U.template bwd2<TWO>(in0[f], TWO ? in1[f] : T(0), dy_of(f), in0[fb],
+                                     TWO ? in1[fb] : T(0), has2 ? dy_of(fb) : T(0), ra, rb);
+                resa = put_lane(resa, ra, k, lane);
+                resb = put_lane(resb, rb, k, lane);
+            }
+            const int fl = f0 + kStride * lane;
+            if (lane < k) {
+                outp[fl] = resa;
+                if (fl + kTrainWaves < E) outp[fl + kTrainWaves] = resb;
             }
         }
     };
