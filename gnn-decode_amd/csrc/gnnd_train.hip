@@ -31,12 +31,23 @@ namespace {
 template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
 constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 
-// softplus and its derivative at h (natural units)
+// softplus and its derivative at h (natural units).  fp64 without libm (the forward's
+// scheme, gnnd_common.h): e = e^-|h| in (0, 1], sp = max(h, 0) + log1p(e),
+// sg = sigmoid(h) = (h >= 0 ? 1 : e) / (1 + e) with a Newton-refined v_rcp_f64; above the
+// threshold sp = h, sg = 1 (torch's Softplus backward)
 __device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg) {
-    if (h > 20.0) { sp = h; sg = 1.0; return; }
-    const double z = exp(h);
-    sp = log1p(z);
-    sg = z / (z + 1.0);
+    const double e = exp_nonpos_f64(-__builtin_fabs(h));
+    const double r = log1p_unit_f64(e);
+    const double d = 1.0 + e;
+    double rc = __builtin_amdgcn_rcp(d);
+    rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
+    rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
+    const double num = h >= 0.0 ? 1.0 : e;
+    double q = num * rc;
+    q = __builtin_fma(__builtin_fma(-q, d, num), rc, q);               // num / d, ~0.5 ulp
+    const bool big = h > 20.0;
+    sp = big ? h : (h > 0.0 ? h + r : r);
+    sg = big ? 1.0 : q;
 }
 __device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg) {
     if (h > 20.f) { sp = h; sg = 1.f; return; }
