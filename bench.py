@@ -19,6 +19,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 import torch
 import torch.distributed as dist
 
@@ -68,6 +70,9 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=12.0,
                    help='bounded CPU-baseline sample (0 disables)')
     p.add_argument('--seed', type=int, default=0)
+    p.add_argument('--weights', default='auto', choices=['auto', 'random'],
+                   help='auto: the shipped trained weights of this model/code when present '
+                        '(gnndecode/weights/<model>_<code>.npz), else random init')
     p.add_argument('--no-graph', action='store_true',
                    help='train mode: eager steps instead of one captured HIP graph per step')
     p.add_argument('--layerwise', action='store_true',
@@ -242,11 +247,18 @@ def main():
     H = gd.codes.get_code(a.code)
     torch.manual_seed(a.seed)
     model = gd.MODELS[a.model](T, H).to(dev).eval()
+    wfile = os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights', f'{a.model}_{a.code}.npz')
+    trained = a.weights == 'auto' and os.path.exists(wfile)
+    if trained:
+        z = np.load(wfile)                       # plain arrays (allow_pickle off)
+        model.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files})
     g = model.graph(dev)
     state = model.state_dict()
     classical = a.model in ('cgnni', 'cbp')
     if classical:
-        x, labels = gd.data.awgn_batch(H, a.batch, codeword_bit=0, seed=a.seed * 1000 + rank,
+        # uniform random codewords (the CGNNI decoder is not symmetric under codeword
+        # translation, so the reference's constant-word input would flatter it)
+        x, labels = gd.data.awgn_batch(H, a.batch, codewords='random', seed=a.seed * 1000 + rank,
                                        device=dev, dtype=dtype)
     else:
         x, labels = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
@@ -311,7 +323,8 @@ def main():
             'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
             'ms_per_step': elapsed / a.steps * 1e3,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': a.dtype, 'data': 'synthetic (on-device AWGN/toric sampler, seeded); random-init weights',
+            'dtype': a.dtype, 'data': 'synthetic (on-device AWGN/toric sampler, seeded); ' +
+                                      ('trained weights' if trained else 'random-init weights'),
             'config': {'workload': f'{a.code} {a.model} decode, T={T}, batch={a.batch}/GPU',
                        'code': a.code, 'model': a.model, 'iters': T, 'batch_per_gpu': a.batch,
                        'global_batch': a.batch * world, 'parallelism': f'dp{world} (codeword shards)',
@@ -319,8 +332,10 @@ def main():
                        'items_per_lane': plan['items_per_lane'],
                        'hard_decision_error_rate': ber,
                        'channel_hard_decision_error_rate': ch_ber,
-                       'weights': 'random init (seeded): compute cost is weight-independent; '
-                                  'BER parity vs the oracle is in cpu_baseline'},
+                       'weights': (f'trained: {os.path.relpath(wfile, ROOT)} (tools/train_cgnni_bch.py)'
+                                   if trained else 'random init (seeded)') +
+                                  ': compute cost is weight-independent; BER parity vs the '
+                                  'oracle is in cpu_baseline'},
             'roofline': {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
                          'frac': achieved / peak, 'traffic': traffic,
                          'kernel': f"{plan['kernel']}<{a.model}, {a.dtype}>",

@@ -176,6 +176,35 @@ def gf2_rank(M):
     return rank
 
 
+def gf2_generator(H):
+    """Generator matrix G [k, V] of the code {c : c H = 0 (mod 2)} for H [V, C] (the
+    reference's orientation): a basis of the GF(2) null space of H^T by Gauss-Jordan
+    elimination.  k = V - rank(H) (BCH(63,45): 45)."""
+    A = np.array(H, np.uint8).T % 2                     # [C, V]
+    rows, V = A.shape
+    piv_cols, r = [], 0
+    for c in range(V):
+        piv = np.nonzero(A[r:, c])[0]
+        if piv.size == 0:
+            continue
+        p = r + piv[0]
+        A[[r, p]] = A[[p, r]]
+        mask = A[:, c].astype(bool)
+        mask[r] = False
+        A[mask] ^= A[r]
+        piv_cols.append(c)
+        r += 1
+        if r == rows:
+            break
+    free = [c for c in range(V) if c not in set(piv_cols)]
+    G = np.zeros((len(free), V), np.uint8)
+    for i, f in enumerate(free):                        # free variable f = 1, pivots solved
+        G[i, f] = 1
+        for j, pc in enumerate(piv_cols):
+            G[i, pc] = A[j, f]
+    return G
+
+
 CODES = {
     'bch_63_45': bch_63_45,
     'toric_4': lambda: toric_code(4),

@@ -16,16 +16,27 @@ import torch
 
 
 def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=0, seed=0, device='cuda',
-               dtype=torch.float32):
+               dtype=torch.float32, codewords='fixed'):
+    """codewords='fixed': every codeword is the constant word `codeword_bit` (the
+    reference's Gen_Data input); 'random': uniform random codewords of H (random GF(2)
+    combinations of the generator rows, codes.gf2_generator), labels = their bits."""
     V, C = H.shape
     g = torch.Generator(device=device).manual_seed(seed)
     snr = torch.tensor([snrs[b % len(snrs)] for b in range(B)], dtype=torch.float32, device=device)
     sigma = torch.sqrt(1.0 / (10 ** (snr / 10)))
-    y = (1 - 2 * float(codeword_bit)) + sigma[:, None] * torch.randn(B, V, generator=g, device=device)
+    if codewords == 'random':
+        from .codes import gf2_generator
+        G = torch.as_tensor(gf2_generator(H), dtype=torch.float32, device=device)
+        msg = torch.randint(0, 2, (B, G.shape[0]), generator=g, device=device).float()
+        bits = torch.remainder(msg @ G, 2)
+    elif codewords == 'fixed':
+        bits = torch.full((B, V), float(codeword_bit), device=device)
+    else:
+        raise ValueError(f'codewords must be "fixed" or "random", got {codewords!r}')
+    y = (1 - 2 * bits) + sigma[:, None] * torch.randn(B, V, generator=g, device=device)
     llr = 2 * y / (sigma[:, None] ** 2)
     x = torch.cat([llr, torch.zeros(B, C, device=device)], dim=1)
-    labels = torch.full((B, V), float(codeword_bit), device=device)
-    return x.reshape(B * (V + C), 1).to(dtype), labels.reshape(B * V, 1).to(dtype)
+    return x.reshape(B * (V + C), 1).to(dtype), bits.reshape(B * V, 1).to(dtype)
 
 
 def toric_batch(H, B, ps=(0.01, 0.02, 0.03, 0.04, 0.05, 0.06, 0.07, 0.08, 0.09, 0.1), seed=0,

@@ -242,6 +242,12 @@ class _Decoder(torch.nn.Module):
         """Flat weights in the gnnd.h layout (model parameter dtype)."""
         return None
 
+    def invalidate_weight_cache(self):
+        """Forget the prepared (packed) weights.  The cache key tracks parameter versions,
+        which device-side updates do not bump: a replayed HIP graph's optimizer step and the
+        fused trainer's gnnd_adam_step.  The trainers call this after every step."""
+        self._wcache = None
+
     def prepared_weights(self, dtype, device):
         key = (dtype, str(device), tuple(p._version for p in self.parameters()),
                tuple(p.data_ptr() for p in self.parameters()))

@@ -15,6 +15,14 @@ import torch.distributed as dist
 from . import ops
 
 
+def _invalidate(model):
+    """Drop the model's cached prepared weights after an optimizer step that ran on the
+    device (graph replay, fused Adam): parameter versions do not see those updates."""
+    fn = getattr(model, 'invalidate_weight_cache', None)
+    if fn is not None:
+        fn()
+
+
 def shard_bounds(global_batch, rank, world):
     """Contiguous codeword shard [start, end) of rank r (sizes differ by at most one)."""
     base, extra = divmod(global_batch, world)
@@ -82,6 +90,11 @@ class Trainer:
         return total
 
     def step(self, data, y):
+        out = self._step(data, y)
+        _invalidate(self.model)
+        return out
+
+    def _step(self, data, y):
         self.model.train()
         if not self.use_graph:
             return self._body(data, y)
@@ -180,6 +193,11 @@ class FusedV24Trainer:
         return total
 
     def step(self, data, y):
+        out = self._step(data, y)
+        _invalidate(self.model)      # parameters changed on the device (gnnd_adam_step)
+        return out
+
+    def _step(self, data, y):
         self.model.train()
         x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
         if not self.use_graph:

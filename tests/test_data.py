@@ -79,3 +79,19 @@ def test_awgn_llr_moments_match_gen_data():
     x1, lab1 = data.awgn_batch(H, 600, snrs=(6,), codeword_bit=1, seed=12, device='cpu')
     assert (lab1.numpy() == 1).all()
     assert _split(x1.numpy(), V, C)[0].mean() < 0
+
+
+def test_random_codewords_satisfy_parity_checks():
+    """codewords='random': labels are codewords of H (c H = 0 mod 2), about half ones, and
+    the LLR signs follow the bits at high SNR."""
+    H = codes.bch_63_45()
+    G = codes.gf2_generator(H)
+    assert G.shape == (45, 63) and codes.gf2_rank(G) == 45
+    assert not ((G.astype(np.int64) @ H) % 2).any()
+    B = 400
+    x, lab = data.awgn_batch(H, B, snrs=(12,), seed=4, device='cpu', codewords='random')
+    c = lab.view(B, 63).numpy().astype(np.int64)
+    assert not ((c @ H) % 2).any()
+    assert 0.4 < c.mean() < 0.6
+    llr = x.view(B, 81)[:, :63].numpy()
+    assert ((llr < 0) == (c == 1)).mean() > 0.999

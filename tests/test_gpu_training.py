@@ -367,3 +367,34 @@ def test_fused_training_large_batch_equals_sum_of_chunks(dtype):
     tol = 1e-10 if dtype == torch.float64 else 2e-4
     assert abs(lf_full - lsum) <= tol * abs(lsum)
     assert (g_full - gsum).abs().max().item() <= tol * gsum.abs().max().item()
+
+
+@pytest.mark.parametrize('kind', ['graph-trainer', 'fused-trainer-eager', 'fused-trainer-graph'])
+def test_eval_after_device_side_training_uses_current_weights(kind):
+    """Optimizer steps that run on the device (HIP-graph replay, gnnd_adam_step) do not bump
+    parameter versions; the eval decode must still use the updated weights."""
+    import gnndecode as gd
+    H = gd.codes.toric_code(4)
+    torch.manual_seed(5)
+    m = gd.MODELS['v24'](3, H).to(DEV).float()
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+    x, y = gd.data.toric_batch(H, 32, seed=2, device=DEV, dtype=torch.float32)
+    data = gd.data.make_batch(x, m.graph(x.device))
+    m.eval()
+    with torch.no_grad():
+        m(data)                                   # fill the prepared-weight cache
+    if kind == 'graph-trainer':
+        tr = gd.train.Trainer(m, lf, lr=1e-2, graph=True, warmup=1)
+    else:
+        m.fused_train = True
+        tr = gd.train.FusedV24Trainer(m, lf, lr=1e-2, graph=(kind == 'fused-trainer-graph'), warmup=1)
+    for _ in range(4):
+        tr.step(data, y)
+    torch.cuda.synchronize()
+    m.eval()
+    with torch.no_grad():
+        got = m(data)
+        fresh = gd.MODELS['v24'](3, H).to(DEV).float().eval()
+        fresh.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+        ref = fresh(data)
+    assert torch.equal(got, ref)
