@@ -87,6 +87,13 @@ def parse():
     return p.parse_args()
 
 
+# provenance of the shipped weights (gnn-decode_amd/gnndecode/weights/README.md)
+WEIGHT_SOURCES = {
+    'cgnni_bch_63_45': 'trained by tools/train_cgnni_bch.py',
+    'v24_toric_5': 'reference checkpoint quantum/new_model/decoder_parameters_epoch67.pkl, converted',
+}
+
+
 def load_pmc(tag):
     """Committed rocprofv3 --pmc summary of this workload (profiles/pmc_<tag>.json) or {}."""
     path = os.path.join(ROOT, 'profiles', f'pmc_{tag}.json')
@@ -297,12 +304,13 @@ def main():
         if world > 1:
             dist.all_reduce(errs)
         # uncoded reference point: hard decision on the channel LLR alone (classical codes)
+        # (quantum: the error rate of not correcting at all, i.e. the fraction of flipped qubits)
         ch_errs = ((x.view(a.batch, g.N)[:, :g.V] < 0).reshape(-1, 1).to(labels.dtype) != labels).sum() \
-            if classical else torch.zeros((), device=dev)
+            if classical else labels.sum()
         if world > 1:
             dist.all_reduce(ch_errs)
     ber = float(errs.item()) / (a.batch * g.V * world)
-    ch_ber = float(ch_errs.item()) / (a.batch * g.V * world) if classical else None
+    ch_ber = float(ch_errs.item()) / (a.batch * g.V * world)
 
     if rank == 0:
         fl, trans = flops_per_codeword(a.model, g, T)
@@ -332,7 +340,7 @@ def main():
                        'items_per_lane': plan['items_per_lane'],
                        'hard_decision_error_rate': ber,
                        'channel_hard_decision_error_rate': ch_ber,
-                       'weights': (f'trained: {os.path.relpath(wfile, ROOT)} (tools/train_cgnni_bch.py)'
+                       'weights': (f'{os.path.relpath(wfile, ROOT)} ({WEIGHT_SOURCES.get(a.model + "_" + a.code, "")})'
                                    if trained else 'random init (seeded)') +
                                   ': compute cost is weight-independent; BER parity vs the '
                                   'oracle is in cpu_baseline'},
