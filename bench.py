@@ -300,9 +300,12 @@ def main():
 
     # hard-decision error rate of this batch (outside the timed region)
     with torch.no_grad():
-        errs = ((out > 0.5).to(labels.dtype) != labels).sum()
+        # one launch: bit errors, frame errors, residual-syndrome / logical failures (toric)
+        lg = None if classical else (torch.as_tensor(gd.codes.toric_logicals(H)) != 0).to(torch.int32)
+        counts = gd.ops.decision_errors(g, lg, out, labels)
         if world > 1:
-            dist.all_reduce(errs)
+            dist.all_reduce(counts)
+        errs = counts[0]
         # uncoded reference point: hard decision on the channel LLR alone (classical codes)
         # (quantum: the error rate of not correcting at all, i.e. the fraction of flipped qubits)
         ch_errs = ((x.view(a.batch, g.N)[:, :g.V] < 0).reshape(-1, 1).to(labels.dtype) != labels).sum() \
@@ -310,6 +313,8 @@ def main():
         if world > 1:
             dist.all_reduce(ch_errs)
     ber = float(errs.item()) / (a.batch * g.V * world)
+    cl = counts.tolist()
+    fer = (cl[1] if classical else cl[2] + cl[3]) / (a.batch * world)
     ch_ber = float(ch_errs.item()) / (a.batch * g.V * world)
 
     if rank == 0:
@@ -339,6 +344,9 @@ def main():
                        'codewords_per_workgroup': plan['cw'], 'lds_bytes_per_workgroup': plan['lds'],
                        'items_per_lane': plan['items_per_lane'],
                        'hard_decision_error_rate': ber,
+                       # classical: codewords with a bit error; toric: residual-syndrome or
+                       # logical failures (quantum/neural_BP.py:333-348)
+                       'frame_error_rate': fer,
                        'channel_hard_decision_error_rate': ch_ber,
                        'weights': (f'{os.path.relpath(wfile, ROOT)} ({WEIGHT_SOURCES.get(a.model + "_" + a.code, "")})'
                                    if trained else 'random init (seeded)') +

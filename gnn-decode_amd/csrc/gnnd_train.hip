@@ -527,6 +527,77 @@ int launch_syndrome_loss(const gnnd_graph* g, const int32_t* lg, int nl, int log
 }
 
 // ---------------------------------------------------------------------------------------
+// hard-decision metrics: bit/frame error counts (the bench's BER/FER; the
+// reference reports losses only) and the toric failure rule of quantum/neural_BP.py:333-348
+// (residual syndrome failure, else logical failure) on the device, one wave per codeword,
+// integer counts (atomics on integers: exact, order-free)
+// ---------------------------------------------------------------------------------------
+// counts[0] bit errors (pred > 0.5 != y), [1] codewords with a bit error, [2] codewords whose
+// residual e = y xor hat(e) violates a check, [3] codewords with zero residual syndrome but
+// odd overlap with a logical row
+template <typename T>
+__global__ void __launch_bounds__(256)
+decision_errors_kernel(GraphView g, const int32_t* __restrict__ lg, int nl,
+                       const T* __restrict__ pred, const T* __restrict__ y,
+                       unsigned long long* __restrict__ counts, int64_t B) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int V = g.V, C = g.C;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* s_e = (uint8_t*)smem + (size_t)wave * ((V + 15) & ~15);
+    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+    if (b >= B) return;                          // whole wave exits (no block barrier below)
+    const T* pb = pred + b * V;
+    const T* yb = y + b * V;
+    int nerr = 0;
+    for (int v = lane; v < V; v += 64) {
+        const int e = (pb[v] > T(0.5)) != (yb[v] > T(0.5));
+        s_e[v] = (uint8_t)e;
+        nerr += e;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int bad_chk = 0;
+    for (int r = lane; r < C; r += 64) {         // lanes over checks (graph CSR)
+        int par = 0;
+        for (int k = g.chk_ptr[r]; k < g.chk_ptr[r + 1]; ++k)
+            par ^= s_e[g.edge_vc[g.chk_edge[k]] & 0xffffu];
+        bad_chk |= par;
+    }
+    int bad_log = 0;
+    for (int l = 0; l < nl; ++l) {               // logical rows: wave parity
+        const int32_t* row = lg + (size_t)l * V;
+        int par = 0;
+        for (int v = lane; v < V; v += 64) par ^= row[v] ? s_e[v] : 0;
+        bad_log |= __builtin_popcountll(__ballot(par)) & 1;
+    }
+    const unsigned long long any_chk = __ballot(bad_chk);
+    for (int o = 32; o >= 1; o >>= 1) nerr += __shfl_xor(nerr, o);
+    if (lane == 0) {
+        if (nerr) {
+            atomicAdd(&counts[0], (unsigned long long)nerr);
+            atomicAdd(&counts[1], 1ull);
+        }
+        if (any_chk) atomicAdd(&counts[2], 1ull);
+        else if (bad_log) atomicAdd(&counts[3], 1ull);
+    }
+}
+
+template <typename T>
+int launch_decision_errors(const gnnd_graph* g, const int32_t* lg, int nl, const void* pred,
+                           const void* y, int64_t* counts, int64_t B, hipStream_t st) {
+    const GraphView& v = g->view;
+    const size_t lds = 4 * (size_t)((v.V + 15) & ~15);
+    GNND_HIP_CHECK(hipMemsetAsync(counts, 0, 4 * sizeof(int64_t), st));
+    if (B == 0) return GNND_OK;
+    const int64_t blocks = (B + 3) / 4;
+    decision_errors_kernel<T><<<(unsigned)blocks, 256, lds, st>>>(
+        v, lg, nl, (const T*)pred, (const T*)y, (unsigned long long*)counts, B);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 // Adam on one flat parameter buffer (torch.optim.Adam, amsgrad/maximize off, the
 // non-capturable update order), device-resident step counter: graph-capturable
 // ---------------------------------------------------------------------------------------
@@ -620,6 +691,20 @@ extern "C" int gnnd_syndrome_loss(const gnnd_graph* g, const int32_t* d_logical,
                                            d_loss_b, d_dpred, batch, st);
     return launch_syndrome_loss<double>(g, d_logical, n_logical, logical_only, d_pred, d_y,
                                         d_loss_b, d_dpred, batch, st);
+}
+
+extern "C" int gnnd_decision_errors(const gnnd_graph* g, const int32_t* d_logical,
+                                    int32_t n_logical, int dtype, const void* d_pred,
+                                    const void* d_y, int64_t* d_counts, int64_t batch,
+                                    void* stream) {
+    if (!g || n_logical < 0 || (n_logical > 0 && !d_logical) || batch < 0 || !d_counts)
+        return GNND_ERR_INVALID_ARG;
+    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
+    if (batch > 0 && (!d_pred || !d_y)) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GNND_F32)
+        return launch_decision_errors<float>(g, d_logical, n_logical, d_pred, d_y, d_counts, batch, st);
+    return launch_decision_errors<double>(g, d_logical, n_logical, d_pred, d_y, d_counts, batch, st);
 }
 
 extern "C" int gnnd_adam_step(int dtype, void* d_param, const void* d_grad, void* d_exp_avg,

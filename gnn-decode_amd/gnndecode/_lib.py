@@ -53,6 +53,7 @@ SIGNATURES = {
     'gnnd_train_bwd': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32,
                               _vp]),
     'gnnd_syndrome_loss': (_int, [_vp, _vp, _i32, _i32, _int, _vp, _vp, _vp, _vp, _i64, _vp]),
+    'gnnd_decision_errors': (_int, [_vp, _vp, _i32, _int, _vp, _vp, _vp, _i64, _vp]),
     'gnnd_adam_step': (_int, [_int, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_double, ctypes.c_double,
                               ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp]),
     'gnnd_status_string': (ctypes.c_char_p, [_int]),

@@ -84,8 +84,15 @@ class ClassicalLoss(torch.nn.Module):
                 + torch.sum((1 - self.lambda_a) * loss_c) / torch.numel(loss_c))
 
 
-def toric_failures(H, logical, y, pred):
-    """(residual-syndrome failures, logical failures) for hard decisions pred > 0.5."""
+def toric_failures(H, logical, y, pred, graph=None):
+    """(residual-syndrome failures, logical failures) for hard decisions pred > 0.5
+    (quantum/neural_BP.py:333-348).  With a TannerGraph of H and CUDA fp32/fp64 tensors the
+    counts come from one HIP launch (ops.decision_errors); otherwise torch ops."""
+    if graph is not None and pred.is_cuda and pred.dtype in (torch.float32, torch.float64):
+        from .ops import decision_errors
+        lg = (torch.as_tensor(logical) != 0).to(torch.int32)
+        c = decision_errors(graph, lg, pred, y).tolist()
+        return int(c[2]), int(c[3])
     Ht = torch.as_tensor(H, dtype=torch.float32, device=pred.device).t()
     lg = torch.as_tensor(logical, dtype=torch.float32, device=pred.device)
     V = Ht.size(1)

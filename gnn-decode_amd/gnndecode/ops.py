@@ -273,6 +273,29 @@ def syndrome_loss(graph, logical_rows, logical_only, pred, y):
     return loss_b, dpred
 
 
+def decision_errors(graph, logical_rows, pred, y):
+    """(bit errors, frame errors, residual-syndrome failures, logical failures) of hard
+    decisions pred > 0.5 against y, one HIP launch (gnnd_decision_errors); int64 tensor [4]
+    on the device (no host sync).  logical_rows: int32 [n_l, V] or None (classical)."""
+    _require_gpu(pred, y)
+    V = graph.V
+    pred = pred.contiguous()
+    y = y.to(pred.dtype).contiguous()
+    B = pred.numel() // V
+    if pred.numel() != B * V or y.numel() != pred.numel():
+        raise ValueError(f'pred/y must hold B*V values (V = {V})')
+    counts = torch.empty(4, dtype=torch.int64, device=pred.device)
+    if logical_rows is None:
+        lg, nl = None, 0
+    else:
+        lg = logical_rows.to(device=pred.device, dtype=torch.int32).contiguous()
+        nl = int(lg.size(0))
+    _lib.call('gnnd_decision_errors', graph.handle, _ptr(lg), nl,
+              dtype_code(pred.dtype), _ptr(pred), _ptr(y), _ptr(counts), B,
+              current_stream(pred.device))
+    return counts
+
+
 class SyndromeLossFn(torch.autograd.Function):
     """Batch-summed syndrome loss; backward scales the kernel's d loss / d pred."""
 

@@ -202,6 +202,18 @@ int gnnd_syndrome_loss(const gnnd_graph* g, const int32_t* d_logical, int32_t n_
                        int32_t logical_only, int dtype, const void* d_pred, const void* d_y,
                        void* d_loss_b, void* d_dpred, int64_t batch, void* stream);
 
+/* Hard-decision metrics of a decoded batch, replacing the O(B) torch.cat
+ * loops of quantum/neural_BP.py:333-348 (FER rule) and the host-side BER counts:
+ *   e = (pred > 0.5) xor (y > 0.5) per bit;
+ *   d_counts[0] = sum of e (bit errors), [1] = codewords with any bit error,
+ *   [2] = codewords with a nonzero residual syndrome H^T e,
+ *   [3] = codewords with zero residual syndrome and an odd overlap with some logical row.
+ * d_pred, d_y: [B*V] in dtype; d_logical: int32 [n_logical][V] 0/1 rows (n_logical = 0 for
+ * classical codes); d_counts: 4 int64 on the device (overwritten).                        */
+int gnnd_decision_errors(const gnnd_graph* g, const int32_t* d_logical, int32_t n_logical,
+                         int dtype, const void* d_pred, const void* d_y, int64_t* d_counts,
+                         int64_t batch, void* stream);
+
 /* Adam (torch.optim.Adam update order, amsgrad/maximize off) on one flat parameter buffer of
  * n values with its two moment buffers; *d_step is the device-resident step count (double,
  * incremented by the call), so a whole training step with the update can be captured in one

@@ -256,3 +256,38 @@ def test_cpu_tensors_fail_loudly(golden):
     g = m.graph(torch.device(DEV))
     with pytest.raises(RuntimeError):
         gd.ops.decode(g, 'cgnni', x, 25, m.prepared_weights(torch.float32, torch.device(DEV)))
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('code', ['toric_5', 'toric_7', 'bch_63_45'])
+def test_decision_errors_kernel_matches_torch(code, dtype):
+    """gnnd_decision_errors (one launch) == the torch formulas: bit/frame error counts and
+    the toric failure rule of quantum/neural_BP.py:333-348."""
+    import gnndecode as gd
+    H = gd.codes.get_code(code)
+    g = gd.TannerGraph(H, device=DEV)
+    V = H.shape[0]
+    gen = torch.Generator(device=DEV).manual_seed(7)
+    B = 777
+    y = (torch.rand(B * V, 1, generator=gen, device=DEV) < 0.05).to(dtype)
+    # predictions: mostly right, some flipped bits, some exact-0.5 ties (not > 0.5)
+    flip = torch.rand(B * V, 1, generator=gen, device=DEV) < 0.01
+    pred = torch.where(flip, 1 - y, y) * 0.8 + 0.1
+    pred[::97] = 0.5
+    pred = pred.to(dtype)
+    logical = gd.codes.toric_logicals(H) if code.startswith('toric') else None
+    lg = None if logical is None else (torch.as_tensor(logical) != 0).to(torch.int32)
+    c = gd.ops.decision_errors(g, lg, pred, y).cpu().tolist()
+    e = ((pred > 0.5).to(dtype) != y).view(B, V)
+    assert c[0] == int(e.sum()) and c[1] == int(e.any(dim=1).sum())
+    if logical is not None:
+        syn, lgf = gd.loss.toric_failures(H, logical, y, pred)          # torch path
+        assert (c[2], c[3]) == (syn, lgf)
+        assert gd.loss.toric_failures(H, logical, y, pred, graph=g) == (syn, lgf)
+    else:
+        Ht = torch.as_tensor(H, dtype=torch.float32, device=DEV).t()
+        bad = (torch.remainder(Ht @ e.float().t(), 2) != 0).any(dim=0)
+        assert c[2] == int(bad.sum()) and c[3] == 0
+    # empty batch
+    z = gd.ops.decision_errors(g, lg, pred[:0], y[:0]).cpu().tolist()
+    assert z == [0, 0, 0, 0]
