@@ -1,25 +1,27 @@
-// gnnd_train.hip — fused training step of decoder_v2_4.
+// gnnd_train.hip — fused training step of decoder_v2_4, its
+// syndrome loss, Adam, and the hard-decision metrics.
 //
 // Forward: the streaming decode kernel with its TAPE instantiation (gnnd_decode_impl.h) runs
 // GNNI.forward (quantum/decoder_v2_4.py:272-294) and records, per iteration and edge, the
 // v->c MLP input ext = S_v - m, the tanh output t and the c->v MLP input u = S_c - t, plus
-// the final messages m^T.  The loss (quantum/decoder_v2_4.py:297-317) stays in torch.
-// Backward (this file): reverse-mode through the whole T-iteration loop in ONE launch, one
-// workgroup per codeword tile, replacing the reference's autograd graph of ~60 small ops
-// per iteration:
+// the final messages m^T.  The loss (quantum/decoder_v2_4.py:297-317) and its gradient are
+// one launch (syndrome_loss_kernel).
+// Backward (this file): reverse-mode through the whole T-iteration loop in ONE launch, each
+// workgroup looping over a strided set of codewords, replacing the reference's autograd
+// graph of ~60 small ops per iteration:
 //   readout  dr_v = -(g_v (1 - p_v)) p_v,  MLP_o backward at m^T  -> dm
 //   t = T-1 .. 0:
 //     A  MLP_c backward at u with dy = dm s_c                      -> du, grads ggc2.mlp
 //     B  dt = LOO_c(du), da = (dt (1 - t^2)) / 2                   (check leave-one-out)
 //     C  MLP_v backward at (ext, x_v) with dy = da                  -> dext, grads ggc1.mlp
 //     D  dm += LOO_v(dext)                                         (residual keeps dm)
-// The MLP phases are UNIT-parallel: a wave walks its share of the tile's edges while each
-// lane owns two of the 128 hidden units (weights in VGPRs), so every weight gradient
-// accumulates in the lane's registers over all edges and iterations with no cross-lane
-// traffic; only d(input) of an edge needs a wave reduction (DPP only, result in lane 63).  The
-// edge phases B/D are edge-parallel leave-one-out sums in LDS.  Per-workgroup gradient
-// partials are summed over the workgroups in a fixed order by a second kernel
-// (deterministic, run-to-run identical).
+// The MLP phases are UNIT-parallel: a wave walks its share of the codeword's edges two at a
+// time while each lane owns two of the 128 hidden units (weights in VGPRs), so every weight
+// gradient accumulates in the lane's registers over all edges, iterations and codewords with
+// no cross-lane traffic; only d(input) of an edge needs a wave reduction (fp32: one
+// permlane-swap + DPP chain for both edges).  The edge phases B/D are edge-parallel
+// leave-one-out sums in LDS.  Per-workgroup gradient partials are summed over the
+// workgroups in a fixed order by a second kernel (deterministic, run-to-run identical).
 // torch's autograd rules are followed: Softplus(beta 1, threshold 20) backward
 // g z / (z + 1), z = e^h (g above the threshold), tanh backward g (1 - t^2), division by 2.
 #include "gnnd_decode_impl.h"
@@ -27,7 +29,7 @@
 
 namespace {
 
-// threads per workgroup: 16 waves (4 per SIMD) in fp32 (88 VGPRs), 8 in fp64 (187 VGPRs)
+// threads per workgroup: 16 waves (4 per SIMD) in fp32 (128 VGPRs), 8 in fp64 (169 VGPRs)
 template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
 constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 
