@@ -546,42 +546,50 @@ decision_errors_kernel(GraphView g, const int32_t* __restrict__ lg, int nl,
     const int V = g.V, C = g.C;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint8_t* s_e = (uint8_t*)smem + (size_t)wave * ((V + 15) & ~15);
-    const int64_t b = (int64_t)blockIdx.x * 4 + wave;
-    if (b >= B) return;                          // whole wave exits (no block barrier below)
-    const T* pb = pred + b * V;
-    const T* yb = y + b * V;
-    int nerr = 0;
-    for (int v = lane; v < V; v += 64) {
-        const int e = (pb[v] > T(0.5)) != (yb[v] > T(0.5));
-        s_e[v] = (uint8_t)e;
-        nerr += e;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int bad_chk = 0;
-    for (int r = lane; r < C; r += 64) {         // lanes over checks (graph CSR)
-        int par = 0;
-        for (int k = g.chk_ptr[r]; k < g.chk_ptr[r + 1]; ++k)
-            par ^= s_e[g.edge_vc[g.chk_edge[k]] & 0xffffu];
-        bad_chk |= par;
-    }
-    int bad_log = 0;
-    for (int l = 0; l < nl; ++l) {               // logical rows: wave parity
-        const int32_t* row = lg + (size_t)l * V;
-        int par = 0;
-        for (int v = lane; v < V; v += 64) par ^= row[v] ? s_e[v] : 0;
-        bad_log |= __builtin_popcountll(__ballot(par)) & 1;
-    }
-    const unsigned long long any_chk = __ballot(bad_chk);
-    for (int o = 32; o >= 1; o >>= 1) nerr += __shfl_xor(nerr, o);
-    if (lane == 0) {
-        if (nerr) {
-            atomicAdd(&counts[0], (unsigned long long)nerr);
-            atomicAdd(&counts[1], 1ull);
+    // each wave loops over codewords (grid-stride) and keeps its counts in registers: one
+    // set of atomics per wave, not per codeword (65 536 codewords on 4 addresses contended)
+    unsigned long long c_bit = 0, c_frame = 0, c_syn = 0, c_log = 0;
+    for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < B; b += (int64_t)gridDim.x * 4) {
+        const T* pb = pred + b * V;
+        const T* yb = y + b * V;
+        int nerr = 0;
+        for (int v = lane; v < V; v += 64) {
+            const int e = (pb[v] > T(0.5)) != (yb[v] > T(0.5));
+            s_e[v] = (uint8_t)e;
+            nerr += e;
         }
-        if (any_chk) atomicAdd(&counts[2], 1ull);
-        else if (bad_log) atomicAdd(&counts[3], 1ull);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int bad_chk = 0;
+        for (int r = lane; r < C; r += 64) {     // lanes over checks (graph CSR)
+            int par = 0;
+            for (int k = g.chk_ptr[r]; k < g.chk_ptr[r + 1]; ++k)
+                par ^= s_e[g.edge_vc[g.chk_edge[k]] & 0xffffu];
+            bad_chk |= par;
+        }
+        int bad_log = 0;
+        for (int l = 0; l < nl; ++l) {           // logical rows: wave parity
+            const int32_t* row = lg + (size_t)l * V;
+            int par = 0;
+            for (int v = lane; v < V; v += 64) par ^= row[v] ? s_e[v] : 0;
+            bad_log |= __builtin_popcountll(__ballot(par)) & 1;
+        }
+        const unsigned long long any_chk = __ballot(bad_chk);
+        for (int o = 32; o >= 1; o >>= 1) nerr += __shfl_xor(nerr, o);
+        c_bit += (unsigned)nerr;
+        c_frame += nerr != 0;
+        c_syn += any_chk != 0;
+        c_log += any_chk == 0 && bad_log;
+        __builtin_amdgcn_wave_barrier();         // s_e reads done before the next writes
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) {
+        if (c_bit) atomicAdd(&counts[0], c_bit);
+        if (c_frame) atomicAdd(&counts[1], c_frame);
+        if (c_syn) atomicAdd(&counts[2], c_syn);
+        if (c_log) atomicAdd(&counts[3], c_log);
     }
 }
 
@@ -592,7 +600,8 @@ int launch_decision_errors(const gnnd_graph* g, const int32_t* lg, int nl, const
     const size_t lds = 4 * (size_t)((v.V + 15) & ~15);
     GNND_HIP_CHECK(hipMemsetAsync(counts, 0, 4 * sizeof(int64_t), st));
     if (B == 0) return GNND_OK;
-    const int64_t blocks = (B + 3) / 4;
+    const int64_t want = (B + 3) / 4;
+    const int64_t blocks = want < 2048 ? want : 2048;     // 8 waves per CU, grid-stride
     decision_errors_kernel<T><<<(unsigned)blocks, 256, lds, st>>>(
         v, lg, nl, (const T*)pred, (const T*)y, (unsigned long long*)counts, B);
     GNND_LAUNCH_CHECK();
