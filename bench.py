@@ -94,6 +94,7 @@ def parse():
 # provenance of the shipped weights (gnn-decode_amd/gnndecode/weights/README.md)
 WEIGHT_SOURCES = {
     'cgnni_bch_63_45': 'trained by tools/train_cgnni_bch.py',
+    'cgnni_ldpc_648_324': 'trained by tools/train_cgnni_bch.py --code ldpc_648_324',
     'v24_toric_5': 'reference checkpoint quantum/new_model/decoder_parameters_epoch67.pkl, converted',
 }
 

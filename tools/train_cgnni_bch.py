@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Train the reference's classical GNNI (classical/CGNNI.py, T = 25) on BCH(63,45) with this
+"""Train the reference's classical GNNI (classical/CGNNI.py, T = 25) on BCH(63,45) (or LDPC) with this
 framework's training path (HIP propagate forward/backward kernels, captured HIP graph) and
 save the weights as .npz (state_dict keys of classical/CGNNI.py).
 
@@ -8,8 +8,8 @@ The reference's own checkpoints were trained on one constant all-ones word
 codewords (codes.gf2_generator) with the reference's loss (classical/CGNNI.py:293-309,
 lambda 0.8) and SNR grid {1..6} dB, Adam (weight decay 5e-4 as the reference).  The
 weights give bench.py a decoder whose hard decisions beat the channel's.
-usage: python tools/train_cgnni_bch.py [--steps 3000] [--batch 256] [--lr 1e-3]
-       [--out gnn-decode_amd/gnndecode/weights/cgnni_bch_63_45.npz]"""
+usage: python tools/train_cgnni_bch.py [--code bch_63_45|ldpc_648_324] [--steps 3000]
+       [--batch 256] [--lr 1e-3] [--out gnn-decode_amd/gnndecode/weights/cgnni_<code>.npz]"""
 import argparse
 import os
 import sys
@@ -39,11 +39,14 @@ def main():
     p.add_argument('--init', default='identity', choices=['identity', 'random'],
                    help='identity: readout MLP = identity, message MLP output 0 (channel '
                         'decisions at step 0); random: the reference init')
-    p.add_argument('--out', default=os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights',
-                                                 'cgnni_bch_63_45.npz'))
+    p.add_argument('--code', default='bch_63_45')
+    p.add_argument('--out', default=None)
     a = p.parse_args()
     dev = torch.device('cuda')
-    H = gd.codes.bch_63_45()
+    if a.out is None:
+        a.out = os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights', f'cgnni_{a.code}.npz')
+    H = gd.codes.get_code(a.code)
+    V = H.shape[0]
     torch.manual_seed(a.seed)
     model = gd.MODELS['cgnni'](25, H).to(dev).train()
     if a.init == 'identity':
@@ -61,7 +64,7 @@ def main():
     tr = gd.train.Trainer(model, lambda pr, y: lf(pr, y, train=True), lr=a.lr,
                           weight_decay=5e-4, graph=True, warmup=2)
     xe, ye = gd.data.awgn_batch(H, 4096, seed=10 ** 6, device=dev, codewords='random')
-    ch = float(((xe.view(4096, -1)[:, :63] < 0).reshape(-1, 1).float() != ye).float().mean())
+    ch = float(((xe.view(4096, -1)[:, :V] < 0).reshape(-1, 1).float() != ye).float().mean())
     best, best_state = 2.0, None
     t0 = time.time()
     data = None
