@@ -95,6 +95,7 @@ def parse():
 WEIGHT_SOURCES = {
     'cgnni_bch_63_45': 'trained by tools/train_cgnni_bch.py',
     'cgnni_ldpc_648_324': 'trained by tools/train_cgnni_bch.py --code ldpc_648_324',
+    'qgnni_toric_5': 'trained by tools/train_qgnni_toric.py',
     'v24_toric_5': 'reference checkpoint quantum/new_model/decoder_parameters_epoch67.pkl, converted',
 }
 
