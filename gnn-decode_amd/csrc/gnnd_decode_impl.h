@@ -1009,10 +1009,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             // {S_v, x_v} arrive as one ds_read_b64 per edge; the leave-one-out and the
             // prior are added by scalar ops (packing them would need moves into {S_a, S_b}
             // / {x_a, x_b} pairs), the rest of the chain is packed
-            auto pre2 = [&](uint32_t sa, uint32_t sb, int ca, int cbb, f32x2 mprev, int ra, int rb,
-                            f32x2& cc) {
-                const SumX<T> pa = s_sx[ca * V + (int)(sa & 0xffffu)];
-                const SumX<T> pb = s_sx[cbb * V + (int)(sb & 0xffffu)];
+            auto pre2v = [&](SumX<T> pa, SumX<T> pb, uint32_t sa, uint32_t sb, f32x2 mprev,
+                             int ra, int rb, f32x2& cc) {
                 f32x2 t;
                 if constexpr (kBase2) {
                     const f32x2 a = {__builtin_fmaf(pa.s - mprev.x, kLog2e, pa.x),
@@ -1046,6 +1044,21 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                 }
                 return t;
             };
+            auto pre2 = [&](uint32_t sa, uint32_t sb, int ca, int cbb, f32x2 mprev, int ra, int rb,
+                            f32x2& cc) {
+                return pre2v(s_sx[ca * V + (int)(sa & 0xffffu)], s_sx[cbb * V + (int)(sb & 0xffffu)],
+                             sa, sb, mprev, ra, rb, cc);
+            };
+            // {S_v, x_v} of an item pair's slots (issued one pair ahead: LDS reads cannot move
+            // above the previous pair's message writes by themselves, the compiler cannot
+            // tell the two arrays apart)
+            auto load_pair = [&](int j, SumX<T> (&px)[R][2]) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    px[r][0] = s_sx[cb[2 * j] * V + (int)(ve[2 * j][r] & 0xffffu)];
+                    px[r][1] = s_sx[cb[2 * j + 1] * V + (int)(ve[2 * j + 1][r] & 0xffffu)];
+                }
+            };
             // c->v update of two edges from the leave-one-out sums u (and sign counts n)
             auto post2 = [&](f32x2 u, f32x2 n, f32x2 scp, f32x2 mprev) {
                 if constexpr (kBase2) {
@@ -1073,13 +1086,13 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                 }
             };
             // item pair (2j, 2j + 1)
-            auto pair_step = [&](auto jc) {
+            auto pair_step = [&](auto jc, const SumX<T> (&px)[R][2]) {
                 constexpr int j = decltype(jc)::value;
                 const int qa = 2 * j, qb = 2 * j + 1;
                 f32x2 tv[R], cv[R], tsum, csum;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    tv[r] = pre2(ve[qa][r], ve[qb][r], cb[qa], cb[qb], m2[j][r], r, r, cv[r]);
+                    tv[r] = pre2v(px[r][0], px[r][1], ve[qa][r], ve[qb][r], m2[j][r], r, r, cv[r]);
                     tsum = r == 0 ? tv[0] : tsum + tv[r];
                     if constexpr (kPairBP) csum = r == 0 ? cv[0] : csum + cv[r];
                 }
@@ -1129,8 +1142,24 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             // in 6 rounds) run the last item pair as the first item alone
             const bool last_item_live = (int)(__builtin_amdgcn_readfirstlane(tid) & ~63) +
                                         (QMAX - 1) * GNND_BLOCK < C * G * CW;
+            // one-pair-ahead reads: measured +1.2 % on BCH CGNNI (4 item pairs per lane),
+            // -1.3 % on LDPC CGNNI (3 pairs) and -0.7 % on C/BP (profiles/r01/experiments)
+#ifndef GNND_NO_PAIR_PREFETCH
+            constexpr bool kAhead = kBase2 && QP >= 4;
+#else
+            constexpr bool kAhead = false;
+#endif
+            SumX<T> pxa[R][2], pxb[R][2];       // current / next pair's {S_v, x_v}
+            if constexpr (kAhead) load_pair(0, pxa);
             static_for<QP>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
+                SumX<T> (&cur)[R][2] = (j & 1) ? pxb : pxa;
+                SumX<T> (&nxt)[R][2] = (j & 1) ? pxa : pxb;
+                if constexpr (kAhead) {
+                    if constexpr (j + 1 < QP) load_pair(j + 1, nxt);
+                } else {
+                    load_pair(j, cur);
+                }
                 if constexpr (!kSolo && j == QP - 1) {
                     if (!last_item_live) {
                         f32x2 tmp[RP];
@@ -1148,7 +1177,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                         return;
                     }
                 }
-                pair_step(jc);
+                pair_step(jc, cur);
             });
             if constexpr (kSolo) solo_step(std::integral_constant<int, QMAX - 1>{}, ms);
         } else
