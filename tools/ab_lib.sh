@@ -1,3 +1,8 @@
+#!/bin/bash
+# A/B of the default libgnnd.so against a tuning build (tools/build_variant.sh NAME FLAGS ->
+# gnn-decode_amd/gnndecode/libgnnd_NAME.so, loaded through GNND_LIB), two runs each, on the
+# workloads below.  usage: tools/build_variant.sh nopf "-DGNND_NO_PAIR_PREFETCH ..." &&
+#                          tools/ab_lib.sh   (variant name nopf hard-wired below)
 set -u
 mkdir -p gpurun_out/ab
 for a in "--model cgnni" "--model qgnni --code toric_5" "--model cgnni --code ldpc_648_324 --batch 131072 --steps 40" "--model cbp"; do
