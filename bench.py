@@ -208,17 +208,17 @@ def train_main(a, world, rank, dev):
     for _ in range(a.warmup):
         tr.step(data, y)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = tr.step(data, y)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     if rank == 0:
@@ -246,12 +246,14 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
-        # bind the RCCL communicator to this rank's GPU (barriers then never touch GPU 0)
+    if world > 1 or 'TORCHELASTIC_RUN_ID' in os.environ:
+        # any torchrun launch (also --nproc-per-node 1) brings up RCCL, so the N>1 code path is
+        # the one a 1-GPU torchrun run exercises; bind the communicator to this rank's GPU
+        # (barriers then never touch GPU 0)
         dist.init_process_group('nccl', device_id=dev)
     if a.mode == 'train':
         train_main(a, world, rank, dev)
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return
     T = a.iters or gd.DEFAULT_ITERS[a.model]
@@ -289,7 +291,7 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -299,13 +301,13 @@ def main():
         step()
     ev1.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kernel_s = ev0.elapsed_time(ev1) / 1e3 / a.steps        # HIP events, same stream
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
@@ -314,14 +316,14 @@ def main():
         # one launch: bit errors, frame errors, residual-syndrome / logical failures (toric)
         lg = None if classical else (torch.as_tensor(gd.codes.toric_logicals(H)) != 0).to(torch.int32)
         counts = gd.ops.decision_errors(g, lg, out, labels)
-        if world > 1:
+        if dist.is_initialized():
             dist.all_reduce(counts)
         errs = counts[0]
         # uncoded reference point: hard decision on the channel LLR alone (classical codes)
         # (quantum: the error rate of not correcting at all, i.e. the fraction of flipped qubits)
         ch_errs = ((x.view(a.batch, g.N)[:, :g.V] < 0).reshape(-1, 1).to(labels.dtype) != labels).sum() \
             if classical else labels.sum()
-        if world > 1:
+        if dist.is_initialized():
             dist.all_reduce(ch_errs)
     ber = float(errs.item()) / (a.batch * g.V * world)
     cl = counts.tolist()
@@ -384,7 +386,7 @@ def main():
         else:
             res['cpu_baseline'] = None
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
