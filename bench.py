@@ -121,9 +121,35 @@ VALU_ISSUE_PER_S = 256 * 2.4e9
 TRANS_OPS_PER_S = 1024 * 64 / 8 * 2.4e9
 
 
+def cpu_model():
+    """`lscpu` "Model name" of this host (read from /proc/cpuinfo, no subprocess)."""
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.lower().startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_workers():
+    """Worker processes for the all-cores leg: the cores this process may run on, capped at
+    16 (the GPU box's CPU share per GPU; os.cpu_count() there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
-    """Time the oracle (numpy restatement, 1 thread) on a bounded sample of this workload
-    and compare its outputs with the GPU outputs for the same codewords."""
+    """Time the oracle (numpy restatement of the reference path) on a bounded sample of this
+    workload: (1) one thread, comparing its outputs with the GPU's on the same codewords
+    (parity, matched BER); (2) all cores: one single-threaded worker process per core
+    (spawned, never forked from this GPU process) decoding further chunks of the same batch;
+    (3) for the fp64 quantum scripts run in fp32 on the GPU, the fp32 oracle beside the fp64
+    one.  `value` is the all-cores figure; the 1-thread figure and the CPU model sit beside it."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import numpy as np
     import gnn_oracle
@@ -141,11 +167,13 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
     cond = model == 'cbp' and x_dev.dtype == torch.float32
     # the quantum scripts compute in fp64: their oracle (the reference's arithmetic) runs in
     # fp64 whatever the GPU dtype
-    ref_dt = np.float64 if model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10') else None
+    quantum = model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10')
+    ref_dt = np.float64 if quantum else None
+    t1 = seconds / 2                      # 1-thread leg, then the all-cores leg
     done, t_total, max_err, mism = 0, 0.0, 0.0, 0
     err_gpu = err_orc = 0
     c_bits = c_gpu = c_orc = 0
-    while t_total < seconds and done + chunk <= x_all.size(0):
+    while t_total < t1 and done + chunk <= x_all.size(0):
         xs = x_all[done:done + chunk].cpu().numpy().reshape(-1, 1)
         if ref_dt is not None:
             xs = xs.astype(ref_dt)
@@ -165,21 +193,92 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
             c_gpu += int(((got > 0.5) != (r64 > 0.5)).sum())
             c_orc += int(((ref > 0.5) != (r64 > 0.5)).sum())
         done += chunk
-    if limiter is not None:
-        limiter.unregister() if hasattr(limiter, 'unregister') else None
-    res = {'value': done / t_total if t_total > 0 else None, 'unit': 'codewords/s',
-           'cores': 1, 'kind': 'port',
+    one_thread = done / t_total if t_total > 0 else None
+    same_prec = None
+    if quantum and x_dev.dtype == torch.float32 and done:
+        xs = x_all[:chunk].cpu().numpy().reshape(-1, 1)           # fp32 oracle, same chunk
+        t0 = time.perf_counter()
+        gnn_oracle.decode(model, H, xs, T, w)
+        same_prec = chunk / (time.perf_counter() - t0)
+    if limiter is not None and hasattr(limiter, 'unregister'):
+        limiter.unregister()
+
+    # all cores: single-threaded worker processes (oracle/cpu_pool.py, a child process that
+    # forks its workers; this GPU process is never forked) over chunks of the same batch
+    nw = cpu_workers()
+    all_cores, sample_all = None, ''
+    if nw > 1 and one_thread:
+        import subprocess
+        import tempfile
+        per = max(1, int(one_thread * t1 / chunk))                 # ~t1 s of chunks per worker
+        n_chunks = min(nw * per, x_all.size(0) // chunk)
+        xs = x_all[:n_chunks * chunk].cpu().numpy().reshape(n_chunks, chunk * g.N, 1)
+        if ref_dt is not None:
+            xs = xs.astype(ref_dt)
+        with tempfile.TemporaryDirectory() as td:
+            sp = os.path.join(td, 'sample.npz')
+            np.savez(sp, model=np.array(model), T=np.array(T), H=np.asarray(H, np.uint8), x=xs,
+                     **{'w/' + k: v for k, v in w.items()})
+            r = subprocess.run([sys.executable, os.path.join(ROOT, 'oracle', 'cpu_pool.py'), sp,
+                                str(nw)], capture_output=True, text=True, timeout=600)
+        if r.returncode == 0 and r.stdout.strip():
+            pr = json.loads(r.stdout.strip().splitlines()[-1])
+            all_cores = pr['codewords'] / pr['seconds']
+            sample_all = (f"; all cores: {pr['codewords']} codewords on {nw} single-threaded "
+                          f"worker processes in {pr['seconds']:.1f} s")
+        else:
+            sample_all = f'; all-cores leg failed: {r.stderr.strip()[-300:]}'
+    res = {'value': all_cores if all_cores else one_thread, 'unit': 'codewords/s',
+           'cores': nw if all_cores else 1, 'kind': 'port',
+           'cpu_model': cpu_model(),
+           'value_1_thread': one_thread,
+           'value_all_cores': all_cores,
            'sample': f'{done} codewords of the same batch (chunks of {chunk}), oracle/gnn_oracle.py '
                      f'numpy restatement ({"fp64" if ref_dt is not None else str(x_dev.dtype)[6:]}), '
-                     f'1 thread, {t_total:.1f} s',
+                     f'1 thread, {t_total:.1f} s' + sample_all,
            'parity_max_abs_err': max_err, 'parity_hard_decision_mismatches': mism,
            'parity_bits_compared': done * g.V,
            # "matched BER": bit error rate of the GPU and of the oracle on the same sample
            'sample_ber_gpu': err_gpu / max(1, done * g.V),
            'sample_ber_oracle': err_orc / max(1, done * g.V)}
+    if same_prec is not None:
+        res['value_1_thread_same_precision_f32'] = same_prec
     if cond:
         res['conditioning_vs_f64_oracle'] = {'bits': c_bits, 'gpu_f32_mismatches': c_gpu,
                                              'oracle_f32_mismatches': c_orc}
+    return res
+
+
+def train_cpu_baseline(H, model, T, x, y, batch, seconds):
+    """The reference's training step restated in CPU torch autograd (oracle/torch_train.py,
+    pinned to the reference-generated gradients) on the same data: 1 thread, then all the
+    cores this host gives the process (torch intra-op threads).  Steps of the reference's
+    BATCH_SIZE = 128 (quantum/decoder_v2_4.py:192), samples/s."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import torch_train
+    w = {k: v.detach().cpu().double().numpy() for k, v in model.state_dict().items()}
+    lg = gd.codes.toric_logicals(H)
+    N, V = H.shape[0] + H.shape[1], H.shape[0]
+    bs = min(128, batch)
+    xs = x.view(-1, N)[:bs].detach().cpu().double().reshape(-1, 1)
+    ys = y.view(-1, V)[:bs].detach().cpu().double()
+    prev = torch.get_num_threads()
+    res = {'unit': 'samples/s', 'kind': 'port', 'cpu_model': cpu_model()}
+    for label, nt in (('1_thread', 1), ('all_cores', cpu_workers())):
+        torch.set_num_threads(nt)
+        st = torch_train.V24Step(H, lg, w, T)
+        st.step(xs, ys)                                    # warm-up (allocator, page-in)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 2:
+            st.step(xs, ys)
+            n += 1
+        res['value_' + label] = n * bs / (time.perf_counter() - t0)
+        res['threads_' + label] = nt
+    torch.set_num_threads(prev)
+    res['value'] = res['value_all_cores']
+    res['cores'] = res['threads_all_cores']
+    res['sample'] = (f'oracle/torch_train.py V24Step (reference forward + LossFunc + backward + Adam, '
+                     f'fp64 as the reference), steps of {bs} samples, ~{seconds / 2:.0f} s per leg')
     return res
 
 
@@ -222,6 +321,26 @@ def train_main(a, world, rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     if rank == 0:
+        step_s = elapsed / a.steps
+        roof = None
+        if model_name == 'v24':
+            # training ~ 3x the forward's algorithmic FLOPs: forward, the
+            # reverse pass through every MLP (2x); transcendentals: forward Softplus + the
+            # backward sigmoid of every unit.  Whole captured step (prepare, forward+tape,
+            # loss, reverse pass, Adam) over its wall time per step.
+            g = model.graph(dev)
+            fl, trans = flops_per_codeword('v24', g, T)
+            peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
+            achieved = 3 * fl * a.batch / step_s / 1e12
+            roof = {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
+                    'frac': achieved / peak, 'traffic': None,
+                    'kernel': 'FusedV24Trainer step (HIP graph: gnnd_train_fwd, gnnd_syndrome_loss, '
+                              'gnnd_train_bwd, gnnd_adam_step)',
+                    'flops_per_sample': 3 * fl, 'transcendentals_per_sample': 2 * trans,
+                    'step_ms': step_s * 1e3}
+        cpu = None
+        if model_name == 'v24' and a.cpu_seconds > 0 and world == 1:
+            cpu = train_cpu_baseline(H, model, T, x, y, a.batch, a.cpu_seconds)
         print(json.dumps({
             'metric': f'training samples/sec (whole node), {model_name} step with RCCL grad all-reduce',
             'value': world * a.batch * a.steps / elapsed, 'unit': 'samples/s', 'n_gpus': world,
@@ -236,7 +355,7 @@ def train_main(a, world, rank, dev):
                                 if fused and not a.torch_trainer else
                                 'fused gnnd_train_fwd/bwd, torch loss/optimizer' if fused
                                 else 'layer-by-layer propagate ops')},
-            'roofline': None, 'cpu_baseline': None}), flush=True)
+            'roofline': roof, 'cpu_baseline': cpu}), flush=True)
 
 
 def main():

@@ -15,11 +15,13 @@ import math
 import torch
 
 
-def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=0, seed=0, device='cuda',
+def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=1, seed=0, device='cuda',
                dtype=torch.float32, codewords='fixed'):
-    """codewords='fixed': every codeword is the constant word `codeword_bit` (the
-    reference's Gen_Data input); 'random': uniform random codewords of H (random GF(2)
-    combinations of the generator rows, codes.gf2_generator), labels = their bits."""
+    """codewords='fixed': every codeword is the constant word `codeword_bit` (default 1:
+    the reference's Gen_Data input is the all-ones word, classical/CGNNI.py:195, modulated
+    to -1; classical/BP.py decodes the all-zeros word, pass 0); 'random': uniform random
+    codewords of H (random GF(2) combinations of the generator rows,
+    codes.gf2_generator), labels = their bits."""
     V, C = H.shape
     g = torch.Generator(device=device).manual_seed(seed)
     snr = torch.tensor([snrs[b % len(snrs)] for b in range(B)], dtype=torch.float32, device=device)

@@ -1,18 +1,44 @@
 """Data-parallel training of the reference decoders.
 
 One process per GPU (`torch.distributed`, backend "nccl" = RCCL on ROCm).  Every rank draws
-its own shard of the global batch, runs the layer-by-layer decoder (HIP propagate forward and
-backward kernels, torch autograd through the MLPs), and the summed loss's gradients are
-all-reduced with SUM in ONE flat bucket (decoder_v2_4 has 1 283 parameters, ~10 KB in
-fp64: latency-bound, a single RCCL call per step).  SUM, not mean: the reference loss is a
-sum over the batch (quantum/decoder_v2_4.py:314-317), so the all-reduced gradient equals the
-single-process full-batch gradient.  Then every rank applies the same Adam step
-(quantum/decoder_v2_4.py:323: lr 3e-4, weight_decay 1e-9), so parameters stay bitwise equal.
+its own shard of the global batch, runs the decoder forward and reverse pass on the HIP
+kernels, and the summed loss's gradients are all-reduced with SUM in ONE flat bucket
+(decoder_v2_4 has 1 283 parameters, ~10 KB in fp64: latency-bound, a single RCCL call per
+step).  SUM, not mean: the reference loss is a sum over the batch
+(quantum/decoder_v2_4.py:314-317), so the all-reduced gradient equals the single-process
+full-batch gradient.  Then every rank applies the same Adam step, so parameters stay
+bitwise equal.
+
+HIP graphs and collectives.  A step is captured in HIP graphs for launch-bound batches, but
+the RCCL all-reduce is NOT captured: with a collective in play (world size > 1, or
+`force_collective`) the step is split into a compute graph (forward, loss, reverse pass ->
+flat gradient) and an optimizer graph (Adam), and the all-reduce of the flat gradient runs
+eagerly on the same stream between the two replays.  Single-rank runs keep one graph.
+
+Optimizer settings per model follow the reference scripts (`REFERENCE_OPTIM`).
 """
 import torch
 import torch.distributed as dist
 
 from . import ops
+
+# (lr, weight_decay) of torch.optim.Adam in each reference training script
+REFERENCE_OPTIM = {
+    'v24': (3e-4, 1e-9),      # quantum/decoder_v2_4.py:193, 323
+    'qgnni': (3e-4, 5e-4),    # quantum/QGNNI.py:161, 294
+    'nbp': (3e-4, 0.0),       # quantum/neural_BP.py:177, 378
+    'v10': (3e-4, 0.0),       # quantum/decoder_v1_0.py:177, 377
+    'v30': (3e-4, 5e-4),      # quantum/decoder_v3_0.py:173, 341
+    'cgnni': (3e-4, 5e-4),    # classical/CGNNI.py:204, 314
+}
+
+
+def reference_optim(model):
+    """(lr, weight_decay) of the reference script that trains `model` (a decoder or kind)."""
+    kind = model if isinstance(model, str) else getattr(model, 'kind', None)
+    if kind not in REFERENCE_OPTIM:
+        raise ValueError(f'no reference optimizer settings for model {kind!r}')
+    return REFERENCE_OPTIM[kind]
 
 
 def _invalidate(model):
@@ -35,10 +61,16 @@ def flat_grads(params):
                       for p in params])
 
 
-def allreduce_grads(params, group=None):
+def _collective(group, force):
+    if not dist.is_available() or not dist.is_initialized():
+        return False
+    return force or dist.get_world_size(group) > 1
+
+
+def allreduce_grads(params, group=None, force=False):
     """all_reduce(SUM) of every parameter gradient as one contiguous bucket."""
     params = [p for p in params if p.requires_grad]
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not _collective(group, force):
         return
     flat = flat_grads(params)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
@@ -51,73 +83,129 @@ def allreduce_grads(params, group=None):
         off += n
 
 
-class Trainer:
-    """zero_grad -> forward -> summed loss -> backward -> all_reduce(SUM) -> Adam.
+class _GraphedStep:
+    """Shared capture logic: `warmup` eager steps on a side stream, then HIP graphs.
 
-    `graph=True` captures that whole step (the layer-by-layer decoder launches ~900 small
-    kernels per step for T = 15) in one HIP graph after a few eager warm-up steps and
-    replays it; inputs are copied into static buffers first.  Same arithmetic, same order.
-    Requires a fixed batch shape and edge_index; Adam runs in its capturable form."""
+    Subclasses provide `_compute(x, y) -> (loss_tensor, [grad tensors])` (no collective)
+    and `_apply()` (the optimizer update from the gradients).  Without a collective both
+    run in ONE captured graph; with one, `_compute` and `_apply` are two graphs and the
+    all-reduce of the gradients (and of the loss) is issued eagerly in between."""
 
-    def __init__(self, model, loss_fn, lr=3e-4, weight_decay=1e-9, group=None, graph=False,
-                 warmup=3, capturable=None):
+    def _init_graph(self, graph, warmup, group, force_collective):
+        if graph and warmup < 1:
+            raise ValueError('graph=True needs warmup >= 1: the first eager step builds the '
+                             'device graph tables and allocator pools that capture reuses')
+        self.use_graph, self.warmup, self.group = graph, warmup, group
+        self.force_collective = force_collective
+        self._g_compute = self._g_apply = None
+        self._eager_steps = 0
+
+    def _dist(self):
+        return _collective(self.group, self.force_collective)
+
+    def _reduce(self, loss, grads):
+        for gr in grads:
+            dist.all_reduce(gr, op=dist.ReduceOp.SUM, group=self.group)
+        dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=self.group)
+
+    def _eager(self, x, y):
+        loss, grads = self._compute(x, y)
+        if self._dist():
+            self._reduce(loss, grads)
+        self._apply()
+        return loss
+
+    def _run(self, x, y):
+        if not self.use_graph:
+            return self._eager(x, y).detach().clone()
+        if self._g_compute is None:
+            if self._eager_steps < self.warmup:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    out = self._eager(x, y).detach().clone()
+                torch.cuda.current_stream().wait_stream(s)
+                self._eager_steps += 1
+                return out
+            self._sx, self._sy = x.clone(), y.clone()
+            self._g_compute = torch.cuda.CUDAGraph()
+            if self._dist():
+                with torch.cuda.graph(self._g_compute):
+                    self._sloss, self._sgrads = self._compute(self._sx, self._sy)
+                self._g_apply = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g_apply):
+                    self._apply()
+            else:
+                with torch.cuda.graph(self._g_compute):
+                    self._sloss, self._sgrads = self._compute(self._sx, self._sy)
+                    self._apply()
+        self._sx.copy_(x)
+        self._sy.copy_(y)
+        self._g_compute.replay()
+        if self._g_apply is not None:
+            self._reduce(self._sloss, self._sgrads)      # eager RCCL between the two graphs
+            self._g_apply.replay()
+        return self._sloss.clone()                       # the static buffer is reused
+
+
+class Trainer(_GraphedStep):
+    """zero_grad -> forward -> summed loss -> backward -> [all_reduce(SUM)] -> Adam, for any
+    model (the layer-by-layer decoder on the HIP propagate kernels and their backward
+    kernels, torch autograd through the MLPs).
+
+    `graph=True` captures the step (~900 small kernels for T = 15) in HIP graphs after
+    `warmup` eager steps (see `_GraphedStep` for where the collective goes).  Requires a
+    fixed batch shape and edge_index; Adam runs in its capturable form.  lr and weight decay
+    default to the reference script's values for the model (`REFERENCE_OPTIM`)."""
+
+    def __init__(self, model, loss_fn, lr=None, weight_decay=None, group=None, graph=False,
+                 warmup=3, capturable=None, force_collective=False):
         self.model = model
         self.loss_fn = loss_fn
-        self.group = group
-        self.use_graph = graph
-        self.warmup = warmup
+        rlr, rwd = reference_optim(model) if getattr(model, 'kind', None) in REFERENCE_OPTIM \
+            else (3e-4, 0.0)
+        lr = rlr if lr is None else lr
+        weight_decay = rwd if weight_decay is None else weight_decay
+        self._init_graph(graph, warmup, group, force_collective)
         # capturable Adam (device-side step count) is required under capture; its update
         # rounds differently from the host-step form, so pass capturable=True to compare an
         # eager run against a graphed one bit for bit
         self.opt = torch.optim.Adam(model.parameters(), lr, weight_decay=weight_decay,
                                     capturable=graph if capturable is None else capturable)
-        self._graph = None
-        self._eager_steps = 0
+        self._edge_index = None
 
-    def _dist(self):
-        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
-
-    def _body(self, data, y):
+    def _compute(self, x, y):
         self.opt.zero_grad(set_to_none=False)
-        pred = self.model(data)
+        # a PyG-style batch (.x, .edge_index) or a plain input tensor
+        pred = self.model(x if self._edge_index is None else _StaticBatch(x, self._edge_index))
         loss = self.loss_fn(pred, y)
         loss.backward()
-        allreduce_grads(self.model.parameters(), self.group)
-        self.opt.step()
-        total = loss.detach().clone()
+        params = [p for p in self.model.parameters() if p.requires_grad]
+        grads = []
         if self._dist():
-            dist.all_reduce(total, op=dist.ReduceOp.SUM, group=self.group)
-        return total
+            # one flat bucket; _apply scatters it back into the .grad tensors
+            self._flat = flat_grads(params)
+            grads = [self._flat]
+        return loss.detach().clone(), grads
+
+    def _apply(self):
+        if self._dist():
+            off = 0
+            for p in self.model.parameters():
+                if not p.requires_grad:
+                    continue
+                n = p.numel()
+                p.grad.copy_(self._flat[off:off + n].view_as(p))
+                off += n
+        self.opt.step()
 
     def step(self, data, y):
-        out = self._step(data, y)
+        self.model.train()
+        self._edge_index = getattr(data, 'edge_index', None)
+        x = data.x if hasattr(data, 'x') else data
+        out = self._run(x, y)
         _invalidate(self.model)
         return out
-
-    def _step(self, data, y):
-        self.model.train()
-        if not self.use_graph:
-            return self._body(data, y)
-        if self._graph is None:
-            if self._eager_steps < self.warmup:
-                # eager warm-up on a side stream (allocator pools, cached graph checks)
-                s = torch.cuda.Stream()
-                s.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(s):
-                    out = self._body(data, y)
-                torch.cuda.current_stream().wait_stream(s)
-                self._eager_steps += 1
-                return out
-            self._sx = data.x.clone()
-            self._sy = y.clone()
-            self._sdata = _StaticBatch(self._sx, data.edge_index)
-            self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph):
-                self._sloss = self._body(self._sdata, self._sy)
-        self._sx.copy_(data.x)
-        self._sy.copy_(y)
-        self._graph.replay()
-        return self._sloss
 
 
 class _StaticBatch:
@@ -126,9 +214,9 @@ class _StaticBatch:
         self.edge_index = edge_index
 
 
-class FusedV24Trainer:
+class FusedV24Trainer(_GraphedStep):
     """decoder_v2_4 training step (quantum/decoder_v2_4.py:320-348) as a handful of HIP
-    launches, the whole step captured in one HIP graph:
+    launches:
 
         prepare weights -> forward with tape (gnnd_train_fwd) -> syndrome loss and
         d loss / d out (gnnd_syndrome_loss) -> reverse pass to the flat gradient
@@ -141,14 +229,17 @@ class FusedV24Trainer:
     state_dict / load_state_dict keep working on the views.  Same update as `Trainer`
     (torch.optim.Adam's order; lr 3e-4, weight decay 1e-9 of the reference)."""
 
-    def __init__(self, model, loss_fn, lr=3e-4, weight_decay=1e-9, betas=(0.9, 0.999), eps=1e-8,
-                 group=None, graph=True, warmup=2):
+    def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
+                 group=None, graph=True, warmup=2, force_collective=False):
         from .models import DecoderV24
         if not isinstance(model, DecoderV24):
             raise TypeError('FusedV24Trainer trains decoder_v2_4 (DecoderV24) models')
-        self.model, self.loss_fn, self.group = model, loss_fn, group
-        self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
-        self.use_graph, self.warmup = graph, warmup
+        rlr, rwd = REFERENCE_OPTIM['v24']
+        self.model, self.loss_fn = model, loss_fn
+        self.lr = rlr if lr is None else lr
+        self.wd = rwd if weight_decay is None else weight_decay
+        self.betas, self.eps = betas, eps
+        self._init_graph(graph, warmup, group, force_collective)
         flat = model.packed_weights().detach().clone().contiguous()
         off = 0
         for seq, split in ((model.ggc1.mlp, True), (model.ggc2.mlp, False), (model.mlp, False)):
@@ -169,13 +260,11 @@ class FusedV24Trainer:
         self.exp_avg = torch.zeros_like(flat)
         self.exp_avg_sq = torch.zeros_like(flat)
         self.step_count = torch.zeros(1, dtype=torch.float64, device=flat.device)
-        self._graph = None
-        self._eager_steps = 0
+        # device graph tables now, never inside a capture
+        model.graph(flat.device)
+        loss_fn._graph(flat.device)
 
-    def _dist(self):
-        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
-
-    def _body(self, x, y):
+    def _compute(self, x, y):
         m = self.model
         g = m.graph(x.device)
         w = self.flat if self.flat.dtype == x.dtype else self.flat.to(x.dtype)
@@ -183,39 +272,16 @@ class FusedV24Trainer:
         lf = self.loss_fn
         loss_b, dpred = ops.syndrome_loss(lf._graph(x.device), lf.logical_rows, lf.logical_only,
                                           out, y)
-        gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
-        total = loss_b.sum()
-        if self._dist():
-            dist.all_reduce(gw, op=dist.ReduceOp.SUM, group=self.group)
-            dist.all_reduce(total, op=dist.ReduceOp.SUM, group=self.group)
-        ops.adam_step(self.flat, gw, self.exp_avg, self.exp_avg_sq, self.step_count, self.lr,
-                      self.betas, self.eps, self.wd)
-        return total
+        self._gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
+        return loss_b.sum(), [self._gw]
+
+    def _apply(self):
+        ops.adam_step(self.flat, self._gw, self.exp_avg, self.exp_avg_sq, self.step_count,
+                      self.lr, self.betas, self.eps, self.wd)
 
     def step(self, data, y):
-        out = self._step(data, y)
-        _invalidate(self.model)      # parameters changed on the device (gnnd_adam_step)
-        return out
-
-    def _step(self, data, y):
         self.model.train()
         x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
-        if not self.use_graph:
-            return self._body(x, y)
-        if self._graph is None:
-            if self._eager_steps < self.warmup:
-                s = torch.cuda.Stream()
-                s.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(s):
-                    out = self._body(x, y)
-                torch.cuda.current_stream().wait_stream(s)
-                self._eager_steps += 1
-                return out
-            self._sx, self._sy = x.clone(), y.clone()
-            self._graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._graph):
-                self._sloss = self._body(self._sx, self._sy)
-        self._sx.copy_(x)
-        self._sy.copy_(y)
-        self._graph.replay()
-        return self._sloss
+        out = self._run(x, y)
+        _invalidate(self.model)      # parameters changed on the device (gnnd_adam_step)
+        return out

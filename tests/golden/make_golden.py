@@ -520,9 +520,145 @@ def gen_neural_bp():
     save('propagate_ops_nbp', **prop)
 
 
+def _repo_codes():
+    """This framework's code constructions (the LDPC H has no reference counterpart: the
+    reference swaps H by hand, classical/CGNNI.py:180-189)."""
+    pkg = os.path.join(os.path.dirname(os.path.dirname(OUT)), 'gnn-decode_amd')
+    if pkg not in sys.path:
+        sys.path.insert(0, pkg)
+    from gnndecode import codes
+    return codes
+
+
+def gen_ldpc():
+    """Config 4's code: 802.11n LDPC(648,324) through the reference's
+    own CGNNI (classical/CGNNI.py) and classical BP (classical/BP.py) classes, H swapped in
+    the way classical/CGNNI.py:180-189 swaps H_BCH for H_LDPC.  CGNNI runs with this
+    framework's trained LDPC weights (gnndecode/weights/cgnni_ldpc_648_324.npz: plain arrays,
+    the reference state_dict keys) and with a seeded default init."""
+    codes = _repo_codes()
+    H = torch.from_numpy(codes.wifi_ldpc_648().astype(np.float32))          # [648, 324]
+    V, C = H.shape
+    save('ldpc_648_324_graph', H=H.numpy().astype(np.uint8),
+         edge_index=single_edge_index(H).numpy())
+    wz = np.load(os.path.join(os.path.dirname(codes.__file__), 'weights', 'cgnni_ldpc_648_324.npz'))
+    trained = {k: torch.from_numpy(wz[k]) for k in wz.files}
+    ns = load_ref('classical/CGNNI.py', {'MessagePassing', 'GatedGraphConv', 'GNNI'})
+    set_seed(401)
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, 1, H
+    rand = {k: v.clone() for k, v in ns['GNNI'](25).state_dict().items()}
+    for tag, sd, bit in (('cgnni_ldpc', trained, 0), ('cgnni_ldpc_randinit', rand, 1)):
+        arrays = dict(sd_to_np(sd))
+        for B, seed in ((2, 402), (6, 403)):
+            llr, _ = awgn_llr(B, V, bit, seed + (7 if bit else 0))
+            x = classical_x(llr, C)
+            arrays[f'x_B{B}'] = x.numpy()
+            for T in (1, 2, 25):
+                out, _ = run_model(ns, H, x, B, T, sd)
+                arrays[f'out_B{B}_T{T}'] = out.numpy()
+        save(tag, **arrays)
+    ns = load_ref('classical/BP.py', {'MessagePassing', 'GatedGraphConv', 'GNNI'})
+    arrays = {}
+    for B, seed in ((2, 404), (6, 405)):
+        llr, _ = awgn_llr(B, V, 0, seed, snrs=(1, 2, 3))
+        x = classical_x(llr, C)
+        arrays[f'x_B{B}'] = x.numpy()
+        for T in (1, 25):
+            out, _ = run_model(ns, H, x, B, T)
+            arrays[f'out_B{B}_T{T}'] = out.numpy()
+    save('bp_ldpc', **arrays)
+
+
+def _gf2_null_space(A):
+    """Basis [k, n] of {v : A v = 0 (mod 2)} for A [m, n] (Gauss-Jordan over GF(2))."""
+    M = (np.asarray(A) % 2).astype(np.int64)
+    m, n = M.shape
+    piv, r = [], 0
+    for c in range(n):
+        p = next((i for i in range(r, m) if M[i, c]), None)
+        if p is None:
+            continue
+        M[[r, p]] = M[[p, r]]
+        for i in range(m):
+            if i != r and M[i, c]:
+                M[i] ^= M[r]
+        piv.append(c)
+        r += 1
+    basis = []
+    for f in (c for c in range(n) if c not in piv):
+        v = np.zeros(n, np.int64)
+        v[f] = 1
+        for i, c in enumerate(piv):
+            v[c] = M[i, f]
+        basis.append(v)
+    return np.array(basis)
+
+
+def gen_fer():
+    """The hard-decision frame-failure count of quantum/neural_BP.py:322-348 (LossFunc with
+    train=0: codewords with a non-zero residual syndrome H^T(y + e_hat) plus codewords with a
+    zero residual syndrome and an odd overlap with some logical row), run with the
+    reference's own LossFunc on (a) the decoder_v2_4 fixture outputs and (b) crafted
+    predictions at L = 5 and L = 7 mixing correct decodes, syndrome failures, zero-syndrome
+    decodes (y + a random vector of the GF(2) null space of H^T: a logical failure when it
+    overlaps a logical row oddly under the reference's plain product, else a success),
+    all-zero predictions and exact-0.5 ties.  The fixture stores pred, y and the count."""
+    sys.path.insert(0, os.path.join(REF, 'quantum'))
+    import error_generate as eg
+    arrays = {}
+    for L, B, seed in ((5, 600, 501), (7, 300, 502)):
+        Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+        H = torch.from_numpy(Hnp).t()
+        hp = eg.H_Prep(H.t())
+        H_prep = torch.from_numpy(hp.get_H_Prep())
+        logical, _ = hp.get_logical(H_prep)
+        V, C = H.shape
+        ns = load_ref('quantum/neural_BP.py', {'LossFunc'}, logical=logical, H=H)
+        lf = ns['LossFunc'](H, H_prep)
+        g = torch.Generator().manual_seed(seed)
+        y = (torch.rand(B, V, generator=g, dtype=torch.float64) < 0.06).double()
+        kind = torch.randint(0, 6, (B,), generator=g)
+        pred = y.clone()
+        null = torch.from_numpy(_gf2_null_space(H.t().numpy())).double()   # H^T n = 0 (mod 2)
+        for b in range(B):
+            k = int(kind[b])
+            if k == 1:                                    # random flips (mostly syndrome failures)
+                f = (torch.rand(V, generator=g) < 0.03).double()
+                pred[b] = (pred[b] + f) % 2
+            elif k in (2, 3):                             # + a zero-syndrome pattern: a pure
+                # logical failure when it overlaps some logical row oddly, else a success
+                sel = torch.rand(null.size(0), generator=g) < 0.5
+                pred[b] = (pred[b] + null[sel].sum(0)) % 2
+            elif k == 4:                                  # predict no error
+                pred[b] = 0
+        soft = torch.where(pred > 0.5, 0.75, 0.25).double()
+        tie = torch.rand(B, V, generator=g) < 0.002       # p == 0.5 is a 0 decision (not > 0.5)
+        soft[tie] = 0.5
+        data = types.SimpleNamespace(y=y.reshape(B * V, 1))
+        with torch.no_grad():
+            cnt = lf(soft.reshape(B * V, 1), data, 0)
+        arrays[f'L{L}/pred'] = soft.reshape(B * V, 1).numpy()
+        arrays[f'L{L}/y'] = y.reshape(B * V, 1).numpy()
+        arrays[f'L{L}/count'] = np.array(float(cnt))
+    # (a) the decoder_v2_4 fixture outputs at B = 32
+    z = np.load(os.path.join(OUT, 'v24_toric5.npz'))
+    L = 5
+    Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+    H = torch.from_numpy(Hnp).t()
+    hp = eg.H_Prep(H.t())
+    H_prep = torch.from_numpy(hp.get_H_Prep())
+    logical, _ = hp.get_logical(H_prep)
+    ns = load_ref('quantum/neural_BP.py', {'LossFunc'}, logical=logical, H=H)
+    data = types.SimpleNamespace(y=torch.from_numpy(z['y_B32']))
+    with torch.no_grad():
+        cnt = ns['LossFunc'](H, H_prep)(torch.from_numpy(z['out_B32_T15']), data, 0)
+    arrays['v24_B32/count'] = np.array(float(cnt))
+    save('fer_rule', **arrays)
+
+
 if __name__ == '__main__':
     torch.set_num_threads(1)
-    which = sys.argv[1:] or ['classical', 'quantum', 'training', 'neural_bp']
+    which = sys.argv[1:] or ['classical', 'quantum', 'training', 'neural_bp', 'ldpc', 'fer']
     if 'classical' in which:
         gen_classical()
     if 'quantum' in which:
@@ -531,3 +667,7 @@ if __name__ == '__main__':
         gen_training()
     if 'neural_bp' in which:
         gen_neural_bp()
+    if 'ldpc' in which:
+        gen_ldpc()
+    if 'fer' in which:
+        gen_fer()

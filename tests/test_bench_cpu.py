@@ -1,0 +1,30 @@
+"""bench.py's CPU-baseline leg on CPU tensors (no GPU): the 1-thread oracle leg, the
+all-cores leg (oracle/cpu_pool.py child process) and the reported fields."""
+import numpy as np
+import torch
+
+import bench
+import gnn_oracle as O
+
+
+def test_cpu_baseline_fields_and_all_cores_leg(golden):
+    from conftest import weights_of
+    z = golden('cgnni_bch')
+    H = golden('bch_63_45_graph')['H']
+    w = {k: torch.from_numpy(np.array(v)) for k, v in weights_of(z).items()}
+    B, V, C = 2048, 63, 18
+    g = torch.Generator().manual_seed(0)
+    llr = 4 + 2 * torch.randn(B, V, generator=g)
+    x = torch.cat([llr, torch.zeros(B, C)], 1).reshape(-1, 1).float()
+    out = torch.from_numpy(O.decode('cgnni', H, x.numpy(), 3, {k: v.numpy() for k, v in w.items()}))
+    labels = torch.zeros(B * V, 1)
+
+    import types
+    G = types.SimpleNamespace(N=V + C, V=V)
+    res = bench.cpu_baseline('cgnni', H, w, x, out, labels, G, 3, 2.0)
+    assert res['value_1_thread'] > 0 and res['parity_hard_decision_mismatches'] == 0
+    assert res['parity_max_abs_err'] == 0.0
+    assert res['cpu_model'] is None or isinstance(res['cpu_model'], str)
+    if bench.cpu_workers() > 1:
+        assert res['value_all_cores'] and res['cores'] == bench.cpu_workers(), res['sample']
+        assert res['value'] == res['value_all_cores']

@@ -28,6 +28,9 @@ DECODERS = [
     ('v24_toric7', 'v24', 'toric_L7_graph'),
     ('nbp_toric4', 'nbp', 'toric_L4_graph'),
     ('v10_toric4', 'v10', 'toric_L4_graph'),
+    ('cgnni_ldpc', 'cgnni', 'ldpc_648_324_graph'),
+    ('cgnni_ldpc_randinit', 'cgnni', 'ldpc_648_324_graph'),
+    ('bp_ldpc', 'cbp', 'ldpc_648_324_graph'),
 ]
 
 
@@ -242,7 +245,7 @@ def test_ldpc_bp_all_zero_codeword_high_snr():
     import gnndecode as gd
     H = gd.codes.wifi_ldpc_648()
     m = gd.ClassicalBP(25, H).to(DEV).eval()
-    x, _ = gd.data.awgn_batch(H, 64, snrs=(6,), seed=3, device=DEV)
+    x, _ = gd.data.awgn_batch(H, 64, snrs=(6,), codeword_bit=0, seed=3, device=DEV)
     out = run_fused(m, x).cpu().numpy()
     assert (out > 0.5).sum() == 0
     ref = O.decode('cbp', H, x.cpu().numpy()[:8 * 972], 25)

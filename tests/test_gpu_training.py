@@ -204,7 +204,7 @@ def test_bp_check_step_backward_matches_torch_autograd(variant):
                                    rtol=1e-9, atol=1e-12 * float(m0.grad.abs().max()))
 
 
-def _dp_worker(rank, world, port, steps, q, fused_trainer=False):
+def _dp_worker(rank, world, port, steps, q, fused_trainer=False, graph=False):
     """One rank of a 2-process data-parallel run on the single GPU (gloo all-reduce of the
     flat gradient; the fused HIP training kernels on cuda:0)."""
     import os
@@ -223,10 +223,12 @@ def _dp_worker(rank, world, port, steps, q, fused_trainer=False):
     y = torch.from_numpy(z['y']).to(DEV).view(-1, H.shape[0])
     s, e = gd.train.shard_bounds(x.size(0), rank, world)
     xs, ys = x[s:e].reshape(-1, 1).contiguous(), y[s:e].reshape(-1, 1).contiguous()
-    if fused_trainer:      # eager steps: the gloo all-reduce is not graph-capturable
-        tr = gd.train.FusedV24Trainer(m, lf, lr=1e-3, graph=False)
+    # graph=True: compute and Adam replay as two HIP graphs with the (gloo) all-reduce issued
+    # eagerly between them (gnndecode/train.py _GraphedStep)
+    if fused_trainer:
+        tr = gd.train.FusedV24Trainer(m, lf, lr=1e-3, graph=graph, warmup=1)
     else:
-        tr = gd.train.Trainer(m, lf, lr=1e-3)
+        tr = gd.train.Trainer(m, lf, lr=1e-3, graph=graph, warmup=1, capturable=True)
     data = gd.data.make_batch(xs, m.graph(xs.device))
     losses = [float(tr.step(data, ys)) for _ in range(steps)]
     flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()
@@ -235,8 +237,11 @@ def _dp_worker(rank, world, port, steps, q, fused_trainer=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('fused_trainer', [False, True], ids=['torch-trainer', 'fused-trainer'])
-def test_two_rank_fused_training_equals_full_batch(golden, fused_trainer):
+@pytest.mark.parametrize('fused_trainer,graph', [(False, False), (True, False), (True, True),
+                                                  (False, True)],
+                         ids=['torch-trainer', 'fused-trainer', 'fused-trainer-graph',
+                              'torch-trainer-graph'])
+def test_two_rank_fused_training_equals_full_batch(golden, fused_trainer, graph):
     """Config 5's data-parallel step with the fused HIP kernels: 2 ranks (gloo, both on the
     one GPU), each a shard of the batch, SUM all-reduce -> same parameters and losses as a
     single full-batch process (the reference loss is a sum)."""
@@ -250,7 +255,7 @@ def test_two_rank_fused_training_equals_full_batch(golden, fused_trainer):
     steps, world = 2, 2
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, steps, q, fused_trainer))
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, steps, q, fused_trainer, graph))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -398,3 +403,45 @@ def test_eval_after_device_side_training_uses_current_weights(kind):
         fresh.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
         ref = fresh(data)
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize('fused', [True, False], ids=['fused-trainer', 'torch-trainer'])
+def test_graphed_step_with_rccl_collective_one_rank(fused):
+    """The multi-GPU step shape on the one-GPU box: a 1-rank RCCL ("nccl") process group with
+    force_collective=True runs the split capture (compute graph -> eager RCCL all_reduce ->
+    Adam graph).  A 1-rank SUM is the identity, so losses and parameters equal the
+    single-graph step bit for bit."""
+    import socket
+    import torch.distributed as dist
+    import gnndecode as gd
+    sock = socket.socket()
+    sock.bind(('127.0.0.1', 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1,
+                            device_id=torch.device(DEV, torch.cuda.current_device()))
+    try:
+        H = gd.codes.toric_code(5)
+        lg = gd.codes.toric_logicals(H)
+        torch.manual_seed(11)
+        a = gd.MODELS['v24'](5, H).to(DEV)
+        b = gd.MODELS['v24'](5, H).to(DEV)
+        b.load_state_dict(a.state_dict())
+        if fused:
+            ta = gd.train.FusedV24Trainer(a, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1)
+            tb = gd.train.FusedV24Trainer(b, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1,
+                                          force_collective=True)
+        else:
+            ta = gd.train.Trainer(a, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1)
+            tb = gd.train.Trainer(b, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1,
+                                  force_collective=True)
+        x, y = gd.data.toric_batch(H, 48, seed=3, device=DEV)
+        for s in range(4):
+            la = ta.step(gd.data.make_batch(x, a.graph(x.device)), y)
+            lb = tb.step(gd.data.make_batch(x, b.graph(x.device)), y)
+            assert la.item() == lb.item()
+        assert tb._g_apply is not None and ta._g_apply is None
+        for k, v in a.state_dict().items():
+            assert torch.equal(b.state_dict()[k], v), k
+    finally:
+        dist.destroy_process_group()

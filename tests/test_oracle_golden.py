@@ -17,6 +17,9 @@ DECODERS = [
     ('v24_toric7', 'v24', 'toric_L7_graph'),
     ('nbp_toric4', 'nbp', 'toric_L4_graph'),
     ('v10_toric4', 'v10', 'toric_L4_graph'),
+    ('cgnni_ldpc', 'cgnni', 'ldpc_648_324_graph'),
+    ('cgnni_ldpc_randinit', 'cgnni', 'ldpc_648_324_graph'),
+    ('bp_ldpc', 'cbp', 'ldpc_648_324_graph'),
 ]
 
 
@@ -77,3 +80,46 @@ def test_toric_failure_metric_counts(golden):
     # predicting no error fails exactly on the codewords with a non-zero syndrome
     nz = int((golden('v24_toric5')['x_B32'].reshape(32, -1)[:, 100:] < 0).any(axis=1).sum())
     assert O.toric_failures(g['H'], g['logical'], y, np.zeros_like(y))[0] == nz
+
+
+@pytest.mark.parametrize('L', [5, 7])
+def test_toric_failure_rule_matches_reference_lossfunc(golden, L):
+    """The oracle's hard FER rule == the reference's own LossFunc(train=0) count
+    (quantum/neural_BP.py:338-348) on crafted decodes: syndrome failures, pure logical
+    failures, stabiliser-equivalent successes, exact-0.5 ties (tests/golden/make_golden.py
+    gen_fer)."""
+    z = golden('fer_rule')
+    g = golden(f'toric_L{L}_graph')
+    syn, lg = O.toric_failures(g['H'], g['logical'], z[f'L{L}/y'], z[f'L{L}/pred'])
+    assert syn + lg == int(z[f'L{L}/count'])
+    assert syn > 0 and lg > 0
+
+
+def test_toric_failure_rule_on_decoder_outputs(golden):
+    z = golden('v24_toric5')
+    g = golden('toric_L5_graph')
+    syn, lg = O.toric_failures(g['H'], g['logical'], z['y_B32'], z['out_B32_T15'])
+    assert syn + lg == int(golden('fer_rule')['v24_B32/count'])
+
+
+def test_ldpc_graph_matches_framework_code(golden):
+    import gnndecode as gd
+    np.testing.assert_array_equal(golden('ldpc_648_324_graph')['H'], gd.codes.wifi_ldpc_648())
+
+
+@pytest.mark.parametrize('L', [5, 7])
+def test_torch_training_restatement_matches_reference_gradients(golden, L):
+    """oracle/torch_train.py (the train-mode CPU baseline) reproduces the reference's own
+    forward, LossFunc and parameter gradients (tests/golden/train_v24_L*.npz)."""
+    import torch
+    import torch_train
+    z = golden(f'train_v24_L{L}')
+    g = golden(f'toric_L{L}_graph')
+    st = torch_train.V24Step(g['H'], g['logical'], weights_of(z), int(z['T']))
+    pred = st.forward(torch.from_numpy(z['x']))
+    np.testing.assert_allclose(pred.detach().numpy().reshape(-1, 1), z['pred'], rtol=1e-10, atol=1e-13)
+    loss = st.loss(pred, torch.from_numpy(z['y']))
+    assert abs(loss.item() - float(z['loss'])) <= 1e-9 * abs(float(z['loss']))
+    loss.backward()
+    for k, p in st.p.items():
+        np.testing.assert_allclose(p.grad.numpy(), z['g/' + k], rtol=1e-8, atol=1e-11)
