@@ -1055,8 +1055,13 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             auto load_pair = [&](int j, SumX<T> (&px)[R][2]) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
+#ifdef GNND_LDS_IDEAL   // timing upper bound only (wrong results): conflict-free addresses
+                    px[r][0] = s_sx[(tid & 63) + 64 * ((r + R * 2 * j) % 15)];
+                    px[r][1] = s_sx[(tid & 63) + 64 * ((r + R * (2 * j + 1)) % 15)];
+#else
                     px[r][0] = s_sx[cb[2 * j] * V + (int)(ve[2 * j][r] & 0xffffu)];
                     px[r][1] = s_sx[cb[2 * j + 1] * V + (int)(ve[2 * j + 1][r] & 0xffffu)];
+#endif
                 }
             };
             // c->v update of two edges from the leave-one-out sums u (and sign counts n)
@@ -1104,8 +1109,14 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     m2[j][r] = post2(Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
+#ifdef GNND_LDS_IDEAL
+                    s_m[(tid & 63) + 64 * ((r + R * qa) % 100)] = m2[j][r].x;
+                    s_m[(tid & 63) + 64 * ((r + R * qb) % 100)] = m2[j][r].y;
+                    (void)mba; (void)mbb;
+#else
                     mba[ve[qa][r] >> 16] = m2[j][r].x * wnext(ve[qa][r]);
                     mbb[ve[qb][r] >> 16] = m2[j][r].y * wnext(ve[qb][r]);
+#endif
                 }
             };
             // one item with its slots in pairs (the same per-edge arithmetic as pair_step:
@@ -1276,9 +1287,15 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     const uint2 o = s_vord[i];
                     const int dp = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));
                     const int v = (int)(o.x & 0xffffu);
+#ifdef GNND_LDS_IDEAL
+                    const T s = var_sum_uniform(s_m + (tid & 63) + 64 * (i & 15), dp);
+                    if (last) out[b0 * V + vsbase + v] = M::readout(s + (kBase2 ? xg[vb * N + v] : s_sx[vsbase + v].x), s_w);
+                    else s_sx[(tid & 63) + 64 * (i % 15)].s = s;
+#else
                     const T s = var_sum_uniform(s_m + vmbase + (int)o.y, dp);
                     if (last) out[b0 * V + vsbase + v] = M::readout(s + (kBase2 ? xg[vb * N + v] : s_sx[vsbase + v].x), s_w);
                     else s_sx[vsbase + v].s = s;
+#endif
                 }
         } else if (vfixed) {
             // CW divides 256: f = tid + k 256 keeps f mod CW, so the lane's codeword and its

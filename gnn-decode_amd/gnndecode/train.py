@@ -201,7 +201,13 @@ class Trainer(_GraphedStep):
 
     def step(self, data, y):
         self.model.train()
-        self._edge_index = getattr(data, 'edge_index', None)
+        ei = getattr(data, 'edge_index', None)
+        if not self.use_graph or self._edge_index is None:
+            self._edge_index = ei
+        elif ei is not None and ei.shape != self._edge_index.shape:
+            raise ValueError('graph=True needs a fixed edge_index shape across steps')
+        # graph mode keeps the first step's edge_index (checked on the device while eager):
+        # a per-batch tensor would need a host-synchronising layout check inside the capture
         x = data.x if hasattr(data, 'x') else data
         out = self._run(x, y)
         _invalidate(self.model)

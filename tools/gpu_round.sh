@@ -2,8 +2,9 @@
 # One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel-trace summary.
 # Every GPU step runs under its own timeout; a crash/timeout (exit >= 124 or signal) ends the
 # script immediately.  Test failures (pytest exit 1) do not stop the bench.
-# usage: tools/gpu_round.sh [tag] [pytest-args...]
+# usage: [STEPS="pytest_gpu smoke bench"] tools/gpu_round.sh [tag] [pytest-args...]
 set -u
+STEPS="${STEPS:-pytest_gpu smoke bench sweep prof pmc}"
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 TAG="${1:-r01}"; shift || true
@@ -13,6 +14,7 @@ export TMPDIR=/tmp
 fatal() { echo "FATAL step $1 exit $2"; exit "$2"; }
 step() {  # name, timeout, cmd...
   local name=$1 to=$2; shift 2
+  case " $STEPS " in *" $name "*) ;; *) return 0;; esac
   echo "=== $name ($(date +%T))"
   timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
@@ -23,11 +25,11 @@ step() {  # name, timeout, cmd...
 }
 rocm-smi --showproductname > "$OUT/rocm-smi.txt" 2>&1 || true
 lscpu | grep -E "Model name|^CPU\(s\)" > "$OUT/lscpu.txt" 2>&1 || true
-step pytest_gpu 900 python -m pytest tests -m gpu -q -x "$@"
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread "$@"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
 step sweep 900 python tools/sweep.py --steps 5
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0
 step pmc 1200 bash tools/pmc.sh "$OUT/pmc"
-python tools/pmc_summary.py "$OUT/pmc" cgnni_bch_63_45_B65536_T25_f32 "$OUT/pmc_cgnni_bch_63_45_B65536_T25_f32.json" > "$OUT/pmc_summary.log" 2>&1 || true
+case " $STEPS " in *" pmc "*) python tools/pmc_summary.py "$OUT/pmc" cgnni_bch_63_45_B65536_T25_f32 "$OUT/pmc_cgnni_bch_63_45_B65536_T25_f32.json" > "$OUT/pmc_summary.log" 2>&1 || true;; esac
 echo "=== done $(date +%T)"
