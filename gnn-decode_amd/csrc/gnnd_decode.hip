@@ -40,6 +40,7 @@ int dispatch_decode(const gnnd_graph* g, int model, int dtype, const void* w, co
         case GNND_CBP: return gnnd_launch_cbp(g, dtype, w, x, out, B, iters, st);
         case GNND_NBP: return gnnd_launch_nbp(g, dtype, w, x, out, B, iters, st);
         case GNND_V10: return gnnd_launch_v10(g, dtype, w, x, out, B, iters, st);
+        case GNND_V30: return gnnd_launch_v30(g, dtype, w, x, out, B, iters, st);
         default: return GNND_ERR_INVALID_ARG;
     }
 }

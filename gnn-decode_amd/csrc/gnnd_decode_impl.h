@@ -38,6 +38,7 @@ constexpr float kLn2 = 0.6931471805599453f;
 // weight offsets in the packed layout (gnnd.h)
 constexpr int kV24Ggc1 = 0, kV24Ggc2 = 513, kV24Mlp = 898;
 constexpr int kMlp10Msg = 0, kMlp10Out = 31;
+constexpr int kV30Count = 137;       // decoder_v3_0 packed weights (gnnd.h)
 
 template <int MODEL> struct ModelTraits {
     static constexpr bool wbp = (MODEL == GNND_NBP || MODEL == GNND_V10);   // weighted BP
@@ -1332,6 +1333,7 @@ int weights_count(int model) {
         case GNND_V24: return 1283;
         case GNND_CBP: case GNND_QBP: return 0;
         case GNND_NBP: case GNND_V10: return -2;
+        case GNND_V30: return kV30Count;
         default: return -1;
     }
 }
@@ -1400,7 +1402,9 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
     const size_t wb = align16((size_t)lds_weights(model) * esz);
     const size_t target = lds_target();
-    const bool light = model != GNND_V24;
+    // light models may take the register-resident kernel; V24 and the GRU edge-state V30
+    // run their own streaming kernels
+    const bool light = model != GNND_V24 && model != GNND_V30;
     // fp64 (the quantum scripts' dtype): the same kernel with scalar math, fewer items per
     // lane (a double message takes two VGPRs) and twice the LDS budget (2 workgroups/CU).
     // Measured faster for the quantum models on the toric code (Q/BP +24 %, QGNNI +35 %,
@@ -1595,3 +1599,4 @@ int gnnd_launch_cgnni(const gnnd_graph*, int, const void*, const void*, void*, i
 int gnnd_launch_cbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_nbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_v10(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_v30(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

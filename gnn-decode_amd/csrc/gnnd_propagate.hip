@@ -4,7 +4,7 @@
 //   V24   quantum/decoder_v2_4.py:132-144   QGNNI quantum/QGNNI.py:101-112
 //   QBP   quantum/BP.py:101-119             CGNNI classical/CGNNI.py:99-108
 //   CBP   classical/BP.py:99-119            NBP   quantum/neural_BP.py:108-131
-//   V10   quantum/decoder_v1_0.py:109-131
+//   V10   quantum/decoder_v1_0.py:109-131   V30   quantum/decoder_v3_0.py:106-118
 // i.e.  out = post( scatter_(aggr, pre(msg), idx_j, dim_size)[idx_j] - pre(msg), extra[idx_j] )
 // with idx_j = edge_index[0] for flow source_to_target and edge_index[1] for
 // target_to_source (quantum/decoder_v2_4.py:89), PyG-1.x scatter_ fill rules
@@ -38,7 +38,7 @@ __host__ __device__ constexpr bool is_qbp(int var) {
 __host__ __device__ constexpr bool is_nbp(int var) { return var == GNND_NBP || var == GNND_V10; }
 
 __host__ __device__ constexpr int out_width(int var, int flow) {
-    return (var == GNND_V24 || (var == GNND_QGNNI && flow == GNND_TARGET_TO_SOURCE) ||
+    return (var == GNND_V24 || var == GNND_V30 || (var == GNND_QGNNI && flow == GNND_TARGET_TO_SOURCE) ||
             (var == GNND_NBP && flow == GNND_SOURCE_TO_TARGET)) ? 2 : 1;
 }
 
@@ -54,10 +54,11 @@ template <int VAR, typename T> __device__ __forceinline__ T bp_tanh(T m) {
     else return g_tanh(g_clamp(m, T(-10), T(10)) / T(2));
 }
 
-// c->v pre-op on the per-edge message (the BP variants also produce the sign indicator)
+// c->v pre-op on the per-edge message (the BP variants also produce the sign indicator;
+// decoder_v3_0 aggregates the raw edge states on both sides, its tanh is commented out)
 template <int VAR, int FLOW, typename T>
 __device__ __forceinline__ T pre_op(T m, T* coeff) {
-    if constexpr (FLOW == GNND_TARGET_TO_SOURCE) {
+    if constexpr (FLOW == GNND_TARGET_TO_SOURCE && VAR != GNND_V30) {
         if constexpr (is_bp(VAR)) {
             T t = bp_tanh<VAR, T>(m);
             *coeff = t < T(0) ? T(1) : T(0);
@@ -224,6 +225,7 @@ int tiled_var(const gnnd_graph* g, int var, int flow, int aggr, const void* m, c
         case GNND_CBP: return tiled_flow<GNND_CBP, T>(g, flow, aggr, m, ex, o, B, st);
         case GNND_NBP: return tiled_flow<GNND_NBP, T>(g, flow, aggr, m, ex, o, B, st);
         case GNND_V10: return tiled_flow<GNND_V10, T>(g, flow, aggr, m, ex, o, B, st);
+        case GNND_V30: return tiled_flow<GNND_V30, T>(g, flow, aggr, m, ex, o, B, st);
     }
     return GNND_ERR_INVALID_ARG;
 }
@@ -404,12 +406,13 @@ int gen_var(int var, int flow, int aggr, const int64_t* ei, int64_t s, int64_t n
         case GNND_CBP: return gen_flow<GNND_CBP, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
         case GNND_NBP: return gen_flow<GNND_NBP, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
         case GNND_V10: return gen_flow<GNND_V10, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
+        case GNND_V30: return gen_flow<GNND_V30, T>(flow, aggr, ei, s, nE, m, ex, dim, o, ws, wb, st);
     }
     return GNND_ERR_INVALID_ARG;
 }
 
 bool valid_common(int var, int flow, int aggr, int dtype) {
-    return var >= GNND_V24 && var <= GNND_V10 &&
+    return var >= GNND_V24 && var <= GNND_V30 &&
            (flow == GNND_SOURCE_TO_TARGET || flow == GNND_TARGET_TO_SOURCE) &&
            aggr >= AG_ADD && aggr <= AG_MAX && (dtype == GNND_F32 || dtype == GNND_F64);
 }
@@ -424,7 +427,7 @@ bool valid_common(int var, int flow, int aggr, int dtype) {
 // ---------------------------------------------------------------------------------------
 template <int VAR, int FLOW, typename T>
 __device__ __forceinline__ T pre_grad(T msg, T gpre) {
-    if constexpr (FLOW == GNND_TARGET_TO_SOURCE) {
+    if constexpr (FLOW == GNND_TARGET_TO_SOURCE && VAR != GNND_V30) {
         T t = g_tanh(msg / T(2));
         return (gpre * (T(1) - t * t)) / T(2);
     } else {
@@ -780,6 +783,7 @@ int bwd_var(bool tiled, int var, int flow, const gnnd_graph* g, const int64_t* e
         GNND_BWD_CASE(GNND_CBP)
         GNND_BWD_CASE(GNND_NBP)
         GNND_BWD_CASE(GNND_V10)
+        GNND_BWD_CASE(GNND_V30)
     }
 #undef GNND_BWD_CASE
     return GNND_ERR_INVALID_ARG;
@@ -792,7 +796,7 @@ bool bwd_needs_extra(int variant, int flow) {
 }  // namespace
 
 extern "C" int gnnd_propagate_width(int variant, int flow) {
-    if (variant < GNND_V24 || variant > GNND_V10) return -1;
+    if (variant < GNND_V24 || variant > GNND_V30) return -1;
     if (flow != GNND_SOURCE_TO_TARGET && flow != GNND_TARGET_TO_SOURCE) return -1;
     return out_width(variant, flow);
 }

@@ -5,6 +5,7 @@
   all-reduce with SUM).  `logical_only=True` is quantum/QGNNI.py:255-290 (Lambda term only).
 * `ClassicalLoss` — classical/CGNNI.py:287-309: lambda * mean BCE + (1 - lambda) * mean
   |sin(pi/2 H^T p)| (train) or mean BCE (test), lambda = 0.8 (classical/CGNNI.py:206).
+* `V30Loss` — quantum/decoder_v3_0.py:293-335 (GRU decoder; the script's batching kept).
 * `toric_failures` — hard FER rule of quantum/neural_BP.py:338-348 (non-zero residual
   syndrome, or zero syndrome with a logical flip).
 
@@ -82,6 +83,42 @@ class ClassicalLoss(torch.nn.Module):
         loss_c = torch.abs(torch.sin(torch.matmul(self.Ht.to(pred.dtype), _cols(pred, self.V)) * math.pi / 2))
         return (torch.sum(self.lambda_a * loss_a) / (-1 * torch.numel(loss_a))
                 + torch.sum((1 - self.lambda_a) * loss_c) / torch.numel(loss_c))
+
+
+class V30Loss(torch.nn.Module):
+    """quantum/decoder_v3_0.py:293-335 (LossFunc of the GRU edge-state decoder), restated
+    literally on `preds` = DecoderV30's [out0, out1]:
+
+        loss = sum |sin(pi/2 H^T (y_0 + res))| + sum BCE(|sin(pi/2 res_p)|, syn)
+
+    with the script's own batching, kept as is: `tmp` is the FIRST codeword's y for every
+    column (the loop extending it is commented out, :308), and the columns of res / res_p
+    are sliced from the [B*N] outputs at stride V (= max(H.size())), not N (:307-310); only
+    syn steps by N.  Needs the decoder input x for the syndrome (`needs_input`: the
+    trainers call loss_fn(pred, y, x))."""
+    needs_input = True
+
+    def __init__(self, H):
+        super().__init__()
+        H = torch.as_tensor(H, dtype=torch.float64)
+        self.a, self.b = max(H.shape), min(H.shape)
+        self.register_buffer('Ht', H.t().contiguous())                      # [C, V]
+
+    def forward(self, preds, y, x):
+        a, b = self.a, self.b
+        N = a + b
+        B = y.numel() // a
+        dev = y.device
+        k = torch.arange(B, device=dev).unsqueeze(1)
+        p0, p1, xf = preds[0].reshape(-1), preds[1].reshape(-1), x.reshape(-1)
+        res = p0[k * a + torch.arange(a, device=dev)].t()                   # [a, B]
+        res_p = p1[k * a + a + torch.arange(b, device=dev)].t()             # [b, B]
+        syn = xf[k * N + a + torch.arange(b, device=dev)].t().to(res_p.dtype)
+        tmp = y.reshape(-1)[:a].unsqueeze(1).to(res.dtype)                  # [a, 1]
+        loss_a = torch.matmul(self.Ht.to(res.dtype), tmp + res)
+        res_p = torch.abs(torch.sin(res_p * math.pi / 2))
+        loss_b = -1 * (1 - syn).mul(torch.log(1 - res_p)) - syn.mul(torch.log(res_p))
+        return torch.abs(torch.sin(loss_a * math.pi / 2)).sum() + loss_b.sum()
 
 
 def toric_failures(H, logical, y, pred, graph=None):

@@ -10,6 +10,8 @@ Each class mirrors one reference script's `GNNI` (paths relative to
   ClassicalBP  classical/BP.py:216-259            (no parameters)
   NeuralBP     quantum/neural_BP.py:236-314       keys layers.{i}.W, layers.{i}.W_p, W, W_p, alpha
   DecoderV10   quantum/decoder_v1_0.py:236-313    keys layers.{i}.W, alpha
+  DecoderV30   quantum/decoder_v3_0.py:199-290    keys ggc{1,2}.mlp{1,2}.*, ggc{1,2}.rnn{1,2}.*,
+                                                  mlp.*  (GRU edge states, two-output readout)
 
 Differences from the reference, all at the call boundary: the parity-check matrix is
 passed to the constructor (`GNNI(Nc, H)`) instead of being read from module globals
@@ -27,7 +29,7 @@ from . import ops
 from .graph import TannerGraph
 from .nn import MessagePassing, ClassicalMessagePassing, message_passing_class
 
-_MP = {v: message_passing_class(v) for v in ('v24', 'qgnni', 'qbp', 'cbp', 'nbp', 'v10')}
+_MP = {v: message_passing_class(v) for v in ('v24', 'qgnni', 'qbp', 'cbp', 'nbp', 'v10', 'v30')}
 _MP['cgnni'] = ClassicalMessagePassing
 
 
@@ -209,6 +211,38 @@ class GraphConvV10(_MP['v10']):
             m = m.mul(self.W.repeat(m.size(0) // self.W.size(0), 1))
         size = size or (x.size(0), x.size(0))
         return self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
+
+
+class GraphConvV30(_MP['v30']):
+    """quantum/decoder_v3_0.py:199-242: propagate (no pre-op, cat extra[idx_j]) -> mlp1 / mlp2
+    (Linear(2,10) ReLU Linear(10,1)) -> GRUCell(input = the edge state, hidden = the MLP
+    output).  Both layers own mlp1, mlp2, rnn1 and rnn2 (ggc1 uses mlp1/rnn1, ggc2
+    mlp2/rnn2), as in the reference, so state_dicts load unchanged."""
+
+    def __init__(self, flow, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        self.mlp1 = _mlp(2, 10, torch.nn.ReLU(), torch.float64)
+        self.mlp2 = _mlp(2, 10, torch.nn.ReLU(), torch.float64)
+        self.rnn1 = torch.nn.GRUCell(1, 1, bias=bias).double()
+        self.rnn2 = torch.nn.GRUCell(1, 1, bias=bias).double()
+
+    def forward(self, m, edge_index, x, size=None):
+        x = x if x.dim() == 2 else x.unsqueeze(-1)
+        size = size or (x.size(0), x.size(0))
+        mes = self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
+        rnn = self.rnn2 if self.flow == 'target_to_source' else self.rnn1
+        dt = rnn.weight_ih.dtype
+        return rnn(m.to(dt), mes.to(dt)).to(m.dtype)
+
+    def update(self, aggr_out):
+        seq = self.mlp2 if self.flow == 'target_to_source' else self.mlp1
+        return _apply_mlp(seq, aggr_out.to(seq[0].weight.dtype)).to(aggr_out.dtype)
+
+
+def _flat_gru(cell):
+    z = torch.zeros(3, dtype=cell.weight_ih.dtype, device=cell.weight_ih.device)
+    return [cell.weight_ih.reshape(-1), cell.weight_hh.reshape(-1),
+            cell.bias_ih.reshape(-1) if cell.bias else z, cell.bias_hh.reshape(-1) if cell.bias else z]
 
 
 # ---------------------------------------------------------------------------------------
@@ -517,6 +551,59 @@ class DecoderV10(_WeightedBP):
         return torch.sigmoid(-res)
 
 
+class DecoderV30(_Decoder):
+    """quantum/decoder_v3_0.py:245-290 (Nc = 15, toric L = 8 in the script): per-edge GRU
+    states updated on the variable side (ggc1) then the check side (ggc2) each iteration.
+    `forward` returns the reference's two-element list [sigmoid(-res), sigmoid(-res_p)],
+    each [B*N, 1]: res = mlp(S_v(m)) + x (check rows: mlp(0) + x_c), res_p = mlp(S_c(m_p))
+    (variable rows: mlp(0)), m_p = the edge states after ggc1 of the last iteration (the
+    script keys that on its module-global Nc; here on self.Nc, the same when they agree)."""
+    kind = 'v30'
+
+    def __init__(self, Nc, H):
+        super().__init__(Nc, H)
+        self.ggc1 = GraphConvV30('source_to_target')
+        self.ggc2 = GraphConvV30('target_to_source')
+        self.mlp = _mlp(1, 10, torch.nn.ReLU(), torch.float64)
+
+    def packed_weights(self):
+        return torch.cat(_flat_mlp(self.ggc1.mlp1) + _flat_gru(self.ggc1.rnn1)
+                         + _flat_mlp(self.ggc2.mlp2) + _flat_gru(self.ggc2.rnn2)
+                         + _flat_mlp(self.mlp))
+
+    def forward(self, data):
+        x, edge_index = data.x, data.edge_index
+        if x.dim() == 1:
+            x = x.unsqueeze(1)
+        if self.fused_ok(x, edge_index):
+            g = self.graph(x.device)
+            out = ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(x.dtype, x.device))
+            n = out.size(0) // 2
+            return [out[:n], out[n:]]
+        if not x.is_cuda:
+            raise RuntimeError('gnndecode runs on the GPU only (HIP/gfx950); move data to cuda')
+        self.graph(x.device)
+        return self.forward_layers(x, edge_index)
+
+    def forward_layers(self, x, ei):
+        ei = self._shifted(ei)
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        m_p = m
+        for i in range(self.Nc):
+            m = self.ggc1(m, ei, x)
+            if i == self.Nc - 1:
+                m_p = m
+            m = self.ggc2(m, ei, x)
+        n = x.size(0)
+        mdt = self.mlp[0].weight.dtype
+        s_v = torch.zeros(n, 1, dtype=m.dtype, device=m.device).index_add_(0, ei[0], m)
+        s_c = torch.zeros(n, 1, dtype=m.dtype, device=m.device).index_add_(0, ei[1], m_p)
+        res = _apply_mlp(self.mlp, s_v.to(mdt)).to(x.dtype) + x
+        res_p = _apply_mlp(self.mlp, s_c.to(mdt)).to(x.dtype)
+        return [torch.sigmoid(-res), torch.sigmoid(-res_p)]
+
+
 MODELS = {'v24': DecoderV24, 'qgnni': QGNNI, 'qbp': QuantumBP, 'cgnni': CGNNI, 'cbp': ClassicalBP,
-          'nbp': NeuralBP, 'v10': DecoderV10}
-DEFAULT_ITERS = {'v24': 15, 'qgnni': 25, 'qbp': 10, 'cgnni': 25, 'cbp': 25, 'nbp': 15, 'v10': 15}
+          'nbp': NeuralBP, 'v10': DecoderV10, 'v30': DecoderV30}
+DEFAULT_ITERS = {'v24': 15, 'qgnni': 25, 'qbp': 10, 'cgnni': 25, 'cbp': 25, 'nbp': 15, 'v10': 15,
+                 'v30': 15}

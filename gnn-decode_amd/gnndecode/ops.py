@@ -10,7 +10,7 @@ import torch
 from . import _lib
 from .graph import TannerGraph, current_stream, dtype_code
 
-MODELS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10')
+MODELS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10', 'v30')
 WEIGHTED_BP = ('nbp', 'v10')      # per-edge weight tables: count depends on the graph and T
 
 
@@ -163,8 +163,14 @@ def prepare_weights(model, flat):
     return out
 
 
+def decode_out_rows(graph, model, B):
+    """Rows of gnnd_decode's output: B*V, or 2*B*N for decoder_v3_0's two-output readout."""
+    return 2 * B * graph.N if model == 'v30' else B * graph.V
+
+
 def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None):
-    """Fused T-iteration decode: x [B*N(,1)] -> P(bit=1) [B*V, 1]."""
+    """Fused T-iteration decode: x [B*N(,1)] -> P(bit=1) [B*V, 1] (v30: [2*B*N, 1], the
+    two readout tensors of quantum/decoder_v3_0.py:287-288 stacked)."""
     _require_gpu(x, prepared_weights)
     x = x.contiguous()
     if x.numel() % graph.N:
@@ -175,8 +181,11 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
         raise ValueError(f'{model}: needs {nw} prepared weights')
     if prepared_weights is not None and prepared_weights.dtype != x.dtype:
         raise TypeError('weights and x must share a dtype')
+    rows = decode_out_rows(graph, model, B)
     if out is None:
-        out = torch.empty(B * graph.V, 1, dtype=x.dtype, device=x.device)
+        out = torch.empty(rows, 1, dtype=x.dtype, device=x.device)
+    elif out.numel() != rows or not out.is_contiguous():
+        raise ValueError(f'out must be a contiguous tensor of {rows} values')
     _lib.call('gnnd_decode', graph.handle, _lib.VARIANT[model], dtype_code(x.dtype),
               _ptr(prepared_weights), _ptr(x), _ptr(out), B, int(iters), current_stream(x.device))
     return out

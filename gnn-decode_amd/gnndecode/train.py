@@ -178,7 +178,9 @@ class Trainer(_GraphedStep):
         self.opt.zero_grad(set_to_none=False)
         # a PyG-style batch (.x, .edge_index) or a plain input tensor
         pred = self.model(x if self._edge_index is None else _StaticBatch(x, self._edge_index))
-        loss = self.loss_fn(pred, y)
+        # losses that need the decoder input too (V30Loss: the syndrome rows of x)
+        loss = (self.loss_fn(pred, y, x) if getattr(self.loss_fn, 'needs_input', False)
+                else self.loss_fn(pred, y))
         loss.backward()
         params = [p for p in self.model.parameters() if p.requires_grad]
         grads = []

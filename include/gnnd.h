@@ -61,10 +61,12 @@ typedef enum gnnd_aggr { GNND_AGGR_ADD = 0, GNND_AGGR_MEAN = 1, GNND_AGGR_MAX = 
  *   CBP    classical/BP.py:99-119           c->v log-domain BP; v->c + extra (F=1)
  *   NBP    quantum/neural_BP.py:108-131     c->v log-domain BP with syndrome, no +-10
  *                                           pre-clamp, p clamp 1 - 1e-15; v->c cat (F=2)
- *   V10    quantum/decoder_v1_0.py:109-131  c->v as NBP; v->c + extra (F=1)              */
+ *   V10    quantum/decoder_v1_0.py:109-131  c->v as NBP; v->c + extra (F=1)
+ *   V30    quantum/decoder_v3_0.py:106-118  no pre-op on either side (edge states
+ *                                           aggregated raw); both flows cat (F=2)        */
 typedef enum gnnd_variant {
     GNND_V24 = 0, GNND_QGNNI = 1, GNND_QBP = 2, GNND_CGNNI = 3, GNND_CBP = 4,
-    GNND_NBP = 5, GNND_V10 = 6
+    GNND_NBP = 5, GNND_V10 = 6, GNND_V30 = 7
 } gnnd_variant;
 
 /* Whole-decoder models for gnnd_decode (same enumerators as gnnd_variant). */
@@ -134,6 +136,10 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  * for `batch` codewords in one launch; messages never leave the CU.
  *   d_x   [B*N]   node features (priors/LLRs at variable rows, syndrome at check rows)
  *   d_out [B*V]   P(bit = 1)  (sigmoid(-readout), clamped for the classical models)
+ *         V30: [2*B*N], the reference's two-output readout (quantum/decoder_v3_0.py:
+ *         274-290): [0, B*N) = sigmoid(-(mlp(S_v) + x)) per node (checks: S = 0),
+ *         [B*N, 2*B*N) = sigmoid(-mlp(S_c(m_p))) per node (variables: S = 0), m_p = the
+ *         v->c edge states of the last iteration
  *   d_w   weights in `dtype` as produced by gnnd_prepare_weights from the packed
  *         state_dict layout below (gnnd_weights_count elements, same count after prepare):
  *     CGNNI: ggc2.mlp2 {W1[10], b1[10], W2[10], b2}, mlp {W1[10], b1[10], W2[10], b2}  = 62
@@ -146,6 +152,12 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  *            for t < T {layers[2t].W[E], layers[2t].W_p[E]}, then W[E], W_p[E], alpha
  *                                                                          = 2 E T + 2 E + 1
  *     V10 (quantum/decoder_v1_0.py): for t < T {layers[2t+1].W[E]}, then alpha  = E T + 1
+ *     V30 (quantum/decoder_v3_0.py, GRU edge states; the unused ggc1.mlp2/rnn2 and
+ *            ggc2.mlp1/rnn1 are not passed):
+ *            ggc1.mlp1 {W1[10][2] row-major, b1[10], W2[10], b2},
+ *            ggc1.rnn1 {weight_ih[3], weight_hh[3], bias_ih[3], bias_hh[3]} (gates r, z, n),
+ *            ggc2.mlp2 {same as ggc1.mlp1}, ggc2.rnn2 {same as rnn1},
+ *            mlp {W1[10], b1[10], W2[10], b2}                                            = 137
  * gnnd_prepare_weights converts that layout into the kernel layout (for the fp32 V24
  * kernel the softplus layers are rescaled to base 2: layer-1 rows * log2(e), layer-2
  * weights * ln(2); every other model/dtype is a plain copy).  Call it once per weights.

@@ -18,6 +18,7 @@ ironmanaudi/GNN-decode (paths relative to /root/reference/GNN-decode/):
                           quantum/decoder_v2_4.py:253-257
 * weighted ("neural") BP  quantum/neural_BP.py:59-143 (propagate), :236-314 (layers, GNNI);
                           quantum/decoder_v1_0.py:60-133, :236-313
+* GRU edge-state GNN      quantum/decoder_v3_0.py:59-122 (propagate), :199-290 (layers, GNNI)
 
 Parity pinning: every function here is checked against golden vectors produced by running the
 reference's own class definitions (tests/golden/make_golden.py) in tests/test_oracle_golden.py.
@@ -30,7 +31,7 @@ Batch layout (A10): graph-major.  `x` is [B*N, 1] with N = V + C
 """
 import numpy as np
 
-SCRIPTS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10')
+SCRIPTS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10', 'v30')
 
 
 def tanner_edges(H):
@@ -98,6 +99,7 @@ def propagate(script, flow, aggr, edge_index, msg, extra, dim_size):
     * nbp   quantum/neural_BP.py:108-131     (c->v BP without the +-10 pre-clamp, p clamp
                                               1 - 1e-15; v->c cat extra[idx_j])
     * v10   quantum/decoder_v1_0.py:109-131  (c->v as nbp; v->c + extra)
+    * v30   quantum/decoder_v3_0.py:106-118  (no pre-op on either side; both flows cat)
     """
     ei = np.asarray(edge_index)
     i, j = (0, 1) if flow == 'target_to_source' else (1, 0)
@@ -133,7 +135,7 @@ def propagate(script, flow, aggr, edge_index, msg, extra, dim_size):
         else:
             out = np.log((dt(1) + out) / (dt(1) - out))
         return out
-    if flow == 'target_to_source':
+    if flow == 'target_to_source' and script != 'v30':
         out = np.tanh(out / dt(2))
     out = _extrinsic(aggr, out, idx, dim_size)
     if script in ('qbp', 'cbp'):                       # v->c
@@ -142,7 +144,7 @@ def propagate(script, flow, aggr, edge_index, msg, extra, dim_size):
         return out if extra is None else out + extra[idx]
     if script == 'qgnni' and flow == 'source_to_target':
         return out + extra[idx]
-    return np.concatenate([out, extra[idx]], axis=1)  # v24 both flows, qgnni c->v
+    return np.concatenate([out, extra[idx]], axis=1)  # v24, v30 both flows, qgnni c->v
 
 
 def _nbp_check_literal(aggr, a, s_e, idx, dim_size):
@@ -357,6 +359,48 @@ def decode_v10(H, w, x, T):
     return sigmoid(-r).reshape(-1, 1)
 
 
+def gru_cell(w, prefix, inp, h):
+    """torch.nn.GRUCell(1, 1)(inp, h) elementwise (ATen gru_cell: r = sig(h_r + i_r),
+    z = sig(h_z + i_z), n = tanh(i_n + r h_n), h' = (h - n) z + n)."""
+    dt = inp.dtype
+    wi = np.asarray(w[prefix + 'weight_ih'], dt).reshape(3)
+    wh = np.asarray(w[prefix + 'weight_hh'], dt).reshape(3)
+    bi = np.asarray(w.get(prefix + 'bias_ih', np.zeros(3)), dt).reshape(3)
+    bh = np.asarray(w.get(prefix + 'bias_hh', np.zeros(3)), dt).reshape(3)
+    gi = [inp * wi[k] + bi[k] for k in range(3)]
+    gh = [h * wh[k] + bh[k] for k in range(3)]
+    r = sigmoid(gh[0] + gi[0])
+    z = sigmoid(gh[1] + gi[1])
+    n = np.tanh(gi[2] + r * gh[2])
+    return (h - n) * z + n
+
+
+def decode_v30(H, w, x, T):
+    """quantum/decoder_v3_0.py:256-290 (fp64, Nc = 15).  Edge states m: ggc1 (:226-229)
+    mes = mlp1([LOO_v(m), x_v]), m = rnn1(m, mes); m_p = m at the last iteration; ggc2
+    mes = mlp2([LOO_c(m), x_c]), m = rnn2(m, mes).  Returns the two readout tensors
+    [B*N, 1]: sigmoid(-(mlp(S_v(m)) + x)) and sigmoid(-mlp(S_c(m_p))) (zero sums on the
+    other side's rows)."""
+    g = _Graph(H)
+    xv, xc = _split_x(g, x)
+    B = xv.shape[0]
+    m = np.zeros((B, g.E), xv.dtype)
+    m_p = m
+    for i in range(T):
+        u = g.sum_var(m)[:, g.v] - m
+        m = gru_cell(w, 'ggc1.rnn1.', m, _edge_mlp(w, 'ggc1.mlp1.', np.stack([u, xv[:, g.v]], -1), relu))
+        if i == T - 1:
+            m_p = m
+        u = g.sum_chk(m)[:, g.c] - m
+        m = gru_cell(w, 'ggc2.rnn2.', m, _edge_mlp(w, 'ggc2.mlp2.', np.stack([u, xc[:, g.c]], -1), relu))
+    sv = np.concatenate([g.sum_var(m), np.zeros((B, g.C), m.dtype)], 1)
+    sc = np.concatenate([np.zeros((B, g.V), m.dtype), g.sum_chk(m_p)], 1)
+    xs = np.concatenate([xv, xc], 1)
+    res = _edge_mlp(w, 'mlp.', sv[..., None], relu) + xs
+    res_p = _edge_mlp(w, 'mlp.', sc[..., None], relu)
+    return sigmoid(-res).reshape(-1, 1), sigmoid(-res_p).reshape(-1, 1)
+
+
 def decode(model, H, x, T, w=None):
     if model == 'cgnni':
         return decode_cgnni(H, w, x, T)
@@ -372,6 +416,8 @@ def decode(model, H, x, T, w=None):
         return decode_nbp(H, w, x, T)
     if model == 'v10':
         return decode_v10(H, w, x, T)
+    if model == 'v30':
+        return decode_v30(H, w, x, T)
     raise ValueError(model)
 
 

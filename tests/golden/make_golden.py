@@ -656,9 +656,76 @@ def gen_fer():
     save('fer_rule', **arrays)
 
 
+def gen_v30():
+    """quantum/decoder_v3_0.py (GRU edge states, two-output readout) at toric L = 5.  The
+    script's module top level is not run (load_ref keeps only the named classes); GNNI.forward
+    reads the module globals rows, cols, BATCH_SIZE and Nc (the iteration whose ggc1 output
+    is kept as m_p), injected here with Nc = T.  No checkpoint ships for this script: seeded
+    default init.  Fixtures: decoder outputs (both tensors) for B in {1, 4}, T in {1, 2, 15};
+    one training step (reference LossFunc, :293-335) with every parameter gradient; one bare
+    propagate() per flow and aggregation."""
+    sys.path.insert(0, os.path.join(REF, 'quantum'))
+    import error_generate as eg
+    L = 5
+    Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+    H = torch.from_numpy(Hnp).t()
+    hp = eg.H_Prep(H.t())
+    H_prep = torch.from_numpy(hp.get_H_Prep())
+    V, C = H.shape
+    N = V + C
+    names = {'MessagePassing', 'GraphConv', 'GNNI', 'LossFunc'}
+    ns = load_ref('quantum/decoder_v3_0.py', names)
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'], ns['Nc'] = V, C, 1, H, 15
+    set_seed(701)
+    sd = {k: v.clone() for k, v in ns['GNNI'](15).state_dict().items()}
+    arrays = dict(sd_to_np(sd))
+    for B, seed in ((1, 702), (4, 703)):
+        x, y = toric_inputs(eg, H, L, [0.05, 0.1], B, seed)
+        arrays[f'x_B{B}'], arrays[f'y_B{B}'] = x.numpy(), y.numpy()
+        for T in (1, 2, 15):
+            ns['Nc'] = T
+            out, _ = run_model(ns, H, x, B, T, sd)
+            arrays[f'out0_B{B}_T{T}'] = out[0].numpy()
+            arrays[f'out1_B{B}_T{T}'] = out[1].numpy()
+    save('v30_toric5', **arrays)
+
+    # one training step at B = 4, T = 15 (reference LossFunc on the two outputs)
+    B, T = 4, 15
+    x, y = toric_inputs(eg, H, L, [0.05, 0.1], B, 704)
+    ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'], ns['Nc'] = V, C, B, H, T
+    model = ns['GNNI'](T)
+    model.load_state_dict(sd)
+    data = types.SimpleNamespace(x=x, edge_index=batch_edge_index(single_edge_index(H), B, N), y=y)
+    pred = model(data)
+    loss = ns['LossFunc'](H, H_prep)(pred, data)
+    loss.backward()
+    save('train_v30_L5', x=x.numpy(), y=y.numpy(), loss=np.array(loss.item()), T=np.array(T),
+         pred0=pred[0].detach().numpy(), pred1=pred[1].detach().numpy(),
+         **sd_to_np(sd), **grads_of(model))
+
+    # bare propagate() per flow / aggregation on random edge states
+    B = 3
+    ei = batch_edge_index(single_edge_index(H), B, N)
+    ei = torch.stack([ei[0], ei[1] + V])
+    g = torch.Generator().manual_seed(705)
+    E = ei.size(1)
+    m = (torch.randn(E, 1, generator=g) * 3).double()
+    xv = torch.randn(B, V, generator=g) * 2
+    xc = torch.where(torch.rand(B, C, generator=g) < 0.3, -1.0, 1.0)
+    extra = torch.cat([xv, xc], dim=1).reshape(B * N, 1).double()
+    prop = {'v30/edge_index': ei.numpy(), 'v30/msg': m.numpy(), 'v30/extra': extra.numpy()}
+    for flow in ('source_to_target', 'target_to_source'):
+        for aggr in ('add', 'max'):
+            mp = ns['MessagePassing'](aggr, flow)
+            with torch.no_grad():
+                out = mp.propagate(edge_index=ei, size=(N * B, N * B), x=m, extra=extra)
+            prop[f'v30/{flow}/{aggr}'] = out.numpy()
+    save('propagate_ops_v30', **prop)
+
+
 if __name__ == '__main__':
     torch.set_num_threads(1)
-    which = sys.argv[1:] or ['classical', 'quantum', 'training', 'neural_bp', 'ldpc', 'fer']
+    which = sys.argv[1:] or ['classical', 'quantum', 'training', 'neural_bp', 'ldpc', 'fer', 'v30']
     if 'classical' in which:
         gen_classical()
     if 'quantum' in which:
@@ -671,3 +738,5 @@ if __name__ == '__main__':
         gen_ldpc()
     if 'fer' in which:
         gen_fer()
+    if 'v30' in which:
+        gen_v30()

@@ -119,7 +119,7 @@ def test_layerwise_operator_path(golden, fx, model, gfx, B, T):
 
 
 def _prop_cases():
-    for fx in ('propagate_ops', 'propagate_ops_nbp'):
+    for fx in ('propagate_ops', 'propagate_ops_nbp', 'propagate_ops_v30'):
         z = np.load(f'tests/golden/{fx}.npz')
         for k in z.files:
             if len(k.split('/')) >= 3:
@@ -140,7 +140,7 @@ def test_propagate_operator(golden, fx, key, path):
     if path == 'tiled':
         gfx = {'v24': 'toric_L5_graph', 'qgnni': 'toric_L4_graph', 'qbp': 'toric_L4_graph',
                'cgnni': 'bch_63_45_graph', 'cbp': 'bch_63_45_graph',
-               'nbp': 'toric_L4_graph', 'v10': 'toric_L4_graph'}[tag]
+               'nbp': 'toric_L4_graph', 'v10': 'toric_L4_graph', 'v30': 'toric_L5_graph'}[tag]
         graph = gd.TannerGraph(golden(gfx)['H'], device=DEV)
         assert graph.is_tiled(ei, graph.V) or aggr == 'mean'
     out = gd.ops.propagate(tag, flow, aggr, ei, msg, extra, extra_np.shape[0], graph=graph)

@@ -47,7 +47,7 @@ def test_oracle_decoder_matches_reference(golden, fx, model, gfx, B, T):
 
 
 def _prop_cases():
-    for fx in ('propagate_ops', 'propagate_ops_nbp'):
+    for fx in ('propagate_ops', 'propagate_ops_nbp', 'propagate_ops_v30'):
         z = np.load(f'tests/golden/{fx}.npz')
         for k in z.files:
             parts = k.split('/')
