@@ -56,6 +56,12 @@ SIGNATURES = {
     'gnnd_decision_errors': (_int, [_vp, _vp, _i32, _int, _vp, _vp, _vp, _i64, _vp]),
     'gnnd_adam_step': (_int, [_int, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_double, ctypes.c_double,
                               ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp]),
+    'gnnd_sample_toric': (_int, [_vp, _int, ctypes.POINTER(ctypes.c_double), _i32, ctypes.c_uint64,
+                                 _i64, _vp, _vp, _i64, _vp]),
+    'gnnd_sample_awgn': (_int, [_vp, _int, ctypes.POINTER(ctypes.c_double), _i32, _vp, _i32, _i32,
+                                ctypes.c_uint64, _i64, _vp, _vp, _i64, _vp]),
+    'gnnd_philox4x32_10': (None, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                  ctypes.POINTER(ctypes.c_uint32)]),
     'gnnd_status_string': (ctypes.c_char_p, [_int]),
     'gnnd_last_hip_error': (_int, []),
     'gnnd_version': (_int, []),

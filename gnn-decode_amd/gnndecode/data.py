@@ -7,21 +7,67 @@
   independent X/Z flips with probability p, prior log((1-p)/p) at the variable rows and
   syndrome (-1)^(H^T e) at the check rows; labels y = e.
 
-The distributions match the reference; the random streams do not (torch generators on the
-device, seeded).  Generation is outside every timed region.
+On a GPU both samplers run as HIP kernels (`gnnd_sample_toric` / `gnnd_sample_awgn`,
+Philox4x32-10 counter-based streams: codeword b draws from (seed, offset + b) only, so a
+data-parallel shard passing offset = its start reproduces its slice of the global batch
+exactly).  `engine='torch'` (and CPU tensors) use the torch-generator formulation, kept as
+the statistical cross-check.  The distributions match the reference; the random streams do
+not (the reference draws with numpy / torch CPU generators).  Generation is outside every
+timed region.
 """
 import math
 
+import numpy as np
 import torch
+
+_GRAPHS = {}
+_GENCOLS = {}
+
+
+def _graph_of(H, device):
+    from .graph import TannerGraph
+    Hn = (np.asarray(H.detach().cpu() if isinstance(H, torch.Tensor) else H) != 0).astype(np.uint8)
+    key = (Hn.shape, hash(Hn.tobytes()), str(torch.device(device)))
+    g = _GRAPHS.get(key)
+    if g is None:
+        if len(_GRAPHS) > 16:
+            _GRAPHS.clear()
+        g = _GRAPHS[key] = TannerGraph(Hn, device=device)
+    return g, key
+
+
+def _engine(engine, device):
+    if engine == 'auto':
+        return 'hip' if torch.device(device).type == 'cuda' else 'torch'
+    if engine not in ('hip', 'torch'):
+        raise ValueError(f'engine must be auto, hip or torch, got {engine!r}')
+    return engine
 
 
 def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=1, seed=0, device='cuda',
-               dtype=torch.float32, codewords='fixed'):
+               dtype=torch.float32, codewords='fixed', offset=0, engine='auto'):
     """codewords='fixed': every codeword is the constant word `codeword_bit` (default 1:
     the reference's Gen_Data input is the all-ones word, classical/CGNNI.py:195, modulated
     to -1; classical/BP.py decodes the all-zeros word, pass 0); 'random': uniform random
     codewords of H (random GF(2) combinations of the generator rows,
-    codes.gf2_generator), labels = their bits."""
+    codes.gf2_generator), labels = their bits.  SNR of codeword b = snrs[(offset + b) %
+    len(snrs)]."""
+    if codewords not in ('fixed', 'random'):
+        raise ValueError(f'codewords must be "fixed" or "random", got {codewords!r}')
+    if _engine(engine, device) == 'hip':
+        from . import ops
+        g, key = _graph_of(H, device)
+        cols, k = None, 0
+        if codewords == 'random':
+            ent = _GENCOLS.get(key)
+            if ent is None:
+                from .codes import gf2_generator
+                c, k = ops.pack_generator_columns(gf2_generator(np.asarray(g.H)))
+                ent = _GENCOLS[key] = (c.to(device), k)
+            cols, k = ent
+        return ops.sample_awgn(g, B, snrs, cols, k, codeword_bit, seed, offset, dtype, device)
+    if offset:
+        raise ValueError('offset needs the HIP sampler (engine="hip")')
     V, C = H.shape
     g = torch.Generator(device=device).manual_seed(seed)
     snr = torch.tensor([snrs[b % len(snrs)] for b in range(B)], dtype=torch.float32, device=device)
@@ -31,10 +77,8 @@ def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=1, seed=0, device='cu
         G = torch.as_tensor(gf2_generator(H), dtype=torch.float32, device=device)
         msg = torch.randint(0, 2, (B, G.shape[0]), generator=g, device=device).float()
         bits = torch.remainder(msg @ G, 2)
-    elif codewords == 'fixed':
-        bits = torch.full((B, V), float(codeword_bit), device=device)
     else:
-        raise ValueError(f'codewords must be "fixed" or "random", got {codewords!r}')
+        bits = torch.full((B, V), float(codeword_bit), device=device)
     y = (1 - 2 * bits) + sigma[:, None] * torch.randn(B, V, generator=g, device=device)
     llr = 2 * y / (sigma[:, None] ** 2)
     x = torch.cat([llr, torch.zeros(B, C, device=device)], dim=1)
@@ -42,7 +86,13 @@ def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=1, seed=0, device='cu
 
 
 def toric_batch(H, B, ps=(0.01, 0.02, 0.03, 0.04, 0.05, 0.06, 0.07, 0.08, 0.09, 0.1), seed=0,
-                device='cuda', dtype=torch.float64):
+                device='cuda', dtype=torch.float64, offset=0, engine='auto'):
+    if _engine(engine, device) == 'hip':
+        from . import ops
+        g, _ = _graph_of(H, device)
+        return ops.sample_toric(g, B, ps, seed, offset, dtype, device)
+    if offset:
+        raise ValueError('offset needs the HIP sampler (engine="hip")')
     Ht = torch.as_tensor(H, dtype=torch.float32, device=device)    # [V, C]
     V, C = Ht.shape
     g = torch.Generator(device=device).manual_seed(seed)

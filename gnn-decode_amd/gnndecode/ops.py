@@ -333,3 +333,64 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, betas=(0.9, 0.999), ep
     _lib.call('gnnd_adam_step', dtype_code(param.dtype), _ptr(param), _ptr(grad), _ptr(exp_avg),
               _ptr(exp_avg_sq), _ptr(step), param.numel(), float(lr), float(betas[0]),
               float(betas[1]), float(eps), float(weight_decay), current_stream(param.device))
+
+
+# ---------------------------------------------------------------------------------------
+# input synthesis (gnnd_sample_*)
+# ---------------------------------------------------------------------------------------
+def _doubles(vals):
+    vals = [float(v) for v in vals]
+    return (ctypes.c_double * len(vals))(*vals), len(vals)
+
+
+def sample_toric(graph, B, ps, seed=0, offset=0, dtype=torch.float64, device=None):
+    """gen_syn inputs on the device (gnnd_sample_toric): x [B*N, 1], y [B*V, 1]."""
+    device = device or graph.device
+    x = torch.empty(B * graph.N, 1, dtype=dtype, device=device)
+    y = torch.empty(B * graph.V, 1, dtype=dtype, device=device)
+    _require_gpu(x)
+    arr, n = _doubles(ps)
+    _lib.call('gnnd_sample_toric', graph.handle, dtype_code(dtype), arr, n, int(seed) & (2**64 - 1),
+              int(offset), _ptr(x), _ptr(y), int(B), current_stream(x.device))
+    return x, y
+
+
+def pack_generator_columns(G):
+    """Generator [k, V] (0/1) -> [V, ceil(k/32)] uint32 column bit masks (int32 storage)."""
+    import numpy as np
+    G = np.asarray(G, dtype=np.uint8)
+    k, V = G.shape
+    kw = (k + 31) // 32
+    cols = np.zeros((V, kw), dtype=np.uint64)
+    for i in range(k):
+        cols[:, i // 32] |= G[i].astype(np.uint64) << np.uint64(i % 32)
+    return torch.from_numpy(cols.astype(np.uint32).view(np.int32)), k
+
+
+def sample_awgn(graph, B, snrs, gen_cols=None, k=0, codeword_bit=1, seed=0, offset=0,
+                dtype=torch.float32, device=None):
+    """Gen_Data inputs on the device (gnnd_sample_awgn): x [B*N, 1], labels [B*V, 1].
+    gen_cols: device int32 [V, ceil(k/32)] from pack_generator_columns (random codewords),
+    or None for the constant word `codeword_bit`."""
+    device = device or graph.device
+    x = torch.empty(B * graph.N, 1, dtype=dtype, device=device)
+    y = torch.empty(B * graph.V, 1, dtype=dtype, device=device)
+    _require_gpu(x)
+    arr, n = _doubles(snrs)
+    if gen_cols is not None:
+        if gen_cols.dtype != torch.int32 or not gen_cols.is_cuda or gen_cols.size(0) != graph.V:
+            raise ValueError('gen_cols must be a device int32 [V, ceil(k/32)] tensor')
+        gen_cols = gen_cols.contiguous()
+    _lib.call('gnnd_sample_awgn', graph.handle, dtype_code(dtype), arr, n, _ptr(gen_cols), int(k),
+              int(codeword_bit), int(seed) & (2**64 - 1), int(offset), _ptr(x), _ptr(y), int(B),
+              current_stream(x.device))
+    return x, y
+
+
+def philox4x32_10(counter, key):
+    """Host mirror of the device generator (known-answer tests)."""
+    c = (ctypes.c_uint32 * 4)(*[int(v) & 0xffffffff for v in counter])
+    kk = (ctypes.c_uint32 * 2)(*[int(v) & 0xffffffff for v in key])
+    out = (ctypes.c_uint32 * 4)()
+    _lib.get().gnnd_philox4x32_10(c, kk, out)
+    return list(out)
