@@ -43,7 +43,10 @@ typedef enum gnnd_status {
     GNND_ERR_ALLOC = 5          /* device allocation failed (graph creation only)       */
 } gnnd_status;
 
-typedef enum gnnd_dtype { GNND_F32 = 0, GNND_F64 = 1 } gnnd_dtype;
+/* GNND_BF16 (gnnd_decode of CGNNI / CBP only): x and out stored as bf16 in HBM, weights
+ * fp32 (gnnd_prepare_weights with GNND_F32), every operation in fp32 — BASELINE config 2's
+ * "bf16" storage mode.                                                                      */
+typedef enum gnnd_dtype { GNND_F32 = 0, GNND_F64 = 1, GNND_BF16 = 2 } gnnd_dtype;
 
 /* `flow` of MessagePassing (quantum/decoder_v2_4.py:73-74,89):
  *   SOURCE_TO_TARGET: aggregate at edge_index[0] (variable nodes)  = v->c message
@@ -233,6 +236,28 @@ int gnnd_decision_errors(const gnnd_graph* g, const int32_t* d_logical, int32_t 
 int gnnd_adam_step(int dtype, void* d_param, const void* d_grad, void* d_exp_avg,
                    void* d_exp_avg_sq, double* d_step, int64_t n, double lr, double beta1,
                    double beta2, double eps, double weight_decay, void* stream);
+
+/* ---- input synthesis ---------------------------------------------------
+ * Decoder inputs in the batch layout above, generated on the device with Philox4x32-10
+ * (counter = {word, global codeword index lo/hi, stream}, key = seed): codeword b of the
+ * call is global codeword offset + b, so data-parallel shards passing offset = shard start
+ * draw exactly the codewords one single-device call over the global batch would.
+ *   gnnd_sample_toric  quantum/error_generate.py:252-278 (gen_syn): p uniform over h_p[n_p]
+ *     (n_p <= 16) per codeword, every variable flips with probability p; d_x [B*N] =
+ *     {log((1-p)/p) at variable rows, (-1)^(H^T e) at check rows}, d_y [B*V] = e.
+ *   gnnd_sample_awgn   classical/CGNNI.py:125-147 (Gen_Data.AWGN, get_post): codeword =
+ *     the constant word codeword_bit (d_gen_cols NULL) or m G for k uniform message bits,
+ *     d_gen_cols [V][ceil(k/32)] uint32 = the generator's columns as bit masks; BPSK
+ *     1 - 2c, sigma^2 = 10^(-SNR/10) with SNR = h_snr_db[(offset + b) % n_snr] (n_snr <= 16);
+ *     d_x [B*N] = {2 y' / sigma^2 at variable rows, 0 at check rows}, d_y [B*V] = c.
+ * gnnd_philox4x32_10 is the host mirror of the generator (known-answer tests).            */
+int gnnd_sample_toric(const gnnd_graph* g, int dtype, const double* h_p, int32_t n_p,
+                      uint64_t seed, int64_t offset, void* d_x, void* d_y, int64_t batch,
+                      void* stream);
+int gnnd_sample_awgn(const gnnd_graph* g, int dtype, const double* h_snr_db, int32_t n_snr,
+                     const uint32_t* d_gen_cols, int32_t k, int32_t codeword_bit, uint64_t seed,
+                     int64_t offset, void* d_x, void* d_y, int64_t batch, void* stream);
+void gnnd_philox4x32_10(const uint32_t* h_ctr4, const uint32_t* h_key2, uint32_t* h_out4);
 
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gnnd_status_string(int status);
