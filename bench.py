@@ -49,6 +49,10 @@ def flops_per_codeword(model, g, T):
         return 20 * E * T + 4 * V, 6 * E * T
     if model == 'v24':
         return 1417 * E * T + 514 * E + 2 * V, 256 * E * T + 128 * E
+    if model == 'v30':
+        # per edge and iteration, both sides: leave-one-out 2, MLP 2->10->1 ReLU 71, GRUCell
+        # 19 (+ 2 sigmoid, 1 tanh); readout MLP 1->10->1 (51) for both outputs of every node
+        return 184 * E * T + 102 * g.N, 6 * E * T + 2 * g.N
     raise ValueError(model)
 
 
@@ -70,7 +74,8 @@ def parse():
     p.add_argument('--code', default='bch_63_45')
     p.add_argument('--batch', type=int, default=65536, help='codewords per GPU')
     p.add_argument('--iters', type=int, default=None)
-    p.add_argument('--dtype', default='f32', choices=['f32', 'f64'])
+    p.add_argument('--dtype', default='f32', choices=['f32', 'f64', 'bf16'],
+                   help='bf16 (decode, classical models): bf16 x/out in HBM, fp32 arithmetic')
     p.add_argument('--cpu-seconds', type=float, default=12.0,
                    help='bounded CPU-baseline sample (0 disables)')
     p.add_argument('--seed', type=int, default=0)
@@ -85,9 +90,10 @@ def parse():
     p.add_argument('--torch-trainer', action='store_true',
                    help='train mode: torch autograd/optimizer Trainer around the fused kernels '
                         'instead of FusedV24Trainer')
-    p.add_argument('--mode', default='decode', choices=['decode', 'train'],
+    p.add_argument('--mode', default='decode', choices=['decode', 'train', 'sample'],
                    help='train = config 5: decoder_v2_4 (or --model qgnni/nbp/v10) training '
-                        'step (DP, RCCL all-reduce)')
+                        'step (DP, RCCL all-reduce); sample = the on-device input synthesis '
+                        'kernel alone (gnnd_sample_*, HBM-write bound)')
     return p.parse_args()
 
 
@@ -143,7 +149,7 @@ def cpu_workers():
     return max(1, min(16, n))
 
 
-def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
+def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds, out_bf16=False):
     """Time the oracle (numpy restatement of the reference path) on a bounded sample of this
     workload: (1) one thread, comparing its outputs with the GPU's on the same codewords
     (parity, matched BER); (2) all cores: one single-threaded worker process per core
@@ -167,7 +173,13 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
     cond = model == 'cbp' and x_dev.dtype == torch.float32
     # the quantum scripts compute in fp64: their oracle (the reference's arithmetic) runs in
     # fp64 whatever the GPU dtype
-    quantum = model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10')
+    quantum = model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10', 'v30')
+
+    def oracle_vars(xs_):
+        r = gnn_oracle.decode(model, H, xs_, T, w)
+        if model == 'v30':                 # first readout tensor, variable rows
+            r = r[0].reshape(-1, g.N)[:, :g.V].reshape(-1, 1)
+        return r
     ref_dt = np.float64 if quantum else None
     t1 = seconds / 2                      # 1-thread leg, then the all-cores leg
     done, t_total, max_err, mism = 0, 0.0, 0.0, 0
@@ -178,9 +190,11 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
         if ref_dt is not None:
             xs = xs.astype(ref_dt)
         t0 = time.perf_counter()
-        ref = gnn_oracle.decode(model, H, xs, T, w)
+        ref = oracle_vars(xs)
         t_total += time.perf_counter() - t0
         got = o_all[done:done + chunk].double().cpu().numpy().reshape(-1, 1)
+        if out_bf16:       # the GPU stored its outputs in bf16: round the oracle's the same way
+            ref = torch.from_numpy(np.ascontiguousarray(ref, np.float32)).bfloat16().double().numpy()
         ref = ref.astype(np.float64)
         max_err = max(max_err, float(np.abs(got - ref).max()))
         mism += int(((got > 0.5) != (ref > 0.5)).sum())
@@ -198,7 +212,7 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds):
     if quantum and x_dev.dtype == torch.float32 and done:
         xs = x_all[:chunk].cpu().numpy().reshape(-1, 1)           # fp32 oracle, same chunk
         t0 = time.perf_counter()
-        gnn_oracle.decode(model, H, xs, T, w)
+        oracle_vars(xs)
         same_prec = chunk / (time.perf_counter() - t0)
     if limiter is not None and hasattr(limiter, 'unregister'):
         limiter.unregister()
@@ -280,6 +294,65 @@ def train_cpu_baseline(H, model, T, x, y, batch, seconds):
     res['sample'] = (f'oracle/torch_train.py V24Step (reference forward + LossFunc + backward + Adam, '
                      f'fp64 as the reference), steps of {bs} samples, ~{seconds / 2:.0f} s per leg')
     return res
+
+
+def sample_main(a, world, rank, dev):
+    """§8(f)1: the on-device input synthesis kernel alone (gnnd_sample_awgn with random
+    codewords for classical codes, gnnd_sample_toric for toric codes), one launch per step
+    over --batch codewords per GPU; each rank draws its slice of the global batch (offset =
+    rank * batch).  HBM-write bound: (N + V) values written per codeword."""
+    H = gd.codes.get_code(a.code)
+    classical = not a.code.startswith('toric')
+    dtype = torch.float64 if a.dtype == 'f64' else torch.float32
+    if a.dtype == 'bf16':
+        raise SystemExit('--mode sample writes f32 or f64')
+    off = rank * a.batch
+
+    def step():
+        if classical:
+            return gd.data.awgn_batch(H, a.batch, codewords='random', seed=a.seed, offset=off,
+                                      device=dev, dtype=dtype)
+        return gd.data.toric_batch(H, a.batch, seed=a.seed, offset=off, device=dev, dtype=dtype)
+
+    for _ in range(max(a.warmup, 3)):
+        step()
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(a.steps):
+        x, y = step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_s = ev0.elapsed_time(ev1) / 1e3 / a.steps
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    if rank == 0:
+        V, C = H.shape
+        esz = 8 if dtype == torch.float64 else 4
+        bytes_step = (V + C + V) * esz * a.batch
+        achieved = bytes_step / kernel_s / 1e9
+        print(json.dumps({
+            'metric': 'synthesized codewords/sec (whole node), on-device decoder-input sampler',
+            'value': world * a.batch * a.steps / elapsed, 'unit': 'codewords/s', 'n_gpus': world,
+            'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': a.dtype,
+            'data': 'synthetic (Philox4x32-10 on device)',
+            'config': {'workload': f'{a.code} {"AWGN random codewords" if classical else "toric gen_syn"} '
+                                   f'sampler, batch={a.batch}/GPU',
+                       'global_batch': a.batch * world, 'parallelism': f'dp{world} (offset shards)'},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+                         'frac': achieved / PEAK_HBM_GBS, 'traffic': None,
+                         'kernel': 'sample_awgn_kernel' if classical else 'sample_toric_kernel',
+                         'bytes_written_per_launch': bytes_step, 'kernel_ms': kernel_s * 1e3},
+            'cpu_baseline': None}), flush=True)
 
 
 def train_main(a, world, rank, dev):
@@ -375,8 +448,17 @@ def main():
         if dist.is_initialized():
             dist.destroy_process_group()
         return
+    if a.mode == 'sample':
+        sample_main(a, world, rank, dev)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
     T = a.iters or gd.DEFAULT_ITERS[a.model]
-    dtype = torch.float32 if a.dtype == 'f32' else torch.float64
+    # bf16: storage type of x / out only (classical models); weights and arithmetic fp32
+    io_dtype = {'f32': torch.float32, 'f64': torch.float64, 'bf16': torch.bfloat16}[a.dtype]
+    dtype = torch.float64 if a.dtype == 'f64' else torch.float32
+    if a.dtype == 'bf16' and a.model not in ('cgnni', 'cbp'):
+        raise SystemExit('--dtype bf16 is the classical models\' storage mode (cgnni, cbp)')
 
     H = gd.codes.get_code(a.code)
     torch.manual_seed(a.seed)
@@ -396,8 +478,10 @@ def main():
                                        device=dev, dtype=dtype)
     else:
         x, labels = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
+    if io_dtype != dtype:
+        x = x.to(io_dtype)                       # bf16 storage (outside the timed region)
     w = model.prepared_weights(dtype, dev)
-    out = torch.empty(a.batch * g.V, 1, dtype=dtype, device=dev)
+    out = torch.empty(gd.ops.decode_out_rows(g, a.model, a.batch), 1, dtype=io_dtype, device=dev)
 
     def step():
         gd.ops.decode(g, a.model, x, T, w, out=out)
@@ -434,7 +518,10 @@ def main():
     with torch.no_grad():
         # one launch: bit errors, frame errors, residual-syndrome / logical failures (toric)
         lg = None if classical else (torch.as_tensor(gd.codes.toric_logicals(H)) != 0).to(torch.int32)
-        counts = gd.ops.decision_errors(g, lg, out, labels)
+        pred = out.float() if io_dtype == torch.bfloat16 else out
+        if a.model == 'v30':                     # variable rows of the first readout tensor
+            pred = out[:a.batch * g.N].view(a.batch, g.N)[:, :g.V].reshape(-1, 1).contiguous()
+        counts = gd.ops.decision_errors(g, lg, pred, labels)
         if dist.is_initialized():
             dist.all_reduce(counts)
         errs = counts[0]
@@ -454,8 +541,8 @@ def main():
         achieved = fl * a.batch / kernel_s / 1e12
         peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
         trans_frac = 2 * trans * a.batch / kernel_s / TRANS_OPS_PER_S
-        esz = 4 if dtype == torch.float32 else 8
-        io_bytes = (g.N + g.V) * esz * a.batch
+        esz = {torch.float32: 4, torch.float64: 8, torch.bfloat16: 2}[io_dtype]
+        io_bytes = (g.N + gd.ops.decode_out_rows(g, a.model, 1)) * esz * a.batch
         plan = gd.ops.decode_plan(g, a.model, dtype)
         tag = f'{a.model}_{a.code}_B{a.batch}_T{T}_{a.dtype}'
         pmc = load_pmc(tag)
@@ -501,7 +588,9 @@ def main():
                          'hbm_io_frac': io_bytes / kernel_s / 1e9 / PEAK_HBM_GBS},
         }
         if a.cpu_seconds > 0 and world == 1:
-            res['cpu_baseline'] = cpu_baseline(a.model, H, state, x, out, labels, g, T, a.cpu_seconds)
+            # the oracle decodes the same (for bf16: widened) inputs in fp32
+            res['cpu_baseline'] = cpu_baseline(a.model, H, state, x.to(dtype), pred, labels, g, T,
+                                               a.cpu_seconds, out_bf16=io_dtype == torch.bfloat16)
         else:
             res['cpu_baseline'] = None
         print(json.dumps(res), flush=True)

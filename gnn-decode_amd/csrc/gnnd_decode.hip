@@ -83,7 +83,8 @@ extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void*
 extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32_t* h_cw,
                                 int32_t* h_lds) {
     if (!g || !h_cw || !h_lds || weights_count(model) == -1) return GNND_ERR_INVALID_ARG;
-    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
+    if (dtype != GNND_F32 && dtype != GNND_F64 && dtype != GNND_BF16) return GNND_ERR_INVALID_ARG;
+    if (dtype == GNND_BF16) dtype = GNND_F32;          // fp32 arithmetic and LDS
     Plan p;
     int rc = make_plan(model, dtype, g, &p);
     if (rc != GNND_OK) return rc;
@@ -94,7 +95,8 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
 
 extern "C" int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan) {
     if (!g || !h_plan || weights_count(model) == -1) return GNND_ERR_INVALID_ARG;
-    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
+    if (dtype != GNND_F32 && dtype != GNND_F64 && dtype != GNND_BF16) return GNND_ERR_INVALID_ARG;
+    if (dtype == GNND_BF16) dtype = GNND_F32;
     Plan p;
     int rc = make_plan(model, dtype, g, &p);
     if (rc != GNND_OK) return rc;
@@ -111,7 +113,7 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
                            void* stream) {
     int nw = weights_count(model);
     if (!g || nw == -1 || batch < 0 || iters < 0) return GNND_ERR_INVALID_ARG;
-    if (dtype != GNND_F32 && dtype != GNND_F64) return GNND_ERR_INVALID_ARG;
+    if (dtype != GNND_F32 && dtype != GNND_F64 && dtype != GNND_BF16) return GNND_ERR_INVALID_ARG;
     if (batch == 0) return GNND_OK;
     if (!d_x || !d_out || ((nw > 0 || nw == -2) && !d_w)) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;

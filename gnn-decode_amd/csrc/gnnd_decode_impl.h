@@ -851,6 +851,24 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     }
 }
 
+// HBM storage type of x / out.  GNND_BF16 keeps the inputs and outputs in bf16 (half the
+// I/O bytes) while every LDS value, register and operation stays fp32: loads widen exactly
+// (bf16 -> fp32 is a 16-bit shift), stores round to nearest even.
+struct bf16_t {
+    uint16_t u;
+};
+template <typename T> __device__ __forceinline__ T io_ld(T v) { return v; }
+__device__ __forceinline__ float io_ld(bf16_t v) { return __uint_as_float((uint32_t)v.u << 16); }
+template <typename TI, typename T> __device__ __forceinline__ TI io_st(T v) {
+    if constexpr (std::is_same_v<TI, bf16_t>) {
+        uint32_t u = __float_as_uint((float)v);
+        u += 0x7fffu + ((u >> 16) & 1u);                 // round to nearest even (finite v)
+        return bf16_t{(uint16_t)(u >> 16)};
+    } else {
+        return (TI)v;
+    }
+}
+
 // sum of dp >= 1 consecutive LDS values in order; dp wave-uniform, so the trip counts and
 // remainder tests are scalar branches and every lane runs unmasked
 template <typename T> __device__ __forceinline__ T var_sum_uniform(const T* mp, int dp) {
@@ -882,10 +900,10 @@ template <typename T> __device__ __forceinline__ T var_sum_uniform(const T* mp, 
 #endif
 // PADR: trailing slots per lane that may be padding (0: none, 1: only the last, R: any;
 // gnnd_graph fills each check's lanes in order, so padding is always trailing)
-template <int MODEL, typename T, int G, int R, int QMAX, int PADR>
+template <int MODEL, typename T, int G, int R, int QMAX, int PADR, typename TI = T>
 __global__ void __launch_bounds__(GNND_BLOCK, GNND_RESIDENT_WAVES)
-decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
-                       T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem,
+decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* __restrict__ x,
+                       TI* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem,
                        FastDiv dV, FastDiv dN, TapeView<T>) {
     using M = EdgeMath<MODEL, T>;
     constexpr bool BP = ModelTraits<MODEL>::bp;
@@ -915,10 +933,10 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
     for (int i = tid; i < V; i += GNND_BLOCK) s_vord[i] = g.vlay[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
-    const T* xg = x + b0 * N;
+    const TI* xg = x + b0 * N;
     for (int i = tid; i < nb * N; i += GNND_BLOCK) {
         int b = fdiv(i, dN), n = i - b * N;
-        T xv = xg[i];
+        T xv = io_ld(xg[i]);
         if (n < V) {
             s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
         } else {
@@ -1270,9 +1288,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     const T xv = s_sx[sbase + v].x;
                     T s2 = T(0);
                     for (int j = 0; j < dv; ++j) s2 += xv * ww.out_p((int)o.y + j);
-                    out[b0 * V + sbase + v] = sigmoid_ref(-(s + s2));
+                    out[b0 * V + sbase + v] = io_st<TI>(sigmoid_ref(-(s + s2)));
                 } else {
-                    out[b0 * V + sbase + v] = M::readout(s + (kBase2 ? xg[b * N + v] : s_sx[sbase + v].x), s_w);
+                    out[b0 * V + sbase + v] = io_st<TI>(M::readout(s + (kBase2 ? io_ld(xg[b * N + v]) : s_sx[sbase + v].x), s_w));
                 }
             } else {
                 s_sx[sbase + v].s = s;
@@ -1290,11 +1308,11 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
                     const int v = (int)(o.x & 0xffffu);
 #ifdef GNND_LDS_IDEAL
                     const T s = var_sum_uniform(s_m + (tid & 63) + 64 * (i & 15), dp);
-                    if (last) out[b0 * V + vsbase + v] = M::readout(s + (kBase2 ? xg[vb * N + v] : s_sx[vsbase + v].x), s_w);
+                    if (last) out[b0 * V + vsbase + v] = io_st<TI>(M::readout(s + (kBase2 ? io_ld(xg[vb * N + v]) : s_sx[vsbase + v].x), s_w));
                     else s_sx[(tid & 63) + 64 * (i % 15)].s = s;
 #else
                     const T s = var_sum_uniform(s_m + vmbase + (int)o.y, dp);
-                    if (last) out[b0 * V + vsbase + v] = M::readout(s + (kBase2 ? xg[vb * N + v] : s_sx[vsbase + v].x), s_w);
+                    if (last) out[b0 * V + vsbase + v] = io_st<TI>(M::readout(s + (kBase2 ? io_ld(xg[vb * N + v]) : s_sx[vsbase + v].x), s_w));
                     else s_sx[vsbase + v].s = s;
 #endif
                 }
@@ -1318,10 +1336,10 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __
             const int b = fdiv(f, dV), v = f - b * V;
             if constexpr (MODEL == GNND_NBP) {
                 T s2 = T(0);
-                for (int k = g.var_ptr[v]; k < g.var_ptr[v + 1]; ++k) s2 += xg[b * N + v] * ww.out_p(k);
-                out[b0 * V + f] = sigmoid_ref(-s2);
+                for (int k = g.var_ptr[v]; k < g.var_ptr[v + 1]; ++k) s2 += io_ld(xg[b * N + v]) * ww.out_p(k);
+                out[b0 * V + f] = io_st<TI>(sigmoid_ref(-s2));
             } else {
-                out[b0 * V + f] = M::readout(xg[b * N + v], s_w);
+                out[b0 * V + f] = io_st<TI>(M::readout(io_ld(xg[b * N + v]), s_w));
             }
         }
 }
@@ -1503,7 +1521,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     return GNND_OK;
 }
 
-template <int MODEL, typename T, int R>
+template <int MODEL, typename T, int R, typename TI = T>
 int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_t B,
                   int iters, hipStream_t st, TapeView<T> tape = {}) {
     const GraphView& g = *p.view;
@@ -1516,7 +1534,7 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         if (p.lds > 64 * 1024)
             GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
-        kern<<<(unsigned)blocks, GNND_BLOCK, p.lds, st>>>(g, (const T*)w, nw, (const T*)x, (T*)out,
+        kern<<<(unsigned)blocks, GNND_BLOCK, p.lds, st>>>(g, (const T*)w, nw, (const TI*)x, (TI*)out,
                                                           B, iters, p.cw, dI, dV, dN, tape);
         GNND_LAUNCH_CHECK();
         return GNND_OK;
@@ -1527,11 +1545,11 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
                 constexpr int G = decltype(gtag)::value;
                 constexpr int P = decltype(ptag)::value;
                 switch (p.q) {
-                    case 3: return go(decode_resident_kernel<MODEL, T, G, R, 3, P>);
-                    case 6: return go(decode_resident_kernel<MODEL, T, G, R, 6, P>);
-                    case 9: if constexpr (R <= 3 && sizeof(T) == 4) return go(decode_resident_kernel<MODEL, T, G, R, 9, P>);
+                    case 3: return go(decode_resident_kernel<MODEL, T, G, R, 3, P, TI>);
+                    case 6: return go(decode_resident_kernel<MODEL, T, G, R, 6, P, TI>);
+                    case 9: if constexpr (R <= 3 && sizeof(T) == 4) return go(decode_resident_kernel<MODEL, T, G, R, 9, P, TI>);
                             break;
-                    case 12: if constexpr (R <= 2 && sizeof(T) == 4) return go(decode_resident_kernel<MODEL, T, G, R, 12, P>);
+                    case 12: if constexpr (R <= 2 && sizeof(T) == 4) return go(decode_resident_kernel<MODEL, T, G, R, 12, P, TI>);
                              break;
                 }
                 return GNND_ERR_UNSUPPORTED;
@@ -1551,13 +1569,17 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
             return by_g(std::integral_constant<int, R>{});
         }
     }
-    if constexpr (MODEL == GNND_V24)
-        if (tape.ext) return go(decode_kernel<MODEL, T, R, true>);
-    return go(decode_kernel<MODEL, T, R>);
+    if constexpr (!std::is_same_v<TI, T>) {
+        return GNND_ERR_UNSUPPORTED;      // bf16 I/O: register-resident plans only
+    } else {
+        if constexpr (MODEL == GNND_V24)
+            if (tape.ext) return go(decode_kernel<MODEL, T, R, true>);
+        return go(decode_kernel<MODEL, T, R>);
+    }
 }
 
 
-template <int MODEL, typename T>
+template <int MODEL, typename T, typename TI = T>
 int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
                     int iters, hipStream_t st, void* tape_base = nullptr) {
     Plan p;
@@ -1571,10 +1593,10 @@ int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out
         tape = TapeView<T>{base, base + n, base + 2 * n, base + 3 * n};
     }
     switch (p.view->R) {
-        case 1: return launch_decode<MODEL, T, 1>(p, w, x, out, B, iters, st, tape);
-        case 2: return launch_decode<MODEL, T, 2>(p, w, x, out, B, iters, st, tape);
-        case 3: return launch_decode<MODEL, T, 3>(p, w, x, out, B, iters, st, tape);
-        case 4: return launch_decode<MODEL, T, 4>(p, w, x, out, B, iters, st, tape);
+        case 1: return launch_decode<MODEL, T, 1, TI>(p, w, x, out, B, iters, st, tape);
+        case 2: return launch_decode<MODEL, T, 2, TI>(p, w, x, out, B, iters, st, tape);
+        case 3: return launch_decode<MODEL, T, 3, TI>(p, w, x, out, B, iters, st, tape);
+        case 4: return launch_decode<MODEL, T, 4, TI>(p, w, x, out, B, iters, st, tape);
     }
     return GNND_ERR_UNSUPPORTED;
 }
@@ -1583,6 +1605,11 @@ template <int MODEL>
 int launch_model(const gnnd_graph* g, int dtype, const void* w, const void* x, void* out,
                  int64_t B, int iters, hipStream_t st) {
     if (dtype == GNND_F32) return launch_decode_r<MODEL, float>(g, w, x, out, B, iters, st);
+    if (dtype == GNND_BF16) {      // bf16 x / out, fp32 arithmetic: the classical fp32 models
+        if constexpr (MODEL == GNND_CGNNI || MODEL == GNND_CBP)
+            return launch_decode_r<MODEL, float, bf16_t>(g, w, x, out, B, iters, st);
+        return GNND_ERR_UNSUPPORTED;
+    }
     return launch_decode_r<MODEL, double>(g, w, x, out, B, iters, st);
 }
 

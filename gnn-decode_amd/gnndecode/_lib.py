@@ -12,7 +12,7 @@ LIB_PATH = os.environ.get('GNND_LIB') or os.path.join(_HERE, 'libgnnd.so')   # G
 
 # enums (include/gnnd.h)
 OK, ERR_INVALID_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_GRAPH, ERR_ALLOC = range(6)
-F32, F64 = 0, 1
+F32, F64, BF16 = 0, 1, 2
 SOURCE_TO_TARGET, TARGET_TO_SOURCE = 0, 1
 AGGR = {'add': 0, 'mean': 1, 'max': 2}
 FLOW = {'source_to_target': SOURCE_TO_TARGET, 'target_to_source': TARGET_TO_SOURCE}

@@ -111,4 +111,6 @@ def dtype_code(dtype):
         return _lib.F32
     if dtype == torch.float64:
         return _lib.F64
-    raise TypeError(f'gnndecode kernels support float32/float64, got {dtype}')
+    if dtype == torch.bfloat16:
+        return _lib.BF16         # storage only (gnnd_decode of the classical models)
+    raise TypeError(f'gnndecode kernels support float32/float64 (bf16 storage), got {dtype}')

@@ -295,7 +295,9 @@ class _Decoder(torch.nn.Module):
         return prep
 
     def fused_ok(self, x, edge_index):
-        if not x.is_cuda or x.dtype not in (torch.float32, torch.float64):
+        dts = (torch.float32, torch.float64, torch.bfloat16) if self.kind in ('cgnni', 'cbp') \
+            else (torch.float32, torch.float64)
+        if not x.is_cuda or x.dtype not in dts:
             return False
         if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
             return False
@@ -310,7 +312,9 @@ class _Decoder(torch.nn.Module):
             x = x.unsqueeze(1)
         if self.fused_ok(x, edge_index):
             g = self.graph(x.device)
-            return ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(x.dtype, x.device))
+            # bf16 inputs (classical models): bf16 storage, fp32 weights and arithmetic
+            wdt = torch.float32 if x.dtype == torch.bfloat16 else x.dtype
+            return ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(wdt, x.device))
         if not x.is_cuda:
             raise RuntimeError('gnndecode runs on the GPU only (HIP/gfx950); move data to cuda')
         self.graph(x.device)      # training: autograd through the HIP propagate kernels

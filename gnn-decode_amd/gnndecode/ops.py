@@ -179,8 +179,9 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     nw = weights_count(model, graph, iters)
     if nw and (prepared_weights is None or prepared_weights.numel() != nw):
         raise ValueError(f'{model}: needs {nw} prepared weights')
-    if prepared_weights is not None and prepared_weights.dtype != x.dtype:
-        raise TypeError('weights and x must share a dtype')
+    wdt = torch.float32 if x.dtype == torch.bfloat16 else x.dtype   # bf16 storage, fp32 math
+    if prepared_weights is not None and prepared_weights.dtype != wdt:
+        raise TypeError(f'{x.dtype} inputs need {wdt} prepared weights')
     rows = decode_out_rows(graph, model, B)
     if out is None:
         out = torch.empty(rows, 1, dtype=x.dtype, device=x.device)
