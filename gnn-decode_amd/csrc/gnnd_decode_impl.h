@@ -243,22 +243,24 @@ struct Mlp10F32 {
     }
 };
 
-// fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1)
-__device__ __forceinline__ double mlp128_sp(const double* w, double u) {
+// fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1); the
+// Softplus is the table-driven form (tab = the kernel's LDS copy of kExpTab | kLogTab)
+__device__ __forceinline__ double mlp128_sp(const double* w, double u, const double* tab) {
     double acc = 0.0;
 #pragma unroll 4
     for (int k = 0; k < 128; ++k) {
         double h = fma(u, w[k], w[128 + k]);
-        acc = fma(softplus_ref(h), w[256 + k], acc);
+        acc = fma(softplus_tab(h, tab), w[256 + k], acc);
     }
     return acc + w[384];
 }
-__device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double u1) {
+__device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double u1,
+                                              const double* tab) {
     double acc = 0.0;
 #pragma unroll 4
     for (int k = 0; k < 128; ++k) {
         double h = fma(u0, w[k], fma(u1, w[128 + k], w[256 + k]));
-        acc = fma(softplus_ref(h), w[384 + k], acc);
+        acc = fma(softplus_tab(h, tab), w[384 + k], acc);
     }
     return acc + w[512];
 }
@@ -533,10 +535,11 @@ template <int MODEL, typename T> struct EdgeMath {
     static constexpr bool kFastBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP);
     // v->c message update and c->v pre-op: a_e = (S_v - m_e) + x_v -> t_e (+ BP sign flag)
     // (fp32 V24 runs the paired-edge path of decode_kernel instead)
-    __device__ static __forceinline__ T pre(T ext, T xv, const T* __restrict__ wv, T& cc) {
+    __device__ static __forceinline__ T pre(T ext, T xv, const T* __restrict__ wv, T& cc,
+                                            const T* tab = nullptr) {
         cc = T(0);
         if constexpr (MODEL == GNND_V24) {
-            return tanh_half_fast(mlp128x2_sp(wv + kV24Ggc1, ext, xv));
+            return tanh_half_fast(mlp128x2_sp(wv + kV24Ggc1, ext, xv, tab));
         } else if constexpr (kFastBP) {
             const float a = ext + xv;
             cc = a < 0.f ? 1.f : 0.f;          // tanh(clamp(a)/2) < 0 exactly when a < 0
@@ -553,9 +556,10 @@ template <int MODEL, typename T> struct EdgeMath {
     }
     // c->v update: u = S_c - t_e (BP: Lambda), n2 = leave-one-out sign count (BP)
     __device__ static __forceinline__ T post(T u, T n2, T sc, T mprev, const Mlp10F32& mlp,
-                                             const T* s_w, const T* __restrict__ wv) {
+                                             const T* s_w, const T* __restrict__ wv,
+                                             const T* tab = nullptr) {
         if constexpr (MODEL == GNND_V24) {
-            return mlp128_sp(wv + kV24Ggc2, u) * sc + mprev;
+            return mlp128_sp(wv + kV24Ggc2, u, tab) * sc + mprev;
         } else if constexpr (MODEL == GNND_QGNNI || MODEL == GNND_CGNNI) {
             T y;
             if constexpr (sizeof(T) == 4) y = mlp(u);
@@ -628,6 +632,15 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     int* s_vptr = (int*)(s_slot + nslot);
     int* s_vslot = s_vptr + V + 1;
     off += (((size_t)nslot + V + 1 + E) * 4 + 15) & ~(size_t)15;
+    // fp64 V24: the Softplus tables (gnnd_common.h kExpTab | kLogTab), indexed per lane
+    constexpr bool kTab = MODEL == GNND_V24 && sizeof(T) == 8;
+    T* s_tab = nullptr;
+    if constexpr (kTab) {
+        s_tab = (T*)(smem + off);
+        off += (size_t)kFp64TabDoubles * 8;
+        for (int i = tid; i < kFp64TabDoubles; i += GNND_BLOCK)
+            s_tab[i] = i < 128 ? kExpTab[i] : kLogTab[i - 128];
+    }
     T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
@@ -750,7 +763,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     mv[r] = mb[r];
                     const SumX<T> p = sxb[sv & 0xffffu];      // padding reads variable 0
                     T cc;
-                    T t = M::pre(p.s - mv[r], p.x, wv, cc);
+                    T t = M::pre(p.s - mv[r], p.x, wv, cc, s_tab);
                     tv[r] = valid ? t : T(0);
                     cf[r] = valid ? cc : T(0);
                     tsum += tv[r];
@@ -791,7 +804,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
             } else {
 #pragma unroll
                 for (int r = 0; r < R; ++r)   // every slot computes; padding slots are never read
-                    mn[r] = M::post(Sc - tv[r], Sc2 - cf[r], sc, mv[r], mlp_msg, s_w, wv);
+                    mn[r] = M::post(Sc - tv[r], Sc2 - cf[r], sc, mv[r], mlp_msg, s_w, wv, s_tab);
             }
             if (act) {
 #pragma unroll
@@ -829,7 +842,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                 if (f + 1 < n) s_m[f + 1] = y.y;
             }
         } else {
-            for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f]);
+            for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f], s_tab);
         }
         __syncthreads();
     }
@@ -1490,7 +1503,8 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const GraphView& g = !v24f32 ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
-    const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4);
+    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)kFp64TabDoubles * 8 : 0;
+    const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab;
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     size_t n = fixed + per >= target ? 1 : (target - fixed) / per;

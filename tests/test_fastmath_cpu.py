@@ -1,6 +1,7 @@
 """The fp64 exp / expm1 / log / tanh / Softplus of the decoders' fp64 paths
 (gnnd_common.h: Taylor exp with a two-part ln2, cancellation-free expm1, atanh-series log,
-tanh via expm1, Softplus as max(x, 0) + log1p(exp(-|x|))) compiled for the HOST with g++
+tanh via expm1, Softplus as max(x, 0) + log1p(exp(-|x|)), and the table-driven exp / log1p /
+Softplus of the fp64 decoder_v2_4 MLPs) compiled for the HOST with g++
 (the device builtins mapped to exact host equivalents) and compared with glibc over random
 arguments spanning the ranges the decoders feed them: every function within 4 ulp."""
 import os
@@ -28,7 +29,9 @@ static double ulp(double a, double b) {
 }
 int main() {
     std::mt19937_64 g(1);
-    double me = 0, ml = 0, mt = 0, mm = 0, ms = 0;
+    double me = 0, ml = 0, mt = 0, mm = 0, ms = 0, mst = 0, met = 0, mlt = 0;
+    static double TAB[kFp64TabDoubles];
+    for (int i = 0; i < kFp64TabDoubles; ++i) TAB[i] = i < 128 ? kExpTab[i] : kLogTab[i - 128];
     std::uniform_real_distribution<double> U(-700, 700), L(-300, 300), T(-12, 12), S(-60, 30);
     for (int i = 0; i < 400000; ++i) {
         double x = U(g) * (i % 4 ? 0.05 : 1.0);
@@ -41,8 +44,13 @@ int main() {
         mm = fmax(mm, ulp(expm1_f64(z), expm1(z)));
         double h = S(g);
         ms = fmax(ms, ulp(softplus_ref(h), h > 20 ? h : log1p(exp(h))));
+        mst = fmax(mst, ulp(softplus_tab(h, TAB), h > 20 ? h : log1p(exp(h))));
+        double yn = -fabs(U(g)) * (i % 4 ? 0.03 : 1.0);
+        met = fmax(met, ulp(exp_tab_nonpos(yn, TAB), exp(yn)));
+        double uu = (i % 3 == 0) ? exp(-fabs(L(g)) * 0.1) : std::uniform_real_distribution<double>(0, 1)(g);
+        mlt = fmax(mlt, ulp(log1p_tab_unit(uu, TAB + 128), log1p(uu)));
     }
-    printf("%.3f %.3f %.3f %.3f %.3f\n", me, ml, mt, mm, ms);
+    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f\n", me, ml, mt, mm, ms, mst, met, mlt);
 }
 '''
 
@@ -52,12 +60,14 @@ def test_fp64_fast_math_ulp(tmp_path):
     src = open(HDR).read()
     a = src.index('__constant__ static const double kSpCoef')
     b = src.index('template <typename T> __device__ __forceinline__ T sigmoid_ref')
-    body = src[a:b].replace('__constant__ static const', 'static const')
+    # (the tables sit inside [a, b): __constant__ arrays become plain static arrays)
+    body = src[a:b].replace('__constant__ static const', 'static const').replace('__restrict__', '')
     body = body.replace('__device__ __forceinline__', 'static inline')
     cpp = tmp_path / 'fastmath.cpp'
     cpp.write_text(PRELUDE + body + MAIN)
     exe = tmp_path / 'fastmath'
     subprocess.run(['g++', '-O2', '-ffp-contract=off', '-o', str(exe), str(cpp), '-lm'], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
-    errs = dict(zip(['exp', 'log', 'tanh', 'expm1', 'softplus'], map(float, out)))
+    errs = dict(zip(['exp', 'log', 'tanh', 'expm1', 'softplus', 'softplus_tab', 'exp_tab',
+                     'log1p_tab'], map(float, out)))
     assert all(v <= 4.0 for v in errs.values()), errs
