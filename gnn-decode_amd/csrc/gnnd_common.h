@@ -47,6 +47,10 @@ struct gnnd_graph {
     GraphView pview;          // ties -> R = 2: paired-edge fp32 V24 streaming at small batch
     GraphView rlay[7];        // rview with the padded message layout for vgroup 2^i (i = 0:
                               // identity); rlay[i].vlay == nullptr if it does not fit 16 bits
+    GraphView rlayx[7];       // the same layouts with one extra position per variable after
+                              // its padded messages, holding x_v (written once per decode,
+                              // never by the check step): the uniform variable sum then
+                              // yields T_v = S_v + x_v directly (T-layout resident models)
     void* dev;                // single device allocation holding every table
     size_t table_bytes;       // bytes of the four CSR/CSC tables (staged to LDS)
 };

@@ -327,15 +327,20 @@ struct Mlp10Pair {
     f32x2 w1b[10];     // {W1_k 2^-s_k, b1_k 2^-s_k}
     f32x2 w20b;        // {W2_0 2^s_0, b2}
     f32x2 w2[5];       // {W2_{2i} 2^s, W2_{2i+1} 2^s}  (w2[0].x unused)
-    __device__ __forceinline__ void load(const float* w, float umax) {
+    // MLP of the affine input u = in_scale v + in_bias with the output scaled by out_scale,
+    // folded into the weights:  W1' = W1 in_scale, b1' = W1 in_bias + b1 (one fp32 fma),
+    // W2' = W2 out_scale, b2' = b2 out_scale; vmax bounds |v| for the clamp scaling
+    __device__ __forceinline__ void load(const float* w, float vmax, float in_scale = 1.f,
+                                         float in_bias = 0.f, float out_scale = 1.f) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
+            const float w1 = w[k] * in_scale, b1 = __builtin_fmaf(w[k], in_bias, w[10 + k]);
             int e;
-            frexpf(fabsf(w[k]) * umax + fabsf(w[10 + k]), &e);
-            w1b[k] = f32x2{uniform(ldexpf(w[k], -e)), uniform(ldexpf(w[10 + k], -e))};
-            const float v = uniform(ldexpf(w[20 + k], e));
+            frexpf(fabsf(w1) * vmax + fabsf(b1), &e);
+            w1b[k] = f32x2{uniform(ldexpf(w1, -e)), uniform(ldexpf(b1, -e))};
+            const float v = uniform(ldexpf(w[20 + k] * out_scale, e));
             if (k & 1) w2[k >> 1].y = v; else w2[k >> 1].x = v;
-            if (k == 0) w20b = f32x2{v, uniform(w[30])};
+            if (k == 0) w20b = f32x2{v, uniform(w[30] * out_scale)};
         }
     }
     __device__ __forceinline__ f32x2 operator()(f32x2 u) const {
@@ -927,6 +932,17 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     constexpr bool kPairBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP ||
                                                 MODEL == GNND_NBP || MODEL == GNND_V10);
     constexpr bool kPair = kBase2 || kPairBP;
+    // T layout (paired GNN and plain-BP models): LDS keeps ONE value per variable,
+    // T_v = S_v + x_v (base-2 scaled for the GNN models: messages m' = m log2 e, so
+    // T'_v = S'_v + x'_v), refreshed by the variable-sum step, plus x_v itself for that
+    // refresh; the check step's v->c argument a_e = T_v - m_e is one packed subtract per
+    // edge pair.  The GNN check step then works in the sigmoid domain: r_e = 1/(1 + 2^a'_e)
+    // = (1 - tanh(a_e/2))/2, check sum R = sum_slots r (padding slots r = 1/2, i.e. t = 0),
+    // leave-one-out u_e = (G R_slots - 1) - 2 (R - r_e) with the affine map folded into the
+    // message MLP's first layer and log2 e into its second (Mlp10Pair::load).  Weighted BP
+    // keeps {S_v, x_v} (its per-edge weights act on S and x separately).
+    constexpr bool WBP0 = ModelTraits<MODEL>::wbp;
+    constexpr bool kTX = kPair && !WBP0;
     constexpr int kLogG = G == 1 ? 0 : G == 2 ? 1 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N;
@@ -941,6 +957,10 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     T* s_m = (T*)(smem + off);                             // [CW][E+1] messages, var-major
     SumX<T>* s_sx = (SumX<T>*)(s_m + (((size_t)CW * E1 + 1) & ~(size_t)1));  // [CW][V]
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
+    // kTX: [CW][V] T_v in place of {S_v, x_v}; x_v lives in the message layout
+    // (gnnd_graph::rlayx: the last position of each variable's run)
+    float* s_t = (float*)s_sx;
+    if constexpr (kTX) s_xc = (T*)(s_t + (size_t)CW * V);
 
     for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
     for (int i = tid; i < V; i += GNND_BLOCK) s_vord[i] = g.vlay[i];
@@ -951,16 +971,28 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         int b = fdiv(i, dN), n = i - b * N;
         T xv = io_ld(xg[i]);
         if (n < V) {
-            s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
+            const T xs = kBase2 ? xv * T(kLog2e) : xv;
+            if constexpr (kTX) s_t[b * V + n] = xs;     // T = 0 + x
+            else s_sx[b * V + n] = SumX<T>{T(0), xs};
         } else {
             s_xc[b * C + n - V] = xv;
         }
     }
     // padded layouts: the positions past a variable's degree are read by the variable sums
     // and never written, so they must hold 0 (s + 0 == s)
-    if (g.vgroup > 1)
+    if (kTX || g.vgroup > 1)
         for (int i = tid; i < CW * E1; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
+    if constexpr (kTX) {
+        // x_v into the last position of its run (after the padded messages: S + 0 + x_v)
+        for (int i = tid; i < nb * V; i += GNND_BLOCK) {
+            const int b = fdiv(i, dV), j = i - b * V;
+            const uint2 o = s_vord[j];
+            const int v = (int)(o.x & 0xffffu);
+            s_m[b * E1 + (int)o.y + (int)(o.x >> 16) - 1] = s_t[b * V + v];
+        }
+        __syncthreads();
+    }
 
     Mlp10F32 mlp_msg;   // scalar-path form (unused: fp32 GNN models run the paired step)
     if constexpr (sizeof(T) == 4 && !kPair && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI))
@@ -994,7 +1026,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     f32x2 ms[RP];              // solo item: {slot 2i, slot 2i+1} (odd R: last pairs itself)
     f32x2 sc2[QP];
     Mlp10Pair mlp2;
-    if constexpr (kBase2) mlp2.load((const float*)s_w + kMlp10Msg, (float)g.max_dc);
+    if constexpr (kBase2)      // input v = R - r_e: u = (G R_slots - 1) - 2 v; output x log2 e
+        mlp2.load((const float*)s_w + kMlp10Msg, (float)(G * R), -2.f, (float)(G * R - 1), kLog2e);
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
         const int f = tid + q * GNND_BLOCK;
@@ -1076,24 +1109,55 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 }
                 return t;
             };
+            // T layout: a = T - m for both edges in one packed subtract.  GNN: r = 1/(1 + 2^a')
+            // (padding slots r = 1/2); BP: {log2|tanh(a/2)|, [a < 0]} (padding 0)
+            auto pre2t = [&](f32x2 tt, uint32_t sa, uint32_t sb, f32x2 mprev, int ra, int rb,
+                             f32x2& cc) {
+                const f32x2 a = tt - mprev;
+                f32x2 t;
+                float pad = 0.f;
+                if constexpr (kBase2) {
+                    f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+                    e = e + f32x2{1.f, 1.f};
+                    t = f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+                    cc = f32x2{0.f, 0.f};
+                    pad = 0.5f;
+                } else {
+                    cc = f32x2{a.x < 0.f ? 1.f : 0.f, a.y < 0.f ? 1.f : 0.f};
+                    t = bp_log2tanh_f32x2(a, MODEL == GNND_QBP ? 1e-20f : 1e-7f);
+                }
+                if constexpr (PADR > 0) {   // padding slot: position == spare
+                    if (ra >= R - PADR && sa >= ((uint32_t)spare << 16)) { t.x = pad; cc.x = 0.f; }
+                    if (rb >= R - PADR && sb >= ((uint32_t)spare << 16)) { t.y = pad; cc.y = 0.f; }
+                }
+                return t;
+            };
             auto pre2 = [&](uint32_t sa, uint32_t sb, int ca, int cbb, f32x2 mprev, int ra, int rb,
                             f32x2& cc) {
-                return pre2v(s_sx[ca * V + (int)(sa & 0xffffu)], s_sx[cbb * V + (int)(sb & 0xffffu)],
-                             sa, sb, mprev, ra, rb, cc);
+                if constexpr (kTX)
+                    return pre2t(f32x2{s_t[ca * V + (int)(sa & 0xffffu)], s_t[cbb * V + (int)(sb & 0xffffu)]},
+                                 sa, sb, mprev, ra, rb, cc);
+                else
+                    return pre2v(s_sx[ca * V + (int)(sa & 0xffffu)], s_sx[cbb * V + (int)(sb & 0xffffu)],
+                                 sa, sb, mprev, ra, rb, cc);
             };
+            // per-slot operand of the paired pre-op: T_v of both edges (T layout) or the two
+            // {S_v, x_v}
+            using PX = std::conditional_t<kTX, f32x2, SumX<T>[2]>;
             // {S_v, x_v} of an item pair's slots (issued one pair ahead: LDS reads cannot move
             // above the previous pair's message writes by themselves, the compiler cannot
             // tell the two arrays apart)
-            auto load_pair = [&](int j, SumX<T> (&px)[R][2]) {
+            auto load_pair = [&](int j, PX (&px)[R]) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-#ifdef GNND_LDS_IDEAL   // timing upper bound only (wrong results): conflict-free addresses
-                    px[r][0] = s_sx[(tid & 63) + 64 * ((r + R * 2 * j) % 15)];
-                    px[r][1] = s_sx[(tid & 63) + 64 * ((r + R * (2 * j + 1)) % 15)];
-#else
-                    px[r][0] = s_sx[cb[2 * j] * V + (int)(ve[2 * j][r] & 0xffffu)];
-                    px[r][1] = s_sx[cb[2 * j + 1] * V + (int)(ve[2 * j + 1][r] & 0xffffu)];
-#endif
+                    const int ia = cb[2 * j] * V + (int)(ve[2 * j][r] & 0xffffu);
+                    const int ib = cb[2 * j + 1] * V + (int)(ve[2 * j + 1][r] & 0xffffu);
+                    if constexpr (kTX) {
+                        px[r] = f32x2{s_t[ia], s_t[ib]};
+                    } else {
+                        px[r][0] = s_sx[ia];
+                        px[r][1] = s_sx[ib];
+                    }
                 }
             };
             // c->v update of two edges from the leave-one-out sums u (and sign counts n)
@@ -1123,13 +1187,16 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 }
             };
             // item pair (2j, 2j + 1)
-            auto pair_step = [&](auto jc, const SumX<T> (&px)[R][2]) {
+            auto pair_step = [&](auto jc, const PX (&px)[R]) {
                 constexpr int j = decltype(jc)::value;
                 const int qa = 2 * j, qb = 2 * j + 1;
                 f32x2 tv[R], cv[R], tsum, csum;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    tv[r] = pre2v(px[r][0], px[r][1], ve[qa][r], ve[qb][r], m2[j][r], r, r, cv[r]);
+                    if constexpr (kTX)
+                        tv[r] = pre2t(px[r], ve[qa][r], ve[qb][r], m2[j][r], r, r, cv[r]);
+                    else
+                        tv[r] = pre2v(px[r][0], px[r][1], ve[qa][r], ve[qb][r], m2[j][r], r, r, cv[r]);
                     tsum = r == 0 ? tv[0] : tsum + tv[r];
                     if constexpr (kPairBP) csum = r == 0 ? cv[0] : csum + cv[r];
                 }
@@ -1141,14 +1208,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     m2[j][r] = post2(Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
-#ifdef GNND_LDS_IDEAL
-                    s_m[(tid & 63) + 64 * ((r + R * qa) % 100)] = m2[j][r].x;
-                    s_m[(tid & 63) + 64 * ((r + R * qb) % 100)] = m2[j][r].y;
-                    (void)mba; (void)mbb;
-#else
                     mba[ve[qa][r] >> 16] = m2[j][r].x * wnext(ve[qa][r]);
                     mbb[ve[qb][r] >> 16] = m2[j][r].y * wnext(ve[qb][r]);
-#endif
                 }
             };
             // one item with its slots in pairs (the same per-edge arithmetic as pair_step:
@@ -1192,12 +1253,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
 #else
             constexpr bool kAhead = false;
 #endif
-            SumX<T> pxa[R][2], pxb[R][2];       // current / next pair's {S_v, x_v}
+            PX pxa[R], pxb[R];                  // current / next pair's operands
             if constexpr (kAhead) load_pair(0, pxa);
             static_for<QP>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                SumX<T> (&cur)[R][2] = (j & 1) ? pxb : pxa;
-                SumX<T> (&nxt)[R][2] = (j & 1) ? pxa : pxb;
+                PX (&cur)[R] = (j & 1) ? pxb : pxa;
+                PX (&nxt)[R] = (j & 1) ? pxa : pxb;
                 if constexpr (kAhead) {
                     if constexpr (j + 1 < QP) load_pair(j + 1, nxt);
                 } else {
@@ -1279,6 +1340,22 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         // (odd stride E+1: no bank conflicts).  Edge (index_add) order within a variable;
         // two-value ds_read2 loads, four values in flight per step, no masking.
         const bool last = it + 1 == iters;
+        // the variable step's result for variable v of codeword b (sum s of its messages):
+        // last iteration -> readout (GNN T layout: s = S' base-2 scaled, S + x = s ln2 + x);
+        // otherwise the check step's operand (T_v = s + x_v, or S_v of {S_v, x_v})
+        auto var_out = [&](int b, int sbase, int v, T s) {
+            if (last) {
+                T r;
+                if constexpr (kTX && kBase2) r = s * kLn2;          // (S' + x') ln2 = S + x
+                else if constexpr (kTX) r = s;                       // S + x
+                else r = s + (kBase2 ? io_ld(xg[b * N + v]) : s_sx[sbase + v].x);
+                out[b0 * V + sbase + v] = io_st<TI>(M::readout(r, s_w));
+            } else if constexpr (kTX) {
+                s_t[sbase + v] = s;                                   // T_v = S_v + x_v
+            } else {
+                s_sx[sbase + v].s = s;
+            }
+        };
         // one variable-item (codeword b, degree-order index i); mbase = b (E+1), sbase = b V
         auto var_item = [&](int b, int i, int mbase, int sbase) {
             const uint2 o = s_vord[i];
@@ -1296,18 +1373,16 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 k += 2;
             }
             if (dv & 1) s += mp[k];
-            if (last) {
-                if constexpr (MODEL == GNND_NBP) {   // + sum_v(x_v W_p)  (neural_BP.py:307-312)
+            if constexpr (MODEL == GNND_NBP) {
+                if (last) {   // + sum_v(x_v W_p)  (neural_BP.py:307-312)
                     const T xv = s_sx[sbase + v].x;
                     T s2 = T(0);
                     for (int j = 0; j < dv; ++j) s2 += xv * ww.out_p((int)o.y + j);
                     out[b0 * V + sbase + v] = io_st<TI>(sigmoid_ref(-(s + s2)));
-                } else {
-                    out[b0 * V + sbase + v] = io_st<TI>(M::readout(s + (kBase2 ? io_ld(xg[b * N + v]) : s_sx[sbase + v].x), s_w));
+                    return;
                 }
-            } else {
-                s_sx[sbase + v].s = s;
             }
+            var_out(b, sbase, v, s);
         };
         if (vuni) {
             // padded layout (GraphView::vlay): the wave's vgroup variables share one padded
@@ -1319,15 +1394,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     const uint2 o = s_vord[i];
                     const int dp = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));
                     const int v = (int)(o.x & 0xffffu);
-#ifdef GNND_LDS_IDEAL
-                    const T s = var_sum_uniform(s_m + (tid & 63) + 64 * (i & 15), dp);
-                    if (last) out[b0 * V + vsbase + v] = io_st<TI>(M::readout(s + (kBase2 ? io_ld(xg[vb * N + v]) : s_sx[vsbase + v].x), s_w));
-                    else s_sx[(tid & 63) + 64 * (i % 15)].s = s;
-#else
-                    const T s = var_sum_uniform(s_m + vmbase + (int)o.y, dp);
-                    if (last) out[b0 * V + vsbase + v] = io_st<TI>(M::readout(s + (kBase2 ? io_ld(xg[vb * N + v]) : s_sx[vsbase + v].x), s_w));
-                    else s_sx[vsbase + v].s = s;
-#endif
+                    var_out(vb, vsbase, v, var_sum_uniform(s_m + vmbase + (int)o.y, dp));
                 }
         } else if (vfixed) {
             // CW divides 256: f = tid + k 256 keeps f mod CW, so the lane's codeword and its
@@ -1452,22 +1519,27 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         // makes its variable sums uniform (GraphView::vlay); weighted BP indexes per-edge
         // weights by edge id and keeps the identity layout
         const bool wbp = model == GNND_NBP || model == GNND_V10;
+        // T-layout models (decode_resident_kernel kTX: the fp32 paired GNN / plain BP) run
+        // on the x-augmented layouts (gnnd_graph::rlayx)
+        const bool tx = dtype == GNND_F32 && !wbp;
         auto lay_of = [&](int cw) -> const GraphView* {
+            const GraphView* lays = tx ? gr->rlayx : gr->rlay;
             if (!wbp && !vlayout_disabled() && GNND_BLOCK % cw == 0 && cw < 64) {
                 int i = 0;
                 while ((cw << i) < 64) ++i;
-                if (gr->rlay[i].vlay) return &gr->rlay[i];
+                if (lays[i].vlay) return &lays[i];
             }
-            return &gr->rlay[0];
+            return &lays[0];
         };
         // resident layout: weights, var order, then [CW][P1] messages, [CW][V] {S, x},
         // [CW][C].  Pick (CW, Q) with Q in kResidentQ maximising lane utilisation
         // CW*IC / (Q*256), ties to the larger tile.
         const size_t fixed = wb + align16((size_t)g.V * 8);
-        auto lds_of = [&](int cw) {
+        auto lds_of = [&](int cw) {     // messages, then {S_v, x_v} (T layout: T_v), x_c
             return fixed + esz * (((size_t)cw * lay_of(cw)->P1 + 1) & ~(size_t)1) +
-                   esz * ((size_t)cw * (2 * (size_t)g.V + g.C));
+                   esz * ((size_t)cw * ((tx ? 1 : 2) * (size_t)g.V + g.C));
         };
+        const bool tx_ok = !tx || gr->rlayx[0].vlay != nullptr;   // else: streaming kernel
         int best = 0, bestq = 0;
         double bestu = 0;
         static const int force_q = [] {
@@ -1485,7 +1557,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
             double u = (double)cw * IC / ((double)q * GNND_BLOCK);
             if (u > bestu + 1e-9 || (u > bestu - 1e-9 && cw > best)) { bestu = u; best = cw; bestq = q; }
         }
-        if (best > 0 && bestu >= 0.5) {
+        if (best > 0 && bestu >= 0.5 && tx_ok) {
             p->view = lay_of(best);
             p->resident = true;
             p->cw = best;

@@ -130,19 +130,15 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     const int ord_off = (off + 1) & ~1;     // uint2 alignment
     // padded variable-major message layouts of the resident kernel (GraphView::vlay), one per
     // wave group size 2^i, i = 1..6: groups of 2^i consecutive var_ord entries share the
-    // group's largest degree; positions run in var_ord order
+    // group's largest degree; positions run in var_ord order.  The x-augmented variants
+    // (i = 0..6) give every variable one more position after its padded messages for x_v.
     const int nsr = (int)plans[1].slot.size();
     struct Layout {
         bool ok = false;
         int P = 0;
         std::vector<int> vlay, slot;     // [2V] {v | dpad << 16, pos}, [nsr] v | pos << 16
     };
-    Layout lays[7];
-    int lay_off[7] = {0};
-    off = ord_off + 2 * V;
-    for (int i = 1; i < 7; ++i) {
-        const int gs = 1 << i;
-        Layout& L = lays[i];
+    auto build_layout = [&](int gs, bool with_x, Layout& L) {
         std::vector<int> epos(E);
         L.vlay.assign(2 * V, 0);
         int pos = 0;
@@ -150,6 +146,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             const int j1 = std::min(V, j0 + gs);
             int dpad = 0;
             for (int j = j0; j < j1; ++j) dpad = std::max(dpad, vptr[vord[j] + 1] - vptr[vord[j]]);
+            if (with_x) ++dpad;              // the x_v position, last in the variable's run
             for (int j = j0; j < j1; ++j) {
                 const int v = vord[j];
                 L.vlay[2 * j] = v | (dpad << 16);
@@ -159,7 +156,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             }
         }
         L.P = pos;
-        if (pos >= 65535) continue;          // positions travel in 16 bits
+        if (pos >= 65535) return;            // positions travel in 16 bits
         L.ok = true;
         L.slot.assign(nsr, pos << 16);       // padding: variable 0, the spare position P
         for (int k = 0; k < nsr; ++k) {
@@ -167,8 +164,19 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             const int e = (int)(sv >> 16);
             if (e < E) L.slot[k] = (int)(sv & 0xffffu) | (epos[e] << 16);
         }
-        lay_off[i] = off;
-        off = (off + 2 * V + nsr + 1) & ~1;  // uint2 alignment of the next layout
+    };
+    Layout lays[7], laysx[7];
+    int lay_off[7] = {0}, layx_off[7] = {0};
+    off = ord_off + 2 * V;
+    for (int i = 0; i < 7; ++i) {
+        for (int x = 0; x < 2; ++x) {
+            if (i == 0 && !x) continue;      // identity layout: positions = edge ids
+            Layout& L = x ? laysx[i] : lays[i];
+            build_layout(1 << i, x != 0, L);
+            if (!L.ok) continue;
+            (x ? layx_off : lay_off)[i] = off;
+            off = (off + 2 * V + nsr + 1) & ~1;  // uint2 alignment of the next layout
+        }
     }
     std::vector<int> table(off);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
@@ -186,10 +194,13 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         table[ord_off + 2 * i] = v | ((vptr[v + 1] - vptr[v]) << 16);
         table[ord_off + 2 * i + 1] = vptr[v];
     }
-    for (int i = 1; i < 7; ++i)
-        if (lays[i].ok) {
-            memcpy(table.data() + lay_off[i], lays[i].vlay.data(), sizeof(int) * 2 * V);
-            memcpy(table.data() + lay_off[i] + 2 * V, lays[i].slot.data(), sizeof(int) * nsr);
+    for (int i = 0; i < 7; ++i)
+        for (int x = 0; x < 2; ++x) {
+            const Layout& L = x ? laysx[i] : lays[i];
+            if (!L.ok) continue;
+            const int o = (x ? layx_off : lay_off)[i];
+            memcpy(table.data() + o, L.vlay.data(), sizeof(int) * 2 * V);
+            memcpy(table.data() + o + 2 * V, L.slot.data(), sizeof(int) * nsr);
         }
 
     gnnd_graph* g = (gnnd_graph*)calloc(1, sizeof(gnnd_graph));
@@ -225,15 +236,19 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         pv.vgroup = 1; pv.spare = E; pv.P1 = E + 1;
     }
     for (int i = 0; i < 7; ++i) {
-        GraphView& lv = g->rlay[i];
-        lv = g->rview;
-        if (i == 0) continue;
-        lv.vgroup = 1 << i;
-        if (!lays[i].ok) { lv.vlay = nullptr; continue; }
-        lv.vlay = (const uint2*)(d + lay_off[i]);
-        lv.slot_ve = (const uint32_t*)(d + lay_off[i] + 2 * V);
-        lv.spare = lays[i].P;
-        lv.P1 = (lays[i].P + 1) | 1;        // odd codeword stride, spare slot included
+        for (int x = 0; x < 2; ++x) {
+            GraphView& lv = x ? g->rlayx[i] : g->rlay[i];
+            const Layout& L = x ? laysx[i] : lays[i];
+            lv = g->rview;
+            if (i == 0 && !x) continue;
+            lv.vgroup = 1 << i;
+            if (!L.ok) { lv.vlay = nullptr; continue; }
+            const int o = (x ? layx_off : lay_off)[i];
+            lv.vlay = (const uint2*)(d + o);
+            lv.slot_ve = (const uint32_t*)(d + o + 2 * V);
+            lv.spare = L.P;
+            lv.P1 = (L.P + 1) | 1;          // odd codeword stride, spare slot included
+        }
     }
     *out = g;
     return GNND_OK;
