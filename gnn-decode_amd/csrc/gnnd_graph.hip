@@ -33,10 +33,31 @@ extern "C" const char* gnnd_status_string(int s) {
     }
 }
 
-extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
-                                 int32_t V, int32_t C, gnnd_graph** out) {
-    if (!out) return GNND_ERR_INVALID_ARG;
-    *out = nullptr;
+namespace {
+
+struct SlotPlan {
+    int G = 0, R = 0, padded = 0, padr = 0;
+    std::vector<uint32_t> slot, slot_ve;
+    std::vector<int> vslot;
+};
+struct Layout {
+    bool ok = false;
+    int P = 0;
+    std::vector<int> vlay, slot;     // [2V] {v | dpad << 16, pos}, [nsr] v | pos << 16
+};
+// everything gnnd_graph_create uploads, built on the host (also checked by
+// gnnd_graph_validate_host without a device)
+struct HostTables {
+    int V = 0, C = 0, E = 0, max_dv = 0, max_dc = 0, nints = 0, ord_off = 0, nsr = 0;
+    int plan_off[3] = {0, 0, 0};
+    SlotPlan plans[3];
+    Layout lays[7], laysx[7];
+    int lay_off[7] = {0}, layx_off[7] = {0};
+    std::vector<int> table;
+};
+
+int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, int32_t V,
+                 int32_t C, HostTables& T) {
     if (!h_var || !h_chk || num_edges <= 0 || V <= 0 || C <= 0) return GNND_ERR_INVALID_ARG;
     // 16-bit packing of v, c and edge ids (E itself marks padding); bounds every degree
     if (V > 65535 || C > 65535 || num_edges > 65535) return GNND_ERR_UNSUPPORTED;
@@ -71,11 +92,6 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         const char* e = getenv("GNND_GROUP_R");
         return e ? atoi(e) : 0;
     }();
-    struct SlotPlan {
-        int G = 0, R = 0, padded = 0, padr = 0;
-        std::vector<uint32_t> slot, slot_ve;
-        std::vector<int> vslot;
-    };
     // tie preference: 0 = smaller R, 1 = larger R, 2 = R = 2 (the paired-edge fp32 V24
     // path at small batches: one edge pair per lane, most lanes per codeword)
     auto build_plan = [&](int pref, SlotPlan& sp) -> bool {
@@ -110,7 +126,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
         }
         return true;
     };
-    SlotPlan plans[3];
+    SlotPlan* plans = T.plans;
     for (int i = 0; i < 3; ++i)
         if (!build_plan(i, plans[i])) return GNND_ERR_UNSUPPORTED;
 
@@ -121,7 +137,7 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     });
 
     const int nints = graph_table_ints(V, C, E);
-    int plan_off[3];
+    int* plan_off = T.plan_off;
     int off = nints;
     for (int i = 0; i < 3; ++i) {
         plan_off[i] = off;
@@ -133,11 +149,6 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     // group's largest degree; positions run in var_ord order.  The x-augmented variants
     // (i = 0..6) give every variable one more position after its padded messages for x_v.
     const int nsr = (int)plans[1].slot.size();
-    struct Layout {
-        bool ok = false;
-        int P = 0;
-        std::vector<int> vlay, slot;     // [2V] {v | dpad << 16, pos}, [nsr] v | pos << 16
-    };
     auto build_layout = [&](int gs, bool with_x, Layout& L) {
         std::vector<int> epos(E);
         L.vlay.assign(2 * V, 0);
@@ -165,8 +176,10 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             if (e < E) L.slot[k] = (int)(sv & 0xffffu) | (epos[e] << 16);
         }
     };
-    Layout lays[7], laysx[7];
-    int lay_off[7] = {0}, layx_off[7] = {0};
+    Layout* lays = T.lays;
+    Layout* laysx = T.laysx;
+    int* lay_off = T.lay_off;
+    int* layx_off = T.layx_off;
     off = ord_off + 2 * V;
     for (int i = 0; i < 7; ++i) {
         for (int x = 0; x < 2; ++x) {
@@ -178,7 +191,8 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             off = (off + 2 * V + nsr + 1) & ~1;  // uint2 alignment of the next layout
         }
     }
-    std::vector<int> table(off);
+    std::vector<int>& table = T.table;
+    table.assign(off, 0);
     memcpy(table.data(), evc.data(), sizeof(int) * E);
     memcpy(table.data() + E, vptr.data(), sizeof(int) * (V + 1));
     memcpy(table.data() + E + V + 1, cptr.data(), sizeof(int) * (C + 1));
@@ -203,6 +217,115 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
             memcpy(table.data() + o + 2 * V, L.slot.data(), sizeof(int) * nsr);
         }
 
+    T.V = V; T.C = C; T.E = E; T.max_dv = max_dv; T.max_dc = max_dc;
+    T.nints = nints; T.ord_off = ord_off; T.nsr = nsr;
+    return GNND_OK;
+}
+
+// Structural invariants of the host tables (the device kernels index with them unchecked):
+// every edge sits in exactly one slot of its check, in edge order, padding trailing; every
+// layout gives each variable a disjoint run holding its edges first (then zero padding and,
+// for the x-augmented layouts, the x_v position last), and its slot table points at them.
+int check_tables(const HostTables& T, int32_t* report) {
+    const int E = T.E, V = T.V, C = T.C;
+    const std::vector<int>& t = T.table;
+    const int* vptr = t.data() + E;
+    const int* cptr = vptr + V + 1;
+    const int* cedge = cptr + C + 1;
+    int fails = 0, nlay = 0;
+    for (int p = 0; p < 3; ++p) {
+        const SlotPlan& sp = T.plans[p];
+        const int GR = sp.G * sp.R;
+        if ((int)sp.slot_ve.size() != C * GR) { ++fails; continue; }
+        for (int c = 0; c < C; ++c) {
+            const int deg = cptr[c + 1] - cptr[c];
+            if (deg > GR) ++fails;
+            for (int i = 0; i < GR; ++i) {
+                const int e = (int)(sp.slot_ve[c * GR + i] >> 16);
+                if (i < deg) {
+                    if (e != cedge[cptr[c] + i] || sp.vslot[e] != c * GR + i) ++fails;
+                    if ((int)(sp.slot_ve[c * GR + i] & 0xffffu) != (int)(t[e] & 0xffff)) ++fails;
+                } else if (e != E) {
+                    ++fails;
+                }
+            }
+            // lanes fill in order: a lane's padding is trailing and at most padr slots
+            for (int gi = 0; gi < sp.G; ++gi) {
+                int pad = 0;
+                for (int r = 0; r < sp.R; ++r) {
+                    const bool isp = (int)(sp.slot_ve[c * GR + gi * sp.R + r] >> 16) == E;
+                    if (!isp && pad) ++fails;
+                    pad += isp;
+                }
+                if (pad > sp.padr) ++fails;
+            }
+        }
+    }
+    for (int x = 0; x < 2; ++x)
+        for (int i = x ? 0 : 1; i < 7; ++i) {
+            const Layout& L = x ? T.laysx[i] : T.lays[i];
+            if (!L.ok) continue;
+            ++nlay;
+            std::vector<int> owner(L.P + 1, -1), epos(E, -1);
+            int expect = 0;
+            for (int j = 0; j < V; ++j) {
+                const int v = L.vlay[2 * j] & 0xffff, dpad = (int)((uint32_t)L.vlay[2 * j] >> 16);
+                const int pos = L.vlay[2 * j + 1];
+                const int deg = vptr[v + 1] - vptr[v];
+                if (pos != expect || dpad < deg + x || pos + dpad > L.P) { ++fails; continue; }
+                expect = pos + dpad;
+                for (int k = 0; k < dpad; ++k) {
+                    if (owner[pos + k] != -1) ++fails;
+                    owner[pos + k] = v;
+                }
+                for (int e = vptr[v]; e < vptr[v + 1]; ++e) epos[e] = pos + (e - vptr[v]);
+            }
+            if (expect != L.P) ++fails;
+            const SlotPlan& sp = T.plans[1];
+            for (int k = 0; k < T.nsr; ++k) {
+                const int e = (int)(sp.slot_ve[k] >> 16);
+                const int want = e < E ? epos[e] : L.P;
+                if ((int)((uint32_t)L.slot[k] >> 16) != want) ++fails;
+            }
+        }
+    if (report) {
+        report[0] = 3;
+        report[1] = nlay;
+        report[2] = E;
+        report[3] = fails;
+    }
+    return fails ? GNND_ERR_GRAPH : GNND_OK;
+}
+
+}  // namespace
+
+// Build every table gnnd_graph_create would upload, on the host only, and check their
+// invariants (no device needed: CPU tests and the host sanitizer build run this).
+// report[4] = {slot plans checked, layouts checked, edges, failures}.
+extern "C" int gnnd_graph_validate_host(const int64_t* h_var, const int64_t* h_chk,
+                                        int64_t num_edges, int32_t V, int32_t C,
+                                        int32_t* h_report4) {
+    HostTables T;
+    const int rc = build_tables(h_var, h_chk, num_edges, V, C, T);
+    if (rc != GNND_OK) return rc;
+    return check_tables(T, h_report4);
+}
+
+extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
+                                 int32_t V, int32_t C, gnnd_graph** out) {
+    if (!out) return GNND_ERR_INVALID_ARG;
+    *out = nullptr;
+    HostTables T;
+    const int rc = build_tables(h_var, h_chk, num_edges, V, C, T);
+    if (rc != GNND_OK) return rc;
+    const int E = T.E, max_dv = T.max_dv, max_dc = T.max_dc, nints = T.nints, ord_off = T.ord_off;
+    const std::vector<int>& table = T.table;
+    const SlotPlan* plans = T.plans;
+    const Layout* lays = T.lays;
+    const Layout* laysx = T.laysx;
+    const int* plan_off = T.plan_off;
+    const int* lay_off = T.lay_off;
+    const int* layx_off = T.layx_off;
     gnnd_graph* g = (gnnd_graph*)calloc(1, sizeof(gnnd_graph));
     if (!g) return GNND_ERR_ALLOC;
     hipError_t err = hipMalloc(&g->dev, sizeof(int) * table.size());

@@ -29,6 +29,7 @@ _int = ctypes.c_int
 SIGNATURES = {
     'gnnd_graph_create': (_int, [_c_i64p, _c_i64p, _i64, _i32, _i32, ctypes.POINTER(_vp)]),
     'gnnd_graph_destroy': (_int, [_vp]),
+    'gnnd_graph_validate_host': (_int, [_c_i64p, _c_i64p, _i64, _i32, _i32, _c_i32p]),
     'gnnd_graph_dims': (_int, [_vp, _c_i32p]),
     'gnnd_check_tiled': (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     'gnnd_propagate_width': (_int, [_int, _int]),

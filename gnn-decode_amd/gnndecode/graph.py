@@ -48,6 +48,8 @@ class TannerGraph:
         _lib.call('gnnd_graph_dims', handle, dims)
         self.max_var_degree, self.max_chk_degree = int(dims[4]), int(dims[5])
         self._tiled_cache = {}
+        from .library import register_graph
+        self.gid = register_graph(self)      # id the gnnd:: torch ops take
 
     @property
     def handle(self):

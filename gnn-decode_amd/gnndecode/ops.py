@@ -80,30 +80,28 @@ def _propagate_bwd(variant, flow, aggr, edge_index, msg, extra, grad_out, dim_si
     return gmsg
 
 
-class _PropagateFn(torch.autograd.Function):
-    """propagate with a HIP backward w.r.t. the per-edge message (extra is data)."""
+def _propagate_impl(variant, flow, aggr, edge_index, msg, extra, dim_size, graph, chk_shift):
+    """gnnd::propagate implementation (gnndecode.library): tiled kernel when `graph` matches
+    the batched edge_index, else the generic kernels."""
+    b = _tiled_batch(graph, edge_index, msg.size(0), dim_size, extra, aggr, chk_shift)
+    return _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size,
+                          (graph, b) if b is not None else None)
 
-    @staticmethod
-    def forward(ctx, msg, variant, flow, aggr, edge_index, extra, dim_size, B):
-        ctx.save_for_backward(msg, edge_index, extra)
-        ctx.args = (variant, flow, aggr, dim_size, B)
-        return _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B)
 
-    @staticmethod
-    def backward(ctx, grad_out):
-        msg, edge_index, extra = ctx.saved_tensors
-        variant, flow, aggr, dim_size, B = ctx.args
-        gmsg = _propagate_bwd(variant, flow, aggr, edge_index, msg, extra, grad_out, dim_size, B)
-        return gmsg, None, None, None, None, None, None, None
+def _propagate_bwd_impl(variant, flow, aggr, edge_index, msg, extra, grad_out, dim_size, graph,
+                        chk_shift):
+    b = _tiled_batch(graph, edge_index, msg.size(0), dim_size, extra, aggr, chk_shift)
+    return _propagate_bwd(variant, flow, aggr, edge_index, msg, extra, grad_out, dim_size,
+                          (graph, b) if b is not None else None)
 
 
 def propagate(variant, flow, aggr, edge_index, msg, extra, dim_size, graph=None, chk_shift=None):
-    """One reference `propagate` body on the device.
+    """One reference `propagate` body on the device (torch op gnnd::propagate).
 
     msg [nE, 1] per-edge message, extra [dim_size, 1] node tensor (or None for CGNNI's
     `post=None`), edge_index int64 [2, nE].  Uses the tiled LDS kernel when `graph` matches
     the batched edge_index, otherwise the generic (atomic) kernels.  Differentiable w.r.t.
-    `msg` (aggr 'add', non-BP bodies) through HIP backward kernels.
+    `msg` (aggr 'add') through HIP backward kernels (gnnd::propagate_bwd).
     Returns [nE, F] with F = propagate_width(variant, flow).
     """
     _require_gpu(edge_index, msg, extra)
@@ -122,13 +120,12 @@ def propagate(variant, flow, aggr, edge_index, msg, extra, dim_size, graph=None,
         raise ValueError('edge_index and message disagree on the number of edges')
     if extra is None and variant != 'cgnni':
         raise ValueError(f'{variant}: propagate needs `extra`')
-    b = _tiled_batch(graph, edge_index, nE, dim_size, extra, aggr, chk_shift)
-    B = (graph, b) if b is not None else None
-    if msg.requires_grad and torch.is_grad_enabled():
-        if aggr != 'add':
-            raise NotImplementedError(f'no backward for aggr={aggr!r}')
-        return _PropagateFn.apply(msg, variant, flow, aggr, edge_index, extra, dim_size, B)
-    return _propagate_fwd(variant, flow, aggr, edge_index, msg, extra, dim_size, B)
+    if msg.requires_grad and torch.is_grad_enabled() and aggr != 'add':
+        raise NotImplementedError(f'no backward for aggr={aggr!r}')
+    from . import library  # noqa: F401  (registers the gnnd:: ops)
+    return torch.ops.gnnd.propagate(variant, flow, aggr, edge_index, msg, extra, int(dim_size),
+                                    graph.gid if graph is not None else -1,
+                                    -1 if chk_shift is None else int(chk_shift))
 
 
 def weights_count(model, graph=None, iters=None):
@@ -183,13 +180,20 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     if prepared_weights is not None and prepared_weights.dtype != wdt:
         raise TypeError(f'{x.dtype} inputs need {wdt} prepared weights')
     rows = decode_out_rows(graph, model, B)
+    from . import library  # noqa: F401  (registers the gnnd:: ops)
     if out is None:
-        out = torch.empty(rows, 1, dtype=x.dtype, device=x.device)
-    elif out.numel() != rows or not out.is_contiguous():
-        raise ValueError(f'out must be a contiguous tensor of {rows} values')
-    _lib.call('gnnd_decode', graph.handle, _lib.VARIANT[model], dtype_code(x.dtype),
-              _ptr(prepared_weights), _ptr(x), _ptr(out), B, int(iters), current_stream(x.device))
+        return torch.ops.gnnd.decode(graph.gid, model, x, int(iters), prepared_weights)
+    if out.numel() != rows or not out.is_contiguous() or out.dtype != x.dtype:
+        raise ValueError(f'out must be a contiguous {x.dtype} tensor of {rows} values')
+    torch.ops.gnnd.decode_out(graph.gid, model, x, int(iters), prepared_weights, out)
     return out
+
+
+def _decode_impl(graph, model, x, iters, prepared_weights, out):
+    """gnnd::decode / gnnd::decode_out implementation (gnndecode.library)."""
+    _lib.call('gnnd_decode', graph.handle, _lib.VARIANT[model], dtype_code(x.dtype),
+              _ptr(prepared_weights), _ptr(x), _ptr(out), x.numel() // graph.N, int(iters),
+              current_stream(x.device))
 
 
 def decode_plan(graph, model, dtype):

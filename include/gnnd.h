@@ -85,6 +85,11 @@ typedef struct gnnd_graph gnnd_graph;   /* opaque; device-resident single-codewo
 int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
                       int32_t num_var, int32_t num_chk, gnnd_graph** out);
 int gnnd_graph_destroy(gnnd_graph* g);
+/* Host-only: build every table gnnd_graph_create would upload and check its structural
+ * invariants (slot plans, padded / x-augmented message layouts); no device needed.
+ * h_report4 = {slot plans checked, layouts checked, edges, invariant failures}.          */
+int gnnd_graph_validate_host(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
+                             int32_t num_var, int32_t num_chk, int32_t* h_report4);
 /* dims[0..5] = V, C, E, N, max variable degree, max check degree */
 int gnnd_graph_dims(const gnnd_graph* g, int32_t* h_dims6);
 
