@@ -10,6 +10,7 @@ from .nn import MessagePassing, ClassicalMessagePassing, message_passing_class
 from .models import (DecoderV24, QGNNI, QuantumBP, CGNNI, ClassicalBP, NeuralBP, DecoderV10,
                      DecoderV30, MODELS, DEFAULT_ITERS, init_weights)
 from . import ops
+from . import library   # registers the gnnd:: torch ops
 
 __all__ = ['TannerGraph', 'MessagePassing', 'ClassicalMessagePassing', 'message_passing_class',
            'DecoderV24', 'QGNNI', 'QuantumBP', 'CGNNI', 'ClassicalBP', 'NeuralBP', 'DecoderV10',

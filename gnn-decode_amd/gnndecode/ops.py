@@ -122,10 +122,36 @@ def propagate(variant, flow, aggr, edge_index, msg, extra, dim_size, graph=None,
         raise ValueError(f'{variant}: propagate needs `extra`')
     if msg.requires_grad and torch.is_grad_enabled() and aggr != 'add':
         raise NotImplementedError(f'no backward for aggr={aggr!r}')
-    from . import library  # noqa: F401  (registers the gnnd:: ops)
-    return torch.ops.gnnd.propagate(variant, flow, aggr, edge_index, msg, extra, int(dim_size),
-                                    graph.gid if graph is not None else -1,
-                                    -1 if chk_shift is None else int(chk_shift))
+    if torch.compiler.is_compiling():
+        # traced (torch.compile / FX): the registered op gnnd::propagate (gnndecode.library)
+        return torch.ops.gnnd.propagate(variant, flow, aggr, edge_index, msg, extra,
+                                        int(dim_size), graph.gid if graph is not None else -1,
+                                        -1 if chk_shift is None else int(chk_shift))
+    # eager: the same implementation without the dispatcher round trip
+    if msg.requires_grad and torch.is_grad_enabled():
+        return _PropagateFn.apply(msg, variant, flow, aggr, edge_index, extra, int(dim_size),
+                                  graph, chk_shift)
+    return _propagate_impl(variant, flow, aggr, edge_index, msg, extra, dim_size, graph, chk_shift)
+
+
+class _PropagateFn(torch.autograd.Function):
+    """Eager autograd of propagate (the traced path uses gnnd::propagate's registered
+    autograd): HIP backward w.r.t. the per-edge message, extra is data."""
+
+    @staticmethod
+    def forward(ctx, msg, variant, flow, aggr, edge_index, extra, dim_size, graph, chk_shift):
+        ctx.save_for_backward(msg, edge_index, extra)
+        ctx.args = (variant, flow, aggr, dim_size, graph, chk_shift)
+        return _propagate_impl(variant, flow, aggr, edge_index, msg, extra, dim_size, graph,
+                               chk_shift)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        msg, edge_index, extra = ctx.saved_tensors
+        variant, flow, aggr, dim_size, graph, chk_shift = ctx.args
+        gmsg = _propagate_bwd_impl(variant, flow, aggr, edge_index, msg, extra,
+                                   grad_out.contiguous(), dim_size, graph, chk_shift)
+        return gmsg, None, None, None, None, None, None, None, None
 
 
 def weights_count(model, graph=None, iters=None):
@@ -167,7 +193,13 @@ def decode_out_rows(graph, model, B):
 
 def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None):
     """Fused T-iteration decode: x [B*N(,1)] -> P(bit=1) [B*V, 1] (v30: [2*B*N, 1], the
-    two readout tensors of quantum/decoder_v3_0.py:287-288 stacked)."""
+    two readout tensors of quantum/decoder_v3_0.py:287-288 stacked).  Traced code
+    (torch.compile / FX) gets the registered ops gnnd::decode / gnnd::decode_out."""
+    if torch.compiler.is_compiling():
+        if out is None:
+            return torch.ops.gnnd.decode(graph.gid, model, x, int(iters), prepared_weights)
+        torch.ops.gnnd.decode_out(graph.gid, model, x, int(iters), prepared_weights, out)
+        return out
     _require_gpu(x, prepared_weights)
     x = x.contiguous()
     if x.numel() % graph.N:
@@ -180,12 +212,11 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     if prepared_weights is not None and prepared_weights.dtype != wdt:
         raise TypeError(f'{x.dtype} inputs need {wdt} prepared weights')
     rows = decode_out_rows(graph, model, B)
-    from . import library  # noqa: F401  (registers the gnnd:: ops)
     if out is None:
-        return torch.ops.gnnd.decode(graph.gid, model, x, int(iters), prepared_weights)
-    if out.numel() != rows or not out.is_contiguous() or out.dtype != x.dtype:
+        out = torch.empty(rows, 1, dtype=x.dtype, device=x.device)
+    elif out.numel() != rows or not out.is_contiguous() or out.dtype != x.dtype:
         raise ValueError(f'out must be a contiguous {x.dtype} tensor of {rows} values')
-    torch.ops.gnnd.decode_out(graph.gid, model, x, int(iters), prepared_weights, out)
+    _decode_impl(graph, model, x, iters, prepared_weights, out)
     return out
 
 
