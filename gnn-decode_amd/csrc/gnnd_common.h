@@ -8,6 +8,48 @@
 #define GNND_BLOCK 256
 
 // ---------------------------------------------------------------------------------------
+// debug build (make debug -> gnndecode/libgnnd_debug.so, -DGNND_DEBUG): the kernels check
+// the table-derived indices they otherwise trust (LDS positions, variable ids, slots) and
+// record a violation as a bit in a per-translation-unit device word (a vector atomic, no
+// trap), clamping the index so the launch still completes; gnnd_debug_flags() collects and
+// clears the words.  Release builds compile the checks away.
+// ---------------------------------------------------------------------------------------
+enum GnndDebugBit {
+    GNND_DBG_LDS_POS = 0,      // message position outside the codeword's LDS run
+    GNND_DBG_VAR = 1,          // variable id >= V
+    GNND_DBG_SLOT = 2,         // slot / edge index out of range
+    GNND_DBG_NODE = 3,         // node index outside the aggregation side
+    GNND_DBG_GRID = 4,         // grid / tile bookkeeping (codeword index, p-grid index)
+};
+#ifdef GNND_DEBUG
+static __device__ unsigned int g_gnnd_debug_word;
+__device__ __forceinline__ int gnnd_dcheck_idx(int i, int n, int bit) {
+    if (i < 0 || i >= n) {
+        atomicOr(&g_gnnd_debug_word, 1u << bit);
+        return i < 0 ? 0 : n - 1;
+    }
+    return i;
+}
+#define GNND_DIDX(i, n, bit) gnnd_dcheck_idx((i), (n), (bit))
+#define GNND_DCHECK(cond, bit) \
+    do { if (!(cond)) atomicOr(&g_gnnd_debug_word, 1u << (bit)); } while (0)
+// per-TU host getter: returns and clears this translation unit's debug word
+#define GNND_DEBUG_TU(name)                                                            \
+    extern "C" unsigned gnnd_debug_take_##name(void) {                                \
+        unsigned v = 0;                                                                \
+        (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_gnnd_debug_word), sizeof(v));       \
+        const unsigned z = 0;                                                          \
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gnnd_debug_word), &z, sizeof(z));         \
+        return v;                                                                      \
+    }
+#else
+#define GNND_DIDX(i, n, bit) (i)
+#define GNND_DCHECK(cond, bit) do { } while (0)
+#define GNND_DEBUG_TU(name) \
+    extern "C" unsigned gnnd_debug_take_##name(void) { return 0; }
+#endif
+
+// ---------------------------------------------------------------------------------------
 // host-side graph (owned by libgnnd, device-resident tables built once per H)
 // ---------------------------------------------------------------------------------------
 struct GraphView {            // passed by value to kernels

@@ -2,6 +2,8 @@
 // per model in gnnd_decode_<model>.hip) and the weight preparation kernel.
 #include "gnnd_decode_impl.h"
 
+GNND_DEBUG_TU(decode)
+
 namespace {
 
 // ---------------------------------------------------------------------------------------
@@ -118,4 +120,33 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
     if (!d_x || !d_out || ((nw > 0 || nw == -2) && !d_w)) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
     return dispatch_decode(g, model, dtype, d_w, d_x, d_out, batch, iters, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// debug build: collect every translation unit's check word (gnnd_common.h GNND_DEBUG_TU)
+// ---------------------------------------------------------------------------------------
+#define GNND_TU_LIST(X) X(graph) X(propagate) X(decode) X(decode_v24) X(decode_qgnni) \
+    X(decode_qbp) X(decode_cgnni) X(decode_cbp) X(decode_nbp) X(decode_v10) X(decode_v30) \
+    X(train) X(sample)
+#define GNND_DECL_TU(n) extern "C" unsigned gnnd_debug_take_##n(void);
+GNND_TU_LIST(GNND_DECL_TU)
+
+extern "C" int gnnd_debug_enabled(void) {
+#ifdef GNND_DEBUG
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+// OR of every translation unit's debug word (GnndDebugBit bits), cleared; synchronises the
+// device first so pending kernels have recorded their checks
+extern "C" int gnnd_debug_flags(uint32_t* h_flags) {
+    if (!h_flags) return GNND_ERR_INVALID_ARG;
+    GNND_HIP_CHECK(hipDeviceSynchronize());
+    unsigned v = 0;
+#define GNND_TAKE_TU(n) v |= gnnd_debug_take_##n();
+    GNND_TU_LIST(GNND_TAKE_TU)
+    *h_flags = v;
+    return GNND_OK;
 }

@@ -426,13 +426,13 @@ template <typename T> struct alignas(2 * sizeof(T)) SumX {
 // indices and the messages are fetched eight at a time (independent LDS reads in flight,
 // clamped addresses, masked adds) instead of one dependent read pair per edge.
 template <typename T>
-__device__ __forceinline__ T var_sum(const T* mb, const int* vslot, int k0, int ke) {
+__device__ __forceinline__ T var_sum(const T* mb, const int* vslot, int k0, int ke, int nslot = 1 << 30) {
     T s = T(0);
     for (int k = k0; k < ke; k += 8) {
         int idx[8];
         T val[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) idx[j] = vslot[min(k + j, ke - 1)];
+        for (int j = 0; j < 8; ++j) idx[j] = GNND_DIDX(vslot[min(k + j, ke - 1)], nslot, GNND_DBG_SLOT);
 #pragma unroll
         for (int j = 0; j < 8; ++j) val[j] = mb[idx[j]];
 #pragma unroll
@@ -766,7 +766,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     const uint32_t sv = sl[r];
                     const bool valid = (int)(sv >> 16) != E;
                     mv[r] = mb[r];
-                    const SumX<T> p = sxb[sv & 0xffffu];      // padding reads variable 0
+                    const SumX<T> p = sxb[GNND_DIDX((int)(sv & 0xffffu), V, GNND_DBG_VAR)];  // padding: variable 0
                     T cc;
                     T t = M::pre(p.s - mv[r], p.x, wv, cc, s_tab);
                     tv[r] = valid ? t : T(0);
@@ -988,8 +988,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         for (int i = tid; i < nb * V; i += GNND_BLOCK) {
             const int b = fdiv(i, dV), j = i - b * V;
             const uint2 o = s_vord[j];
-            const int v = (int)(o.x & 0xffffu);
-            s_m[b * E1 + (int)o.y + (int)(o.x >> 16) - 1] = s_t[b * V + v];
+            const int v = GNND_DIDX((int)(o.x & 0xffffu), V, GNND_DBG_VAR);
+            s_m[b * E1 + GNND_DIDX((int)o.y + (int)(o.x >> 16) - 1, E1, GNND_DBG_LDS_POS)] = s_t[b * V + v];
         }
         __syncthreads();
     }
@@ -1150,8 +1150,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             auto load_pair = [&](int j, PX (&px)[R]) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const int ia = cb[2 * j] * V + (int)(ve[2 * j][r] & 0xffffu);
-                    const int ib = cb[2 * j + 1] * V + (int)(ve[2 * j + 1][r] & 0xffffu);
+                    const int ia = cb[2 * j] * V + GNND_DIDX((int)(ve[2 * j][r] & 0xffffu), V, GNND_DBG_VAR);
+                    const int ib = cb[2 * j + 1] * V + GNND_DIDX((int)(ve[2 * j + 1][r] & 0xffffu), V, GNND_DBG_VAR);
                     if constexpr (kTX) {
                         px[r] = f32x2{s_t[ia], s_t[ib]};
                     } else {
@@ -1208,8 +1208,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     m2[j][r] = post2(Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
-                    mba[ve[qa][r] >> 16] = m2[j][r].x * wnext(ve[qa][r]);
-                    mbb[ve[qb][r] >> 16] = m2[j][r].y * wnext(ve[qb][r]);
+                    mba[GNND_DIDX((int)(ve[qa][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].x * wnext(ve[qa][r]);
+                    mbb[GNND_DIDX((int)(ve[qb][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].y * wnext(ve[qb][r]);
                 }
             };
             // one item with its slots in pairs (the same per-edge arithmetic as pair_step:
@@ -1238,8 +1238,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
                     msp[i] = post2(f32x2{Sc, Sc} - tv[i], f32x2{Sc2, Sc2} - cv[i],
                                   f32x2{(float)sc[q], (float)sc[q]}, msp[i]);
-                    mb[ve[q][r0] >> 16] = msp[i].x * wnext(ve[q][r0]);
-                    if (r1 != r0) mb[ve[q][r1] >> 16] = msp[i].y * wnext(ve[q][r1]);
+                    mb[GNND_DIDX((int)(ve[q][r0] >> 16), E1, GNND_DBG_LDS_POS)] = msp[i].x * wnext(ve[q][r0]);
+                    if (r1 != r0) mb[GNND_DIDX((int)(ve[q][r1] >> 16), E1, GNND_DBG_LDS_POS)] = msp[i].y * wnext(ve[q][r1]);
                 }
             };
             // waves whose last work item is idle (tile rounds not filled: LDPC 1 296 items
@@ -1289,6 +1289,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         for (int q = 0; q < QMAX; ++q) {
             T tv[R], cf[R];
             T tsum = T(0), csum = T(0);
+            GNND_DCHECK(cb[q] < CW, GNND_DBG_GRID);
             const SumX<T>* sxb = s_sx + cb[q] * V;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -1394,6 +1395,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     const uint2 o = s_vord[i];
                     const int dp = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));
                     const int v = (int)(o.x & 0xffffu);
+                    GNND_DCHECK(v < V && (int)o.y + dp <= E1, GNND_DBG_LDS_POS);
                     var_out(vb, vsbase, v, var_sum_uniform(s_m + vmbase + (int)o.y, dp));
                 }
         } else if (vfixed) {

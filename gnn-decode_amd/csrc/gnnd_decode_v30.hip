@@ -118,7 +118,7 @@ decode_v30_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
             for (int r = 0; r < R; ++r) {
                 const uint32_t sv = sl[r];
                 const bool valid = (int)(sv >> 16) != E;
-                const SumX<T> p = sxb[sv & 0xffffu];    // padding slots read variable 0
+                const SumX<T> p = sxb[GNND_DIDX((int)(sv & 0xffffu), V, GNND_DBG_VAR)];   // padding: variable 0
                 const T me = mb[r];
                 m1[r] = v30_gru(w_rnn1, me, v30_mlp(w_mlp1, p.s - me, p.x));
                 tsum += valid ? m1[r] : T(0);
@@ -137,7 +137,7 @@ decode_v30_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
         if (last) break;
         for (int f = tid; f < nV; f += GNND_BLOCK) {
             const int b = fdiv(f, dV), v = f - b * V;
-            s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
+            s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1], nslot);
         }
         __syncthreads();
     }
@@ -191,6 +191,8 @@ int launch_v30_r(const gnnd_graph* gr, const void* w, const void* x, void* out, 
 }
 
 }  // namespace
+
+GNND_DEBUG_TU(decode_v30)
 
 int gnnd_launch_v30(const gnnd_graph* g, int dtype, const void* w, const void* x, void* out,
                     int64_t B, int iters, hipStream_t st) {

@@ -19,6 +19,9 @@ int set_hip_error(hipError_t e) {
 }
 
 extern "C" int gnnd_last_hip_error(void) { return g_last_hip_error; }
+
+GNND_DEBUG_TU(graph)
+
 extern "C" int gnnd_version(void) { return GNND_VERSION; }
 
 extern "C" const char* gnnd_status_string(int s) {

@@ -160,7 +160,7 @@ propagate_tiled_kernel(GraphView g, const T* __restrict__ msg, const T* __restri
     for (int f = tid; f < nE; f += GNND_BLOCK) {
         int b = fdiv(f, dE), e = f - b * E;
         uint32_t vc = s_evc[e];
-        int j = VARSIDE ? (int)(vc & 0xffffu) : (int)(vc >> 16);
+        int j = GNND_DIDX(VARSIDE ? (int)(vc & 0xffffu) : (int)(vc >> 16), NJ, GNND_DBG_NODE);
         T val = s_agg[b * NJ + j] - s_src[f];
         T val2 = T(0);
         if constexpr (BP) val2 = s_agg2[b * NJ + j] - s_src2[f];
@@ -794,6 +794,8 @@ bool bwd_needs_extra(int variant, int flow) {
 }
 
 }  // namespace
+
+GNND_DEBUG_TU(propagate)
 
 extern "C" int gnnd_propagate_width(int variant, int flow) {
     if (variant < GNND_V24 || variant > GNND_V30) return -1;

@@ -96,7 +96,7 @@ sample_toric_kernel(GraphView g, ToricParams P, T* __restrict__ x, T* __restrict
     const int VQ = (V + 3) >> 2;
     for (int i = tid; i < nb * VQ; i += GNND_BLOCK) {
         const int b = i / VQ, q = i - b * VQ;
-        const int pi = s_p[b];
+        const int pi = GNND_DIDX(s_p[b], P.np, GNND_DBG_GRID);
         const U4 r = draw((uint32_t)q, P.offset + b0 + b, kStreamE, P.k0, P.k1);
         const uint32_t u[4] = {r.x, r.y, r.z, r.w};
         const uint32_t thr = P.thr[pi];
@@ -117,7 +117,7 @@ sample_toric_kernel(GraphView g, ToricParams P, T* __restrict__ x, T* __restrict
         const int b = i / C, c = i - b * C;
         uint32_t par = 0;
         for (int k = g.chk_ptr[c], ke = g.chk_ptr[c + 1]; k < ke; ++k)
-            par ^= s_e[b * V + (int)(g.edge_vc[g.chk_edge[k]] & 0xffffu)];
+            par ^= s_e[b * V + GNND_DIDX((int)(g.edge_vc[g.chk_edge[k]] & 0xffffu), V, GNND_DBG_VAR)];
         x[(b0 + b) * N + V + c] = par ? T(-1) : T(1);
     }
 }
@@ -194,6 +194,8 @@ int tile_codewords(int N) {
 }
 
 }  // namespace
+
+GNND_DEBUG_TU(sample)
 
 // host mirror of the generator (known-answer tests, tests/test_sample_cpu.py)
 extern "C" void gnnd_philox4x32_10(const uint32_t* ctr4, const uint32_t* key2, uint32_t* out4) {

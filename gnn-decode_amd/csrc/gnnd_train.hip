@@ -25,6 +25,8 @@
 // torch's autograd rules are followed: Softplus(beta 1, threshold 20) backward
 // g z / (z + 1), z = e^h (g above the threshold), tanh backward g (1 - t^2), division by 2.
 #include "gnnd_decode_impl.h"
+
+GNND_DEBUG_TU(train)
 #include <type_traits>
 
 namespace {

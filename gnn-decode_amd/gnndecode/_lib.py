@@ -63,6 +63,8 @@ SIGNATURES = {
                                 ctypes.c_uint64, _i64, _vp, _vp, _i64, _vp]),
     'gnnd_philox4x32_10': (None, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                   ctypes.POINTER(ctypes.c_uint32)]),
+    'gnnd_debug_enabled': (_int, []),
+    'gnnd_debug_flags': (_int, [ctypes.POINTER(ctypes.c_uint32)]),
     'gnnd_status_string': (ctypes.c_char_p, [_int]),
     'gnnd_last_hip_error': (_int, []),
     'gnnd_version': (_int, []),

@@ -264,6 +264,14 @@ int gnnd_sample_awgn(const gnnd_graph* g, int dtype, const double* h_snr_db, int
                      int64_t offset, void* d_x, void* d_y, int64_t batch, void* stream);
 void gnnd_philox4x32_10(const uint32_t* h_ctr4, const uint32_t* h_key2, uint32_t* h_out4);
 
+/* ---- debug build (make debug -> libgnnd_debug.so, -DGNND_DEBUG) ----------------------------
+ * The kernels check the table-derived indices they otherwise trust and record violations
+ * as bits (0 LDS position, 1 variable id, 2 slot, 3 node, 4 grid) instead of faulting;
+ * gnnd_debug_flags synchronises the device and returns (and clears) their OR.  In release
+ * builds gnnd_debug_enabled() is 0 and the flags are always 0.                             */
+int gnnd_debug_enabled(void);
+int gnnd_debug_flags(uint32_t* h_flags);
+
 /* ---- misc ----------------------------------------------------------------------------- */
 const char* gnnd_status_string(int status);
 int gnnd_last_hip_error(void);          /* hipError_t of the last GNND_ERR_HIP, per thread */
