@@ -45,6 +45,8 @@ def flops_per_codeword(model, g, T):
         return 17 * E * T + 4 * V, 6 * E * T
     if model == 'nbp':
         return 22 * E * T + 4 * E + 4 * V, 6 * E * T
+    if model == 'v22':           # nbp + a readout (2 E products/sums + sigmoid) every iteration
+        return 26 * E * T + 4 * E * T + 4 * V * T, 6 * E * T + V * T
     if model == 'v10':
         return 20 * E * T + 4 * V, 6 * E * T
     if model == 'v24':
@@ -173,12 +175,14 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds, out_bf1
     cond = model == 'cbp' and x_dev.dtype == torch.float32
     # the quantum scripts compute in fp64: their oracle (the reference's arithmetic) runs in
     # fp64 whatever the GPU dtype
-    quantum = model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10', 'v30')
+    quantum = model in ('qbp', 'qgnni', 'v24', 'nbp', 'v10', 'v30', 'v22')
 
     def oracle_vars(xs_):
         r = gnn_oracle.decode(model, H, xs_, T, w)
         if model == 'v30':                 # first readout tensor, variable rows
             r = r[0].reshape(-1, g.N)[:, :g.V].reshape(-1, 1)
+        if model == 'v22':                 # the last layer's readout
+            r = r[-1]
         return r
     ref_dt = np.float64 if quantum else None
     t1 = seconds / 2                      # 1-thread leg, then the all-cores leg
@@ -469,7 +473,9 @@ def main():
         z = np.load(wfile)                       # plain arrays (allow_pickle off)
         model.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files})
     g = model.graph(dev)
-    state = model.state_dict()
+    state = dict(model.state_dict())
+    if a.model == 'v22':                         # the oracle takes the edge types with the weights
+        state['edge_types'] = model.types
     classical = a.model in ('cgnni', 'cbp')
     if classical:
         # uniform random codewords (the CGNNI decoder is not symmetric under codeword
@@ -481,7 +487,7 @@ def main():
     if io_dtype != dtype:
         x = x.to(io_dtype)                       # bf16 storage (outside the timed region)
     w = model.prepared_weights(dtype, dev)
-    out = torch.empty(gd.ops.decode_out_rows(g, a.model, a.batch), 1, dtype=io_dtype, device=dev)
+    out = torch.empty(gd.ops.decode_out_rows(g, a.model, a.batch, T), 1, dtype=io_dtype, device=dev)
 
     def step():
         gd.ops.decode(g, a.model, x, T, w, out=out)
@@ -521,6 +527,8 @@ def main():
         pred = out.float() if io_dtype == torch.bfloat16 else out
         if a.model == 'v30':                     # variable rows of the first readout tensor
             pred = out[:a.batch * g.N].view(a.batch, g.N)[:, :g.V].reshape(-1, 1).contiguous()
+        if a.model == 'v22':                     # the last layer's readout
+            pred = out[-a.batch * g.V:]
         counts = gd.ops.decision_errors(g, lg, pred, labels)
         if dist.is_initialized():
             dist.all_reduce(counts)
@@ -542,7 +550,7 @@ def main():
         peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
         trans_frac = 2 * trans * a.batch / kernel_s / TRANS_OPS_PER_S
         esz = {torch.float32: 4, torch.float64: 8, torch.bfloat16: 2}[io_dtype]
-        io_bytes = (g.N + gd.ops.decode_out_rows(g, a.model, 1)) * esz * a.batch
+        io_bytes = (g.N + gd.ops.decode_out_rows(g, a.model, 1, T)) * esz * a.batch
         plan = gd.ops.decode_plan(g, a.model, dtype)
         tag = f'{a.model}_{a.code}_B{a.batch}_T{T}_{a.dtype}'
         pmc = load_pmc(tag)

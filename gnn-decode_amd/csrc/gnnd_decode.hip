@@ -43,6 +43,7 @@ int dispatch_decode(const gnnd_graph* g, int model, int dtype, const void* w, co
         case GNND_NBP: return gnnd_launch_nbp(g, dtype, w, x, out, B, iters, st);
         case GNND_V10: return gnnd_launch_v10(g, dtype, w, x, out, B, iters, st);
         case GNND_V30: return gnnd_launch_v30(g, dtype, w, x, out, B, iters, st);
+        case GNND_V22: return gnnd_launch_v22(g, dtype, w, x, out, B, iters, st);
         default: return GNND_ERR_INVALID_ARG;
     }
 }
@@ -68,7 +69,7 @@ extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void*
                                     void* stream) {
     int n = weights_count(model);
     if (n == -1 || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
-    if (n < 0) return GNND_ERR_UNSUPPORTED;     // NBP/V10: decode takes the packed layout as is
+    if (n < 0) return GNND_ERR_UNSUPPORTED;     // NBP/V10/V22: decode takes the packed layout as is
     if (n == 0) return GNND_OK;
     if (!d_w || !d_prepared || d_w == d_prepared) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
@@ -116,7 +117,8 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
     int nw = weights_count(model);
     if (!g || nw == -1 || batch < 0 || iters < 0) return GNND_ERR_INVALID_ARG;
     if (dtype != GNND_F32 && dtype != GNND_F64 && dtype != GNND_BF16) return GNND_ERR_INVALID_ARG;
-    if (batch == 0) return GNND_OK;
+    // nothing to write: an empty batch, or decoder_v2_2's per-layer readout list at T = 0
+    if (batch == 0 || (model == GNND_V22 && iters == 0)) return GNND_OK;
     if (!d_x || !d_out || ((nw > 0 || nw == -2) && !d_w)) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
     return dispatch_decode(g, model, dtype, d_w, d_x, d_out, batch, iters, st);
@@ -127,7 +129,7 @@ extern "C" int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void
 // ---------------------------------------------------------------------------------------
 #define GNND_TU_LIST(X) X(graph) X(propagate) X(decode) X(decode_v24) X(decode_qgnni) \
     X(decode_qbp) X(decode_cgnni) X(decode_cbp) X(decode_nbp) X(decode_v10) X(decode_v30) \
-    X(train) X(sample)
+    X(decode_v22) X(train) X(sample)
 #define GNND_DECL_TU(n) extern "C" unsigned gnnd_debug_take_##n(void);
 GNND_TU_LIST(GNND_DECL_TU)
 

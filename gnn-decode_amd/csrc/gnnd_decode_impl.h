@@ -41,7 +41,7 @@ constexpr int kMlp10Msg = 0, kMlp10Out = 31;
 constexpr int kV30Count = 137;       // decoder_v3_0 packed weights (gnnd.h)
 
 template <int MODEL> struct ModelTraits {
-    static constexpr bool wbp = (MODEL == GNND_NBP || MODEL == GNND_V10);   // weighted BP
+    static constexpr bool wbp = (MODEL == GNND_NBP || MODEL == GNND_V10 || MODEL == GNND_V22);   // weighted BP
     static constexpr bool bp = (MODEL == GNND_QBP || MODEL == GNND_CBP || wbp);
 };
 
@@ -167,7 +167,7 @@ template <int MODEL, typename T> struct WbpW {
     __device__ __forceinline__ T out_w(int e) const { return w[(size_t)2 * T_ * E + e]; }          // NBP W
     __device__ __forceinline__ T out_p(int e) const { return w[(size_t)(2 * T_ + 1) * E + e]; }    // NBP W_p
     __device__ __forceinline__ T alpha() const {
-        return MODEL == GNND_NBP ? w[(size_t)2 * T_ * E + 2 * E] : w[(size_t)T_ * E];
+        return MODEL == GNND_V10 ? w[(size_t)T_ * E] : w[(size_t)2 * T_ * E + 2 * E];
     }
 };
 
@@ -930,7 +930,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     constexpr bool kBase2 = sizeof(T) == 4 && (MODEL == GNND_CGNNI || MODEL == GNND_QGNNI);
     // fp32 GNN and BP models run the check step on edge PAIRS (packed VALU, see below)
     constexpr bool kPairBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP ||
-                                                MODEL == GNND_NBP || MODEL == GNND_V10);
+                                                MODEL == GNND_NBP || MODEL == GNND_V10 ||
+                                                MODEL == GNND_V22);
     constexpr bool kPair = kBase2 || kPairBP;
     // T layout (paired GNN and plain-BP models): LDS keeps ONE value per variable,
     // T_v = S_v + x_v (base-2 scaled for the GNN models: messages m' = m log2 e, so
@@ -1091,7 +1092,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     const int ea = (int)(sa >> 16), eb = (int)(sb >> 16);
                     const int xa = ea < E ? ea : 0, xb = eb < E ? eb : 0;
                     f32x2 a;
-                    if constexpr (MODEL == GNND_NBP)
+                    if constexpr (MODEL == GNND_NBP || MODEL == GNND_V22)
                         a = f32x2{(pa.s - mprev.x * ww.msg(it, xa)) + pa.x * ww.prior(it, xa),
                                   (pb.s - mprev.y * ww.msg(it, xb)) + pb.x * ww.prior(it, xb)};
                     else
@@ -1301,7 +1302,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 else if constexpr (WBP) {
                     const int e = (int)(sv >> 16), ec = e < E ? e : 0;
                     T a;
-                    if constexpr (MODEL == GNND_NBP)
+                    if constexpr (MODEL == GNND_NBP || MODEL == GNND_V22)
                         a = (p.s - m[q][r] * ww.msg(it, ec)) + p.x * ww.prior(it, ec);
                     else
                         a = ((p.s - m[q][r]) + p.x) * ww.chk(it, ec);
@@ -1362,6 +1363,26 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             const uint2 o = s_vord[i];
             const int v = (int)(o.x & 0xffffu), dv = (int)(o.x >> 16);
             const T* mp = s_m + mbase + (int)o.y;
+            if constexpr (MODEL == GNND_V22) {
+                // decoder_v2_2.py:333-347: the check step publishes raw messages (identity
+                // layout: positions = edge ids); the variable step forms the next layer's
+                // S'_v = sum_e m_e W_{t+1}[e] (its v->c input, as in neural_BP) and the
+                // iteration's readout sigmoid(-(sum_e m_e W[e] + sum_e x_v W_pr[e])), every
+                // sum in edge (index_add) order
+                const int e0 = (int)o.y;
+                const T xv = s_sx[sbase + v].x;
+                T sn = T(0), so = T(0), s2 = T(0);
+                for (int k = 0; k < dv; ++k) {
+                    const T mk = mp[k];
+                    so += mk * ww.out_w(e0 + k);
+                    s2 += xv * ww.out_p(e0 + k);
+                    if (!last) sn += mk * ww.msg(it + 1, e0 + k);
+                }
+                out[(size_t)it * (size_t)B * V + (size_t)b0 * V + sbase + v] =
+                    io_st<TI>(sigmoid_ref(-(so + s2)));
+                if (!last) s_sx[sbase + v].s = sn;
+                return;
+            }
             T s = T(0);
             int k = 0;
             for (; k + 4 <= dv; k += 4) {
@@ -1413,7 +1434,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         }
         __syncthreads();
     }
-    if (iters == 0)
+    if (iters == 0 && MODEL != GNND_V22)        // (V22: zero iterations, empty readout list)
         for (int f = tid; f < nb * V; f += GNND_BLOCK) {
             const int b = fdiv(f, dV), v = f - b * V;
             if constexpr (MODEL == GNND_NBP) {
@@ -1432,13 +1453,13 @@ int weights_count(int model) {
         case GNND_CGNNI: case GNND_QGNNI: return 62;
         case GNND_V24: return 1283;
         case GNND_CBP: case GNND_QBP: return 0;
-        case GNND_NBP: case GNND_V10: return -2;
+        case GNND_NBP: case GNND_V10: case GNND_V22: return -2;
         case GNND_V30: return kV30Count;
         default: return -1;
     }
 }
 int64_t decode_weights_count(int model, int E, int iters) {
-    if (model == GNND_NBP) return 2 * (int64_t)E * iters + 2 * (int64_t)E + 1;
+    if (model == GNND_NBP || model == GNND_V22) return 2 * (int64_t)E * iters + 2 * (int64_t)E + 1;
     if (model == GNND_V10) return (int64_t)E * iters + 1;
     return weights_count(model);
 }
@@ -1510,7 +1531,8 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     // Measured faster for the quantum models on the toric code (Q/BP +24 %, QGNNI +35 %,
     // decoder_v1_0 +11 %) and slower for the classical ones on BCH (-8..-10 %, whose
     // reference dtype is fp32 anyway): quantum models only.
-    const bool quantum = model == GNND_QBP || model == GNND_QGNNI || model == GNND_NBP || model == GNND_V10;
+    const bool quantum = model == GNND_QBP || model == GNND_QGNNI || model == GNND_NBP ||
+                         model == GNND_V10 || model == GNND_V22;
     const bool f64res = dtype == GNND_F64 && quantum && !f64_resident_disabled();
     if (light && (dtype == GNND_F32 || f64res) && gr->rview.G <= 16 && !resident_disabled()) {
         const GraphView& g = gr->rview;          // instantiated group sizes 1..16
@@ -1520,7 +1542,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         // consecutive var_ord entries per step, so the layout padded for that group size
         // makes its variable sums uniform (GraphView::vlay); weighted BP indexes per-edge
         // weights by edge id and keeps the identity layout
-        const bool wbp = model == GNND_NBP || model == GNND_V10;
+        const bool wbp = model == GNND_NBP || model == GNND_V10 || model == GNND_V22;
         // T-layout models (decode_resident_kernel kTX: the fp32 paired GNN / plain BP) run
         // on the x-augmented layouts (gnnd_graph::rlayx)
         const bool tx = dtype == GNND_F32 && !wbp;
@@ -1657,8 +1679,9 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
             return by_g(std::integral_constant<int, R>{});
         }
     }
-    if constexpr (!std::is_same_v<TI, T>) {
-        return GNND_ERR_UNSUPPORTED;      // bf16 I/O: register-resident plans only
+    if constexpr (!std::is_same_v<TI, T> || MODEL == GNND_V22) {
+        // bf16 I/O and decoder_v2_2's per-iteration readout: register-resident plans only
+        return GNND_ERR_UNSUPPORTED;
     } else {
         if constexpr (MODEL == GNND_V24)
             if (tape.ext) return go(decode_kernel<MODEL, T, R, true>);
@@ -1715,3 +1738,4 @@ int gnnd_launch_cbp(const gnnd_graph*, int, const void*, const void*, void*, int
 int gnnd_launch_nbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_v10(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_v30(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+int gnnd_launch_v22(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

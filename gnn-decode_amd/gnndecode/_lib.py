@@ -16,7 +16,7 @@ F32, F64, BF16 = 0, 1, 2
 SOURCE_TO_TARGET, TARGET_TO_SOURCE = 0, 1
 AGGR = {'add': 0, 'mean': 1, 'max': 2}
 FLOW = {'source_to_target': SOURCE_TO_TARGET, 'target_to_source': TARGET_TO_SOURCE}
-VARIANT = {'v24': 0, 'qgnni': 1, 'qbp': 2, 'cgnni': 3, 'cbp': 4, 'nbp': 5, 'v10': 6, 'v30': 7}
+VARIANT = {'v24': 0, 'qgnni': 1, 'qbp': 2, 'cgnni': 3, 'cbp': 4, 'nbp': 5, 'v10': 6, 'v30': 7, 'v22': 8}
 
 _c_i64p = ctypes.POINTER(ctypes.c_int64)
 _c_i32p = ctypes.POINTER(ctypes.c_int32)

@@ -125,6 +125,31 @@ def toric_code(L):
     return H.T.copy()
 
 
+def toric_edge_types(L):
+    """Edge type in [0, 8) of every edge of toric_code(L), in reference edge order (sorted
+    by (v, c): H.to_sparse()._indices()).  Restates the `H_prime` labels that
+    quantum/error_generate.py:92-124 writes beside H (0.2, 1, 2, 3 for a Z check's qubits
+    j, j+L, right, (j+2L) mod 2L^2; 4.2, 5, 6, 7 for an X check's (j-L) mod 2L^2, left, j,
+    j+L; `.long()` truncates to 0..7) — the one-hot edge features of
+    quantum/decoder_v2_2.py:226-250.  (The shipped generate_PCM returns a different
+    matrix, `H_one`, with labels up to 31, as its second value.)"""
+    n = 2 * L * L
+    g = L * L - 1
+    label = {}
+    for i in range(g):
+        r, col = divmod(i, L)
+        j = 2 * L * r + col
+        right = j + L + 1 if col != L - 1 else j + 1
+        left = j - 1 if col != 0 else j - 1 + L
+        for q, t in ((j, 0), (j + L, 1), (right, 2), ((j + 2 * L) % n, 3)):
+            label[(q, i)] = t
+        for q, t in (((j - L) % n, 4), (left, 5), (j, 6), (j + L, 7)):
+            label[(n + q, g + i)] = t
+    H = toric_code(L)
+    vs, cs = np.nonzero(H)                 # row-major: sorted by (v, c)
+    return np.array([label[(int(v), int(c))] for v, c in zip(vs, cs)], np.int64)
+
+
 # ---------------------------------------------------------------------------------------
 # 802.11n LDPC(648, 324), Z = 27 (SURVEY.md Appendix D; UNVERIFIED base matrix)
 # ---------------------------------------------------------------------------------------

@@ -48,9 +48,11 @@ def graph_of(gid):
     return g
 
 
-def _out_rows(gid, model, B):
+def _out_rows(gid, model, B, iters=1):
     V, C, N, E = _DIMS[gid]
-    return 2 * B * N if model == 'v30' else B * V
+    if model == 'v30':
+        return 2 * B * N
+    return iters * B * V if model == 'v22' else B * V
 
 
 # ---------------------------------------------------------------------------------------
@@ -112,7 +114,7 @@ torch.library.register_autograd('gnnd::propagate', _prop_backward, setup_context
 def decode(graph_id: int, model: str, x: Tensor, iters: int, weights: Optional[Tensor]) -> Tensor:
     from . import ops
     g = graph_of(graph_id)
-    out = torch.empty(ops.decode_out_rows(g, model, x.numel() // g.N), 1, dtype=x.dtype,
+    out = torch.empty(ops.decode_out_rows(g, model, x.numel() // g.N, iters), 1, dtype=x.dtype,
                       device=x.device)
     ops._decode_impl(g, model, x, iters, weights, out)
     return out
@@ -121,7 +123,7 @@ def decode(graph_id: int, model: str, x: Tensor, iters: int, weights: Optional[T
 @decode.register_fake
 def _decode_fake(graph_id, model, x, iters, weights):
     N = _DIMS[graph_id][2]
-    return x.new_empty(_out_rows(graph_id, model, x.numel() // N), 1)
+    return x.new_empty(_out_rows(graph_id, model, x.numel() // N, iters), 1)
 
 
 @torch.library.custom_op('gnnd::decode_out', mutates_args=('out',), device_types='cuda')

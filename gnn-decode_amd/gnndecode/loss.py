@@ -6,6 +6,8 @@
 * `ClassicalLoss` — classical/CGNNI.py:287-309: lambda * mean BCE + (1 - lambda) * mean
   |sin(pi/2 H^T p)| (train) or mean BCE (test), lambda = 0.8 (classical/CGNNI.py:206).
 * `V30Loss` — quantum/decoder_v3_0.py:293-335 (GRU decoder; the script's batching kept).
+* `PerLayerLoss` — quantum/decoder_v2_2.py:350-380: SyndromeLoss summed over the per-layer
+  readout list of DecoderV22 (train), or the last layer (test).
 * `toric_failures` — hard FER rule of quantum/neural_BP.py:338-348 (non-zero residual
   syndrome, or zero syndrome with a logical flip).
 
@@ -119,6 +121,24 @@ class V30Loss(torch.nn.Module):
         res_p = torch.abs(torch.sin(res_p * math.pi / 2))
         loss_b = -1 * (1 - syn).mul(torch.log(1 - res_p)) - syn.mul(torch.log(res_p))
         return torch.abs(torch.sin(loss_a * math.pi / 2)).sum() + loss_b.sum()
+
+
+class PerLayerLoss(torch.nn.Module):
+    """quantum/decoder_v2_2.py:350-380 (LossFunc of the edge-type decoder, whose GNNI returns
+    one readout per layer): train=True sums the syndrome + logical loss of SyndromeLoss over
+    EVERY layer's readout (in layer order), train=False takes the last layer only."""
+
+    def __init__(self, H, logical, fused=True):
+        super().__init__()
+        self.inner = SyndromeLoss(H, logical, fused=fused)
+
+    def forward(self, preds, y, train=True):
+        preds = preds if train else preds[-1:]
+        loss = None
+        for p in preds:
+            term = self.inner(p, y)
+            loss = term if loss is None else loss + term
+        return loss
 
 
 def toric_failures(H, logical, y, pred, graph=None):

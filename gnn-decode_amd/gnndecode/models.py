@@ -12,6 +12,8 @@ Each class mirrors one reference script's `GNNI` (paths relative to
   DecoderV10   quantum/decoder_v1_0.py:236-313    keys layers.{i}.W, alpha
   DecoderV30   quantum/decoder_v3_0.py:199-290    keys ggc{1,2}.mlp{1,2}.*, ggc{1,2}.rnn{1,2}.*,
                                                   mlp.*  (GRU edge states, two-output readout)
+  DecoderV22   quantum/decoder_v2_2.py:272-347    keys layers.{i}.W, layers.{i}.W_p, W, W_pr,
+                                                  weight  (edge-type weights, per-layer readout)
 
 Differences from the reference, all at the call boundary: the parity-check matrix is
 passed to the constructor (`GNNI(Nc, H)`) instead of being read from module globals
@@ -195,6 +197,32 @@ class GraphConvNBP(_MP['nbp']):
         if self.flow == 'source_to_target':
             B = aggr_out.size(0) // self.W_p.size(0)
             return aggr_out[:, 0:1] + aggr_out[:, 1:2].mul(self.W_p.repeat(B, 1))
+        return aggr_out
+
+
+class GraphConvV22(_MP['nbp']):
+    """quantum/decoder_v2_2.py:272-296: neural_BP's layer (the script's propagate body is
+    neural_BP.py's) with W, W_p shared by the 8 edge types: `m.mul(feat_onehot) @ W` is
+    m_e W[type(e)] exactly (one non-zero product per row), so the layer gathers W[type]."""
+
+    def __init__(self, flow, types, aggr='add', bias=True):
+        super().__init__(aggr, flow)
+        self.W = torch.nn.Parameter(torch.ones(8, 1, dtype=torch.float64))
+        self.W_p = torch.nn.Parameter(torch.ones(8, 1, dtype=torch.float64))
+        self.register_buffer('types', types, persistent=False)
+
+    def forward(self, m, edge_index, x, prev=None, size=None):
+        x = x if x.dim() == 2 else x.unsqueeze(-1)
+        if self.flow == 'source_to_target':
+            w = self.W[self.types.to(m.device)]
+            m = m.mul(w.repeat(m.size(0) // w.size(0), 1))
+        size = size or (x.size(0), x.size(0))
+        return self.propagate(edge_index=edge_index, size=size, x=m, extra=x)
+
+    def update(self, aggr_out):
+        if self.flow == 'source_to_target':
+            wp = self.W_p[self.types.to(aggr_out.device)]
+            return aggr_out[:, 0:1] + aggr_out[:, 1:2].mul(wp.repeat(aggr_out.size(0) // wp.size(0), 1))
         return aggr_out
 
 
@@ -607,7 +635,87 @@ class DecoderV30(_Decoder):
         return [torch.sigmoid(-res), torch.sigmoid(-res_p)]
 
 
+def _toric_types(H):
+    """Edge types of a toric H (codes.toric_edge_types), or None if H is not toric_code(L)."""
+    from . import codes
+    V, C = H.shape
+    L = int(round((V / 4) ** 0.5))
+    if L < 2 or 4 * L * L != V or 2 * L * L - 2 != C:
+        return None
+    if not torch.equal(H.to(torch.uint8), torch.as_tensor(codes.toric_code(L)).to(torch.uint8)):
+        return None
+    return torch.as_tensor(codes.toric_edge_types(L))
+
+
+class DecoderV22(_WeightedBP):
+    """quantum/decoder_v2_2.py:299-347 (Nc = 25, toric L = 6 in the script): neural BP with
+    the per-layer weights W, W_p, the readout W, W_pr shared by the 8 edge types (the script's
+    one-hot `feat_onehot` from H_prime; `edge_types` [E] in reference edge order, default
+    codes.toric_edge_types for a toric H) and residual m_p @ sigmoid(weight).  `forward`
+    returns the script's list of Nc per-layer readouts sigmoid(-(S_v(m_t W) + S_v(x W_pr))),
+    each [B*V, 1]; the fused decoder computes all of them in one launch."""
+    kind = 'v22'
+
+    def __init__(self, Nc, H, edge_types=None):
+        _Decoder.__init__(self, Nc, H)
+        self.E = int(self.H.sum())
+        types = _toric_types(self.H) if edge_types is None else torch.as_tensor(edge_types)
+        if types is None:
+            raise ValueError('DecoderV22 needs edge_types [E] for a non-toric H')
+        types = types.to(torch.long).reshape(-1)
+        if types.numel() != self.E or int(types.min()) < 0 or int(types.max()) > 7:
+            raise ValueError('edge_types must hold E values in [0, 8)')
+        layers = []
+        for _ in range(Nc):
+            layers.append(GraphConvV22('source_to_target', types))
+            layers.append(GraphConvV22('target_to_source', types))
+        self.layers = torch.nn.Sequential(*layers)
+        self.register_buffer('types', types, persistent=False)
+        self.W = torch.nn.Parameter(torch.ones(8, 1, dtype=torch.float64))
+        self.W_pr = torch.nn.Parameter(torch.ones(8, 1, dtype=torch.float64) * 0.5)
+        self.weight = torch.nn.Parameter(torch.full((1, 1), -4.0, dtype=torch.float64))
+
+    def packed_weights(self):
+        """gnnd.h V22 layout: the NBP per-edge tables with every type weight expanded."""
+        t = self.types.to(self.W.device)
+        per = [torch.cat([self.layers[2 * i].W[t].reshape(-1), self.layers[2 * i].W_p[t].reshape(-1)])
+               for i in range(self.Nc)]
+        return torch.cat(per + [self.W[t].reshape(-1), self.W_pr[t].reshape(-1),
+                                torch.sigmoid(self.weight).reshape(-1)])
+
+    def forward(self, data):
+        x, edge_index = data.x, data.edge_index
+        if x.dim() == 1:
+            x = x.unsqueeze(1)
+        if self.fused_ok(x, edge_index):
+            g = self.graph(x.device)
+            out = ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(x.dtype, x.device))
+            return list(out.chunk(self.Nc, 0)) if self.Nc else []
+        if not x.is_cuda:
+            raise RuntimeError('gnndecode runs on the GPU only (HIP/gfx950); move data to cuda')
+        self.graph(x.device)
+        return self.forward_layers(x, edge_index)
+
+    def forward_layers(self, x, ei):
+        B = x.size(0) // (self.rows + self.cols)
+        ei = self._shifted(ei)
+        t = self.types.to(x.device)
+        m = torch.zeros(ei.size(1), 1, dtype=x.dtype, device=x.device)
+        alpha = torch.sigmoid(self.weight).to(x.dtype)
+        results = []
+        for i in range(0, len(self.layers), 2):
+            m_p = m
+            m = self.layers[i](m, ei, x)
+            m = self.layers[i + 1](m, ei, x) + torch.matmul(m_p, alpha)
+            results.append(m)
+        prior = x[ei[0]].mul(self.W_pr[t].repeat(B, 1).to(x.dtype))
+        sp = self._var_rows(self._var_sum(prior, ei, x.size(0)), B)
+        w = self.W[t].repeat(B, 1).to(x.dtype)
+        return [torch.sigmoid(-(self._var_rows(self._var_sum(r.mul(w), ei, x.size(0)), B) + sp))
+                for r in results]
+
+
 MODELS = {'v24': DecoderV24, 'qgnni': QGNNI, 'qbp': QuantumBP, 'cgnni': CGNNI, 'cbp': ClassicalBP,
-          'nbp': NeuralBP, 'v10': DecoderV10, 'v30': DecoderV30}
+          'nbp': NeuralBP, 'v10': DecoderV10, 'v30': DecoderV30, 'v22': DecoderV22}
 DEFAULT_ITERS = {'v24': 15, 'qgnni': 25, 'qbp': 10, 'cgnni': 25, 'cbp': 25, 'nbp': 15, 'v10': 15,
-                 'v30': 15}
+                 'v30': 15, 'v22': 25}

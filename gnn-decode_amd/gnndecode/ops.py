@@ -10,8 +10,8 @@ import torch
 from . import _lib
 from .graph import TannerGraph, current_stream, dtype_code
 
-MODELS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10', 'v30')
-WEIGHTED_BP = ('nbp', 'v10')      # per-edge weight tables: count depends on the graph and T
+MODELS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10', 'v30', 'v22')
+WEIGHTED_BP = ('nbp', 'v10', 'v22')      # per-edge weight tables: count depends on the graph and T
 
 
 def _ptr(t):
@@ -186,14 +186,18 @@ def prepare_weights(model, flat):
     return out
 
 
-def decode_out_rows(graph, model, B):
-    """Rows of gnnd_decode's output: B*V, or 2*B*N for decoder_v3_0's two-output readout."""
-    return 2 * B * graph.N if model == 'v30' else B * graph.V
+def decode_out_rows(graph, model, B, iters=1):
+    """Rows of gnnd_decode's output: B*V, 2*B*N for decoder_v3_0's two-output readout,
+    iters*B*V for decoder_v2_2's per-iteration readout list."""
+    if model == 'v30':
+        return 2 * B * graph.N
+    return iters * B * graph.V if model == 'v22' else B * graph.V
 
 
 def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None):
     """Fused T-iteration decode: x [B*N(,1)] -> P(bit=1) [B*V, 1] (v30: [2*B*N, 1], the
-    two readout tensors of quantum/decoder_v3_0.py:287-288 stacked).  Traced code
+    two readout tensors of quantum/decoder_v3_0.py:287-288 stacked; v22: [T*B*V, 1], the
+    per-iteration readouts of quantum/decoder_v2_2.py:341-347 stacked).  Traced code
     (torch.compile / FX) gets the registered ops gnnd::decode / gnnd::decode_out."""
     if torch.compiler.is_compiling():
         if out is None:
@@ -211,7 +215,7 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     wdt = torch.float32 if x.dtype == torch.bfloat16 else x.dtype   # bf16 storage, fp32 math
     if prepared_weights is not None and prepared_weights.dtype != wdt:
         raise TypeError(f'{x.dtype} inputs need {wdt} prepared weights')
-    rows = decode_out_rows(graph, model, B)
+    rows = decode_out_rows(graph, model, B, int(iters))
     if out is None:
         out = torch.empty(rows, 1, dtype=x.dtype, device=x.device)
     elif out.numel() != rows or not out.is_contiguous() or out.dtype != x.dtype:

@@ -29,6 +29,7 @@ REFERENCE_OPTIM = {
     'nbp': (3e-4, 0.0),       # quantum/neural_BP.py:177, 378
     'v10': (3e-4, 0.0),       # quantum/decoder_v1_0.py:177, 377
     'v30': (3e-4, 5e-4),      # quantum/decoder_v3_0.py:173, 341
+    'v22': (2e-4, 0.0),       # quantum/decoder_v2_2.py:207, 408
     'cgnni': (3e-4, 5e-4),    # classical/CGNNI.py:204, 314
 }
 

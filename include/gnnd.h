@@ -66,10 +66,13 @@ typedef enum gnnd_aggr { GNND_AGGR_ADD = 0, GNND_AGGR_MEAN = 1, GNND_AGGR_MAX = 
  *                                           pre-clamp, p clamp 1 - 1e-15; v->c cat (F=2)
  *   V10    quantum/decoder_v1_0.py:109-131  c->v as NBP; v->c + extra (F=1)
  *   V30    quantum/decoder_v3_0.py:106-118  no pre-op on either side (edge states
- *                                           aggregated raw); both flows cat (F=2)        */
+ *                                           aggregated raw); both flows cat (F=2)
+ *   V22    quantum/decoder_v2_2.py:133-160  the NBP body (the script's propagate is
+ *                                           neural_BP.py's); decoder only: gnnd_propagate_*
+ *                                           take NBP for it                              */
 typedef enum gnnd_variant {
     GNND_V24 = 0, GNND_QGNNI = 1, GNND_QBP = 2, GNND_CGNNI = 3, GNND_CBP = 4,
-    GNND_NBP = 5, GNND_V10 = 6, GNND_V30 = 7
+    GNND_NBP = 5, GNND_V10 = 6, GNND_V30 = 7, GNND_V22 = 8
 } gnnd_variant;
 
 /* Whole-decoder models for gnnd_decode (same enumerators as gnnd_variant). */
@@ -148,6 +151,9 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  *         274-290): [0, B*N) = sigmoid(-(mlp(S_v) + x)) per node (checks: S = 0),
  *         [B*N, 2*B*N) = sigmoid(-mlp(S_c(m_p))) per node (variables: S = 0), m_p = the
  *         v->c edge states of the last iteration
+ *         V22: [iters*B*V], the reference's per-iteration readout list (quantum/
+ *         decoder_v2_2.py:333-347): block t = sigmoid(-(S_v(m_t W) + S_v(x W_pr))) after
+ *         iteration t (register-resident plans only: GNND_ERR_UNSUPPORTED otherwise)
  *   d_w   weights in `dtype` as produced by gnnd_prepare_weights from the packed
  *         state_dict layout below (gnnd_weights_count elements, same count after prepare):
  *     CGNNI: ggc2.mlp2 {W1[10], b1[10], W2[10], b2}, mlp {W1[10], b1[10], W2[10], b2}  = 62
@@ -160,6 +166,10 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  *            for t < T {layers[2t].W[E], layers[2t].W_p[E]}, then W[E], W_p[E], alpha
  *                                                                          = 2 E T + 2 E + 1
  *     V10 (quantum/decoder_v1_0.py): for t < T {layers[2t+1].W[E]}, then alpha  = E T + 1
+ *     V22 (quantum/decoder_v2_2.py, weights shared by the 8 edge types of H_prime): the NBP
+ *            layout with every type weight expanded per edge, w[e] = W[type(e)]:
+ *            for t < T {layers[2t].W[type][E], layers[2t].W_p[type][E]}, then
+ *            W[type][E], W_pr[type][E], sigmoid(weight)               = 2 E T + 2 E + 1
  *     V30 (quantum/decoder_v3_0.py, GRU edge states; the unused ggc1.mlp2/rnn2 and
  *            ggc2.mlp1/rnn1 are not passed):
  *            ggc1.mlp1 {W1[10][2] row-major, b1[10], W2[10], b2},
@@ -169,7 +179,7 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  * gnnd_prepare_weights converts that layout into the kernel layout (for the fp32 V24
  * kernel the softplus layers are rescaled to base 2: layer-1 rows * log2(e), layer-2
  * weights * ln(2); every other model/dtype is a plain copy).  Call it once per weights.
- * gnnd_weights_count is the graph-independent count (GNND_ERR_UNSUPPORTED for NBP/V10,
+ * gnnd_weights_count is the graph-independent count (GNND_ERR_UNSUPPORTED for NBP/V10/V22,
  * whose packed layout is passed to gnnd_decode as is, without preparation);
  * gnnd_decode_weights_count covers every model for a graph and iteration count.         */
 int gnnd_weights_count(int model, int64_t* h_count);

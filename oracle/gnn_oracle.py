@@ -31,7 +31,7 @@ Batch layout (A10): graph-major.  `x` is [B*N, 1] with N = V + C
 """
 import numpy as np
 
-SCRIPTS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10', 'v30')
+SCRIPTS = ('v24', 'qgnni', 'qbp', 'cgnni', 'cbp', 'nbp', 'v10', 'v30', 'v22')
 
 
 def tanner_edges(H):
@@ -342,6 +342,30 @@ def decode_nbp(H, w, x, T):
     return sigmoid(-r).reshape(-1, 1)
 
 
+def decode_v22(H, w, x, T):
+    """quantum/decoder_v2_2.py:318-347 (fp64, Nc = 25): decode_nbp with every weight shared
+    by edge type (`m.mul(feat_onehot) @ W` = m_e W[type(e)], :284, :292, :339, :342; types
+    w['edge_types'] [E] in reference edge order), residual m_p @ sigmoid(weight) (:336), and
+    the readout taken after EVERY layer pair (:337-346): returns the list of T arrays
+    sigmoid(-(sum_v m_t W + sum_v x_v W_pr)), each [B*V, 1]."""
+    g = _Graph(H)
+    xv, xc = _split_x(g, x)
+    dt = xv.dtype.type
+    ty = np.asarray(w['edge_types']).reshape(-1).astype(np.int64)
+    tw = lambda key: np.asarray(w[key], dt).reshape(-1)[ty]
+    m = np.zeros((xv.shape[0], g.E), xv.dtype)
+    alpha = sigmoid(np.asarray(w['weight'], dt).reshape(()))
+    results = []
+    for t in range(T):
+        m_p = m
+        mw = m * tw(f'layers.{2 * t}.W')
+        a = (g.sum_var(mw)[:, g.v] - mw) + xv[:, g.v] * tw(f'layers.{2 * t}.W_p')
+        m = _nbp_check(g, a, xc) + m_p * alpha
+        results.append(m)
+    sp = g.sum_var(xv[:, g.v] * tw('W_pr'))
+    return [sigmoid(-(g.sum_var(r * tw('W')) + sp)).reshape(-1, 1) for r in results]
+
+
 def decode_v10(H, w, x, T):
     """quantum/decoder_v1_0.py:282-313 (fp64, Nc = 15).  Layer 2t (source_to_target,
     :245-252): a = LOO_v(m) + x_v; layer 2t+1: a * W (per edge), BP check step; residual
@@ -418,6 +442,8 @@ def decode(model, H, x, T, w=None):
         return decode_v10(H, w, x, T)
     if model == 'v30':
         return decode_v30(H, w, x, T)
+    if model == 'v22':
+        return decode_v22(H, w, x, T)
     raise ValueError(model)
 
 

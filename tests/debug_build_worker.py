@@ -23,7 +23,8 @@ def main():
              ('qgnni', 'toric_5', torch.float32), ('qgnni', 'toric_5', torch.float64),
              ('qbp', 'toric_5', torch.float32), ('v24', 'toric_5', torch.float32),
              ('v24', 'toric_5', torch.float64), ('nbp', 'toric_4', torch.float32),
-             ('v10', 'toric_4', torch.float64), ('v30', 'toric_5', torch.float64)]
+             ('v10', 'toric_4', torch.float64), ('v30', 'toric_5', torch.float64),
+             ('v22', 'toric_4', torch.float64), ('v22', 'toric_4', torch.float32)]
     for model, code, dt in cases:
         H = gd.codes.get_code(code)
         torch.manual_seed(1)

@@ -723,9 +723,104 @@ def gen_v30():
     save('propagate_ops_v30', **prop)
 
 
+def _ref_edge_types(eg_path, L, H):
+    """The 8 edge types of quantum/decoder_v2_2.py:226-250 from the reference itself: the
+    shipped generate_PCM builds them as its local `H_prime` (error_generate.py:92-124) but
+    returns `H_one` instead, so the function is exec'd with its return changed to
+    (H, H_prime).  Types = H_prime.long() at the edges, reference edge order."""
+    tree = ast.parse(open(eg_path).read(), eg_path)
+    fns = [n for n in tree.body if isinstance(n, ast.FunctionDef)]   # generate_PCM + helpers
+    fn = [n for n in fns if n.name == 'generate_PCM'][0]
+    ret = [n for n in ast.walk(fn) if isinstance(n, ast.Return)][-1]
+    ret.value = ast.Tuple(elts=[ast.Name('H', ast.Load()), ast.Name('H_prime', ast.Load())],
+                          ctx=ast.Load())
+    ns = {'np': np, 'math': math, 'torch': torch}
+    exec(compile(ast.fix_missing_locations(ast.Module(body=fns, type_ignores=[])), eg_path,
+                 'exec'), ns)
+    Hc, Hp = ns['generate_PCM'](2 * L * L - 2, L)
+    assert np.array_equal(np.asarray(Hc).T, H.numpy())
+    Hp = torch.from_numpy(np.asarray(Hp)).t()               # [V, C] like H
+    idx = single_edge_index(H)
+    return Hp[idx[0], idx[1]].to(torch.long)
+
+
+def gen_v22():
+    """quantum/decoder_v2_2.py (neural BP with edge-type-shared weights, per-layer readout
+    list) at toric L = 4, Nc = 25.  The script's module top level cannot run against the
+    shipped error_generate (its H_prime, the `generate_PCM` second value, now carries labels
+    up to 31 and `feat_onehot.scatter_` into 8 columns fails); load_ref keeps the classes
+    and the fixtures inject `feat_onehot` built from the reference's own 8-type H_prime
+    (_ref_edge_types) with rows/cols/BATCH_SIZE/H/nb_digits/logical.  Weights: the script's
+    init (ones, W_pr 0.5, weight -4) perturbed seeded so every path is exercised.
+    Fixtures: per-layer readouts for B in {1, 8}, T in {1, 2, 25}; one training step
+    (reference LossFunc, train=1: the sum over all layers) with every parameter gradient."""
+    sys.path.insert(0, os.path.join(REF, 'quantum'))
+    import error_generate as eg
+    L, NC = 4, 25
+    Hnp, _ = eg.generate_PCM(2 * L * L - 2, L)
+    H = torch.from_numpy(Hnp).t()
+    hp = eg.H_Prep(H.t())
+    H_prep = torch.from_numpy(hp.get_H_Prep())
+    logical, _ = hp.get_logical(H_prep)
+    V, C = H.shape
+    N = V + C
+    types_ = _ref_edge_types(os.path.join(REF, 'quantum', 'error_generate.py'), L, H)
+    E = types_.numel()
+    onehot = torch.zeros(E, 8, dtype=torch.float64)
+    onehot.scatter_(1, types_.unsqueeze(1), 1)
+
+    def setup(B):
+        ns['rows'], ns['cols'], ns['BATCH_SIZE'], ns['H'] = V, C, B, H
+        ns['feat_onehot'] = onehot.repeat(B, 1)
+
+    ns = load_ref('quantum/decoder_v2_2.py', {'MessagePassing', 'GraphConv', 'GNNI', 'LossFunc'},
+                  nb_digits=8, logical=logical)
+    setup(1)
+    set_seed(221)
+    model = ns['GNNI'](NC)
+    with torch.no_grad():
+        for k, p in model.named_parameters():
+            if k == 'weight':
+                p.fill_(-1.0)
+            else:
+                p.mul_(1 + 0.25 * torch.randn(p.shape, dtype=p.dtype))
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    arrays = dict(sd_to_np(sd))
+    arrays['edge_types'] = types_.numpy()
+    for B, xs in ((1, 222), (8, 223)):
+        x, y = toric_inputs(eg, H, L, [0.05, 0.1], B, xs)
+        arrays[f'x_B{B}'], arrays[f'y_B{B}'] = x.numpy(), y.numpy()
+        setup(B)
+        for T in (1, 2, NC):
+            m = ns['GNNI'](T)
+            m.load_state_dict({k: v for k, v in sd.items()
+                               if not k.startswith('layers.') or int(k.split('.')[1]) < 2 * T})
+            data = types.SimpleNamespace(x=x, edge_index=batch_edge_index(single_edge_index(H), B, N))
+            with torch.no_grad():
+                out = m(data)
+            assert len(out) == T
+            arrays[f'out_B{B}_T{T}'] = torch.stack([o.reshape(-1) for o in out]).numpy()
+    save('v22_toric4', **arrays)
+
+    # one training step at B = 4, T = NC (reference LossFunc, train=1: every layer's readout)
+    B = 4
+    x, y = toric_inputs(eg, H, L, [0.05, 0.1], B, 224)
+    setup(B)
+    model = ns['GNNI'](NC)
+    model.load_state_dict(sd)
+    data = types.SimpleNamespace(x=x, edge_index=batch_edge_index(single_edge_index(H), B, N), y=y)
+    pred = model(data)
+    loss = ns['LossFunc'](H, H_prep)(pred, data, 1)
+    loss.backward()
+    save('train_v22_L4', x=x.numpy(), y=y.numpy(), loss=np.array(loss.item()), T=np.array(NC),
+         edge_types=types_.numpy(), pred=torch.stack([p.detach().reshape(-1) for p in pred]).numpy(),
+         **sd_to_np(sd), **grads_of(model))
+
+
 if __name__ == '__main__':
     torch.set_num_threads(1)
-    which = sys.argv[1:] or ['classical', 'quantum', 'training', 'neural_bp', 'ldpc', 'fer', 'v30']
+    which = sys.argv[1:] or ['classical', 'quantum', 'training', 'neural_bp', 'ldpc', 'fer', 'v30',
+                             'v22']
     if 'classical' in which:
         gen_classical()
     if 'quantum' in which:
@@ -740,3 +835,5 @@ if __name__ == '__main__':
         gen_fer()
     if 'v30' in which:
         gen_v30()
+    if 'v22' in which:
+        gen_v22()

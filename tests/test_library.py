@@ -15,7 +15,7 @@ def test_ops_registered():
         assert hasattr(torch.ops.gnnd, name), name
 
 
-@pytest.mark.parametrize('model,rows', [('cgnni', 10 * 63), ('v30', 2 * 10 * 81)])
+@pytest.mark.parametrize('model,rows', [('cgnni', 10 * 63), ('v30', 2 * 10 * 81), ('v22', 25 * 10 * 63)])
 def test_decode_fake_kernel_shapes(model, rows):
     gid = 10_000 + len(library._DIMS)
     library._DIMS[gid] = (63, 18, 81, 432)
