@@ -363,7 +363,7 @@ def train_main(a, world, rank, dev):
     """Config 5: decoder_v2_4 training on the toric code (default L=7), each rank a shard of
     size --batch, one flat all_reduce(SUM) of the gradient per step (gnndecode.train)."""
     code = a.code if a.code.startswith('toric') else 'toric_7'
-    model_name = a.model if a.model in ('v24', 'qgnni', 'nbp', 'v10') else 'v24'
+    model_name = a.model if a.model in ('v24', 'qgnni', 'nbp', 'v10', 'v22', 'v30') else 'v24'
     T = a.iters or gd.DEFAULT_ITERS[model_name]
     dtype = torch.float64 if a.dtype == 'f64' else torch.float32
     H = gd.codes.get_code(code)
@@ -372,8 +372,13 @@ def train_main(a, world, rank, dev):
     fused = model_name == 'v24' and not a.layerwise
     if model_name == 'v24':
         model.fused_train = fused
-    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
-                              logical_only=(model_name == 'qgnni')).to(dev)
+    if model_name == 'v22':          # decoder_v2_2's LossFunc: every layer's readout
+        lf = gd.loss.PerLayerLoss(H, gd.codes.toric_logicals(H)).to(dev)
+    elif model_name == 'v30':        # decoder_v3_0's LossFunc (two-output readout)
+        lf = gd.loss.V30Loss(H).to(dev)
+    else:
+        lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
+                                  logical_only=(model_name == 'qgnni')).to(dev)
     if fused and not a.torch_trainer:
         # prepare -> fwd+tape -> syndrome loss -> reverse pass -> [all_reduce] -> Adam, one HIP graph
         tr = gd.train.FusedV24Trainer(model, lf, graph=not a.no_graph, warmup=2)
