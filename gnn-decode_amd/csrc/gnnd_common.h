@@ -523,6 +523,16 @@ template <int G> __device__ __forceinline__ float group_sum_c(float v) {
     if constexpr (G > 32) v += __shfl_xor(v, 32);
     return v;
 }
+// the same butterfly as a product (the fp32 BP check step's magnitude products)
+template <int G> __device__ __forceinline__ float group_prod_c(float v) {
+    if constexpr (G > 1) v *= dpp_mov<0xB1>(v);
+    if constexpr (G > 2) v *= dpp_mov<0x4E>(v);
+    if constexpr (G > 4) v *= dpp_mov<0x141>(v);
+    if constexpr (G > 8) v *= dpp_mov<0x140>(v);
+    if constexpr (G > 16) v *= __shfl_xor(v, 16);
+    if constexpr (G > 32) v *= __shfl_xor(v, 32);
+    return v;
+}
 // fp64: the same butterfly, each step moving the two 32-bit halves with DPP
 template <int CTRL> __device__ __forceinline__ double dpp_mov(double v) {
     const int2 h = __builtin_bit_cast(int2, v);

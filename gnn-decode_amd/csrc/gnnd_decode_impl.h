@@ -527,6 +527,50 @@ __device__ __forceinline__ f32x2 bp_msg_f32x2(f32x2 lam2, f32x2 n, float hi) {
     }
 }
 
+// PRODUCT form of the same check step (the paired resident kernel): exp(S_c(log|t|) -
+// log|t_e|) = prod_{e' != e} |t_e'|, so the check node multiplies the clamped magnitudes
+// max(|t|, lo) (padding slots: 1) and the leave-one-out value is prod * rcp(|t_e|) — one
+// v_rcp_f32 per edge in place of a v_log_f32 and a v_exp_f32, and no log/exp round trip
+// (the product of <= dc factors in [lo, 1] keeps ~dc ulp relative error where the log sum
+// of magnitudes up to |log2 lo| keeps ~dc ulp of THAT sum, amplified by exp2).  Products
+// below the fp32 range flush to 0 exactly where the reference's exp(sum) underflows.
+__device__ __forceinline__ f32x2 bp_abstanh_f32x2(f32x2 a, float lo) {
+    const f32x2 z = f32x2{fminf(fabsf(a.x), 10.f), fminf(fabsf(a.y), 10.f)} * 0.5f;
+    const f32x2 z2 = z * z;
+    f32x2 tp = __builtin_elementwise_fma(z2, f32x2{62.f / 2835.f, 62.f / 2835.f},
+                                         f32x2{-17.f / 315.f, -17.f / 315.f});
+    tp = __builtin_elementwise_fma(z2, tp, f32x2{2.f / 15.f, 2.f / 15.f});
+    tp = __builtin_elementwise_fma(z2, tp, f32x2{-1.f / 3.f, -1.f / 3.f});
+    tp = __builtin_elementwise_fma(z2 * z, tp, z);
+    const f32x2 ea = z * (-2.f * kLog2e);
+    const f32x2 e = {__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+    const f32x2 d = f32x2{1.f, 1.f} + e;
+    const f32x2 te = (f32x2{1.f, 1.f} - e) * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    const f32x2 t = {z.x < 0.3f ? tp.x : te.x, z.y < 0.3f ? tp.y : te.y};
+    return f32x2{fmaxf(t.x, lo), fmaxf(t.y, lo)};
+}
+// m from the leave-one-out magnitude product q and the sign count n
+template <bool QUANTUM>
+__device__ __forceinline__ f32x2 bp_msg_prod_f32x2(f32x2 q, f32x2 n, float hi) {
+    const f32x2 h = n * 0.5f;
+    const f32x2 par = __builtin_elementwise_fma(f32x2{__builtin_floorf(h.x), __builtin_floorf(h.y)},
+                                                f32x2{-2.f, -2.f}, n);
+    const f32x2 sgn = __builtin_elementwise_fma(par, f32x2{-2.f, -2.f}, f32x2{1.f, 1.f});
+    f32x2 p = q * sgn;
+    p = f32x2{__builtin_amdgcn_fmed3f(p.x, -hi, hi), __builtin_amdgcn_fmed3f(p.y, -hi, hi)};
+    const f32x2 up = f32x2{1.f, 1.f} + p, dn = f32x2{1.f, 1.f} - p;
+    if constexpr (QUANTUM)
+        return (f32x2{__builtin_amdgcn_logf(up.x), __builtin_amdgcn_logf(up.y)} -
+                f32x2{__builtin_amdgcn_logf(dn.x), __builtin_amdgcn_logf(dn.y)}) * kLn2;
+    else {
+        const f32x2 r = up * f32x2{__builtin_amdgcn_rcpf(dn.x), __builtin_amdgcn_rcpf(dn.y)};
+        return f32x2{__builtin_amdgcn_logf(r.x), __builtin_amdgcn_logf(r.y)} * kLn2;
+    }
+}
+__device__ __forceinline__ f32x2 rcp2(f32x2 v) {
+    return f32x2{__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)};
+}
+
 // compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
 template <int N, typename F, int I = 0> __device__ __forceinline__ void static_for(F&& f) {
     if constexpr (I < N) {
@@ -933,6 +977,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                                                 MODEL == GNND_NBP || MODEL == GNND_V10 ||
                                                 MODEL == GNND_V22);
     constexpr bool kPair = kBase2 || kPairBP;
+    // plain fp32 BP (CBP, QBP): the check step multiplies magnitudes (bp_abstanh_f32x2)
+#ifndef GNND_BP_LOGSUM
+    constexpr bool kProd = kPairBP && !ModelTraits<MODEL>::wbp;
+#else
+    constexpr bool kProd = false;
+#endif
     // T layout (paired GNN and plain-BP models): LDS keeps ONE value per variable,
     // T_v = S_v + x_v (base-2 scaled for the GNN models: messages m' = m log2 e, so
     // T'_v = S'_v + x'_v), refreshed by the variable-sum step, plus x_v itself for that
@@ -1123,6 +1173,10 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     t = f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
                     cc = f32x2{0.f, 0.f};
                     pad = 0.5f;
+                } else if constexpr (kProd) {
+                    cc = f32x2{a.x < 0.f ? 1.f : 0.f, a.y < 0.f ? 1.f : 0.f};
+                    t = bp_abstanh_f32x2(a, MODEL == GNND_QBP ? 1e-20f : 1e-7f);
+                    pad = 1.f;
                 } else {
                     cc = f32x2{a.x < 0.f ? 1.f : 0.f, a.y < 0.f ? 1.f : 0.f};
                     t = bp_log2tanh_f32x2(a, MODEL == GNND_QBP ? 1e-20f : 1e-7f);
@@ -1171,10 +1225,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     return __builtin_elementwise_fma(mprev, f32x2{(float)alpha, (float)alpha},
                                                      wbp_out2(u, n, scp));
                 } else if constexpr (MODEL == GNND_QBP) {
-                    return bp_msg_f32x2<true>(u, __builtin_elementwise_fma(f32x2{1.f, 1.f} - scp,
-                                                  f32x2{0.5f, 0.5f}, n), cst<float>(1 - 1e-12));
+                    const f32x2 nq = __builtin_elementwise_fma(f32x2{1.f, 1.f} - scp, f32x2{0.5f, 0.5f}, n);
+                    if constexpr (kProd) return bp_msg_prod_f32x2<true>(u, nq, cst<float>(1 - 1e-12));
+                    else return bp_msg_f32x2<true>(u, nq, cst<float>(1 - 1e-12));
                 } else {
-                    return bp_msg_f32x2<false>(u, n, cst<float>(1 - 1e-7));
+                    if constexpr (kProd) return bp_msg_prod_f32x2<false>(u, n, cst<float>(1 - 1e-7));
+                    else return bp_msg_f32x2<false>(u, n, cst<float>(1 - 1e-7));
                 }
             };
             // NBP publishes m already weighted by the next layer's W (or the readout W) for
@@ -1198,17 +1254,20 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                         tv[r] = pre2t(px[r], ve[qa][r], ve[qb][r], m2[j][r], r, r, cv[r]);
                     else
                         tv[r] = pre2v(px[r][0], px[r][1], ve[qa][r], ve[qb][r], m2[j][r], r, r, cv[r]);
-                    tsum = r == 0 ? tv[0] : tsum + tv[r];
+                    if constexpr (kProd) tsum = r == 0 ? tv[0] : tsum * tv[r];
+                    else tsum = r == 0 ? tv[0] : tsum + tv[r];
                     if constexpr (kPairBP) csum = r == 0 ? cv[0] : csum + cv[r];
                 }
-                const f32x2 Sc = {group_sum_c<G>(tsum.x), group_sum_c<G>(tsum.y)};
+                f32x2 Sc;
+                if constexpr (kProd) Sc = f32x2{group_prod_c<G>(tsum.x), group_prod_c<G>(tsum.y)};
+                else Sc = f32x2{group_sum_c<G>(tsum.x), group_sum_c<G>(tsum.y)};
                 f32x2 Sc2 = {0.f, 0.f};
                 if constexpr (kPairBP) Sc2 = f32x2{group_sum_c<G>(csum.x), group_sum_c<G>(csum.y)};
                 T* mba = s_m + cb[qa] * E1;
                 T* mbb = s_m + cb[qb] * E1;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    m2[j][r] = post2(Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
+                    m2[j][r] = post2(kProd ? Sc * rcp2(tv[r]) : Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
                     mba[GNND_DIDX((int)(ve[qa][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].x * wnext(ve[qa][r]);
                     mbb[GNND_DIDX((int)(ve[qb][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].y * wnext(ve[qb][r]);
                 }
@@ -1223,21 +1282,27 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 for (int i = 0; i < RP; ++i) {
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
                     tv[i] = pre2(ve[q][r0], ve[q][r1], cb[q], cb[q], msp[i], r0, r1, cv[i]);
-                    tsum = i == 0 ? tv[0].x : tsum + tv[i].x;
-                    if (2 * i + 1 < R) tsum = tsum + tv[i].y;
+                    if constexpr (kProd) {
+                        tsum = i == 0 ? tv[0].x : tsum * tv[i].x;
+                        if (2 * i + 1 < R) tsum = tsum * tv[i].y;
+                    } else {
+                        tsum = i == 0 ? tv[0].x : tsum + tv[i].x;
+                        if (2 * i + 1 < R) tsum = tsum + tv[i].y;
+                    }
                     if constexpr (kPairBP) {
                         csum = i == 0 ? cv[0].x : csum + cv[i].x;
                         if (2 * i + 1 < R) csum = csum + cv[i].y;
                     }
                 }
-                const float Sc = group_sum_c<G>(tsum);
+                const float Sc = kProd ? group_prod_c<G>(tsum) : group_sum_c<G>(tsum);
                 float Sc2 = 0.f;
                 if constexpr (kPairBP) Sc2 = group_sum_c<G>(csum);
                 T* mb = s_m + cb[q] * E1;
 #pragma unroll
                 for (int i = 0; i < RP; ++i) {
                     const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
-                    msp[i] = post2(f32x2{Sc, Sc} - tv[i], f32x2{Sc2, Sc2} - cv[i],
+                    msp[i] = post2(kProd ? f32x2{Sc, Sc} * rcp2(tv[i]) : f32x2{Sc, Sc} - tv[i],
+                                  f32x2{Sc2, Sc2} - cv[i],
                                   f32x2{(float)sc[q], (float)sc[q]}, msp[i]);
                     mb[GNND_DIDX((int)(ve[q][r0] >> 16), E1, GNND_DBG_LDS_POS)] = msp[i].x * wnext(ve[q][r0]);
                     if (r1 != r0) mb[GNND_DIDX((int)(ve[q][r1] >> 16), E1, GNND_DBG_LDS_POS)] = msp[i].y * wnext(ve[q][r1]);
