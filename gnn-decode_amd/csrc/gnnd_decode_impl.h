@@ -358,38 +358,95 @@ struct Mlp10Pair {
     }
 };
 
-// wg: the MLP's prepared weights in global memory (uniform address: scalar loads)
+template <int N, typename F, int I = 0> __device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, F, I + 1>(static_cast<F&&>(f));
+    }
+}
+// The unit sum in a FIXED order independent of how the units are spread over lanes: chain j
+// (0..3) accumulates units k = 4i + j (i ascending), chain 0 starting from the linear part,
+// and the MLP value is (c0 + c1) + (c2 + c3).  A call evaluates NC consecutive chains from
+// J0 and returns their sum in that tree (NC = 4: the whole MLP; NC = 2 / 1: a half / a
+// quarter, the unit-split small-batch kernel combining the other waves' parts through LDS),
+// so every split gives the same bits.  TWO: the 2-input MLP (u0 -> W1a', u1 -> W1b').
+// wg: the MLP's prepared weights in global memory (uniform address: scalar loads; J0 is a
+// template argument so the weight offsets stay compile-time).
+template <int NC, int J0, bool TWO>
+__device__ __forceinline__ f32x2 mlp128_chains(const float* __restrict__ wg, const V24Lin& lin,
+                                               f32x2 u0, f32x2 u1) {
+    const f32x2* wb = (const f32x2*)wg;                      // {W1b'_k, b1'_k}
+    const f32x2* wa = (const f32x2*)(wg + 256);              // W1a' pairs (TWO)
+    const f32x2* w2 = (const f32x2*)(wg + (TWO ? 384 : 256));
+    f32x2 c[NC];
+#pragma unroll
+    for (int jj = 0; jj < NC; ++jj) c[jj] = f32x2{0.f, 0.f};
+    if constexpr (J0 == 0) {
+        if constexpr (TWO)
+            c[0] = __builtin_elementwise_fma(u0, f32x2{lin.a0, lin.a0},
+                       __builtin_elementwise_fma(u1, f32x2{lin.a1, lin.a1}, f32x2{lin.b, lin.b}));
+        else
+            c[0] = __builtin_elementwise_fma(u0, f32x2{lin.a0, lin.a0}, f32x2{lin.b, lin.b});
+    }
+    constexpr int kUnroll = NC == 1 ? 8 : NC == 2 ? 4 : 2;   // 8 units per loop trip
+#pragma unroll kUnroll
+    for (int i = 0; i < 32; ++i) {
+        static_for<NC>([&](auto jc) {
+            constexpr int j = J0 + decltype(jc)::value;         // chain (unit k = 4i + j)
+            const int k = 4 * i + j;
+            f32x2 h;
+            if constexpr (TWO) {
+                const f32x2 a = wa[k >> 1];
+                h = (j & 1) ? pk_fma_hi(u0, a, pk_fma_sb(u1, wb[k])) : pk_fma_lo(u0, a, pk_fma_sb(u1, wb[k]));
+            } else {
+                h = pk_fma_sb(u0, wb[k]);
+            }
+            f32x2& cj = c[decltype(jc)::value];
+            cj = (j & 1) ? pk_fma_hi(softplus_tail2(h), w2[k >> 1], cj)
+                         : pk_fma_lo(softplus_tail2(h), w2[k >> 1], cj);
+        });
+    }
+    if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
+    else if constexpr (NC == 2) return c[0] + c[1];
+    else return c[0];
+}
 __device__ __forceinline__ f32x2 mlp128_sp2(const float* __restrict__ wg, const V24Lin& lin,
                                             f32x2 u) {
-    const f32x2* wb = (const f32x2*)wg;
-    const f32x2* w2 = (const f32x2*)(wg + 256);
-    f32x2 acc0 = __builtin_elementwise_fma(u, f32x2{lin.a0, lin.a0}, f32x2{lin.b, lin.b});
-    f32x2 acc1 = {0.f, 0.f};                 // even units -> acc0, odd units -> acc1
-#pragma unroll 8
-    for (int j = 0; j < 64; ++j) {
-        const f32x2 h0 = pk_fma_sb(u, wb[2 * j]), h1 = pk_fma_sb(u, wb[2 * j + 1]);
-        acc0 = pk_fma_lo(softplus_tail2(h0), w2[j], acc0);
-        acc1 = pk_fma_hi(softplus_tail2(h1), w2[j], acc1);
-    }
-    return acc0 + acc1;
+    return mlp128_chains<4, 0, false>(wg, lin, u, u);
 }
 __device__ __forceinline__ f32x2 mlp128x2_sp2(const float* __restrict__ wg, const V24Lin& lin,
                                               f32x2 u0, f32x2 u1) {
-    const f32x2* wb = (const f32x2*)wg;            // {W1b'_k, b1'_k}
-    const f32x2* wa = (const f32x2*)(wg + 256);    // W1a' pairs
-    const f32x2* w2 = (const f32x2*)(wg + 384);
-    f32x2 acc0 = __builtin_elementwise_fma(u0, f32x2{lin.a0, lin.a0},
-                     __builtin_elementwise_fma(u1, f32x2{lin.a1, lin.a1}, f32x2{lin.b, lin.b}));
-    f32x2 acc1 = {0.f, 0.f};
-#pragma unroll 8
-    for (int j = 0; j < 64; ++j) {
-        const f32x2 a = wa[j];
-        const f32x2 h0 = pk_fma_lo(u0, a, pk_fma_sb(u1, wb[2 * j]));
-        const f32x2 h1 = pk_fma_hi(u0, a, pk_fma_sb(u1, wb[2 * j + 1]));
-        acc0 = pk_fma_lo(softplus_tail2(h0), w2[j], acc0);
-        acc1 = pk_fma_hi(softplus_tail2(h1), w2[j], acc1);
+    return mlp128_chains<4, 0, true>(wg, lin, u0, u1);
+}
+// unit-split evaluation (decode_kernel US > 1): wave-uniform `sub` selects this wave's
+// chains; the US partial sums meet in LDS (buf = [US][GNND_BLOCK] f32x2, one of two buffers
+// used alternately so one barrier per call suffices) and every wave combines them in the
+// tree above.  All threads of the workgroup must call it (barrier).
+template <int US, bool TWO>
+__device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, const V24Lin& lin,
+                                              f32x2 u0, f32x2 u1, int sub, f32x2* buf, int itid) {
+    if constexpr (US == 1) {
+        return mlp128_chains<4, 0, TWO>(wg, lin, u0, u1);
+    } else {
+        f32x2 p;
+        if constexpr (US == 2) {
+            p = sub == 0 ? mlp128_chains<2, 0, TWO>(wg, lin, u0, u1)
+                         : mlp128_chains<2, 2, TWO>(wg, lin, u0, u1);
+        } else {
+            static_assert(US == 4, "unit split 1, 2 or 4");
+            switch (sub) {
+                case 0: p = mlp128_chains<1, 0, TWO>(wg, lin, u0, u1); break;
+                case 1: p = mlp128_chains<1, 1, TWO>(wg, lin, u0, u1); break;
+                case 2: p = mlp128_chains<1, 2, TWO>(wg, lin, u0, u1); break;
+                default: p = mlp128_chains<1, 3, TWO>(wg, lin, u0, u1); break;
+            }
+        }
+        buf[sub * GNND_BLOCK + itid] = p;
+        __syncthreads();
+        if constexpr (US == 2) return buf[itid] + buf[GNND_BLOCK + itid];
+        else return (buf[itid] + buf[GNND_BLOCK + itid]) +
+                    (buf[2 * GNND_BLOCK + itid] + buf[3 * GNND_BLOCK + itid]);
     }
-    return acc0 + acc1;
 }
 // linear parts, identical in every thread (fixed summation order)
 __device__ __forceinline__ V24Lin v24_lin1(const float* __restrict__ wg) {
@@ -572,12 +629,6 @@ __device__ __forceinline__ f32x2 rcp2(f32x2 v) {
 }
 
 // compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
-template <int N, typename F, int I = 0> __device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<N, F, I + 1>(static_cast<F&&>(f));
-    }
-}
 
 template <int MODEL, typename T> struct EdgeMath {
     static constexpr bool BP = ModelTraits<MODEL>::bp;
@@ -663,8 +714,11 @@ template <typename T> struct TapeView {
     T* mT;    // [B][E]
 };
 
-template <int MODEL, typename T, int R, bool TAPE = false>
-__global__ void __launch_bounds__(GNND_BLOCK)
+// US (unit split, fp32 decoder_v2_4 small batches): US waves share each wave of work items,
+// each evaluating a quarter / half of every 128-hidden MLP's units (mlp128_split), so a
+// latency-bound batch of a few codewords per workgroup keeps 4 / 2 times as many waves busy.
+template <int MODEL, typename T, int R, bool TAPE = false, int US = 1>
+__global__ void __launch_bounds__(GNND_BLOCK * US)
 decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
               T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
               FastDiv dN, TapeView<T> tape) {
@@ -673,6 +727,12 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
+    constexpr int NT = GNND_BLOCK * US;
+    static_assert(US == 1 || (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2),
+                  "unit split: fp32 decoder_v2_4 on one slot pair per lane");
+    // work-item lane (0..255) and the wave's unit chunk: waves w = US i + sub share item wave i
+    const int sub = US > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) % US) : 0;
+    const int itid = US > 1 ? ((tid >> 6) / US) * 64 + (tid & 63) : tid;
 
     T* s_w = (T*)smem;
     size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
@@ -687,27 +747,29 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     if constexpr (kTab) {
         s_tab = (T*)(smem + off);
         off += (size_t)kFp64TabDoubles * 8;
-        for (int i = tid; i < kFp64TabDoubles; i += GNND_BLOCK)
+        for (int i = tid; i < kFp64TabDoubles; i += NT)
             s_tab[i] = i < 128 ? kExpTab[i] : kLogTab[i - 128];
     }
     T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
+    // unit split: two [US][256] f32x2 buffers for the MLP partial sums (8-byte aligned)
+    f32x2* s_part = (f32x2*)(((uintptr_t)(s_xc + (size_t)CW * C) + 7) & ~(uintptr_t)7);
 
-    for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
-    for (int i = tid; i < nslot; i += GNND_BLOCK) s_slot[i] = g.slot_ve[i];   // v | e << 16
-    for (int i = tid; i <= V; i += GNND_BLOCK) s_vptr[i] = g.var_ptr[i];
-    for (int i = tid; i < E; i += GNND_BLOCK) s_vslot[i] = g.vslot[i];
+    for (int i = tid; i < nw; i += NT) s_w[i] = w[i];
+    for (int i = tid; i < nslot; i += NT) s_slot[i] = g.slot_ve[i];   // v | e << 16
+    for (int i = tid; i <= V; i += NT) s_vptr[i] = g.var_ptr[i];
+    for (int i = tid; i < E; i += NT) s_vslot[i] = g.vslot[i];
     const int64_t b0 = (int64_t)blockIdx.x * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     const T* xg = x + b0 * N;
-    for (int i = tid; i < nb * N; i += GNND_BLOCK) {
+    for (int i = tid; i < nb * N; i += NT) {
         int b = fdiv(i, dN), n = i - b * N;
         T xv = xg[i];
         if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
         else s_xc[b * C + n - V] = xv;
     }
-    for (int i = tid; i < nb * nslot; i += GNND_BLOCK) s_m[i] = T(0);
+    for (int i = tid; i < nb * nslot; i += NT) s_m[i] = T(0);
     __syncthreads();
 
     // 128-hidden weights stream through the scalar cache into SGPRs (uniform addresses):
@@ -734,8 +796,9 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     const int nV = nb * V;
     for (int it = 0; it < iters; ++it) {
         for (int f0 = 0; f0 < nItem; f0 += GNND_BLOCK) {
-            const int f = f0 + tid;
+            const int f = f0 + itid;
             const bool act = f < nItem;
+            const bool own = act && sub == 0;            // the unit-split waves' writer
             const int fc = act ? f : nItem - 1;          // idle groups compute on a copy
             const int b = fdiv(fc, dItem);
             const int rem = fc - b * IC;
@@ -761,8 +824,8 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 #pragma unroll
                 for (int r = 0; r < R; r += 2) {
                     const int r1 = r + 1 < R ? r + 1 : r;
-                    const f32x2 a = mlp128x2_sp2(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
-                                                 f32x2{xs[r], xs[r1]});
+                    const f32x2 a = mlp128_split<US, true>(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
+                                                           f32x2{xs[r], xs[r1]}, sub, s_part, itid);
                     tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
                     if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
                 }
@@ -770,7 +833,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 #pragma unroll
                     for (int r = 0; r < R; ++r) {
                         const int e = (int)(sl[r] >> 16);
-                        if (act && e != E) {
+                        if (own && e != E) {
                             const size_t row = ((size_t)it * B + b0 + b) * E + e;
                             tape.ext[row] = ext[r];
                             tape.t[row] = tv[r];
@@ -835,14 +898,16 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int e = (int)(sl[r] >> 16);
-                    if (act && e != E) tape.u[((size_t)it * B + b0 + b) * E + e] = Sc - tv[r];
+                    if (own && e != E) tape.u[((size_t)it * B + b0 + b) * E + e] = Sc - tv[r];
                 }
             }
             if constexpr (kV24F32) {
 #pragma unroll
                 for (int r = 0; r < R; r += 2) {
                     const int r1 = r + 1 < R ? r + 1 : r;
-                    const f32x2 y = mlp128_sp2(v24.g + kV24Ggc2, v24.l2, f32x2{Sc - tv[r], Sc - tv[r1]});
+                    const f32x2 uu = {Sc - tv[r], Sc - tv[r1]};
+                    const f32x2 y = mlp128_split<US, false>(v24.g + kV24Ggc2, v24.l2, uu, uu, sub,
+                                                            s_part + US * GNND_BLOCK, itid);
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
                 }
@@ -855,14 +920,14 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                 for (int r = 0; r < R; ++r)   // every slot computes; padding slots are never read
                     mn[r] = M::post(Sc - tv[r], Sc2 - cf[r], sc, mv[r], mlp_msg, s_w, wv, s_tab);
             }
-            if (act) {
+            if (own) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) mb[r] = mn[r];
             }
         }
         __syncthreads();
         if (it + 1 == iters) break;
-        for (int f = tid; f < nV; f += GNND_BLOCK) {
+        for (int f = tid; f < nV; f += NT) {
             const int b = fdiv(f, dV), v = f - b * V;
             if constexpr (MODEL == GNND_NBP)   // S_v of the next layer's weighted messages
                 s_sx[f].s = var_sum_w(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1],
@@ -874,7 +939,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     }
 
     if constexpr (TAPE) {
-        for (int f = tid; f < nb * nslot; f += GNND_BLOCK) {
+        for (int f = tid; f < nb * nslot; f += NT) {
             const int b = f / nslot, sl = f - b * nslot;
             const int e = (int)(s_slot[sl] >> 16);
             if (e != E) tape.mT[(size_t)(b0 + b) * E + e] = s_m[f];
@@ -884,19 +949,19 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
         if constexpr (kV24F32) {
             const int n = nb * nslot;
-            for (int f = 2 * tid; f < n; f += 2 * GNND_BLOCK) {
+            for (int f = 2 * tid; f < n; f += 2 * NT) {
                 const int f1 = f + 1 < n ? f + 1 : f;
                 const f32x2 y = mlp128_sp2(v24.g + kV24Mlp, v24.l3, f32x2{s_m[f], s_m[f1]});
                 s_m[f] = y.x;
                 if (f + 1 < n) s_m[f + 1] = y.y;
             }
         } else {
-            for (int f = tid; f < nb * nslot; f += GNND_BLOCK) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f], s_tab);
+            for (int f = tid; f < nb * nslot; f += NT) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f], s_tab);
         }
         __syncthreads();
     }
     T* og = out + b0 * V;
-    for (int f = tid; f < nV; f += GNND_BLOCK) {
+    for (int f = tid; f < nV; f += NT) {
         const int b = fdiv(f, dV), v = f - b * V;
         if constexpr (MODEL == GNND_NBP) {
             // sum_v(m W) + sum_v(x_v W_p)  (neural_BP.py:307-312), each in edge order
@@ -1579,7 +1644,18 @@ struct Plan {
     int cw;       // codewords per workgroup
     int q;        // work items per lane (resident)
     size_t lds;   // bytes of dynamic LDS
+    int us = 1;   // unit split of the streaming kernel (fp32 decoder_v2_4, small batches)
 };
+
+// GNND_V24_SPLIT=1|2|4 forces the fp32 decoder_v2_4 unit split (A/B); default by batch
+int v24_split_forced() {
+    static int v = [] {
+        const char* e = getenv("GNND_V24_SPLIT");
+        const int n = e ? atoi(e) : 0;
+        return n == 1 || n == 2 || n == 4 ? n : 0;
+    }();
+    return v;
+}
 
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
@@ -1693,6 +1769,15 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     p->cw = (int)n;
     p->q = 0;
     p->lds = fixed + n * per;
+    // fp32 decoder_v2_4 at one codeword per workgroup (training steps, small decodes) is
+    // latency-bound: one wave per SIMD walks 128 hidden units per edge pair.  Split the units
+    // over US waves (B <= 256: 4, one 16-wave workgroup per CU; B <= 512: 2)
+    p->us = 1;
+    if (v24f32 && n == 1 && g.R <= 2) {
+        const int forced = v24_split_forced();
+        p->us = forced ? forced : B <= 256 ? 4 : B <= 512 ? 2 : 1;
+    }
+    if (p->us > 1) p->lds = align16(p->lds) + (size_t)2 * p->us * GNND_BLOCK * 8 + 8;
     return GNND_OK;
 }
 
@@ -1705,12 +1790,12 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
     const int nw = lds_weights(MODEL);
     const FastDiv dI = make_fastdiv(p.resident ? p.cw : g.C * g.G);
     const FastDiv dV = make_fastdiv(g.V), dN = make_fastdiv(g.N);
-    auto go = [&](auto kern) -> int {
+    auto go = [&](auto kern, int us = 1) -> int {
         if (p.lds > 64 * 1024)
             GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
-        kern<<<(unsigned)blocks, GNND_BLOCK, p.lds, st>>>(g, (const T*)w, nw, (const TI*)x, (TI*)out,
-                                                          B, iters, p.cw, dI, dV, dN, tape);
+        kern<<<(unsigned)blocks, GNND_BLOCK * us, p.lds, st>>>(g, (const T*)w, nw, (const TI*)x, (TI*)out,
+                                                               B, iters, p.cw, dI, dV, dN, tape);
         GNND_LAUNCH_CHECK();
         return GNND_OK;
     };
@@ -1748,6 +1833,13 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         // bf16 I/O and decoder_v2_2's per-iteration readout: register-resident plans only
         return GNND_ERR_UNSUPPORTED;
     } else {
+        if constexpr (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2) {
+            if (p.us == 4) return tape.ext ? go(decode_kernel<MODEL, T, R, true, 4>, 4)
+                                           : go(decode_kernel<MODEL, T, R, false, 4>, 4);
+            if (p.us == 2) return tape.ext ? go(decode_kernel<MODEL, T, R, true, 2>, 2)
+                                           : go(decode_kernel<MODEL, T, R, false, 2>, 2);
+        }
+        if (p.us != 1) return GNND_ERR_UNSUPPORTED;
         if constexpr (MODEL == GNND_V24)
             if (tape.ext) return go(decode_kernel<MODEL, T, R, true>);
         return go(decode_kernel<MODEL, T, R>);
