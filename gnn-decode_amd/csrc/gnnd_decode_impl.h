@@ -421,15 +421,20 @@ __device__ __forceinline__ f32x2 mlp128x2_sp2(const float* __restrict__ wg, cons
 // unit-split evaluation (decode_kernel US > 1): wave-uniform `sub` selects this wave's
 // chains; the US partial sums meet in LDS (buf = [US][GNND_BLOCK] f32x2, one of two buffers
 // used alternately so one barrier per call suffices) and every wave combines them in the
-// tree above.  All threads of the workgroup must call it (barrier).
+// tree above.  All threads of the workgroup must call it (barrier).  idle (wave-uniform):
+// the wave holds no live work item (its result is never stored) and skips the units, so
+// the SIMDs' issue goes to the live item waves only.
 template <int US, bool TWO>
 __device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, const V24Lin& lin,
-                                              f32x2 u0, f32x2 u1, int sub, f32x2* buf, int itid) {
+                                              f32x2 u0, f32x2 u1, int sub, f32x2* buf, int itid,
+                                              bool idle) {
+    f32x2 p = {0.f, 0.f};
     if constexpr (US == 1) {
-        return mlp128_chains<4, 0, TWO>(wg, lin, u0, u1);
+        if (!idle) p = mlp128_chains<4, 0, TWO>(wg, lin, u0, u1);
+        return p;
     } else {
-        f32x2 p;
-        if constexpr (US == 2) {
+        if (idle) {
+        } else if constexpr (US == 2) {
             p = sub == 0 ? mlp128_chains<2, 0, TWO>(wg, lin, u0, u1)
                          : mlp128_chains<2, 2, TWO>(wg, lin, u0, u1);
         } else {
@@ -799,6 +804,8 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
             const int f = f0 + itid;
             const bool act = f < nItem;
             const bool own = act && sub == 0;            // the unit-split waves' writer
+            // no live item in this wave (last round of a partial tile): skip the 128-unit MLPs
+            const bool widle = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= nItem;
             const int fc = act ? f : nItem - 1;          // idle groups compute on a copy
             const int b = fdiv(fc, dItem);
             const int rem = fc - b * IC;
@@ -825,7 +832,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                 for (int r = 0; r < R; r += 2) {
                     const int r1 = r + 1 < R ? r + 1 : r;
                     const f32x2 a = mlp128_split<US, true>(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
-                                                           f32x2{xs[r], xs[r1]}, sub, s_part, itid);
+                                                           f32x2{xs[r], xs[r1]}, sub, s_part, itid, widle);
                     tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
                     if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
                 }
@@ -907,7 +914,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     const int r1 = r + 1 < R ? r + 1 : r;
                     const f32x2 uu = {Sc - tv[r], Sc - tv[r1]};
                     const f32x2 y = mlp128_split<US, false>(v24.g + kV24Ggc2, v24.l2, uu, uu, sub,
-                                                            s_part + US * GNND_BLOCK, itid);
+                                                            s_part + US * GNND_BLOCK, itid, widle);
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
                 }
