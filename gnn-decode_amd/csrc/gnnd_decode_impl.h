@@ -753,7 +753,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         s_tab = (T*)(smem + off);
         off += (size_t)kFp64TabDoubles * 8;
         for (int i = tid; i < kFp64TabDoubles; i += NT)
-            s_tab[i] = i < 128 ? kExpTab[i] : kLogTab[i - 128];
+            s_tab[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
     }
     T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}

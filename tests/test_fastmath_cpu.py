@@ -31,7 +31,7 @@ int main() {
     std::mt19937_64 g(1);
     double me = 0, ml = 0, mt = 0, mm = 0, ms = 0, mst = 0, met = 0, mlt = 0;
     static double TAB[kFp64TabDoubles];
-    for (int i = 0; i < kFp64TabDoubles; ++i) TAB[i] = i < 128 ? kExpTab[i] : kLogTab[i - 128];
+    for (int i = 0; i < kFp64TabDoubles; ++i) TAB[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
     std::uniform_real_distribution<double> U(-700, 700), L(-300, 300), T(-12, 12), S(-60, 30);
     for (int i = 0; i < 400000; ++i) {
         double x = U(g) * (i % 4 ? 0.05 : 1.0);
@@ -48,7 +48,7 @@ int main() {
         double yn = -fabs(U(g)) * (i % 4 ? 0.03 : 1.0);
         met = fmax(met, ulp(exp_tab_nonpos(yn, TAB), exp(yn)));
         double uu = (i % 3 == 0) ? exp(-fabs(L(g)) * 0.1) : std::uniform_real_distribution<double>(0, 1)(g);
-        mlt = fmax(mlt, ulp(log1p_tab_unit(uu, TAB + 128), log1p(uu)));
+        mlt = fmax(mlt, ulp(log1p_tab_unit(uu, TAB + kExpTabN), log1p(uu)));
     }
     printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f\n", me, ml, mt, mm, ms, mst, met, mlt);
 }

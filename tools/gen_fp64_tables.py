@@ -3,7 +3,7 @@
 kExpTab / kLogTab).  Values are computed with 60-digit decimal arithmetic and rounded to
 the nearest double (float(Decimal) rounds correctly); printed as C hex-float literals.
 
-  kExpTab[j] = 2^(j/128),                   j = 0..127
+  kExpTab[j] = 2^(j/256),                   j = 0..255
   kLogTab[2j] = r_j = RN(1 / (1 + j/256)),  kLogTab[2j+1] = RN(-ln r_j)   (exact r_j), j = 0..256
 
 usage: python tools/gen_fp64_tables.py   (prints the two C arrays)"""
@@ -13,15 +13,15 @@ getcontext().prec = 60
 
 
 def main():
-    exp_tab = [float(Decimal(2) ** (Decimal(j) / 128)) for j in range(128)]
+    exp_tab = [float(Decimal(2) ** (Decimal(j) / 256)) for j in range(256)]
     log_tab = []
     for j in range(257):
         c = Decimal(1) + Decimal(j) / 256
         r = float(Decimal(1) / c)                    # the double r_j
         lr = -(Decimal(r).ln())                      # -ln of the EXACT double r_j
         log_tab += [r, float(lr)]
-    print('__constant__ static const double kExpTab[128] = {')
-    for i in range(0, 128, 4):
+    print('__constant__ static const double kExpTab[256] = {')
+    for i in range(0, 256, 4):
         print('    ' + ', '.join(v.hex() for v in exp_tab[i:i + 4]) + ',')
     print('};')
     print('__constant__ static const double kLogTab[514] = {')
