@@ -192,3 +192,22 @@ def test_decision_errors_kernel_on_decoder_outputs(golden):
     c = gd.ops.decision_errors(g, lg, torch.as_tensor(z['out_B32_T15'], device=DEV),
                                torch.as_tensor(z['y_B32'], device=DEV)).cpu().tolist()
     assert c[2] + c[3] == int(golden('fer_rule')['v24_B32/count'])
+
+
+def test_v24_f32_unit_split_bit_identical():
+    """fp32 decoder_v2_4 small-batch unit split: decode_kernel runs US = 4 (B <= 256) or 2
+    (B <= 512) waves per item wave at one codeword per workgroup and US = 1 above, all on the
+    R = 2 slot table below B = 4096.  The 128 hidden units are summed in one fixed chain order
+    (gnnd_decode_impl.h mlp128_chains), so every codeword decodes to the SAME BITS under every
+    split and tile: slices decoded alone (US = 4 / 2) equal the B = 1024 decode (US = 1)."""
+    import gnndecode as gd
+    w = _shipped('v24_toric_5')
+    m, H = _model('v24', 'toric_5', 15, w)
+    B = 1024
+    x, _ = gd.data.toric_batch(H, B, seed=5, device=DEV, dtype=torch.float32)
+    _, full = _decode(m, x)
+    full = full.view(B, -1)
+    xb = x.view(B, -1)
+    for b0, n in ((0, 128), (128, 300), (700, 256), (1000, 24), (1023, 1)):
+        _, part = _decode(m, xb[b0:b0 + n].reshape(-1, 1).contiguous())
+        assert torch.equal(part.view(n, -1), full[b0:b0 + n]), (b0, n)
