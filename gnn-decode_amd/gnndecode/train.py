@@ -116,6 +116,13 @@ class _GraphedStep:
         self._apply()
         return loss
 
+    def static_inputs(self):
+        """(x, y) buffers the captured step reads (None before the capture): write the next
+        batch into them to skip the per-step input copies."""
+        if not self.use_graph or self._g_compute is None:
+            return None
+        return self._sx, self._sy
+
     def _run(self, x, y):
         if not self.use_graph:
             return self._eager(x, y).detach().clone()
@@ -140,8 +147,12 @@ class _GraphedStep:
                 with torch.cuda.graph(self._g_compute):
                     self._sloss, self._sgrads = self._compute(self._sx, self._sy)
                     self._apply()
-        self._sx.copy_(x)
-        self._sy.copy_(y)
+        # inputs already in the graph's static buffers (static_inputs(): a sampler writing
+        # there directly) need no copy
+        if x.data_ptr() != self._sx.data_ptr():
+            self._sx.copy_(x)
+        if y.data_ptr() != self._sy.data_ptr():
+            self._sy.copy_(y)
         self._g_compute.replay()
         if self._g_apply is not None:
             self._reduce(self._sloss, self._sgrads)      # eager RCCL between the two graphs
