@@ -93,6 +93,32 @@ __device__ __forceinline__ void wave_sum2(float a, float b, float& ra, float& rb
     ra = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
     rb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
 }
+// totals of FOUR wave64 values (two pairs): the two permlane32 folds as above, then ONE
+// v_permlane16_swap between the two folded vectors leaves one edge per 16-lane row, and one
+// four-step row DPP chain finishes all four (wave_sum2 twice: two swaps16 and two chains).
+// Row order of the swap: GNND_PL16_MAP 0 -> rows {a, c, b, d}, 1 -> {c, a, d, b}.
+#ifndef GNND_PL16_MAP
+#define GNND_PL16_MAP 0
+#endif
+__device__ __forceinline__ void wave_sum4(f32x2 ab, f32x2 cd, float& ra, float& rb, float& rc,
+                                          float& rd) {
+    const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_int(ab.x), __float_as_int(ab.y), false, false);
+    const float v1 = __int_as_float(s1[0]) + __int_as_float(s1[1]);      // lanes 0-31 a, 32-63 b
+    const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_int(cd.x), __float_as_int(cd.y), false, false);
+    const float v2 = __int_as_float(s2[0]) + __int_as_float(s2[1]);      // c | d
+    const auto s3 = __builtin_amdgcn_permlane16_swap(__float_as_int(v1), __float_as_int(v2), false, false);
+    float v = __int_as_float(s3[0]) + __int_as_float(s3[1]);
+    v += __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x140, 0xf>(__float_as_int(v)));
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    if (GNND_PL16_MAP == 0) { ra = r0; rc = r1; rb = r2; rd = r3; }
+    else { rc = r0; ra = r1; rd = r2; rb = r3; }
+}
 template <int CTRL, int ROWS> __device__ __forceinline__ double dpp_d(double v) {
     const long long b = __double_as_longlong(v);
     const int lo = dpp_i<CTRL, ROWS>((int)b), hi = dpp_i<CTRL, ROWS>((int)(b >> 32));
@@ -192,6 +218,26 @@ template <typename T> struct Units {
     template <bool TWO>
     __device__ __forceinline__ void bwd2_f32(float xa0, float xa1, float dya, float xb0, float xb1,
                                              float dyb, float& ra, float& rb) {
+        const f32x2 p = bwd2_f32_part<TWO>(xa0, xa1, dya, xb0, xb1, dyb);
+        wave_sum2(p.x, p.y, ra, rb);
+        ra *= kLn2;
+        rb *= kLn2;
+    }
+    // four edges: two pairs' unit work, one shared wave reduction (wave_sum4)
+    template <bool TWO>
+    __device__ __forceinline__ void bwd4_f32(const float (&x0)[4], const float (&x1)[4],
+                                             const float (&dy)[4], float (&r)[4]) {
+        const f32x2 pab = bwd2_f32_part<TWO>(x0[0], x1[0], dy[0], x0[1], x1[1], dy[1]);
+        const f32x2 pcd = bwd2_f32_part<TWO>(x0[2], x1[2], dy[2], x0[3], x1[3], dy[3]);
+        wave_sum4(pab, pcd, r[0], r[1], r[2], r[3]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r[i] *= kLn2;
+    }
+    // the per-lane unit work of two edges: weight-gradient partials accumulated, returns the
+    // lane's d input partials (log2 units) of both edges, to be wave-reduced
+    template <bool TWO>
+    __device__ __forceinline__ f32x2 bwd2_f32_part(float xa0, float xa1, float dya, float xb0,
+                                                   float xb1, float dyb) {
         const f32x2 x0 = {xa0, xb0}, x1 = {xa1, xb1}, dy = {dya, dyb};
         f32x2 p = {0.f, 0.f};
 #pragma unroll
@@ -216,9 +262,7 @@ template <typename T> struct Units {
         }
         gb2 += dya;
         gb2 += dyb;
-        wave_sum2(p.x, p.y, ra, rb);
-        ra *= kLn2;
-        rb *= kLn2;
+        return p;
     }
     // add this wave's gradients into the workgroup accumulator (packed plain layout)
     template <bool TWO>
@@ -284,6 +328,36 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     // lanes after every 64 steps (no per-step exec-masked lane-0 stores).
     auto unit_pass = [&](auto& U, auto two_tag, const T* in0, const T* in1, auto dy_of, T* outp) {
         constexpr bool TWO = decltype(two_tag)::value;
+        if constexpr (sizeof(T) == 4) {
+            // fp32: four edges f + i W (i = 0..3) per wave step, one shared reduction
+            constexpr int W = kTrainWaves, kStride4 = 4 * kTrainWaves;
+            for (int f0 = wave; f0 < E; f0 += 64 * kStride4) {
+                float res[4] = {0.f, 0.f, 0.f, 0.f};
+                int k = 0;
+                for (int f = f0; f < E && k < 64; f += kStride4, ++k) {
+                    float a0[4], a1[4], dy[4], r[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int fi = f + i * W;
+                        const bool ok = fi < E;
+                        const int fc = ok ? fi : f;
+                        a0[i] = in0[fc];
+                        a1[i] = TWO ? in1[fc] : 0.f;
+                        dy[i] = ok ? dy_of(fc) : 0.f;
+                    }
+                    U.template bwd4_f32<TWO>(a0, a1, dy, r);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) res[i] = put_lane(res[i], r[i], k, lane);
+                }
+                const int fl = f0 + kStride4 * lane;
+                if (lane < k) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (fl + i * W < E) outp[fl + i * W] = res[i];
+                }
+            }
+            return;
+        }
         constexpr int kStride = 2 * kTrainWaves;
         for (int f0 = wave; f0 < E; f0 += 64 * kStride) {
             T resa = T(0), resb = T(0);
