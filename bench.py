@@ -384,7 +384,8 @@ def train_main(a, world, rank, dev):
         tr = gd.train.FusedV24Trainer(model, lf, graph=not a.no_graph, warmup=2)
     else:
         tr = gd.train.Trainer(model, lf, graph=not a.no_graph, warmup=2)   # captured after 2 eager steps
-    x, y = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
+    x, y = gd.data.toric_batch(H, a.batch, seed=a.seed, offset=rank * a.batch, device=dev,
+                               dtype=dtype)
     data = gd.data.make_batch(x, model.graph(dev))
     for _ in range(a.warmup):
         tr.step(data, y)
@@ -487,13 +488,17 @@ def main():
     if a.model == 'v22':                         # the oracle takes the edge types with the weights
         state['edge_types'] = model.types
     classical = a.model in ('cgnni', 'cbp')
+    # each rank draws its slice [rank*batch, (rank+1)*batch) of ONE global batch (Philox keyed
+    # by the global codeword index): the all-reduced BER/FER counts of an N-GPU run equal a
+    # single-GPU decode of the same N*batch codewords
+    off = rank * a.batch
     if classical:
         # uniform random codewords (the CGNNI decoder is not symmetric under codeword
         # translation, so the reference's constant-word input would flatter it)
-        x, labels = gd.data.awgn_batch(H, a.batch, codewords='random', seed=a.seed * 1000 + rank,
+        x, labels = gd.data.awgn_batch(H, a.batch, codewords='random', seed=a.seed, offset=off,
                                        device=dev, dtype=dtype)
     else:
-        x, labels = gd.data.toric_batch(H, a.batch, seed=a.seed * 1000 + rank, device=dev, dtype=dtype)
+        x, labels = gd.data.toric_batch(H, a.batch, seed=a.seed, offset=off, device=dev, dtype=dtype)
     if io_dtype != dtype:
         x = x.to(io_dtype)                       # bf16 storage (outside the timed region)
     w = model.prepared_weights(dtype, dev)

@@ -80,6 +80,12 @@ struct GraphView {            // passed by value to kernels
     // The identity layout (vgroup 1) is var_ord with positions = edge ids, spare = E.
     const uint2* vlay;        // [V]
     int vgroup, spare, P1;
+    // where this graph's rows sit in the caller's batch layout.  A whole graph: identity
+    // (xs = N, xv0 = 0, xc0 = V, os = V, o0 = 0, es = E, e0 = 0).  A COMPONENT of a split
+    // graph (gnnd_graph::comp) addresses its slice of the parent codeword's rows: variable v
+    // of codeword b is x row b*xs + xv0 + v and out row b*os + o0 + v, check c is x row
+    // b*xs + xc0 + c, edge e is per-edge row b*es + e0 + e (training tape, m^T).
+    int xs, xv0, xc0, os, o0, es, e0;
 };
 #define GNND_SLOT_PAD 0x80000000u   // padding slot: variable 0, flag bit 31
 
@@ -95,7 +101,18 @@ struct gnnd_graph {
                               // yields T_v = S_v + x_v directly (T-layout resident models)
     void* dev;                // single device allocation holding every table
     size_t table_bytes;       // bytes of the four CSR/CSC tables (staged to LDS)
+    // Disconnected Tanner graphs (the toric code's X and Z halves): ncomp >= 2 equal-shaped
+    // components, each a contiguous variable range, check range and edge range, with the
+    // same slot plans.  comp[k] is component k as a graph of its own (local ids, addressing
+    // fields pointing into the parent rows); dcomp is a device array [3][ncomp] of the
+    // components' view / rview / pview, so ONE launch can run every component of every
+    // codeword as independent workgroups (no exchange: the components share no edge).
+    int ncomp;                // 1: not split
+    gnnd_graph* comp[8];
+    GraphView* dcomp;
+    int nosplit;              // gnnd_graph_set_split(g, 0): decode / train the graph whole
 };
+constexpr int kMaxComp = 8;
 
 // int tables staged to LDS in this order: edge_vc[E], var_ptr[V+1], chk_ptr[C+1], chk_edge[E]
 __host__ __device__ inline int graph_table_ints(int V, int C, int E) {

@@ -89,7 +89,7 @@ extern "C" int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32
     if (dtype != GNND_F32 && dtype != GNND_F64 && dtype != GNND_BF16) return GNND_ERR_INVALID_ARG;
     if (dtype == GNND_BF16) dtype = GNND_F32;          // fp32 arithmetic and LDS
     Plan p;
-    int rc = make_plan(model, dtype, g, &p);
+    int rc = plan_for(model, dtype, g, &p);
     if (rc != GNND_OK) return rc;
     *h_cw = p.cw;
     *h_lds = (int32_t)p.lds;
@@ -101,7 +101,7 @@ extern "C" int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32
     if (dtype != GNND_F32 && dtype != GNND_F64 && dtype != GNND_BF16) return GNND_ERR_INVALID_ARG;
     if (dtype == GNND_BF16) dtype = GNND_F32;
     Plan p;
-    int rc = make_plan(model, dtype, g, &p);
+    int rc = plan_for(model, dtype, g, &p);
     if (rc != GNND_OK) return rc;
     h_plan[0] = p.cw;
     h_plan[1] = (int32_t)p.lds;

@@ -365,13 +365,13 @@ template <int N, typename F, int I = 0> __device__ __forceinline__ void static_f
     }
 }
 // The unit sum in a FIXED order independent of how the units are spread over lanes: chain j
-// (0..3) accumulates units k = 4i + j (i ascending), chain 0 starting from the linear part,
-// and the MLP value is (c0 + c1) + (c2 + c3).  A call evaluates NC consecutive chains from
-// J0 and returns their sum in that tree (NC = 4: the whole MLP; NC = 2 / 1: a half / a
-// quarter, the unit-split small-batch kernel combining the other waves' parts through LDS),
-// so every split gives the same bits.  TWO: the 2-input MLP (u0 -> W1a', u1 -> W1b').
-// wg: the MLP's prepared weights in global memory (uniform address: scalar loads; J0 is a
-// template argument so the weight offsets stay compile-time).
+// (0..7) accumulates units k = 8i + j (i ascending), chain 0 starting from the linear part,
+// and the MLP value is ((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7)).  A call evaluates
+// NC consecutive chains from J0 and returns their sum in that tree (NC = 8: the whole MLP;
+// NC = 4 / 2 / 1: a half / quarter / eighth, the unit-split small-batch kernel combining the
+// other waves' parts through LDS), so every split gives the same bits.  TWO: the 2-input MLP
+// (u0 -> W1a', u1 -> W1b').  wg: the MLP's prepared weights in global memory (uniform
+// address: scalar loads; J0 is a template argument so the weight offsets stay compile-time).
 template <int NC, int J0, bool TWO>
 __device__ __forceinline__ f32x2 mlp128_chains(const float* __restrict__ wg, const V24Lin& lin,
                                                f32x2 u0, f32x2 u1) {
@@ -388,12 +388,12 @@ __device__ __forceinline__ f32x2 mlp128_chains(const float* __restrict__ wg, con
         else
             c[0] = __builtin_elementwise_fma(u0, f32x2{lin.a0, lin.a0}, f32x2{lin.b, lin.b});
     }
-    constexpr int kUnroll = NC == 1 ? 8 : NC == 2 ? 4 : 2;   // 8 units per loop trip
+    constexpr int kUnroll = 8 / NC;                          // 8 units per loop trip
 #pragma unroll kUnroll
-    for (int i = 0; i < 32; ++i) {
+    for (int i = 0; i < 16; ++i) {
         static_for<NC>([&](auto jc) {
-            constexpr int j = J0 + decltype(jc)::value;         // chain (unit k = 4i + j)
-            const int k = 4 * i + j;
+            constexpr int j = J0 + decltype(jc)::value;         // chain (unit k = 8i + j)
+            const int k = 8 * i + j;
             f32x2 h;
             if constexpr (TWO) {
                 const f32x2 a = wa[k >> 1];
@@ -406,51 +406,60 @@ __device__ __forceinline__ f32x2 mlp128_chains(const float* __restrict__ wg, con
                          : pk_fma_lo(softplus_tail2(h), w2[k >> 1], cj);
         });
     }
-    if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
+    if constexpr (NC == 8) return ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
+    else if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
     else if constexpr (NC == 2) return c[0] + c[1];
     else return c[0];
 }
 __device__ __forceinline__ f32x2 mlp128_sp2(const float* __restrict__ wg, const V24Lin& lin,
                                             f32x2 u) {
-    return mlp128_chains<4, 0, false>(wg, lin, u, u);
+    return mlp128_chains<8, 0, false>(wg, lin, u, u);
 }
 __device__ __forceinline__ f32x2 mlp128x2_sp2(const float* __restrict__ wg, const V24Lin& lin,
                                               f32x2 u0, f32x2 u1) {
-    return mlp128_chains<4, 0, true>(wg, lin, u0, u1);
+    return mlp128_chains<8, 0, true>(wg, lin, u0, u1);
 }
+// item lanes per workgroup of the unit-split streaming kernel: 256, except US = 8 (128 item
+// lanes x 8 waves each = 1024 threads; taken when a codeword's items fit 128 lanes)
+template <int US> constexpr int unit_split_lanes() { return US == 8 ? 128 : GNND_BLOCK; }
 // unit-split evaluation (decode_kernel US > 1): wave-uniform `sub` selects this wave's
-// chains; the US partial sums meet in LDS (buf = [US][GNND_BLOCK] f32x2, one of two buffers
-// used alternately so one barrier per call suffices) and every wave combines them in the
-// tree above.  All threads of the workgroup must call it (barrier).  idle (wave-uniform):
-// the wave holds no live work item (its result is never stored) and skips the units, so
-// the SIMDs' issue goes to the live item waves only.
+// chains; the US partial sums meet in LDS (buf = [US][IL] f32x2, IL = unit_split_lanes, one of
+// two buffers used alternately so one barrier per call suffices) and every wave combines them
+// in the tree above.  All threads of the workgroup must call it (barrier).  idle
+// (wave-uniform): the wave holds no live work item (its result is never stored) and skips the
+// units, so the SIMDs' issue goes to the live item waves only.
 template <int US, bool TWO>
 __device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, const V24Lin& lin,
                                               f32x2 u0, f32x2 u1, int sub, f32x2* buf, int itid,
                                               bool idle) {
+    constexpr int IL = unit_split_lanes<US>();
     f32x2 p = {0.f, 0.f};
     if constexpr (US == 1) {
-        if (!idle) p = mlp128_chains<4, 0, TWO>(wg, lin, u0, u1);
+        if (!idle) p = mlp128_chains<8, 0, TWO>(wg, lin, u0, u1);
         return p;
     } else {
-        if (idle) {
-        } else if constexpr (US == 2) {
-            p = sub == 0 ? mlp128_chains<2, 0, TWO>(wg, lin, u0, u1)
-                         : mlp128_chains<2, 2, TWO>(wg, lin, u0, u1);
-        } else {
-            static_assert(US == 4, "unit split 1, 2 or 4");
+        static_assert(US == 2 || US == 4 || US == 8, "unit split 1, 2, 4 or 8");
+        constexpr int NC = 8 / US;
+        if (!idle) {
             switch (sub) {
-                case 0: p = mlp128_chains<1, 0, TWO>(wg, lin, u0, u1); break;
-                case 1: p = mlp128_chains<1, 1, TWO>(wg, lin, u0, u1); break;
-                case 2: p = mlp128_chains<1, 2, TWO>(wg, lin, u0, u1); break;
-                default: p = mlp128_chains<1, 3, TWO>(wg, lin, u0, u1); break;
+                case 0: p = mlp128_chains<NC, 0, TWO>(wg, lin, u0, u1); break;
+                case 1: p = mlp128_chains<NC, NC, TWO>(wg, lin, u0, u1); break;
+                case 2: if constexpr (US >= 4) p = mlp128_chains<NC, (2 * NC) & 7, TWO>(wg, lin, u0, u1); break;
+                case 3: if constexpr (US >= 4) p = mlp128_chains<NC, (3 * NC) & 7, TWO>(wg, lin, u0, u1); break;
+                case 4: if constexpr (US == 8) p = mlp128_chains<1, 4, TWO>(wg, lin, u0, u1); break;
+                case 5: if constexpr (US == 8) p = mlp128_chains<1, 5, TWO>(wg, lin, u0, u1); break;
+                case 6: if constexpr (US == 8) p = mlp128_chains<1, 6, TWO>(wg, lin, u0, u1); break;
+                default: if constexpr (US == 8) p = mlp128_chains<1, 7, TWO>(wg, lin, u0, u1); break;
             }
         }
-        buf[sub * GNND_BLOCK + itid] = p;
+        buf[sub * IL + itid] = p;
         __syncthreads();
-        if constexpr (US == 2) return buf[itid] + buf[GNND_BLOCK + itid];
-        else return (buf[itid] + buf[GNND_BLOCK + itid]) +
-                    (buf[2 * GNND_BLOCK + itid] + buf[3 * GNND_BLOCK + itid]);
+        if constexpr (US == 2) return buf[itid] + buf[IL + itid];
+        else if constexpr (US == 4)
+            return (buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid]);
+        else
+            return ((buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid])) +
+                   ((buf[4 * IL + itid] + buf[5 * IL + itid]) + (buf[6 * IL + itid] + buf[7 * IL + itid]));
     }
 }
 // linear parts, identical in every thread (fixed summation order)
@@ -722,17 +731,28 @@ template <typename T> struct TapeView {
 // US (unit split, fp32 decoder_v2_4 small batches): US waves share each wave of work items,
 // each evaluating a quarter / half of every 128-hidden MLP's units (mlp128_split), so a
 // latency-bound batch of a few codewords per workgroup keeps 4 / 2 times as many waves busy.
+// Split graphs (gnnd_graph::comp, `views` non-null): blocks [k*cblk, (k+1)*cblk) decode
+// component k of every codeword, each block a tile of CW codewords of that component's graph
+// views[k]; the component's rows are addressed through its GraphView addressing fields.
 template <int MODEL, typename T, int R, bool TAPE = false, int US = 1>
-__global__ void __launch_bounds__(GNND_BLOCK * US)
-decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict__ x,
+__global__ void __launch_bounds__(unit_split_lanes<US>() * US)
+decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict__ x,
               T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
-              FastDiv dN, TapeView<T> tape) {
+              FastDiv dN, TapeView<T> tape, const GraphView* __restrict__ views, int cblk) {
     using M = EdgeMath<MODEL, T>;
     constexpr bool BP = ModelTraits<MODEL>::bp;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    int blk = blockIdx.x;
+    GraphView g = g0;
+    if (views) {                       // uniform: component k of the split graph
+        const int k = blk / cblk;
+        g = views[k];
+        blk -= k * cblk;
+    }
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
-    constexpr int NT = GNND_BLOCK * US;
+    constexpr int IL = unit_split_lanes<US>();        // work-item lanes
+    constexpr int NT = IL * US;
     static_assert(US == 1 || (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2),
                   "unit split: fp32 decoder_v2_4 on one slot pair per lane");
     // work-item lane (0..255) and the wave's unit chunk: waves w = US i + sub share item wave i
@@ -758,21 +778,21 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
-    // unit split: two [US][256] f32x2 buffers for the MLP partial sums (8-byte aligned)
+    // unit split: two [US][IL] f32x2 buffers for the MLP partial sums (8-byte aligned)
     f32x2* s_part = (f32x2*)(((uintptr_t)(s_xc + (size_t)CW * C) + 7) & ~(uintptr_t)7);
 
     for (int i = tid; i < nw; i += NT) s_w[i] = w[i];
     for (int i = tid; i < nslot; i += NT) s_slot[i] = g.slot_ve[i];   // v | e << 16
     for (int i = tid; i <= V; i += NT) s_vptr[i] = g.var_ptr[i];
     for (int i = tid; i < E; i += NT) s_vslot[i] = g.vslot[i];
-    const int64_t b0 = (int64_t)blockIdx.x * CW;
+    const int64_t b0 = (int64_t)blk * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
-    const T* xg = x + b0 * N;
+    // the tile's rows (whole graph: one contiguous run of nb*N values)
     for (int i = tid; i < nb * N; i += NT) {
         int b = fdiv(i, dN), n = i - b * N;
-        T xv = xg[i];
-        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xv};
-        else s_xc[b * C + n - V] = xv;
+        const T* xr = x + (size_t)(b0 + b) * g.xs;
+        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xr[g.xv0 + n]};
+        else s_xc[b * C + n - V] = xr[g.xc0 + n - V];
     }
     for (int i = tid; i < nb * nslot; i += NT) s_m[i] = T(0);
     __syncthreads();
@@ -800,7 +820,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
     const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
     const int nV = nb * V;
     for (int it = 0; it < iters; ++it) {
-        for (int f0 = 0; f0 < nItem; f0 += GNND_BLOCK) {
+        for (int f0 = 0; f0 < nItem; f0 += IL) {
             const int f = f0 + itid;
             const bool act = f < nItem;
             const bool own = act && sub == 0;            // the unit-split waves' writer
@@ -841,7 +861,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     for (int r = 0; r < R; ++r) {
                         const int e = (int)(sl[r] >> 16);
                         if (own && e != E) {
-                            const size_t row = ((size_t)it * B + b0 + b) * E + e;
+                            const size_t row = ((size_t)it * B + b0 + b) * g.es + g.e0 + e;
                             tape.ext[row] = ext[r];
                             tape.t[row] = tv[r];
                         }
@@ -889,7 +909,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     if constexpr (BP) csum += cf[r];
                     if constexpr (TAPE) {
                         if (act && valid) {
-                            const size_t row = ((size_t)it * B + b0 + b) * E + (int)(sv >> 16);
+                            const size_t row = ((size_t)it * B + b0 + b) * g.es + g.e0 + (int)(sv >> 16);
                             tape.ext[row] = p.s - mv[r];
                             tape.t[row] = t;
                         }
@@ -905,7 +925,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int e = (int)(sl[r] >> 16);
-                    if (own && e != E) tape.u[((size_t)it * B + b0 + b) * E + e] = Sc - tv[r];
+                    if (own && e != E) tape.u[((size_t)it * B + b0 + b) * g.es + g.e0 + e] = Sc - tv[r];
                 }
             }
             if constexpr (kV24F32) {
@@ -914,7 +934,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
                     const int r1 = r + 1 < R ? r + 1 : r;
                     const f32x2 uu = {Sc - tv[r], Sc - tv[r1]};
                     const f32x2 y = mlp128_split<US, false>(v24.g + kV24Ggc2, v24.l2, uu, uu, sub,
-                                                            s_part + US * GNND_BLOCK, itid, widle);
+                                                            s_part + US * IL, itid, widle);
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
                 }
@@ -949,7 +969,7 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         for (int f = tid; f < nb * nslot; f += NT) {
             const int b = f / nslot, sl = f - b * nslot;
             const int e = (int)(s_slot[sl] >> 16);
-            if (e != E) tape.mT[(size_t)(b0 + b) * E + e] = s_m[f];
+            if (e != E) tape.mT[(size_t)(b0 + b) * g.es + g.e0 + e] = s_m[f];
         }
     }
     if constexpr (MODEL == GNND_V24) {
@@ -967,9 +987,9 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
         }
         __syncthreads();
     }
-    T* og = out + b0 * V;
     for (int f = tid; f < nV; f += NT) {
         const int b = fdiv(f, dV), v = f - b * V;
+        const size_t orow = (size_t)(b0 + b) * g.os + g.o0 + v;
         if constexpr (MODEL == GNND_NBP) {
             // sum_v(m W) + sum_v(x_v W_p)  (neural_BP.py:307-312), each in edge order
             const int k0 = s_vptr[v], ke = s_vptr[v + 1];
@@ -977,10 +997,10 @@ decode_kernel(GraphView g, const T* __restrict__ w, int nw, const T* __restrict_
             const T xv = s_sx[f].x;
             T s2 = T(0);
             for (int k = k0; k < ke; ++k) s2 += xv * ww.out_p(k);
-            og[f] = sigmoid_ref(-(s1 + s2));
+            out[orow] = sigmoid_ref(-(s1 + s2));
         } else {
             const T s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
-            og[f] = M::readout(s + s_sx[f].x, s_w);
+            out[orow] = M::readout(s + s_sx[f].x, s_w);
         }
     }
 }
@@ -1652,14 +1672,25 @@ struct Plan {
     int q;        // work items per lane (resident)
     size_t lds;   // bytes of dynamic LDS
     int us = 1;   // unit split of the streaming kernel (fp32 decoder_v2_4, small batches)
+    int ncomp = 1;                       // split graph: components per codeword (streaming)
+    const GraphView* dviews = nullptr;   // device [ncomp] views of the plan's kind
 };
 
-// GNND_V24_SPLIT=1|2|4 forces the fp32 decoder_v2_4 unit split (A/B); default by batch
+// GNND_NO_SPLIT=1: decode split graphs whole (A/B of the component split)
+bool split_disabled() {
+    static bool v = [] {
+        const char* e = getenv("GNND_NO_SPLIT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+// GNND_V24_SPLIT=1|2|4|8 forces the fp32 decoder_v2_4 unit split (A/B); default by batch
 int v24_split_forced() {
     static int v = [] {
         const char* e = getenv("GNND_V24_SPLIT");
         const int n = e ? atoi(e) : 0;
-        return n == 1 || n == 2 || n == 4 ? n : 0;
+        return n == 1 || n == 2 || n == 4 || n == 8 ? n : 0;
     }();
     return v;
 }
@@ -1778,14 +1809,43 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     p->lds = fixed + n * per;
     // fp32 decoder_v2_4 at one codeword per workgroup (training steps, small decodes) is
     // latency-bound: one wave per SIMD walks 128 hidden units per edge pair.  Split the units
-    // over US waves (B <= 256: 4, one 16-wave workgroup per CU; B <= 512: 2)
+    // over US waves (B <= 256: 8 when a codeword's work items fit 128 lanes (1024 threads),
+    // else 4, one 16-wave workgroup per CU; B <= 512: 2).  The partial-sum buffers must fit.
     p->us = 1;
     if (v24f32 && n == 1 && g.R <= 2) {
         const int forced = v24_split_forced();
-        p->us = forced ? forced : B <= 256 ? 4 : B <= 512 ? 2 : 1;
+        const bool fit128 = (size_t)g.C * g.G <= 128;
+        int us = forced ? forced : B <= 256 ? (fit128 ? 8 : 4) : B <= 512 ? 2 : 1;
+        if (us == 8 && !fit128) us = 4;
+        const size_t il = us == 8 ? 128 : GNND_BLOCK;
+        if (us > 1 && align16(p->lds) + (size_t)2 * us * il * 8 + 8 <= kLdsMax) {
+            p->us = us;
+            p->lds = align16(p->lds) + (size_t)2 * us * il * 8 + 8;
+        }
     }
-    if (p->us > 1) p->lds = align16(p->lds) + (size_t)2 * p->us * GNND_BLOCK * 8 + 8;
     return GNND_OK;
+}
+
+// The launch plan, split over the graph's components where that applies: decoder_v2_4's
+// streaming kernel on a split graph (gnnd_graph::comp) decodes each component of a codeword in
+// its own workgroup(s); the plan is made for component 0 (all components share its shape and
+// slot plans) at the launch's B * ncomp component-codewords.
+int plan_for(int model, int dtype, const gnnd_graph* g, Plan* p, int64_t B = INT64_MAX) {
+    if (model == GNND_V24 && g->ncomp > 1 && g->dcomp && !g->nosplit && !split_disabled()) {
+        const int K = g->ncomp;
+        const gnnd_graph* c0 = g->comp[0];
+        const int64_t BK = B > INT64_MAX / K ? INT64_MAX : B * K;
+        const int rc = make_plan(model, dtype, c0, p, BK);
+        if (rc != GNND_OK) return rc;
+        if (!p->resident) {
+            const int kind = p->view == &c0->view ? 0 : p->view == &c0->rview ? 1 : 2;
+            if (kind == 2 && p->view != &c0->pview) return GNND_ERR_UNSUPPORTED;
+            p->ncomp = K;
+            p->dviews = g->dcomp + (size_t)kind * K;
+            return GNND_OK;
+        }
+    }
+    return make_plan(model, dtype, g, p, B);
 }
 
 template <int MODEL, typename T, int R, typename TI = T>
@@ -1803,6 +1863,21 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
         kern<<<(unsigned)blocks, GNND_BLOCK * us, p.lds, st>>>(g, (const T*)w, nw, (const TI*)x, (TI*)out,
                                                                B, iters, p.cw, dI, dV, dN, tape);
+        GNND_LAUNCH_CHECK();
+        return GNND_OK;
+    };
+    // the streaming kernel: every component of a split graph in the same launch
+    auto go_s = [&](auto kern, int us = 1) -> int {
+        if (p.lds > 64 * 1024)
+            GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
+        const int64_t grid = blocks * p.ncomp;
+        if (grid > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
+        const int il = us == 8 ? 128 : GNND_BLOCK;          // unit_split_lanes<US>()
+        kern<<<(unsigned)grid, il * us, p.lds, st>>>(g, (const T*)w, nw, (const TI*)x, (TI*)out,
+                                                             B, iters, p.cw, dI, dV, dN, tape,
+                                                             p.ncomp > 1 ? p.dviews : nullptr,
+                                                             (int)blocks);
         GNND_LAUNCH_CHECK();
         return GNND_OK;
     };
@@ -1841,15 +1916,17 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         return GNND_ERR_UNSUPPORTED;
     } else {
         if constexpr (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2) {
-            if (p.us == 4) return tape.ext ? go(decode_kernel<MODEL, T, R, true, 4>, 4)
-                                           : go(decode_kernel<MODEL, T, R, false, 4>, 4);
-            if (p.us == 2) return tape.ext ? go(decode_kernel<MODEL, T, R, true, 2>, 2)
-                                           : go(decode_kernel<MODEL, T, R, false, 2>, 2);
+            if (p.us == 8) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 8>, 8)
+                                           : go_s(decode_kernel<MODEL, T, R, false, 8>, 8);
+            if (p.us == 4) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 4>, 4)
+                                           : go_s(decode_kernel<MODEL, T, R, false, 4>, 4);
+            if (p.us == 2) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 2>, 2)
+                                           : go_s(decode_kernel<MODEL, T, R, false, 2>, 2);
         }
         if (p.us != 1) return GNND_ERR_UNSUPPORTED;
         if constexpr (MODEL == GNND_V24)
-            if (tape.ext) return go(decode_kernel<MODEL, T, R, true>);
-        return go(decode_kernel<MODEL, T, R>);
+            if (tape.ext) return go_s(decode_kernel<MODEL, T, R, true>);
+        return go_s(decode_kernel<MODEL, T, R>);
     }
 }
 
@@ -1858,7 +1935,7 @@ template <int MODEL, typename T, typename TI = T>
 int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
                     int iters, hipStream_t st, void* tape_base = nullptr) {
     Plan p;
-    int rc = make_plan(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p, B);
+    int rc = plan_for(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p, B);
     if (rc != GNND_OK) return rc;
     TapeView<T> tape{};
     if (tape_base) {                        // [ext | u | t] x [iters][B][E], then mT [B][E]

@@ -314,9 +314,11 @@ extern "C" int gnnd_graph_validate_host(const int64_t* h_var, const int64_t* h_c
     return check_tables(T, h_report4);
 }
 
-extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
-                                 int32_t V, int32_t C, gnnd_graph** out) {
-    if (!out) return GNND_ERR_INVALID_ARG;
+namespace {
+
+// one graph without component analysis (gnnd_graph_create adds it)
+int create_single(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, int32_t V,
+                  int32_t C, gnnd_graph** out) {
     *out = nullptr;
     HostTables T;
     const int rc = build_tables(h_var, h_chk, num_edges, V, C, T);
@@ -345,6 +347,8 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     gv.chk_ptr = d + E + V + 1;
     gv.chk_edge = d + E + V + 1 + C + 1;
     gv.var_ord = (const uint2*)(d + ord_off);
+    gv.xs = V + C; gv.xv0 = 0; gv.xc0 = V; gv.os = V; gv.o0 = 0; gv.es = E; gv.e0 = 0;
+    g->ncomp = 1;
     g->rview = gv;
     g->pview = gv;
     for (int i = 0; i < 3; ++i) {
@@ -380,11 +384,142 @@ extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int
     return GNND_OK;
 }
 
-extern "C" int gnnd_graph_destroy(gnnd_graph* g) {
-    if (!g) return GNND_ERR_INVALID_ARG;
-    hipError_t err = hipFree(g->dev);
+int destroy_graph(gnnd_graph* g) {
+    hipError_t err = hipSuccess;
+    for (int k = 0; k < g->ncomp && g->ncomp > 1; ++k)
+        if (g->comp[k]) {
+            const int rc = destroy_graph(g->comp[k]);
+            if (rc != GNND_OK && err == hipSuccess) err = (hipError_t)gnnd_last_hip_error();
+        }
+    if (g->dcomp) {
+        const hipError_t e = hipFree(g->dcomp);
+        if (err == hipSuccess) err = e;
+    }
+    const hipError_t e = hipFree(g->dev);
+    if (err == hipSuccess) err = e;
     free(g);
     return err == hipSuccess ? GNND_OK : set_hip_error(err);
+}
+
+bool same_plan(const GraphView& a, const GraphView& b) {
+    return a.V == b.V && a.C == b.C && a.E == b.E && a.max_dv == b.max_dv &&
+           a.max_dc == b.max_dc && a.G == b.G && a.R == b.R && a.padded == b.padded &&
+           a.padr == b.padr;
+}
+
+// Connected components of the Tanner graph (union-find over variables through checks).
+// The split is kept only when there are 2..kMaxComp components, each a contiguous variable
+// range with a contiguous check range (so its edges are contiguous in the (v, c) order too),
+// all of one shape and slot plan: then every component decodes as an independent codeword
+// of a smaller graph, in its own workgroup.  The toric code (quantum/error_generate.py:39-132,
+// H = [[H_x, 0], [0, H_z]] up to the removed rows) splits into its X and Z halves.
+void split_components(gnnd_graph* g, const int64_t* h_var, const int64_t* h_chk) {
+    const int V = g->view.V, C = g->view.C, E = g->view.E;
+    std::vector<int> par(V);
+    for (int v = 0; v < V; ++v) par[v] = v;
+    auto find = [&](int v) {
+        while (par[v] != v) v = par[v] = par[par[v]];
+        return v;
+    };
+    std::vector<int> cfirst(C, -1);
+    for (int e = 0; e < E; ++e) {
+        const int v = (int)h_var[e], c = (int)h_chk[e];
+        if (cfirst[c] < 0) { cfirst[c] = v; continue; }
+        const int a = find(v), b = find(cfirst[c]);
+        if (a != b) par[a < b ? b : a] = a < b ? a : b;     // root = smallest variable
+    }
+    // components in order of their first variable; contiguity: variable v's root changes
+    // only at component boundaries
+    std::vector<int> vstart;
+    for (int v = 0; v < V; ++v)
+        if (find(v) == v) vstart.push_back(v);
+    const int K = (int)vstart.size();
+    if (K < 2 || K > kMaxComp || V % K) return;
+    for (int v = 0; v < V; ++v) {
+        int k = (int)(std::upper_bound(vstart.begin(), vstart.end(), v) - vstart.begin()) - 1;
+        if (find(v) != vstart[k]) return;                     // not a contiguous range
+    }
+    const int Vk = V / K;
+    for (int k = 0; k < K; ++k)
+        if (vstart[k] != k * Vk) return;                      // unequal sizes
+    if (C % K || E % K) return;
+    const int Ck = C / K, Ek = E / K;
+    for (int c = 0; c < C; ++c)                               // check ranges contiguous, ordered
+        if (cfirst[c] < 0 || cfirst[c] / Vk != c / Ck) return;
+    for (int k = 0; k < K; ++k)                               // edge ranges (sorted by v)
+        if ((int)h_var[k * Ek] / Vk != k || (int)h_var[k * Ek + Ek - 1] / Vk != k) return;
+    gnnd_graph* comp[kMaxComp] = {};
+    std::vector<int64_t> sv(Ek), sc(Ek);
+    bool ok = true;
+    for (int k = 0; k < K && ok; ++k) {
+        for (int i = 0; i < Ek; ++i) {
+            sv[i] = h_var[k * Ek + i] - (int64_t)k * Vk;
+            sc[i] = h_chk[k * Ek + i] - (int64_t)k * Ck;
+        }
+        ok = create_single(sv.data(), sc.data(), Ek, Vk, Ck, &comp[k]) == GNND_OK;
+        if (ok && k > 0)
+            ok = same_plan(comp[k]->view, comp[0]->view) && same_plan(comp[k]->rview, comp[0]->rview) &&
+                 same_plan(comp[k]->pview, comp[0]->pview);
+    }
+    std::vector<GraphView> dv(3 * (size_t)K);
+    if (ok) {
+        for (int k = 0; k < K; ++k) {
+            gnnd_graph* ck = comp[k];
+            auto patch = [&](GraphView& v) {
+                v.xs = V + C; v.xv0 = k * Vk; v.xc0 = V + k * Ck;
+                v.os = V; v.o0 = k * Vk;
+                v.es = E; v.e0 = k * Ek;
+            };
+            patch(ck->view); patch(ck->rview); patch(ck->pview);
+            for (int i = 0; i < 7; ++i) { patch(ck->rlay[i]); patch(ck->rlayx[i]); }
+            dv[k] = ck->view;
+            dv[K + k] = ck->rview;
+            dv[2 * K + k] = ck->pview;
+        }
+        ok = hipMalloc(&g->dcomp, sizeof(GraphView) * dv.size()) == hipSuccess;
+        if (ok && hipMemcpy(g->dcomp, dv.data(), sizeof(GraphView) * dv.size(),
+                            hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(g->dcomp);
+            ok = false;
+        }
+        if (!ok) g->dcomp = nullptr;
+    }
+    if (!ok) {
+        for (int k = 0; k < K; ++k)
+            if (comp[k]) destroy_graph(comp[k]);
+        (void)hipGetLastError();
+        return;
+    }
+    g->ncomp = K;
+    for (int k = 0; k < K; ++k) g->comp[k] = comp[k];
+}
+
+}  // namespace
+
+extern "C" int gnnd_graph_create(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
+                                 int32_t V, int32_t C, gnnd_graph** out) {
+    if (!out) return GNND_ERR_INVALID_ARG;
+    const int rc = create_single(h_var, h_chk, num_edges, V, C, out);
+    if (rc != GNND_OK) return rc;
+    split_components(*out, h_var, h_chk);
+    return GNND_OK;
+}
+
+extern "C" int gnnd_graph_destroy(gnnd_graph* g) {
+    if (!g) return GNND_ERR_INVALID_ARG;
+    return destroy_graph(g);
+}
+
+extern "C" int gnnd_graph_components(const gnnd_graph* g, int32_t* h_ncomp) {
+    if (!g || !h_ncomp) return GNND_ERR_INVALID_ARG;
+    *h_ncomp = g->ncomp;
+    return GNND_OK;
+}
+
+extern "C" int gnnd_graph_set_split(gnnd_graph* g, int32_t enable) {
+    if (!g) return GNND_ERR_INVALID_ARG;
+    g->nosplit = enable ? 0 : 1;
+    return GNND_OK;
 }
 
 extern "C" int gnnd_graph_dims(const gnnd_graph* g, int32_t* d) {

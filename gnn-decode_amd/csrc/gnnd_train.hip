@@ -286,13 +286,24 @@ template <typename T> struct Units {
     }
 };
 
+// Split graphs (views non-null): blocks [k*cblk, (k+1)*cblk) run component k (graph views[k],
+// rows addressed through its GraphView addressing fields) of codewords j, j + cblk, ...
 template <typename T, int kTrainThreads = train_threads<T>()>
 __global__ void __launch_bounds__(kTrainThreads)
-v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
+v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                const T* __restrict__ p, const T* __restrict__ gp, TapeView<T> tape,
-               T* __restrict__ gpart, int64_t B, int iters) {
+               T* __restrict__ gpart, int64_t B, int iters, const GraphView* __restrict__ views,
+               int cblk) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int V = g.V, C = g.C, E = g.E, N = g.N;
+    GraphView g = g0;
+    int blk = blockIdx.x, nblk = gridDim.x;
+    if (views) {                       // uniform: component k
+        const int k = blk / cblk;
+        g = views[k];
+        blk -= k * cblk;
+        nblk = cblk;
+    }
+    const int V = g.V, C = g.C, E = g.E;
     constexpr int kTrainWaves = kTrainThreads / 64;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: edge loops on SALU
@@ -387,9 +398,9 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
     // persistent over codewords b = blockIdx.x, blockIdx.x + gridDim.x, ...: the lanes'
     // gradient registers accumulate across all of them (one partial row per workgroup, any
     // batch size, LDS independent of B)
-    for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    for (int64_t b = blk; b < B; b += nblk) {
         auto prefetch = [&](int it) {
-            const size_t trow = ((size_t)it * B + b) * E;
+            const size_t trow = ((size_t)it * B + b) * g.es + g.e0;
 #pragma unroll
             for (int i = 0; i < kPF; ++i) {
                 const int f = tid + i * kTrainThreads;
@@ -402,7 +413,7 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
                 const int f = tid + i * kTrainThreads;
                 if (f < E) { s_u[f] = pu[i]; s_t[f] = pt[i]; s_ext[f] = pe[i]; }
             }
-            const size_t trow = ((size_t)it * B + b) * E;
+            const size_t trow = ((size_t)it * B + b) * g.es + g.e0;
             for (int f = tid + kPF * kTrainThreads; f < E; f += kTrainThreads) {
                 s_u[f] = tape.u[trow + f];
                 s_t[f] = tape.t[trow + f];
@@ -411,14 +422,14 @@ v24_bwd_kernel(GraphView g, const T* __restrict__ w, const T* __restrict__ x,
         };
         if (iters > 0) prefetch(iters - 1);
         // readout inputs: m^T into s_u, d loss / d r per edge into s_da; per-edge x_v, s_c
-        const T* xb = x + (size_t)b * N;
+        const T* xb = x + (size_t)b * g.xs;
         for (int f = tid; f < E; f += kTrainThreads) {
             const uint32_t vc = s_evc[f];
-            const size_t bv = (size_t)b * V + (int)(vc & 0xffffu);
+            const size_t bv = (size_t)b * g.os + g.o0 + (int)(vc & 0xffffu);
             const T pv = p[bv];
-            s_xv[f] = xb[vc & 0xffffu];
-            s_sc[f] = xb[V + (int)(vc >> 16)];
-            s_u[f] = tape.mT[(size_t)b * E + f];
+            s_xv[f] = xb[g.xv0 + (int)(vc & 0xffffu)];
+            s_sc[f] = xb[g.xc0 + (int)(vc >> 16)];
+            s_u[f] = tape.mT[(size_t)b * g.es + g.e0 + f];
             s_da[f] = -((gp[bv] * (T(1) - pv)) * pv);     // p = sigmoid(-r)
         }
         __syncthreads();
@@ -488,19 +499,35 @@ __global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __r
 // larger batches loop (each workgroup a fixed, strided set of codewords: deterministic)
 constexpr int64_t kTrainMaxBlocks = 1024;
 int64_t train_blocks(int64_t B) { return B < kTrainMaxBlocks ? B : kTrainMaxBlocks; }
+// the reverse pass on a split graph: each component of a codeword in its own workgroup
+bool train_split(const gnnd_graph* g) {
+    return g->ncomp > 1 && g->dcomp && !g->nosplit && !split_disabled();
+}
+// workgroups per component and in all (<= kTrainMaxBlocks gradient rows)
+int64_t train_cblk(const gnnd_graph* g, int64_t B) {
+    if (!train_split(g)) return train_blocks(B);
+    const int64_t per = kTrainMaxBlocks / g->ncomp;
+    return B < per ? B : per;
+}
+int64_t train_rows(const gnnd_graph* g, int64_t B) {
+    return train_split(g) ? train_cblk(g, B) * g->ncomp : train_blocks(B);
+}
 size_t train_lds(const gnnd_graph* g, int esz) {
     const GraphView& v = g->view;
     return (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
            (size_t)esz * (8 * (size_t)v.E + kV24W);
 }
 
+// gw == nullptr: leave the per-workgroup partial rows in ws (gnnd_train_bwd_partial)
 template <typename T>
 int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* out,
                const void* gout, const void* tape, void* gw, void* ws, int64_t ws_bytes,
                int64_t B, int iters, hipStream_t st) {
-    const int64_t blocks = train_blocks(B);
+    const bool split = train_split(g);
+    const gnnd_graph* gk = split ? g->comp[0] : g;        // components share one shape
+    const int64_t cblk = train_cblk(g, B), blocks = train_rows(g, B);
     if ((int64_t)blocks * kV24W * (int64_t)sizeof(T) > ws_bytes) return GNND_ERR_INVALID_ARG;
-    const size_t lds = train_lds(g, sizeof(T));
+    const size_t lds = train_lds(gk, sizeof(T));
     if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     auto kern = v24_bwd_kernel<T>;
     if (lds > 64 * 1024)
@@ -509,10 +536,11 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     const size_t n = (size_t)iters * B * g->view.E;
     T* base = (T*)tape;
     TapeView<T> tv{base, base + n, base + 2 * n, base + 3 * n};
-    kern<<<(unsigned)blocks, train_threads<T>(), lds, st>>>(g->view, (const T*)w, (const T*)x,
-                                                      (const T*)out, (const T*)gout, tv, (T*)ws,
-                                                      B, iters);
+    kern<<<(unsigned)blocks, train_threads<T>(), lds, st>>>(
+        gk->view, (const T*)w, (const T*)x, (const T*)out, (const T*)gout, tv, (T*)ws, B, iters,
+        split ? g->dcomp : nullptr, (int)cblk);   // dcomp[0..K): the components' `view`
     GNND_LAUNCH_CHECK();
+    if (!gw) return GNND_OK;
     grad_reduce_kernel<T><<<(kV24W + 255) / 256, 256, 0, st>>>((const T*)ws, (int)blocks, (T*)gw);
     GNND_LAUNCH_CHECK();
     return GNND_OK;
@@ -716,29 +744,156 @@ int launch_decision_errors(const gnnd_graph* g, const int32_t* lg, int nl, const
 // t = step + 1;  p += -(lr / (1 - b1^t)) * (m / (sqrt(v) / sqrt(1 - b2^t) + eps)).
 // Bias corrections in double (torch computes them as Python floats).  ONE workgroup: the
 // counter is read by every thread and written back after a barrier.
+// one parameter's update (shared by adam_kernel and train_update_kernel: same code, same bits)
+template <typename T> struct AdamCoef {
+    T step_size, bc2s, w1, tb2, w2, te, twd;
+    bool decay;
+    // bias corrections of step t (double pow, as torch computes them on the host)
+    __device__ static T step_size_of(double t, double lr, double b1) { return (T)(lr / (1.0 - pow(b1, t))); }
+    __device__ static T bc2s_of(double t, double b2) { return (T)sqrt(1.0 - pow(b2, t)); }
+    __device__ AdamCoef(T ss, T bc, double b1, double b2, double eps, double wd)
+        : step_size(ss), bc2s(bc), w1((T)(1.0 - b1)), tb2((T)b2), w2((T)(1.0 - b2)), te((T)eps),
+          twd((T)wd), decay(wd != 0.0) {}
+};
+template <typename T>
+__device__ __forceinline__ T adam_one(const AdamCoef<T>& c, T pi, T gi, T& mi_io, T& vi_io) {
+    if (c.decay) gi = __builtin_fma(c.twd, pi, gi);
+    const T mi = __builtin_fma(c.w1, gi - mi_io, mi_io);
+    const T vi = __builtin_fma(c.w2 * gi, gi, vi_io * c.tb2);
+    mi_io = mi;
+    vi_io = vi;
+    const T denom = sqrt(vi) / c.bc2s + c.te;
+    return __builtin_fma(-c.step_size, mi / denom, pi);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(1024)
 adam_kernel(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ m, T* __restrict__ v,
             double* __restrict__ step, int64_t n, double lr, double b1, double b2, double eps,
             double wd) {
     const double t = step[0] + 1.0;
-    const T step_size = (T)(lr / (1.0 - pow(b1, t)));
-    const T bc2s = (T)sqrt(1.0 - pow(b2, t));
-    const T w1 = (T)(1.0 - b1), tb2 = (T)b2, w2 = (T)(1.0 - b2), te = (T)eps, twd = (T)wd;
+    const AdamCoef<T> c(AdamCoef<T>::step_size_of(t, lr, b1), AdamCoef<T>::bc2s_of(t, b2), b1, b2,
+                        eps, wd);
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const T pi = p[i];
-        T gi = g[i];
-        if (wd != 0.0) gi = gi + twd * pi;
-        const T mi = m[i] + w1 * (gi - m[i]);
-        T vi = v[i] * tb2;
-        vi = vi + (w2 * gi) * gi;
+        T mi = m[i], vi = v[i];
+        p[i] = adam_one(c, p[i], g[i], mi, vi);
         m[i] = mi;
         v[i] = vi;
-        const T denom = sqrt(vi) / bc2s + te;
-        p[i] = pi + (-step_size) * (mi / denom);
     }
     __syncthreads();
     if (threadIdx.x == 0) step[0] = t;
+}
+
+// ---------------------------------------------------------------------------------------
+// fused optimizer epilogue of a training step (gnnd_train_update): per parameter i
+//   REDUCE  g_i = fixed-order sum of the reverse pass's per-workgroup rows (16 lanes per
+//           parameter: lane j sums rows j, j+16, ... in order, then a fixed LDS tree), written
+//           to grad (if given); otherwise g_i = grad[i] (an all-reduced gradient)
+//   LOSS    block 0 also sums the per-codeword losses in a fixed order -> loss[0]
+//   ADAM    torch.optim.Adam's update (adam_kernel's order) of param/exp_avg/exp_avg_sq, then
+//           the kernel-layout copy of the updated weight (gnnd_prepare_weights' mapping) into
+//           prepared, so the next step's forward needs no prepare launch
+// The step count is read by one lane per block before that block arrives on `sync` (an
+// agent-scope atomic counter); the last block to arrive writes step + 1 and re-arms the
+// counter.  Nothing else crosses workgroups: one launch replaces grad_reduce, the loss sum,
+// Adam and prepare (four ~5 us launches of the single-rank step).
+// ---------------------------------------------------------------------------------------
+constexpr int kUpdLanes = 16;               // lanes per parameter in the row reduction
+
+// plain packed index i of decoder_v2_4 -> (prepared index, scale) of the fp32 kernel layout
+// (prepare_v24_f32_kernel in gnnd_decode.hip)
+__device__ __forceinline__ int v24_prep_index(int i, float& scale) {
+    if (i < kV24Ggc2) {                       // ggc1.mlp: W1a, W1b, b1, W2, b2
+        const int k = i & 127;
+        if (i < 128) { scale = kLog2e; return 256 + k; }
+        if (i < 256) { scale = kLog2e; return 2 * k; }
+        if (i < 384) { scale = kLog2e; return 2 * k + 1; }
+        scale = i < 512 ? kLn2 : 1.f;
+        return i;
+    }
+    const int base = i < kV24Mlp ? kV24Ggc2 : kV24Mlp;   // ggc2.mlp / mlp: W1, b1, W2, b2
+    const int l = i - base, k = l & 127;
+    if (l < 128) { scale = kLog2e; return base + 2 * k; }
+    if (l < 256) { scale = kLog2e; return base + 2 * k + 1; }
+    scale = l < 384 ? kLn2 : 1.f;
+    return i;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+train_update_kernel(const T* __restrict__ rows, int nrows, T* __restrict__ grad,
+                    const T* __restrict__ loss_b, int64_t nloss, T* __restrict__ loss,
+                    T* __restrict__ p, T* __restrict__ m, T* __restrict__ v,
+                    double* __restrict__ step, uint32_t* __restrict__ sync, int n, double lr,
+                    double b1, double b2, double eps, double wd, T* __restrict__ prepared,
+                    int prep_v24_f32) {
+    __shared__ T s_red[256];
+    __shared__ double s_t;
+    __shared__ T s_coef[2];
+    const int tid = threadIdx.x, j = tid % kUpdLanes, q = tid / kUpdLanes;
+    const int i = blockIdx.x * (256 / kUpdLanes) + q;
+    const bool adam = p != nullptr;
+    if (adam && tid == 0) {                   // bias corrections once per block (double pow)
+        s_t = step[0] + 1.0;
+        s_coef[0] = AdamCoef<T>::step_size_of(s_t, lr, b1);
+        s_coef[1] = AdamCoef<T>::bc2s_of(s_t, b2);
+    }
+    T gi = T(0);
+    if (rows) {
+        T s = T(0);
+        if (i < n)
+            for (int r = j; r < nrows; r += kUpdLanes) s += rows[(size_t)r * kV24W + i];
+        s_red[tid] = s;
+        __syncthreads();
+        // fixed tree over the 16 lanes of one parameter
+        for (int o = kUpdLanes / 2; o >= 1; o >>= 1) {
+            if (j < o) s_red[tid] += s_red[tid + o];
+            __syncthreads();
+        }
+        gi = s_red[q * kUpdLanes];
+        if (grad && j == 0 && i < n) grad[i] = gi;
+    } else if (i < n && j == 0) {
+        gi = grad[i];
+    }
+    if (loss_b && blockIdx.x == 0) {          // per-codeword losses, fixed order
+        __syncthreads();
+        T s = T(0);
+        for (int64_t b = tid; b < nloss; b += 256) s += loss_b[b];
+        s_red[tid] = s;
+        __syncthreads();
+        for (int o = 128; o >= 1; o >>= 1) {
+            if (tid < o) s_red[tid] += s_red[tid + o];
+            __syncthreads();
+        }
+        if (tid == 0) loss[0] = s_red[0];
+    }
+    if (!adam) return;
+    __syncthreads();                          // s_t (and every use of step) before arrival
+    const double t = s_t;
+    if (j == 0 && i < n) {
+        const AdamCoef<T> c(s_coef[0], s_coef[1], b1, b2, eps, wd);
+        T mi = m[i], vi = v[i];
+        const T np = adam_one(c, p[i], gi, mi, vi);
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = np;
+        if (prepared) {
+            if (prep_v24_f32) {
+                float sc;
+                const int k = v24_prep_index(i, sc);
+                prepared[k] = (T)((float)np * sc);
+            } else {
+                prepared[i] = np;
+            }
+        }
+    }
+    if (tid == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {          // every block has read the step count
+            step[0] = t;
+            __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 }  // namespace
@@ -764,7 +919,7 @@ extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const v
 extern "C" int gnnd_train_bwd_workspace(const gnnd_graph* g, int model, int dtype,
                                         int64_t batch, int64_t* h_bytes) {
     if (!train_args_ok(g, model, dtype, batch, 0) || !h_bytes) return GNND_ERR_INVALID_ARG;
-    *h_bytes = train_blocks(batch) * (int64_t)kV24W * (dtype == GNND_F64 ? 8 : 4);
+    *h_bytes = train_rows(g, batch) * (int64_t)kV24W * (dtype == GNND_F64 ? 8 : 4);
     return GNND_OK;
 }
 
@@ -786,6 +941,61 @@ extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const v
                                  workspace_bytes, batch, iters, st);
     return launch_bwd<double>(g, d_w, d_x, d_out, d_grad_out, d_tape, d_grad_w, d_workspace,
                               workspace_bytes, batch, iters, st);
+}
+
+extern "C" int gnnd_train_bwd_rows(const gnnd_graph* g, int model, int dtype, int64_t batch,
+                                   int64_t* h_rows) {
+    if (!train_args_ok(g, model, dtype, batch, 0) || !h_rows) return GNND_ERR_INVALID_ARG;
+    *h_rows = batch > 0 ? train_rows(g, batch) : 0;
+    return GNND_OK;
+}
+
+extern "C" int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype, const void* d_w,
+                                      const void* d_x, const void* d_out, const void* d_grad_out,
+                                      const void* d_tape, void* d_workspace, int64_t workspace_bytes,
+                                      int64_t batch, int32_t iters, void* stream) {
+    if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
+    if (batch == 0) return GNND_OK;
+    if (!d_w || !d_x || !d_out || !d_grad_out || !d_tape || !d_workspace) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GNND_F32)
+        return launch_bwd<float>(g, d_w, d_x, d_out, d_grad_out, d_tape, nullptr, d_workspace,
+                                 workspace_bytes, batch, iters, st);
+    return launch_bwd<double>(g, d_w, d_x, d_out, d_grad_out, d_tape, nullptr, d_workspace,
+                              workspace_bytes, batch, iters, st);
+}
+
+extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64_t n_rows,
+                                 void* d_grad, const void* d_loss_b, int64_t batch, void* d_loss,
+                                 void* d_param, void* d_exp_avg, void* d_exp_avg_sq,
+                                 double* d_step, uint32_t* d_sync, double lr, double beta1,
+                                 double beta2, double eps, double weight_decay, void* d_prepared,
+                                 void* stream) {
+    if (model != GNND_V24 || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
+    if (n_rows < 0 || batch < 0 || n_rows > 0x7fffffff) return GNND_ERR_INVALID_ARG;
+    if (n_rows > 0 && !d_rows) return GNND_ERR_INVALID_ARG;
+    if (n_rows == 0 && !d_grad) return GNND_ERR_INVALID_ARG;          // nothing to update from
+    if (batch > 0 && (!d_loss_b) != (!d_loss)) return GNND_ERR_INVALID_ARG;
+    const bool adam = d_param != nullptr;
+    if (adam && (!d_exp_avg || !d_exp_avg_sq || !d_step || !d_sync)) return GNND_ERR_INVALID_ARG;
+    if (!adam && d_prepared) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    const int blocks = (kV24W + 256 / kUpdLanes - 1) / (256 / kUpdLanes);
+    const bool lossb = batch > 0 && d_loss_b;
+    if (dtype == GNND_F32)
+        train_update_kernel<float><<<blocks, 256, 0, st>>>(
+            n_rows ? (const float*)d_rows : nullptr, (int)n_rows, (float*)d_grad,
+            lossb ? (const float*)d_loss_b : nullptr, batch, (float*)d_loss, (float*)d_param,
+            (float*)d_exp_avg, (float*)d_exp_avg_sq, d_step, d_sync, kV24W, lr, beta1, beta2, eps,
+            weight_decay, (float*)d_prepared, 1);
+    else
+        train_update_kernel<double><<<blocks, 256, 0, st>>>(
+            n_rows ? (const double*)d_rows : nullptr, (int)n_rows, (double*)d_grad,
+            lossb ? (const double*)d_loss_b : nullptr, batch, (double*)d_loss, (double*)d_param,
+            (double*)d_exp_avg, (double*)d_exp_avg_sq, d_step, d_sync, kV24W, lr, beta1, beta2,
+            eps, weight_decay, (double*)d_prepared, 0);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
 }
 
 extern "C" int gnnd_syndrome_loss(const gnnd_graph* g, const int32_t* d_logical, int32_t n_logical,

@@ -31,6 +31,8 @@ SIGNATURES = {
     'gnnd_graph_destroy': (_int, [_vp]),
     'gnnd_graph_validate_host': (_int, [_c_i64p, _c_i64p, _i64, _i32, _i32, _c_i32p]),
     'gnnd_graph_dims': (_int, [_vp, _c_i32p]),
+    'gnnd_graph_components': (_int, [_vp, _c_i32p]),
+    'gnnd_graph_set_split': (_int, [_vp, _i32]),
     'gnnd_check_tiled': (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     'gnnd_propagate_width': (_int, [_int, _int]),
     'gnnd_propagate_tiled': (_int, [_vp, _int, _int, _int, _int, _vp, _vp, _vp, _i64, _vp]),
@@ -53,6 +55,12 @@ SIGNATURES = {
     'gnnd_train_bwd_workspace': (_int, [_vp, _int, _int, _i64, _c_i64p]),
     'gnnd_train_bwd': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32,
                               _vp]),
+    'gnnd_train_bwd_rows': (_int, [_vp, _int, _int, _i64, _c_i64p]),
+    'gnnd_train_bwd_partial': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64,
+                                      _i32, _vp]),
+    'gnnd_train_update': (_int, [_int, _int, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
+                                 _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, ctypes.c_double, _vp, _vp]),
     'gnnd_syndrome_loss': (_int, [_vp, _vp, _i32, _i32, _int, _vp, _vp, _vp, _vp, _i64, _vp]),
     'gnnd_decision_errors': (_int, [_vp, _vp, _i32, _int, _vp, _vp, _vp, _i64, _vp]),
     'gnnd_adam_step': (_int, [_int, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_double, ctypes.c_double,

@@ -21,18 +21,31 @@ import numpy as np
 import torch
 
 _GRAPHS = {}
-_GENCOLS = {}
+
+
+def _resolved(device):
+    """torch.device with the index resolved ('cuda' -> the current device), so a cached
+    graph never serves another GPU after a set_device."""
+    d = torch.device(device)
+    if d.type == 'cuda' and d.index is None:
+        d = torch.device('cuda', torch.cuda.current_device())
+    return d
 
 
 def _graph_of(H, device):
+    """Cached device graph of H (keyed by content and the resolved device).  A TannerGraph
+    passed as H is used as is: no host copy or hashing of H inside a caller's timed loop."""
     from .graph import TannerGraph
+    if isinstance(H, TannerGraph):
+        return H, None
+    dev = _resolved(device)
     Hn = (np.asarray(H.detach().cpu() if isinstance(H, torch.Tensor) else H) != 0).astype(np.uint8)
-    key = (Hn.shape, hash(Hn.tobytes()), str(torch.device(device)))
+    key = (Hn.shape, hash(Hn.tobytes()), str(dev))
     g = _GRAPHS.get(key)
     if g is None:
-        if len(_GRAPHS) > 16:
+        if len(_GRAPHS) > 32:
             _GRAPHS.clear()
-        g = _GRAPHS[key] = TannerGraph(Hn, device=device)
+        g = _GRAPHS[key] = TannerGraph(Hn, device=dev)
     return g, key
 
 
@@ -56,14 +69,14 @@ def awgn_batch(H, B, snrs=(1, 2, 3, 4, 5, 6), codeword_bit=1, seed=0, device='cu
         raise ValueError(f'codewords must be "fixed" or "random", got {codewords!r}')
     if _engine(engine, device) == 'hip':
         from . import ops
-        g, key = _graph_of(H, device)
+        g, _ = _graph_of(H, device)
         cols, k = None, 0
         if codewords == 'random':
-            ent = _GENCOLS.get(key)
+            ent = getattr(g, '_gen_cols', None)        # generator columns, cached on the graph
             if ent is None:
                 from .codes import gf2_generator
                 c, k = ops.pack_generator_columns(gf2_generator(np.asarray(g.H)))
-                ent = _GENCOLS[key] = (c.to(device), k)
+                ent = g._gen_cols = (c.to(g.device), k)
             cols, k = ent
         return ops.sample_awgn(g, B, snrs, cols, k, codeword_bit, seed, offset, dtype, device)
     if offset:

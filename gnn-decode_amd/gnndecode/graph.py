@@ -55,6 +55,18 @@ class TannerGraph:
     def handle(self):
         return self._handle
 
+    @property
+    def components(self):
+        """Disconnected components libgnnd split the graph into (1 = not split): decoder_v2_4
+        decodes and trains each component of a codeword in its own workgroup."""
+        n = ctypes.c_int32()
+        _lib.call('gnnd_graph_components', self._handle, ctypes.byref(n))
+        return int(n.value)
+
+    def set_split(self, enable):
+        """Use (default) or bypass the component split for this graph (A/B and tests)."""
+        _lib.call('gnnd_graph_set_split', self._handle, int(bool(enable)))
+
     def __del__(self):
         h = getattr(self, '_handle', None)
         if h is not None and h.value:

@@ -281,6 +281,37 @@ def train_backward(graph, model, plain_weights, x, out, grad_out, tape, iters):
     return gw
 
 
+def train_backward_partial(graph, model, plain_weights, x, out, grad_out, tape, iters, ws=None):
+    """gnnd_train_bwd_partial: the reverse pass leaving its per-workgroup gradient rows in a
+    workspace.  Returns (workspace, rows); reduce with train_update."""
+    B = x.numel() // graph.N
+    dt = dtype_code(x.dtype)
+    nr = ctypes.c_int64()
+    _lib.call('gnnd_train_bwd_rows', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nr))
+    nb = ctypes.c_int64()
+    _lib.call('gnnd_train_bwd_workspace', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nb))
+    if ws is None or ws.numel() < nb.value:
+        ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
+    grad_out = grad_out.contiguous()
+    _lib.call('gnnd_train_bwd_partial', graph.handle, _lib.VARIANT[model], dt, _ptr(plain_weights),
+              _ptr(x), _ptr(out), _ptr(grad_out), _ptr(tape), _ptr(ws), nb.value, B, int(iters),
+              current_stream(x.device))
+    return ws, int(nr.value)
+
+
+def train_update(model, dtype, rows=None, n_rows=0, grad=None, loss_b=None, loss=None,
+                 param=None, exp_avg=None, exp_avg_sq=None, step=None, sync=None, lr=3e-4,
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, prepared=None, device=None):
+    """gnnd_train_update: reduce the reverse pass's rows (and the per-codeword losses) and/or
+    apply Adam + the kernel-layout weight copy, in one launch (see include/gnnd.h)."""
+    dev = device or (param.device if param is not None else grad.device)
+    _lib.call('gnnd_train_update', _lib.VARIANT[model], dtype_code(dtype), _ptr(rows), int(n_rows),
+              _ptr(grad), _ptr(loss_b), 0 if loss_b is None else loss_b.numel(), _ptr(loss),
+              _ptr(param), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(step), _ptr(sync), float(lr),
+              float(betas[0]), float(betas[1]), float(eps), float(weight_decay), _ptr(prepared),
+              current_stream(dev))
+
+
 class FusedTrainFn(torch.autograd.Function):
     """out = decode(weights, x) with a one-launch HIP backward to the packed weights."""
 

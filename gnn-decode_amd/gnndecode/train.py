@@ -235,19 +235,24 @@ class _StaticBatch:
 
 
 class FusedV24Trainer(_GraphedStep):
-    """decoder_v2_4 training step (quantum/decoder_v2_4.py:320-348) as a handful of HIP
-    launches:
+    """decoder_v2_4 training step (quantum/decoder_v2_4.py:320-348) as four HIP launches:
 
-        prepare weights -> forward with tape (gnnd_train_fwd) -> syndrome loss and
-        d loss / d out (gnnd_syndrome_loss) -> reverse pass to the flat gradient
-        (gnnd_train_bwd) -> [one RCCL all_reduce(SUM) of that gradient] -> Adam on the
-        flat parameter buffer (gnnd_adam_step)
+        forward with tape (gnnd_train_fwd) -> syndrome loss and d loss / d out
+        (gnnd_syndrome_loss) -> reverse pass to per-workgroup gradient rows
+        (gnnd_train_bwd_partial) -> fused epilogue (gnnd_train_update: fixed-order row
+        reduction, the batch loss, Adam, and the kernel-layout weights the next forward reads)
+
+    With a collective in play the epilogue is split around the RCCL all_reduce(SUM) of the
+    flat gradient: update(rows -> gradient, loss) -> all_reduce -> update(Adam, weights).
+    On a split Tanner graph (the toric code's two disconnected halves, TannerGraph.components)
+    the forward and the reverse pass run every component of a codeword in its own workgroup.
 
     The model's parameters are re-bound as VIEWS of one flat buffer in the gnnd.h packed
     layout, so nothing is packed, split, zeroed or accumulated per parameter (the torch
     path, `Trainer`, spends ~80 small kernels per step on that, the loss graph and Adam).
-    state_dict / load_state_dict keep working on the views.  Same update as `Trainer`
-    (torch.optim.Adam's order; lr 3e-4, weight decay 1e-9 of the reference)."""
+    state_dict / load_state_dict keep working on the views (an in-place change of a
+    parameter re-prepares the kernel-layout weights before the next step).  Same update as
+    `Trainer` (torch.optim.Adam's order; lr 3e-4, weight decay 1e-9 of the reference)."""
 
     def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
                  group=None, graph=True, warmup=2, force_collective=False):
@@ -280,28 +285,62 @@ class FusedV24Trainer(_GraphedStep):
         self.exp_avg = torch.zeros_like(flat)
         self.exp_avg_sq = torch.zeros_like(flat)
         self.step_count = torch.zeros(1, dtype=torch.float64, device=flat.device)
+        self._sync = torch.zeros(1, dtype=torch.int32, device=flat.device)   # gnnd_train_update
+        self._loss = torch.zeros((), dtype=flat.dtype, device=flat.device)
+        self._gw = torch.zeros_like(flat)
+        # kernel-layout weights of the current parameters: written by the fused epilogue after
+        # every update, re-prepared here when the parameters change outside the trainer
+        self.prepared = ops.prepare_weights('v24', flat)
+        self._prep_version = flat._version
         # device graph tables now, never inside a capture
         model.graph(flat.device)
         loss_fn._graph(flat.device)
 
+    def _refresh_prepared(self):
+        if self.flat._version != self._prep_version:
+            self.prepared.copy_(ops.prepare_weights('v24', self.flat))
+            self._prep_version = self.flat._version
+
     def _compute(self, x, y):
         m = self.model
         g = m.graph(x.device)
-        w = self.flat if self.flat.dtype == x.dtype else self.flat.to(x.dtype)
-        out, tape = ops.train_forward(g, m.kind, x, ops.prepare_weights(m.kind, w), m.Nc)
         lf = self.loss_fn
+        if self.flat.dtype != x.dtype:           # mixed precision: the unfused update path
+            w = self.flat.to(x.dtype)
+            out, tape = ops.train_forward(g, m.kind, x, ops.prepare_weights(m.kind, w), m.Nc)
+            loss_b, dpred = ops.syndrome_loss(lf._graph(x.device), lf.logical_rows,
+                                              lf.logical_only, out, y)
+            self._gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
+            self._pending = None
+            return loss_b.sum(), [self._gw]
+        out, tape = ops.train_forward(g, m.kind, x, self.prepared, m.Nc)
         loss_b, dpred = ops.syndrome_loss(lf._graph(x.device), lf.logical_rows, lf.logical_only,
                                           out, y)
-        self._gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
-        return loss_b.sum(), [self._gw]
+        ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
+        if self._dist():
+            # rows -> flat gradient and batch loss, for the all-reduce
+            ops.train_update('v24', x.dtype, rows=ws, n_rows=nrows, grad=self._gw,
+                             loss_b=loss_b, loss=self._loss)
+            self._pending = None
+            return self._loss, [self._gw]
+        self._pending = (ws, nrows, loss_b)      # reduced by the fused epilogue in _apply
+        return self._loss, []
 
     def _apply(self):
-        ops.adam_step(self.flat, self._gw, self.exp_avg, self.exp_avg_sq, self.step_count,
-                      self.lr, self.betas, self.eps, self.wd)
+        kw = dict(param=self.flat, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq,
+                  step=self.step_count, sync=self._sync, lr=self.lr, betas=self.betas,
+                  eps=self.eps, weight_decay=self.wd, prepared=self.prepared)
+        if self._pending is not None:            # single rank: everything in one launch
+            ws, nrows, loss_b = self._pending
+            ops.train_update('v24', self.flat.dtype, rows=ws, n_rows=nrows, loss_b=loss_b,
+                             loss=self._loss, **kw)
+        else:                                    # the (all-reduced) flat gradient
+            ops.train_update('v24', self.flat.dtype, grad=self._gw, **kw)
 
     def step(self, data, y):
         self.model.train()
         x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
+        self._refresh_prepared()
         out = self._run(x, y)
-        _invalidate(self.model)      # parameters changed on the device (gnnd_adam_step)
+        _invalidate(self.model)      # parameters changed on the device (gnnd_train_update)
         return out

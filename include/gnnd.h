@@ -95,6 +95,14 @@ int gnnd_graph_validate_host(const int64_t* h_var, const int64_t* h_chk, int64_t
                              int32_t num_var, int32_t num_chk, int32_t* h_report4);
 /* dims[0..5] = V, C, E, N, max variable degree, max check degree */
 int gnnd_graph_dims(const gnnd_graph* g, int32_t* h_dims6);
+/* Connected components the graph was split into (1 = not split).  A Tanner graph made of
+ * 2..8 equal-shaped components, each a contiguous variable range with a contiguous check
+ * range (the toric code of quantum/error_generate.py:39-132: its X and Z halves), is decoded
+ * and trained by decoder_v2_4 with every component of a codeword in its own workgroup (the
+ * components share no edge, so nothing is exchanged; results are the same as whole-graph
+ * decoding up to fp32 summation order).  Set GNND_NO_SPLIT=1 to disable.                  */
+int gnnd_graph_components(const gnnd_graph* g, int32_t* h_ncomp);
+int gnnd_graph_set_split(gnnd_graph* g, int32_t enable);   /* 0: decode / train it whole */
 
 /* Check on the device that a batched edge_index (int64, rows 0/1 at d_edge_index and
  * d_edge_index + row_stride, num_batched_edges columns) is the single graph tiled over
@@ -219,6 +227,32 @@ int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const void* d_w, c
                    const void* d_out, const void* d_grad_out, const void* d_tape,
                    void* d_grad_w, void* d_workspace, int64_t workspace_bytes, int64_t batch,
                    int32_t iters, void* stream);
+/* The reverse pass without its reduction: leaves gnnd_train_bwd_rows() per-workgroup
+ * gradient rows [rows][1283] in d_workspace, for gnnd_train_update to reduce (fused with
+ * the optimizer).  On a split graph (gnnd_graph_components > 1) every component of a
+ * codeword runs in its own workgroup.                                                     */
+int gnnd_train_bwd_rows(const gnnd_graph* g, int model, int dtype, int64_t batch,
+                        int64_t* h_rows);
+int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype, const void* d_w,
+                           const void* d_x, const void* d_out, const void* d_grad_out,
+                           const void* d_tape, void* d_workspace, int64_t workspace_bytes,
+                           int64_t batch, int32_t iters, void* stream);
+/* Fused optimizer epilogue of a decoder_v2_4 training step (one launch):
+ *   n_rows > 0: d_grad[i] = fixed-order sum of the rows (d_grad may be NULL: not stored);
+ *   n_rows = 0: the gradient is read from d_grad (e.g. after an all-reduce of it);
+ *   d_loss_b [batch] non-NULL: *d_loss = fixed-order sum of the per-codeword losses;
+ *   d_param non-NULL: gnnd_adam_step's update of the 1283 plain packed weights (moments
+ *   d_exp_avg / d_exp_avg_sq, device step count *d_step incremented once), then, if
+ *   d_prepared is non-NULL, gnnd_prepare_weights' kernel layout of the updated weights into
+ *   d_prepared.  d_sync: one device uint32, zero before the first call (the kernel leaves it
+ *   zero); it orders the step-count update across the launch's workgroups.
+ * Single-rank step: bwd_partial -> update(rows, loss, Adam, prepare).  Data-parallel step:
+ * bwd_partial -> update(rows -> d_grad, loss) -> all_reduce(d_grad) -> update(0 rows, Adam). */
+int gnnd_train_update(int model, int dtype, const void* d_rows, int64_t n_rows, void* d_grad,
+                      const void* d_loss_b, int64_t batch, void* d_loss, void* d_param,
+                      void* d_exp_avg, void* d_exp_avg_sq, double* d_step, uint32_t* d_sync,
+                      double lr, double beta1, double beta2, double eps, double weight_decay,
+                      void* d_prepared, void* stream);
 
 /* ---- training objective ------------------------------------------------
  * Syndrome loss of quantum/decoder_v2_4.py:297-317 (logical_only != 0: the Lambda term of

@@ -195,9 +195,11 @@ def test_decision_errors_kernel_on_decoder_outputs(golden):
 
 
 def test_v24_f32_unit_split_bit_identical():
-    """fp32 decoder_v2_4 small-batch unit split: decode_kernel runs US = 4 (B <= 256) or 2
-    (B <= 512) waves per item wave at one codeword per workgroup and US = 1 above, all on the
-    R = 2 slot table below B = 4096.  The 128 hidden units are summed in one fixed chain order
+    """fp32 decoder_v2_4 small-batch unit split: decode_kernel runs US = 8 (a component-codeword's
+    items fit 128 lanes) or 4 (B*ncomp <= 256), 2 (<= 512) waves per item wave at one codeword
+    per workgroup and US = 1 above, all on the R = 2 slot table below B = 4096 (the toric graph
+    is split into its two components, B*ncomp = 2B).  The 128 hidden units are summed in one
+    fixed chain order
     (gnnd_decode_impl.h mlp128_chains), so every codeword decodes to the SAME BITS under every
     split and tile: slices decoded alone (US = 4 / 2) equal the B = 1024 decode (US = 1)."""
     import gnndecode as gd

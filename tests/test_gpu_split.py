@@ -1,0 +1,142 @@
+"""Component split of disconnected Tanner graphs (gnnd_graph::comp, TannerGraph.components).
+
+The toric code's H is block diagonal (quantum/error_generate.py:39-132: X and Z halves, every
+logical row inside one half), so decoder_v2_4 decodes and trains each component of a codeword
+in its own workgroup.  The components share no edge and the per-edge arithmetic is the same,
+so the split decode must equal the whole-graph decode BIT FOR BIT (forward outputs and the
+training tape); the reverse pass sums its per-workgroup gradient rows in a different grouping
+(fp rounding only).  Also: the fused optimizer epilogue (gnnd_train_update) against the
+separate reduce / Adam / prepare kernels."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _toric(L):
+    import gnndecode as gd
+    return gd.codes.toric_code(L)
+
+
+def test_components_detected():
+    import gnndecode as gd
+    for L in (4, 5, 7):
+        assert gd.TannerGraph(_toric(L), device=DEV).components == 2
+    assert gd.TannerGraph(gd.codes.bch_63_45(), device=DEV).components == 1
+    assert gd.TannerGraph(gd.codes.get_code('ldpc_648_324'), device=DEV).components == 1
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('L,B', [(5, 1), (5, 128), (7, 128), (7, 700), (5, 5000)])
+def test_split_decode_is_bit_identical(dtype, L, B):
+    import gnndecode as gd
+    H = _toric(L)
+    torch.manual_seed(L)
+    m = gd.MODELS['v24'](15, H).to(DEV).to(dtype).eval()
+    g = m.graph(DEV)
+    assert g.components == 2
+    x, _ = gd.data.toric_batch(H, B, seed=B, device=DEV, dtype=dtype)
+    w = m.prepared_weights(dtype, DEV)
+    try:
+        g.set_split(True)
+        a = gd.ops.decode(g, 'v24', x, 15, w)
+        g.set_split(False)
+        b = gd.ops.decode(g, 'v24', x, 15, w)
+    finally:
+        g.set_split(True)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('B', [3, 128, 1500])
+def test_split_training_tape_and_gradient(dtype, B):
+    """Training forward (output + every tape row) bit-identical split vs whole; reverse-pass
+    gradient equal up to the grouping of its fixed-order row sums."""
+    import gnndecode as gd
+    H = _toric(5)
+    torch.manual_seed(2)
+    T = 6
+    m = gd.MODELS['v24'](T, H).to(DEV).to(dtype)
+    g = m.graph(DEV)
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+    x, y = gd.data.toric_batch(H, B, seed=7, device=DEV, dtype=dtype)
+    flat = m.packed_weights().detach().to(dtype).contiguous()
+    prep = gd.ops.prepare_weights('v24', flat)
+    res = []
+    try:
+        for split in (True, False):
+            g.set_split(split)
+            out, tape = gd.ops.train_forward(g, 'v24', x, prep, T)
+            _, dpred = gd.ops.syndrome_loss(lf._graph(DEV), lf.logical_rows, False, out, y)
+            gw = gd.ops.train_backward(g, 'v24', flat, x, out, dpred, tape, T)
+            res.append((out, tape, gw))
+    finally:
+        g.set_split(True)
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    ga, gb = res[0][2].double(), res[1][2].double()
+    assert (ga - gb).abs().max().item() <= tol * max(1.0, gb.abs().max().item())
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_fused_update_matches_separate_kernels(dtype):
+    """gnnd_train_update (row reduction + loss sum + Adam + kernel-layout weights, one launch)
+    vs gnnd_train_bwd's reduction, torch.sum, gnnd_adam_step and gnnd_prepare_weights."""
+    import gnndecode as gd
+    n = 1283
+    gen = torch.Generator(device='cpu').manual_seed(4)
+    for rows in (1, 7, 256, 1024):
+        R = torch.randn(rows, n, generator=gen, dtype=torch.float64).to(dtype).to(DEV)
+        loss_b = torch.rand(333, generator=gen, dtype=torch.float64).to(dtype).to(DEV)
+        p0 = torch.randn(n, generator=gen, dtype=torch.float64).to(dtype).to(DEV)
+        pa, pb = p0.clone(), p0.clone()
+        ma, va, mb, vb = (torch.zeros_like(p0) for _ in range(4))
+        sa = torch.zeros(1, dtype=torch.float64, device=DEV)
+        sb = torch.zeros(1, dtype=torch.float64, device=DEV)
+        sync = torch.zeros(1, dtype=torch.int32, device=DEV)
+        loss = torch.zeros((), dtype=dtype, device=DEV)
+        grad = torch.zeros_like(p0)
+        prep = torch.zeros_like(p0)
+        for it in range(3):
+            gd.ops.train_update('v24', dtype, rows=R, n_rows=rows, grad=grad, loss_b=loss_b,
+                                loss=loss, param=pa, exp_avg=ma, exp_avg_sq=va, step=sa, sync=sync,
+                                lr=1e-3, weight_decay=1e-9, prepared=prep)
+            ref_g = R.double().sum(0)
+            tol = 1e-12 if dtype == torch.float64 else 2e-5
+            assert (grad.double() - ref_g).abs().max().item() <= tol * max(1.0, ref_g.abs().max().item())
+            assert abs(loss.item() - loss_b.double().sum().item()) <= tol * loss_b.double().sum().item()
+            gd.ops.adam_step(pb, grad.clone(), mb, vb, sb, 1e-3, (0.9, 0.999), 1e-8, 1e-9)
+            assert torch.equal(pa, pb), (rows, it)
+            assert torch.equal(prep, gd.ops.prepare_weights('v24', pa)), (rows, it)
+            assert sa.item() == it + 1 and sync.item() == 0
+
+
+def test_fused_trainer_split_vs_whole_graph():
+    """FusedV24Trainer on the split graph follows the whole-graph trainer (fp64, toric d=7,
+    one-codeword-per-workgroup and looping batches)."""
+    import gnndecode as gd
+    H = _toric(7)
+    lg = gd.codes.toric_logicals(H)
+    for B in (16, 1100):
+        torch.manual_seed(0)
+        a = gd.MODELS['v24'](5, H).to(DEV)
+        b = gd.MODELS['v24'](5, H).to(DEV)
+        b.load_state_dict(a.state_dict())
+        ta = gd.train.FusedV24Trainer(a, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1)
+        tb = gd.train.FusedV24Trainer(b, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1)
+        gb = b.graph(torch.device(DEV, torch.cuda.current_device()))   # the trainer's graph
+        gb.set_split(False)
+        try:
+            for s in range(3):
+                x, y = gd.data.toric_batch(H, B, seed=s, device=DEV)
+                la = ta.step(gd.data.make_batch(x, a.graph(DEV)), y)
+                lb = tb.step(gd.data.make_batch(x, gb), y)
+                assert abs(la.item() - lb.item()) <= 1e-11 * max(1.0, abs(lb.item()))
+        finally:
+            gb.set_split(True)
+        for k, v in a.state_dict().items():
+            torch.testing.assert_close(b.state_dict()[k], v, rtol=1e-10, atol=1e-13)
+        assert ta.step_count.item() == 3.0
