@@ -779,7 +779,9 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
     // unit split: two [US][IL] f32x2 buffers for the MLP partial sums (8-byte aligned)
-    f32x2* s_part = (f32x2*)(((uintptr_t)(s_xc + (size_t)CW * C) + 7) & ~(uintptr_t)7);
+    // (offset arithmetic on the __shared__ base keeps the LDS address space: ds_* accesses,
+    // not flat ones as through an integer cast of the pointer)
+    f32x2* s_part = (f32x2*)(smem + ((((char*)(s_xc + (size_t)CW * C) - smem) + 7) & ~(ptrdiff_t)7));
 
     for (int i = tid; i < nw; i += NT) s_w[i] = w[i];
     for (int i = tid; i < nslot; i += NT) s_slot[i] = g.slot_ve[i];   // v | e << 16

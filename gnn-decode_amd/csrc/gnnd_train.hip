@@ -286,6 +286,18 @@ template <typename T> struct Units {
     }
 };
 
+// The syndrome loss fused into the reverse pass (y non-null): instead of reading d loss /
+// d p from gnnd_syndrome_loss, each workgroup computes the loss terms of its codeword's
+// component (check rows of the component graph; logical rows = per-variable bit masks, every
+// row's support inside one component) and their gradient itself, and writes the component's
+// loss to loss_b[b * ncomp + k].  Same per-row and per-variable summation orders as
+// syndrome_loss_kernel except the logical rows (summed in variable order here).
+template <typename T> struct BwdLoss {
+    const T* y;                  // [B*V] labels (nullptr: gp holds d loss / d p)
+    const uint32_t* lmask;       // [V] logical-row bit masks of the WHOLE graph's variables
+    int nl, logical_only, ncomp;
+    T* loss_b;                   // [B * ncomp]
+};
 // Split graphs (views non-null): blocks [k*cblk, (k+1)*cblk) run component k (graph views[k],
 // rows addressed through its GraphView addressing fields) of codewords j, j + cblk, ...
 template <typename T, int kTrainThreads = train_threads<T>()>
@@ -293,14 +305,14 @@ __global__ void __launch_bounds__(kTrainThreads)
 v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                const T* __restrict__ p, const T* __restrict__ gp, TapeView<T> tape,
                T* __restrict__ gpart, int64_t B, int iters, const GraphView* __restrict__ views,
-               int cblk) {
+               int cblk, BwdLoss<T> lossp) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     GraphView g = g0;
-    int blk = blockIdx.x, nblk = gridDim.x;
+    int blk = blockIdx.x, nblk = gridDim.x, comp = 0;
     if (views) {                       // uniform: component k
-        const int k = blk / cblk;
-        g = views[k];
-        blk -= k * cblk;
+        comp = blk / cblk;
+        g = views[comp];
+        blk -= comp * cblk;
         nblk = cblk;
     }
     const int V = g.V, C = g.C, E = g.E;
@@ -323,10 +335,39 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     T* s_xv = s_ext + E;                     // [E] x_{v(e)}  (prior of the edge's variable)
     T* s_sc = s_xv + E;                      // [E] s_{c(e)}  (syndrome of the edge's check)
     T* s_acc = s_sc + E;                     // [1283] workgroup gradient accumulator
+    // fused loss (lossp.y): [V] y + p, p, d loss / d p; [C + nl] row gradients, row terms;
+    // int [V] logical masks, [nl] row lengths, [nl][V] row variable lists
+    const bool floss = lossp.y != nullptr;
+    const int nl = floss ? lossp.nl : 0, nr = C + nl;
+    T* s_ls = s_acc + kV24W;
+    T* s_pv = s_ls + V;
+    T* s_gpv = s_pv + V;
+    T* s_lg = s_gpv + V;
+    T* s_lt = s_lg + nr;
+    uint32_t* s_lmask = (uint32_t*)(s_lt + nr);
+    int* s_lcnt = (int*)(s_lmask + V);
+    int* s_lvar = s_lcnt + nl;
 
     const int* gtab = (const int*)g.edge_vc;
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     for (int i = tid; i < kV24W; i += kTrainThreads) s_acc[i] = T(0);
+    if (floss) {
+        for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
+        __syncthreads();
+        // logical row l as the list of its (local) variables, increasing: wave l, ballots
+        for (int l = wave; l < nl; l += kTrainWaves) {
+            int cnt = 0;
+            for (int v0 = 0; v0 < V; v0 += 64) {
+                const int v = v0 + lane;
+                const bool in = v < V && ((s_lmask[v] >> l) & 1u);
+                const uint64_t bal = __ballot(in);
+                if (in) s_lvar[l * V + cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = v;
+                cnt += __builtin_popcountll(bal);
+            }
+            if (lane == 0) s_lcnt[l] = cnt;
+        }
+    }
     Units<T> uv, uc, uo;                     // ggc1.mlp, ggc2.mlp, mlp
     uv.load2(w + kV24Ggc1, lane);
     uc.load1(w + kV24Ggc2, lane);
@@ -423,14 +464,59 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
         if (iters > 0) prefetch(iters - 1);
         // readout inputs: m^T into s_u, d loss / d r per edge into s_da; per-edge x_v, s_c
         const T* xb = x + (size_t)b * g.xs;
+        if (floss) {
+            // quantum/decoder_v2_4.py:297-317 on this component: s = y + p; rows -> |sin| terms
+            // and d|sin(pi/2 s_r)| / d s_r; d loss / d p_v = sum over v's rows
+            const size_t ob = (size_t)b * g.os + g.o0;
+            for (int v = tid; v < V; v += kTrainThreads) {
+                const T pv = p[ob + v];
+                s_pv[v] = pv;
+                s_ls[v] = lossp.y[ob + v] + pv;
+            }
+            __syncthreads();
+            const T kPi = T(M_PI);
+            for (int r = tid; r < nr; r += kTrainThreads) {
+                T sr = T(0);
+                if (r < C) {
+                    for (int k = s_cptr[r]; k < s_cptr[r + 1]; ++k) sr += s_ls[s_evc[s_cedge[k]] & 0xffffu];
+                } else {
+                    const int l = r - C;
+                    for (int i = 0; i < s_lcnt[l]; ++i) sr += s_ls[s_lvar[l * V + i]];
+                }
+                const T xr = sr * kPi / T(2);
+                const T sn = sin(xr);
+                const T gr = (sn > T(0) ? T(1) : sn < T(0) ? T(-1) : T(0)) * cos(xr) * (kPi / T(2));
+                const bool on = r >= C || !lossp.logical_only;
+                s_lg[r] = on ? gr : T(0);
+                s_lt[r] = on ? (sn < T(0) ? -sn : sn) : T(0);
+            }
+            __syncthreads();
+            for (int v = tid; v < V; v += kTrainThreads) {
+                T d = T(0);
+                for (int k = s_vptr[v]; k < s_vptr[v + 1]; ++k) d += s_lg[s_evc[k] >> 16];
+                const uint32_t m = s_lmask[v];
+                for (int l = 0; l < nl; ++l)
+                    if ((m >> l) & 1u) d += s_lg[C + l];
+                s_gpv[v] = d;
+            }
+            if (wave == 0) {                  // the component's loss, fixed order
+                T t = T(0);
+                for (int r = lane; r < nr; r += 64) t += s_lt[r];
+                t = wave_sum(t);
+                if (lane == 0) lossp.loss_b[(size_t)b * lossp.ncomp + comp] = t;
+            }
+            __syncthreads();
+        }
         for (int f = tid; f < E; f += kTrainThreads) {
             const uint32_t vc = s_evc[f];
-            const size_t bv = (size_t)b * g.os + g.o0 + (int)(vc & 0xffffu);
-            const T pv = p[bv];
-            s_xv[f] = xb[g.xv0 + (int)(vc & 0xffffu)];
+            const int v = (int)(vc & 0xffffu);
+            const size_t bv = (size_t)b * g.os + g.o0 + v;
+            const T pv = floss ? s_pv[v] : p[bv];
+            const T gv = floss ? s_gpv[v] : gp[bv];
+            s_xv[f] = xb[g.xv0 + v];
             s_sc[f] = xb[g.xc0 + (int)(vc >> 16)];
             s_u[f] = tape.mT[(size_t)b * g.es + g.e0 + f];
-            s_da[f] = -((gp[bv] * (T(1) - pv)) * pv);     // p = sigmoid(-r)
+            s_da[f] = -((gv * (T(1) - pv)) * pv);     // p = sigmoid(-r)
         }
         __syncthreads();
 
@@ -512,22 +598,28 @@ int64_t train_cblk(const gnnd_graph* g, int64_t B) {
 int64_t train_rows(const gnnd_graph* g, int64_t B) {
     return train_split(g) ? train_cblk(g, B) * g->ncomp : train_blocks(B);
 }
-size_t train_lds(const gnnd_graph* g, int esz) {
+size_t train_lds(const gnnd_graph* g, int esz, int nl = -1) {   // nl >= 0: fused loss
     const GraphView& v = g->view;
-    return (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
-           (size_t)esz * (8 * (size_t)v.E + kV24W);
+    size_t n = (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
+               (size_t)esz * (8 * (size_t)v.E + kV24W);
+    if (nl >= 0)
+        n += (size_t)esz * (3 * (size_t)v.V + 2 * ((size_t)v.C + nl)) +
+             4 * ((size_t)v.V + nl + (size_t)nl * v.V);
+    return n;
 }
 
-// gw == nullptr: leave the per-workgroup partial rows in ws (gnnd_train_bwd_partial)
+// gw == nullptr: leave the per-workgroup partial rows in ws (gnnd_train_bwd_partial);
+// lossp.y non-null: the syndrome loss fused in (gnnd_train_bwd_loss_partial)
 template <typename T>
 int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* out,
                const void* gout, const void* tape, void* gw, void* ws, int64_t ws_bytes,
-               int64_t B, int iters, hipStream_t st) {
+               int64_t B, int iters, hipStream_t st, BwdLoss<T> lossp = {}) {
     const bool split = train_split(g);
     const gnnd_graph* gk = split ? g->comp[0] : g;        // components share one shape
     const int64_t cblk = train_cblk(g, B), blocks = train_rows(g, B);
     if ((int64_t)blocks * kV24W * (int64_t)sizeof(T) > ws_bytes) return GNND_ERR_INVALID_ARG;
-    const size_t lds = train_lds(gk, sizeof(T));
+    lossp.ncomp = split ? g->ncomp : 1;
+    const size_t lds = train_lds(gk, sizeof(T), lossp.y ? lossp.nl : -1);
     if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     auto kern = v24_bwd_kernel<T>;
     if (lds > 64 * 1024)
@@ -538,7 +630,7 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     TapeView<T> tv{base, base + n, base + 2 * n, base + 3 * n};
     kern<<<(unsigned)blocks, train_threads<T>(), lds, st>>>(
         gk->view, (const T*)w, (const T*)x, (const T*)out, (const T*)gout, tv, (T*)ws, B, iters,
-        split ? g->dcomp : nullptr, (int)cblk);   // dcomp[0..K): the components' `view`
+        split ? g->dcomp : nullptr, (int)cblk, lossp);   // dcomp[0..K): the components' `view`
     GNND_LAUNCH_CHECK();
     if (!gw) return GNND_OK;
     grad_reduce_kernel<T><<<(kV24W + 255) / 256, 256, 0, st>>>((const T*)ws, (int)blocks, (T*)gw);
@@ -648,7 +740,10 @@ int launch_syndrome_loss(const gnnd_graph* g, const int32_t* lg, int nl, int log
     if (nl > 32) return GNND_ERR_UNSUPPORTED;    // logical rows as per-variable bit masks
     const size_t tab = ((size_t)(2 * v.E + v.C + 2 * v.V + 2) * 4 + 15) & ~(size_t)15;
     const size_t lds = tab + 4 * (size_t)(v.V + v.C + nl) * sizeof(T);
-    if (lds > 64 * 1024) return GNND_ERR_UNSUPPORTED;
+    if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;   // SyndromeLoss falls back to torch
+    if (lds > 64 * 1024)
+        GNND_HIP_CHECK(hipFuncSetAttribute((const void*)syndrome_loss_kernel<T>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t blocks = (B + 3) / 4;
     syndrome_loss_kernel<T><<<(unsigned)blocks, 256, lds, st>>>(
         v, lg, nl, logical_only, (const T*)pred, (const T*)y, (T*)loss_b, (T*)dpred, B);
@@ -963,6 +1058,35 @@ extern "C" int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype,
                                  workspace_bytes, batch, iters, st);
     return launch_bwd<double>(g, d_w, d_x, d_out, d_grad_out, d_tape, nullptr, d_workspace,
                               workspace_bytes, batch, iters, st);
+}
+
+extern "C" int gnnd_train_loss_count(const gnnd_graph* g, int64_t batch, int64_t* h_count) {
+    if (!g || batch < 0 || !h_count) return GNND_ERR_INVALID_ARG;
+    *h_count = batch * (train_split(g) ? g->ncomp : 1);
+    return GNND_OK;
+}
+
+extern "C" int gnnd_train_bwd_loss_partial(const gnnd_graph* g, int model, int dtype,
+                                           const void* d_w, const void* d_x, const void* d_out,
+                                           const void* d_y, const uint32_t* d_logical_mask,
+                                           int32_t n_logical, int32_t logical_only,
+                                           const void* d_tape, void* d_loss_b, void* d_workspace,
+                                           int64_t workspace_bytes, int64_t batch, int32_t iters,
+                                           void* stream) {
+    if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
+    if (n_logical < 0 || n_logical > 32 || (n_logical > 0 && !d_logical_mask)) return GNND_ERR_INVALID_ARG;
+    if (batch == 0) return GNND_OK;
+    if (!d_w || !d_x || !d_out || !d_y || !d_tape || !d_loss_b || !d_workspace) return GNND_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GNND_F32)
+        return launch_bwd<float>(g, d_w, d_x, d_out, d_out, d_tape, nullptr, d_workspace,
+                                 workspace_bytes, batch, iters, st,
+                                 BwdLoss<float>{(const float*)d_y, d_logical_mask, n_logical,
+                                                logical_only, 1, (float*)d_loss_b});
+    return launch_bwd<double>(g, d_w, d_x, d_out, d_out, d_tape, nullptr, d_workspace,
+                              workspace_bytes, batch, iters, st,
+                              BwdLoss<double>{(const double*)d_y, d_logical_mask, n_logical,
+                                              logical_only, 1, (double*)d_loss_b});
 }
 
 extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64_t n_rows,

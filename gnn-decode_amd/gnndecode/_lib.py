@@ -58,6 +58,9 @@ SIGNATURES = {
     'gnnd_train_bwd_rows': (_int, [_vp, _int, _int, _i64, _c_i64p]),
     'gnnd_train_bwd_partial': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64,
                                       _i32, _vp]),
+    'gnnd_train_loss_count': (_int, [_vp, _i64, _c_i64p]),
+    'gnnd_train_bwd_loss_partial': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
+                                           _vp, _vp, _vp, _i64, _i64, _i32, _vp]),
     'gnnd_train_update': (_int, [_int, _int, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                  _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                  ctypes.c_double, ctypes.c_double, _vp, _vp]),

@@ -16,6 +16,8 @@ views ([B*V,1] -> [B, V] -> transpose), identical values.
 """
 import math
 
+import numpy as np
+
 import torch
 
 
@@ -55,6 +57,54 @@ class SyndromeLoss(torch.nn.Module):
             c = self._casts[key] = t.to(dtype)
         return c
 
+    def logical_mask(self, device):
+        """int32 [V] bit masks of the logical rows (bit l: variable in row l), for the reverse
+        pass's fused loss (gnnd_train_bwd_loss_partial); None if there are more than 32 rows."""
+        nl = int(self.logical_rows.size(0))
+        if nl > 32:
+            return None
+        key = ('lmask', torch.device(device))
+        m = self._casts.get(key)
+        if m is None:
+            rows = (self.logical_rows.cpu().numpy() != 0).astype(np.int64)
+            bits = (rows << np.arange(nl, dtype=np.int64)[:, None]).sum(0) if nl else np.zeros(self.V, np.int64)
+            m = self._casts[key] = torch.as_tensor(bits.astype(np.uint32).view(np.int32), device=device)
+        return m
+
+    def rows_within_components(self, ncomp):
+        """True iff every logical row's support lies inside one of `ncomp` equal contiguous
+        variable blocks (the split Tanner graph's components)."""
+        if ncomp <= 1:
+            return True
+        rows = self.logical_rows.cpu().numpy() != 0
+        Vk = self.V // ncomp
+        for r in rows:
+            blocks = {int(v) // Vk for v in np.nonzero(r)[0]}
+            if len(blocks) > 1:
+                return False
+        return True
+
+    def per_codeword(self, pred, y):
+        """(loss per codeword [B], d loss / d pred): the fused kernel, or the reference formula
+        under autograd where the kernel does not apply (more than 32 logical rows, or graph
+        tables beyond the LDS budget)."""
+        from . import _lib, ops
+        if pred.is_cuda and pred.dtype in (torch.float32, torch.float64):
+            try:
+                return ops.syndrome_loss(self._graph(pred.device), self.logical_rows,
+                                         self.logical_only, pred, y)
+            except _lib.GnndError as e:
+                if e.status != _lib.ERR_UNSUPPORTED:
+                    raise
+        with torch.enable_grad():
+            p = pred.detach().clone().requires_grad_(True)
+            s = _cols(y, self.V).to(p.dtype) + _cols(p, self.V)              # [V, B]
+            t = torch.abs(torch.sin(torch.matmul(self._cast(self.logical, p.dtype), s) * math.pi / 2)).sum(0)
+            if not self.logical_only:
+                t = torch.abs(torch.sin(torch.matmul(self._cast(self.Ht, p.dtype), s) * math.pi / 2)).sum(0) + t
+            t.sum().backward()
+        return t.detach(), p.grad
+
     def reference_forward(self, pred, y):
         s = _cols(y, self.V).to(pred.dtype) + _cols(pred, self.V)
         loss = torch.abs(torch.sin(torch.matmul(self._cast(self.logical, pred.dtype), s) * math.pi / 2)).sum()
@@ -64,9 +114,14 @@ class SyndromeLoss(torch.nn.Module):
 
     def forward(self, pred, y):
         if self.fused and pred.is_cuda and pred.dtype in (torch.float32, torch.float64):
+            from . import _lib
             from .ops import SyndromeLossFn
-            return SyndromeLossFn.apply(pred, y, self._graph(pred.device), self.logical_rows,
-                                        self.logical_only)
+            try:
+                return SyndromeLossFn.apply(pred, y, self._graph(pred.device), self.logical_rows,
+                                            self.logical_only)
+            except _lib.GnndError as e:      # > 32 logical rows / tables beyond the LDS budget
+                if e.status != _lib.ERR_UNSUPPORTED:
+                    raise
         return self.reference_forward(pred, y)
 
 

@@ -299,6 +299,29 @@ def train_backward_partial(graph, model, plain_weights, x, out, grad_out, tape, 
     return ws, int(nr.value)
 
 
+def train_backward_loss_partial(graph, model, plain_weights, x, out, y, logical_mask, n_logical,
+                                logical_only, tape, iters, ws=None):
+    """gnnd_train_bwd_loss_partial: the reverse pass with the syndrome loss fused in (no
+    d loss / d out tensor).  Returns (workspace, rows, per-codeword-and-component losses)."""
+    B = x.numel() // graph.N
+    dt = dtype_code(x.dtype)
+    nr = ctypes.c_int64()
+    _lib.call('gnnd_train_bwd_rows', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nr))
+    nb = ctypes.c_int64()
+    _lib.call('gnnd_train_bwd_workspace', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nb))
+    nl = ctypes.c_int64()
+    _lib.call('gnnd_train_loss_count', graph.handle, B, ctypes.byref(nl))
+    if ws is None or ws.numel() < nb.value:
+        ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
+    loss_b = torch.empty(max(nl.value, 1), dtype=x.dtype, device=x.device)[:nl.value]
+    y = y.to(x.dtype).contiguous()
+    _lib.call('gnnd_train_bwd_loss_partial', graph.handle, _lib.VARIANT[model], dt,
+              _ptr(plain_weights), _ptr(x), _ptr(out), _ptr(y), _ptr(logical_mask), int(n_logical),
+              int(bool(logical_only)), _ptr(tape), _ptr(loss_b), _ptr(ws), nb.value, B, int(iters),
+              current_stream(x.device))
+    return ws, int(nr.value), loss_b
+
+
 def train_update(model, dtype, rows=None, n_rows=0, grad=None, loss_b=None, loss=None,
                  param=None, exp_avg=None, exp_avg_sq=None, step=None, sync=None, lr=3e-4,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, prepared=None, device=None):

@@ -239,7 +239,9 @@ class FusedV24Trainer(_GraphedStep):
 
         forward with tape (gnnd_train_fwd) -> syndrome loss and d loss / d out
         (gnnd_syndrome_loss) -> reverse pass to per-workgroup gradient rows
-        (gnnd_train_bwd_partial) -> fused epilogue (gnnd_train_update: fixed-order row
+        (gnnd_train_bwd_partial; with the syndrome loss of a SyndromeLoss computed inside
+        it, gnnd_train_bwd_loss_partial, the loss launch goes too) -> fused epilogue
+        (gnnd_train_update: fixed-order row
         reduction, the batch loss, Adam, and the kernel-layout weights the next forward reads)
 
     With a collective in play the epilogue is split around the RCCL all_reduce(SUM) of the
@@ -255,7 +257,7 @@ class FusedV24Trainer(_GraphedStep):
     `Trainer` (torch.optim.Adam's order; lr 3e-4, weight decay 1e-9 of the reference)."""
 
     def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
-                 group=None, graph=True, warmup=2, force_collective=False):
+                 group=None, graph=True, warmup=2, force_collective=False, fuse_loss=True):
         from .models import DecoderV24
         if not isinstance(model, DecoderV24):
             raise TypeError('FusedV24Trainer trains decoder_v2_4 (DecoderV24) models')
@@ -264,6 +266,7 @@ class FusedV24Trainer(_GraphedStep):
         self.lr = rlr if lr is None else lr
         self.wd = rwd if weight_decay is None else weight_decay
         self.betas, self.eps = betas, eps
+        self.fuse_loss, self._fuse_ok = fuse_loss, {}
         self._init_graph(graph, warmup, group, force_collective)
         flat = model.packed_weights().detach().clone().contiguous()
         off = 0
@@ -296,6 +299,20 @@ class FusedV24Trainer(_GraphedStep):
         model.graph(flat.device)
         loss_fn._graph(flat.device)
 
+    def _fused_loss_mask(self, g, device):
+        """Logical-row masks for the reverse pass's fused loss, or None (loss kernel path):
+        needs a SyndromeLoss with <= 32 logical rows, each inside one graph component."""
+        from .loss import SyndromeLoss
+        lf = self.loss_fn
+        if not self.fuse_loss or not isinstance(lf, SyndromeLoss):
+            return None
+        key = (g.components, str(device))
+        ok = self._fuse_ok.get(key)
+        if ok is None:
+            ok = self._fuse_ok[key] = (lf.logical_rows.size(0) <= 32 and
+                                       lf.rows_within_components(g.components))
+        return lf.logical_mask(device) if ok else None
+
     def _refresh_prepared(self):
         if self.flat._version != self._prep_version:
             self.prepared.copy_(ops.prepare_weights('v24', self.flat))
@@ -308,15 +325,20 @@ class FusedV24Trainer(_GraphedStep):
         if self.flat.dtype != x.dtype:           # mixed precision: the unfused update path
             w = self.flat.to(x.dtype)
             out, tape = ops.train_forward(g, m.kind, x, ops.prepare_weights(m.kind, w), m.Nc)
-            loss_b, dpred = ops.syndrome_loss(lf._graph(x.device), lf.logical_rows,
-                                              lf.logical_only, out, y)
+            loss_b, dpred = lf.per_codeword(out, y)
             self._gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
             self._pending = None
             return loss_b.sum(), [self._gw]
         out, tape = ops.train_forward(g, m.kind, x, self.prepared, m.Nc)
-        loss_b, dpred = ops.syndrome_loss(lf._graph(x.device), lf.logical_rows, lf.logical_only,
-                                          out, y)
-        ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
+        lmask = self._fused_loss_mask(g, x.device)
+        if lmask is not None:
+            # the syndrome loss computed inside the reverse pass (no loss launch)
+            ws, nrows, loss_b = ops.train_backward_loss_partial(
+                g, m.kind, self.flat, x, out, y, lmask, lf.logical_rows.size(0), lf.logical_only,
+                tape, m.Nc)
+        else:
+            loss_b, dpred = lf.per_codeword(out, y)
+            ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
         if self._dist():
             # rows -> flat gradient and batch loss, for the all-reduce
             ops.train_update('v24', x.dtype, rows=ws, n_rows=nrows, grad=self._gw,

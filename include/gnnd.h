@@ -237,6 +237,20 @@ int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype, const void
                            const void* d_x, const void* d_out, const void* d_grad_out,
                            const void* d_tape, void* d_workspace, int64_t workspace_bytes,
                            int64_t batch, int32_t iters, void* stream);
+/* The reverse pass with the syndrome loss of gnnd_syndrome_loss fused in: d_y [B*V] labels,
+ * d_logical_mask [V] uint32 = bit l set iff variable v is in logical row l (n_logical <= 32;
+ * on a split graph every row's support must lie inside one component).  Each workgroup
+ * computes the loss terms of its codeword (component) and their gradient itself; the losses
+ * go to d_loss_b [gnnd_train_loss_count(batch)] (one per codeword and component, in codeword
+ * order); the batch loss is their sum (gnnd_train_update sums them).  Rows as
+ * gnnd_train_bwd_partial.                                                                  */
+int gnnd_train_loss_count(const gnnd_graph* g, int64_t batch, int64_t* h_count);
+int gnnd_train_bwd_loss_partial(const gnnd_graph* g, int model, int dtype, const void* d_w,
+                                const void* d_x, const void* d_out, const void* d_y,
+                                const uint32_t* d_logical_mask, int32_t n_logical,
+                                int32_t logical_only, const void* d_tape, void* d_loss_b,
+                                void* d_workspace, int64_t workspace_bytes, int64_t batch,
+                                int32_t iters, void* stream);
 /* Fused optimizer epilogue of a decoder_v2_4 training step (one launch):
  *   n_rows > 0: d_grad[i] = fixed-order sum of the rows (d_grad may be NULL: not stored);
  *   n_rows = 0: the gradient is read from d_grad (e.g. after an all-reduce of it);

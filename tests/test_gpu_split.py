@@ -140,3 +140,89 @@ def test_fused_trainer_split_vs_whole_graph():
         for k, v in a.state_dict().items():
             torch.testing.assert_close(b.state_dict()[k], v, rtol=1e-10, atol=1e-13)
         assert ta.step_count.item() == 3.0
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('logical_only', [False, True])
+@pytest.mark.parametrize('split', [True, False])
+def test_fused_loss_reverse_pass_matches_loss_kernel(dtype, logical_only, split):
+    """gnnd_train_bwd_loss_partial (syndrome loss computed per codeword component inside the
+    reverse pass) = gnnd_syndrome_loss + gnnd_train_bwd_partial: per-codeword losses and the
+    reduced gradient."""
+    import gnndecode as gd
+    H = _toric(5)
+    torch.manual_seed(4)
+    T = 5
+    m = gd.MODELS['v24'](T, H).to(DEV).to(dtype)
+    g = m.graph(DEV)
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H), logical_only=logical_only).to(DEV)
+    assert lf.rows_within_components(2)
+    B = 300
+    x, y = gd.data.toric_batch(H, B, seed=9, device=DEV, dtype=dtype)
+    flat = m.packed_weights().detach().to(dtype).contiguous()
+    prep = gd.ops.prepare_weights('v24', flat)
+    try:
+        g.set_split(split)
+        K = g.components if split else 1
+        out, tape = gd.ops.train_forward(g, 'v24', x, prep, T)
+        loss_b, dpred = gd.ops.syndrome_loss(lf._graph(DEV), lf.logical_rows, logical_only, out, y)
+        ws, nrows = gd.ops.train_backward_partial(g, 'v24', flat, x, out, dpred, tape, T)
+        ga = torch.zeros_like(flat)
+        gd.ops.train_update('v24', dtype, rows=ws, n_rows=nrows, grad=ga, device=x.device)
+        ws2, nrows2, lb2 = gd.ops.train_backward_loss_partial(
+            g, 'v24', flat, x, out, y, lf.logical_mask(x.device), lf.logical_rows.size(0),
+            logical_only, tape, T)
+        gb = torch.zeros_like(flat)
+        gd.ops.train_update('v24', dtype, rows=ws2, n_rows=nrows2, grad=gb, device=x.device)
+    finally:
+        g.set_split(True)
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    assert lb2.numel() == B * K
+    per_cw = lb2.view(B, K).double().sum(1)
+    assert (per_cw - loss_b.double()).abs().max().item() <= tol * max(1.0, loss_b.abs().max().item())
+    tolg = 1e-11 if dtype == torch.float64 else 1e-4
+    assert (ga.double() - gb.double()).abs().max().item() <= tolg * max(1.0, ga.abs().max().item())
+
+
+def test_fused_trainer_fused_loss_vs_loss_kernel():
+    import gnndecode as gd
+    H = _toric(7)
+    lg = gd.codes.toric_logicals(H)
+    torch.manual_seed(1)
+    a = gd.MODELS['v24'](4, H).to(DEV)
+    b = gd.MODELS['v24'](4, H).to(DEV)
+    b.load_state_dict(a.state_dict())
+    ta = gd.train.FusedV24Trainer(a, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1)
+    tb = gd.train.FusedV24Trainer(b, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=True, warmup=1,
+                                  fuse_loss=False)
+    for s in range(3):
+        x, y = gd.data.toric_batch(H, 64, seed=20 + s, device=DEV)
+        la = ta.step(gd.data.make_batch(x, a.graph(x.device)), y)
+        lb = tb.step(gd.data.make_batch(x, b.graph(x.device)), y)
+        assert abs(la.item() - lb.item()) <= 1e-11 * max(1.0, abs(lb.item()))
+    for k, v in a.state_dict().items():
+        torch.testing.assert_close(b.state_dict()[k], v, rtol=1e-10, atol=1e-13)
+
+
+def test_syndrome_loss_large_code_uses_big_lds_or_falls_back():
+    """toric L = 20 (fp64) exceeded the loss kernel's 64 KB cap and raised; the cap is
+    now the device limit (opt-in LDS), and beyond it SyndromeLoss falls back to the reference
+    formula (L = 32)."""
+    import gnndecode as gd
+    for L in (20, 32):
+        H = _toric(L)
+        lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+        B, V = 6, H.shape[0]
+        gen = torch.Generator(device='cpu').manual_seed(L)
+        pred = torch.rand(B * V, 1, generator=gen, dtype=torch.float64).to(DEV)
+        y = (torch.rand(B * V, 1, generator=gen) < 0.05).double().to(DEV)
+        p1 = pred.clone().requires_grad_(True)
+        p2 = pred.clone().requires_grad_(True)
+        l1 = lf(p1, y)
+        l1.backward()
+        l2 = lf.reference_forward(p2, y)
+        l2.backward()
+        assert abs(l1.item() - l2.item()) <= 1e-10 * abs(l2.item())
+        torch.testing.assert_close(p1.grad, p2.grad, rtol=1e-10, atol=1e-12)
+        lb, dp = lf.per_codeword(pred, y)
+        assert abs(lb.sum().item() - l2.item()) <= 1e-10 * abs(l2.item())
