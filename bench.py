@@ -92,6 +92,9 @@ def parse():
     p.add_argument('--torch-trainer', action='store_true',
                    help='train mode: torch autograd/optimizer Trainer around the fused kernels '
                         'instead of FusedV24Trainer')
+    p.add_argument('--configs', default='auto', choices=['auto', 'on', 'off'],
+                   help='decode mode: also time BASELINE configs 3-5 in the same process and nest '
+                        'them under "configs" (auto: for the default headline workload)')
     p.add_argument('--mode', default='decode', choices=['decode', 'train', 'sample'],
                    help='train = config 5: decoder_v2_4 (or --model qgnni/nbp/v10) training '
                         'step (DP, RCCL all-reduce); sample = the on-device input synthesis '
@@ -151,7 +154,8 @@ def cpu_workers():
     return max(1, min(16, n))
 
 
-def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds, out_bf16=False):
+def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds, out_bf16=False,
+                 all_cores_leg=True, chunk=512):
     """Time the oracle (numpy restatement of the reference path) on a bounded sample of this
     workload: (1) one thread, comparing its outputs with the GPU's on the same codewords
     (parity, matched BER); (2) all cores: one single-threaded worker process per core
@@ -167,7 +171,6 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds, out_bf1
     except Exception:
         limiter = None
     w = {k: v.detach().cpu().numpy() for k, v in state.items()}
-    chunk = 512
     x_all = x_dev.view(-1, g.N)
     o_all = out_dev.view(-1, g.V)
     # fp32 classical BP is ill-conditioned near its clamps: also decode the first chunks in
@@ -189,7 +192,7 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds, out_bf1
     done, t_total, max_err, mism = 0, 0.0, 0.0, 0
     err_gpu = err_orc = 0
     c_bits = c_gpu = c_orc = 0
-    while t_total < t1 and done + chunk <= x_all.size(0):
+    while (t_total < t1 or done == 0) and done + chunk <= x_all.size(0):
         xs = x_all[done:done + chunk].cpu().numpy().reshape(-1, 1)
         if ref_dt is not None:
             xs = xs.astype(ref_dt)
@@ -225,7 +228,7 @@ def cpu_baseline(model, H, state, x_dev, out_dev, labels, g, T, seconds, out_bf1
     # forks its workers; this GPU process is never forked) over chunks of the same batch
     nw = cpu_workers()
     all_cores, sample_all = None, ''
-    if nw > 1 and one_thread:
+    if nw > 1 and one_thread and all_cores_leg:
         import subprocess
         import tempfile
         per = max(1, int(one_thread * t1 / chunk))                 # ~t1 s of chunks per worker
@@ -359,9 +362,11 @@ def sample_main(a, world, rank, dev):
             'cpu_baseline': None}), flush=True)
 
 
-def train_main(a, world, rank, dev):
+def train_run(a, world, rank, dev, cpu='full'):
     """Config 5: decoder_v2_4 training on the toric code (default L=7), each rank a shard of
-    size --batch, one flat all_reduce(SUM) of the gradient per step (gnndecode.train)."""
+    size --batch, one flat all_reduce(SUM) of the gradient per step (gnndecode.train).
+    cpu='full': the CPU training baseline; 'parity': the first step's loss against the fp64
+    oracle step on the same batch and weights; 'off'.  Returns the result dict on rank 0."""
     code = a.code if a.code.startswith('toric') else 'toric_7'
     model_name = a.model if a.model in ('v24', 'qgnni', 'nbp', 'v10', 'v22', 'v30') else 'v24'
     T = a.iters or gd.DEFAULT_ITERS[model_name]
@@ -379,6 +384,9 @@ def train_main(a, world, rank, dev):
     else:
         lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
                                   logical_only=(model_name == 'qgnni')).to(dev)
+    parity = None
+    if cpu == 'parity' and rank == 0 and model_name == 'v24':
+        parity = train_parity(H, model, lf, T, dev, dtype, a.seed)
     if fused and not a.torch_trainer:
         # prepare -> fwd+tape -> syndrome loss -> reverse pass -> [all_reduce] -> Adam, one HIP graph
         tr = gd.train.FusedV24Trainer(model, lf, graph=not a.no_graph, warmup=2)
@@ -398,8 +406,10 @@ def train_main(a, world, rank, dev):
     if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
+    fused_tr = isinstance(tr, gd.train.FusedV24Trainer)
     for _ in range(a.steps):
-        loss = tr.step(data, y)
+        # the loss stays in the step's static buffer (read after the timed region), no copy
+        loss = tr.step(data, y, copy_loss=False) if fused_tr else tr.step(data, y)
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
@@ -426,10 +436,10 @@ def train_main(a, world, rank, dev):
                               'gnnd_train_bwd, gnnd_adam_step)',
                     'flops_per_sample': 3 * fl, 'transcendentals_per_sample': 2 * trans,
                     'step_ms': step_s * 1e3}
-        cpu = None
-        if model_name == 'v24' and a.cpu_seconds > 0 and world == 1:
-            cpu = train_cpu_baseline(H, model, T, x, y, a.batch, a.cpu_seconds)
-        print(json.dumps({
+        cpu_res = None
+        if model_name == 'v24' and a.cpu_seconds > 0 and world == 1 and cpu == 'full':
+            cpu_res = train_cpu_baseline(H, model, T, x, y, a.batch, a.cpu_seconds)
+        return {
             'metric': f'training samples/sec (whole node), {model_name} step with RCCL grad all-reduce',
             'value': world * a.batch * a.steps / elapsed, 'unit': 'samples/s', 'n_gpus': world,
             'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3,
@@ -442,32 +452,47 @@ def train_main(a, world, rank, dev):
                        'path': ('FusedV24Trainer: gnnd_train_fwd/bwd + gnnd_syndrome_loss + gnnd_adam_step'
                                 if fused and not a.torch_trainer else
                                 'fused gnnd_train_fwd/bwd, torch loss/optimizer' if fused
-                                else 'layer-by-layer propagate ops')},
-            'roofline': roof, 'cpu_baseline': cpu}), flush=True)
+                                else 'layer-by-layer propagate ops'),
+                       'graph_components': model.graph(dev).components},
+            'roofline': roof, 'cpu_baseline': cpu_res, 'parity': parity}
+    return None
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
-    if world > 1 or 'TORCHELASTIC_RUN_ID' in os.environ:
-        # any torchrun launch (also --nproc-per-node 1) brings up RCCL, so the N>1 code path is
-        # the one a 1-GPU torchrun run exercises; bind the communicator to this rank's GPU
-        # (barriers then never touch GPU 0)
-        dist.init_process_group('nccl', device_id=dev)
-    if a.mode == 'train':
-        train_main(a, world, rank, dev)
-        if dist.is_initialized():
-            dist.destroy_process_group()
-        return
-    if a.mode == 'sample':
-        sample_main(a, world, rank, dev)
-        if dist.is_initialized():
-            dist.destroy_process_group()
-        return
+def train_parity(H, model, lf, T, dev, dtype, seed, n=64):
+    """Bounded parity sample of the training objective: the fused GPU forward + syndrome loss
+    of the model's initial weights on n seeded codewords, against the reference training step's
+    forward + LossFunc (oracle/torch_train.py V24Step, fp64) on the same codewords."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import torch_train
+    w = {k: v.detach().cpu().double().numpy() for k, v in model.state_dict().items()}
+    lg = gd.codes.toric_logicals(H)
+    N, V = H.shape[0] + H.shape[1], H.shape[0]
+    x, y = gd.data.toric_batch(H, n, seed=seed + 7, device=dev, dtype=dtype)
+    was = model.training
+    model.eval()
+    with torch.no_grad():
+        pred = model(gd.data.make_batch(x, model.graph(dev)))
+        loss_gpu = float(lf(pred, y))
+    model.train(was)
+    st = torch_train.V24Step(H, lg, w, T)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        ref = st.forward(x.view(-1, N).cpu().double().reshape(-1, 1))
+        loss_ref = float(st.loss(ref, y.view(-1, V).cpu().double()))
+    got = pred.view(-1, V).double().cpu()
+    return {'codewords': n, 'loss_gpu': loss_gpu, 'loss_oracle_f64': loss_ref,
+            'loss_rel_err': abs(loss_gpu - loss_ref) / max(1e-30, abs(loss_ref)),
+            'pred_max_abs_err': float((got - ref).abs().max()),
+            'hard_decision_mismatches': int(((got > 0.5) != (ref > 0.5)).sum()),
+            'oracle': 'oracle/torch_train.py V24Step forward + LossFunc (fp64)',
+            'oracle_seconds': time.perf_counter() - t0}
+
+
+def decode_run(a, world, rank, dev, cpu='full'):
+    """One decode workload (a.model / a.code / a.batch per GPU / a.dtype): K timed launches,
+    BER/FER, roofline; cpu='full' times the oracle (1 thread + all cores), 'parity' only a
+    bounded 1-thread oracle sample for matched-BER parity, 'off' none.  Returns the result
+    dict on rank 0 (None elsewhere)."""
     T = a.iters or gd.DEFAULT_ITERS[a.model]
     # bf16: storage type of x / out only (classical models); weights and arithmetic fp32
     io_dtype = {'f32': torch.float32, 'f64': torch.float64, 'bf16': torch.bfloat16}[a.dtype]
@@ -610,12 +635,81 @@ def main():
                          'hbm_io_bytes_per_launch': io_bytes,
                          'hbm_io_frac': io_bytes / kernel_s / 1e9 / PEAK_HBM_GBS},
         }
-        if a.cpu_seconds > 0 and world == 1:
+        if a.cpu_seconds > 0 and world == 1 and cpu != 'off':
             # the oracle decodes the same (for bf16: widened) inputs in fp32
             res['cpu_baseline'] = cpu_baseline(a.model, H, state, x.to(dtype), pred, labels, g, T,
-                                               a.cpu_seconds, out_bf16=io_dtype == torch.bfloat16)
+                                               a.cpu_seconds, out_bf16=io_dtype == torch.bfloat16,
+                                               all_cores_leg=cpu == 'full',
+                                               chunk=512 if cpu == 'full' else 128)
         else:
             res['cpu_baseline'] = None
+        return res
+    return None
+
+
+# BASELINE.json configs[2..4] timed in the same process as the headline (configs[1]) and
+# nested under "configs" of its JSON line: (name, mode, overrides).  Config 5's entries fix the
+# GLOBAL batch (per-GPU batch = global / world): an N-GPU run of the driver then measures the
+# strong scaling of the reference's batch directly (t_N(global) vs the 1-GPU line's t_1).
+SUB_CONFIGS = [
+    ('config3_toric5_v24_f64', 'decode', dict(model='v24', code='toric_5', batch=65536, dtype='f64',
+                                              steps=10, warmup=2, prewarm_s=0.3)),
+    ('config4_ldpc648_cgnni_shard', 'decode', dict(model='cgnni', code='ldpc_648_324', batch=131072,
+                                                   dtype='f32', steps=20, warmup=2, prewarm_s=0.3)),
+    ('config5_toric7_v24_train_global128', 'train', dict(model='v24', code='toric_7', gbatch=128,
+                                                          dtype='f32', steps=30, warmup=3)),
+    ('config5_toric7_v24_train_global1024', 'train', dict(model='v24', code='toric_7', gbatch=1024,
+                                                           dtype='f32', steps=30, warmup=3)),
+]
+
+
+def sub_config_results(a, world, rank, dev):
+    out = {}
+    for name, mode, ov in SUB_CONFIGS:
+        sa = argparse.Namespace(**vars(a))
+        for k, v in ov.items():
+            setattr(sa, k, v)
+        sa.iters, sa.weights, sa.seed = None, 'auto', a.seed
+        sa.cpu_seconds = min(a.cpu_seconds, 2.0)
+        t0 = time.perf_counter()
+        if mode == 'train':
+            sa.batch = max(1, sa.gbatch // world)
+            sa.no_graph = sa.layerwise = sa.torch_trainer = False
+            r = train_run(sa, world, rank, dev, cpu='parity')
+        else:
+            r = decode_run(sa, world, rank, dev, cpu='parity')
+        if rank == 0:
+            r['wall_s'] = time.perf_counter() - t0
+            out[name] = r
+    return out
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1 or 'TORCHELASTIC_RUN_ID' in os.environ:
+        # any torchrun launch (also --nproc-per-node 1) brings up RCCL, so the N>1 code path is
+        # the one a 1-GPU torchrun run exercises; bind the communicator to this rank's GPU
+        # (barriers then never touch GPU 0)
+        dist.init_process_group('nccl', device_id=dev)
+    res = None
+    if a.mode == 'train':
+        res = train_run(a, world, rank, dev, cpu='full')
+    elif a.mode == 'sample':
+        sample_main(a, world, rank, dev)
+    else:
+        res = decode_run(a, world, rank, dev)
+        # the default run (the headline workload) also times every other BASELINE config
+        headline = a.model == 'cgnni' and a.code == 'bch_63_45' and a.dtype == 'f32'
+        if (a.configs == 'on' or (a.configs == 'auto' and headline)):
+            sub = sub_config_results(a, world, rank, dev)
+            if rank == 0:
+                res['configs'] = sub
+    if rank == 0 and res is not None:
         print(json.dumps(res), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

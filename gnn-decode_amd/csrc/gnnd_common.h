@@ -537,6 +537,43 @@ __device__ __forceinline__ double softplus_tab(double x, const double* __restric
     return x > 20.0 ? x : y;
 }
 
+// The fp64 decoder_v2_4 MLP form: the same tables at the accuracy the fp64 parity contract
+// needs (outputs within rtol 1e-10 of the reference; every Softplus here within 1e-14
+// ABSOLUTE of glibc over the decoders' range, tests/test_fastmath_cpu.py) instead of <= 3 ulp:
+//   exp:   one-part ln2/256 reduction (kd * ulp(ln2/256) <= 2e-16 relative for |y| <= 40;
+//          below that e^y < 5e-18 absolute), degree-4 Taylor (r^5/120 <= 4e-17 relative);
+//   log1p: m = 1 + u rounded (the dropped rounding error c is <= 1.1e-16 absolute), degree-4
+//          series of log1p(t), |t| <= 2^-9 (t^5/5 <= 6e-15 absolute).
+// ~26 fp64 VALU + 2 LDS reads per unit instead of ~33 + 2 (the table pair r_j, l_j is one
+// 16-byte read).
+__device__ __forceinline__ double exp_tab_nonpos_lite(double y, const double* __restrict__ et) {
+    const double tk = __builtin_fma(y, 369.32993046757462, kRoundMagic);   // 256 / ln2
+    const double kd = tk - kRoundMagic;                                // exact
+    const double r = __builtin_fma(-kd, 6.93147180559945309417e-01 / 256, y);
+    double p = __builtin_fma(r, 1.0 / 24, 1.0 / 6);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    const int k = round_magic_lo(tk);
+    return __builtin_ldexp(et[k & (kExpTabN - 1)] * p, k >> 8);
+}
+__device__ __forceinline__ double log1p_tab_unit_lite(double u, const double* __restrict__ lt) {
+    const double m = 1.0 + u;
+    const int j = round_magic_lo(__builtin_fma(u, 256.0, kRoundMagic));    // rint(256 u): 0..256
+    const double rj = lt[2 * j], lj = lt[2 * j + 1];
+    const double t = __builtin_fma(m, rj, -1.0);
+    double q = __builtin_fma(t, -0.25, 1.0 / 3);
+    q = __builtin_fma(q, t, -0.5);
+    return lj + __builtin_fma(q * t, t, t);
+}
+__device__ __forceinline__ double softplus_tab_lite(double x, const double* __restrict__ tab) {
+    const double y = -__builtin_fabs(x);
+    const double r = log1p_tab_unit_lite(exp_tab_nonpos_lite(y > -745.0 ? y : -745.0, tab),
+                                         tab + kExpTabN);
+    const double v = __builtin_fmax(x, 0.0) + r;
+    return x > 20.0 ? x : v;
+}
+
 template <typename T> __device__ __forceinline__ T sigmoid_ref(T x) {
     return T(1) / (T(1) + g_exp(-x));
 }

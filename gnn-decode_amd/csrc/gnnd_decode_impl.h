@@ -244,13 +244,14 @@ struct Mlp10F32 {
 };
 
 // fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1); the
-// Softplus is the table-driven form (tab = the kernel's LDS copy of kExpTab | kLogTab)
+// Softplus is the table-driven form at the parity contract's accuracy (softplus_tab_lite;
+// tab = the kernel's LDS copy of kExpTab | kLogTab)
 __device__ __forceinline__ double mlp128_sp(const double* w, double u, const double* tab) {
     double acc = 0.0;
 #pragma unroll 4
     for (int k = 0; k < 128; ++k) {
         double h = fma(u, w[k], w[128 + k]);
-        acc = fma(softplus_tab(h, tab), w[256 + k], acc);
+        acc = fma(softplus_tab_lite(h, tab), w[256 + k], acc);
     }
     return acc + w[384];
 }
@@ -260,7 +261,7 @@ __device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double
 #pragma unroll 4
     for (int k = 0; k < 128; ++k) {
         double h = fma(u0, w[k], fma(u1, w[128 + k], w[256 + k]));
-        acc = fma(softplus_tab(h, tab), w[384 + k], acc);
+        acc = fma(softplus_tab_lite(h, tab), w[384 + k], acc);
     }
     return acc + w[512];
 }
@@ -1811,13 +1812,15 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     p->lds = fixed + n * per;
     // fp32 decoder_v2_4 at one codeword per workgroup (training steps, small decodes) is
     // latency-bound: one wave per SIMD walks 128 hidden units per edge pair.  Split the units
-    // over US waves (B <= 256: 8 when a codeword's work items fit 128 lanes (1024 threads),
-    // else 4, one 16-wave workgroup per CU; B <= 512: 2).  The partial-sum buffers must fit.
+    // over US waves (B <= 256: 4, one 16-wave workgroup per CU; B <= 512: 2; US = 8 runs 128
+    // item lanes (1024 threads) when a codeword's items fit them).  The partial sums must fit.
     p->us = 1;
     if (v24f32 && n == 1 && g.R <= 2) {
         const int forced = v24_split_forced();
         const bool fit128 = (size_t)g.C * g.G <= 128;
-        int us = forced ? forced : B <= 256 ? (fit128 ? 8 : 4) : B <= 512 ? 2 : 1;
+        // (US = 8 measured slower than 4 on the split toric-7 step, r03c: 0.283 vs 0.276 ms at
+        // B = 128 -- the per-item overhead repeats in every split wave; forced only)
+        int us = forced ? forced : B <= 256 ? 4 : B <= 512 ? 2 : 1;
         if (us == 8 && !fit128) us = 4;
         const size_t il = us == 8 ? 128 : GNND_BLOCK;
         if (us > 1 && align16(p->lds) + (size_t)2 * us * il * 8 + 8 <= kLdsMax) {

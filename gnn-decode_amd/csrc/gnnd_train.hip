@@ -28,6 +28,7 @@
 
 GNND_DEBUG_TU(train)
 #include <type_traits>
+#include <stdlib.h>
 
 namespace {
 
@@ -148,11 +149,24 @@ template <typename T> struct Units {
     f32x2 pgw1a[2], pgw1b[2], pgb1[2], pgw2[2];  // fp32 packed path: per-edge-half partials
     float s1a[2], s1b[2], sb1[2];                // fp32: layer 1 in log2 units (x log2 e)
     __device__ void zero_packed() {
+        zero_pg();
         for (int j = 0; j < 2; ++j) {
-            pgw1a[j] = pgw1b[j] = pgb1[j] = pgw2[j] = f32x2{0.f, 0.f};
             s1a[j] = (float)w1a[j] * kLog2e;
             s1b[j] = (float)w1b[j] * kLog2e;
             sb1[j] = (float)b1[j] * kLog2e;
+        }
+    }
+    // fp32: the per-edge-half partials live for one pass over the edges only (zero_pg at its
+    // start, fold at its end): between passes only the scalar gradients stay in registers
+    __device__ __forceinline__ void zero_pg() {
+        for (int j = 0; j < 2; ++j) pgw1a[j] = pgw1b[j] = pgb1[j] = pgw2[j] = f32x2{0.f, 0.f};
+    }
+    __device__ __forceinline__ void fold() {
+        for (int j = 0; j < 2; ++j) {
+            gw1a[j] += pgw1a[j].x + pgw1a[j].y;
+            gw1b[j] += pgw1b[j].x + pgw1b[j].y;
+            gb1[j] += pgb1[j].x + pgb1[j].y;
+            gw2[j] += (pgw2[j].x + pgw2[j].y) * kLn2;
         }
     }
     __device__ void load1(const T* __restrict__ w, int lane) {    // {W1, b1, W2, b2}
@@ -266,14 +280,9 @@ template <typename T> struct Units {
     }
     // add this wave's gradients into the workgroup accumulator (packed plain layout)
     template <bool TWO>
-    __device__ void flush(T* acc, int lane) {
+    __device__ void flush(T* acc, int lane, bool folded) {
         if constexpr (sizeof(T) == 4)
-            for (int j = 0; j < 2; ++j) {
-                gw1a[j] += pgw1a[j].x + pgw1a[j].y;
-                gw1b[j] += pgw1b[j].x + pgw1b[j].y;
-                gb1[j] += pgb1[j].x + pgb1[j].y;
-                gw2[j] += (pgw2[j].x + pgw2[j].y) * kLn2;
-            }
+            if (!folded) fold();
         for (int j = 0; j < 2; ++j) {
             const int k = lane + 64 * j;
             if constexpr (TWO) {
@@ -381,25 +390,52 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     auto unit_pass = [&](auto& U, auto two_tag, const T* in0, const T* in1, auto dy_of, T* outp) {
         constexpr bool TWO = decltype(two_tag)::value;
         if constexpr (sizeof(T) == 4) {
-            // fp32: four edges f + i W (i = 0..3) per wave step, one shared reduction
+            // fp32: four edges f + i W (i = 0..3) per wave step, one shared reduction; the next
+            // step's inputs are read from LDS before this step's unit work (latency hidden)
             constexpr int W = kTrainWaves, kStride4 = 4 * kTrainWaves;
+            // 8-wave workgroups (256 VGPRs per lane): the per-half partials are pass-local and the
+            // next step's inputs are read ahead; 16-wave ones (128 VGPRs) keep every MLP's
+            // partials resident and read each step's inputs in place (no register spills)
+            constexpr bool kPipe = kTrainThreads <= 512;
+            if constexpr (kPipe) U.zero_pg();
+            auto load = [&](int f, float (&a0)[4], float (&a1)[4], float (&dy)[4]) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int fi = f + i * W;
+                    const bool ok = fi < E;
+                    const int fc = ok ? fi : f;
+                    a0[i] = in0[fc];
+                    a1[i] = TWO ? in1[fc] : 0.f;
+                    dy[i] = ok ? dy_of(fc) : 0.f;
+                }
+            };
             for (int f0 = wave; f0 < E; f0 += 64 * kStride4) {
                 float res[4] = {0.f, 0.f, 0.f, 0.f};
                 int k = 0;
-                for (int f = f0; f < E && k < 64; f += kStride4, ++k) {
-                    float a0[4], a1[4], dy[4], r[4];
+                if constexpr (kPipe) {
+                    float a0[4], a1[4], dy[4];
+                    load(f0, a0, a1, dy);
+                    for (int f = f0; f < E && k < 64; f += kStride4, ++k) {
+                        float b0[4], b1[4], dyn[4], r[4];
+                        const int fn = f + kStride4;
+                        if (fn < E && k + 1 < 64) load(fn, b0, b1, dyn);   // wave-uniform
+                        U.template bwd4_f32<TWO>(a0, a1, dy, r);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int fi = f + i * W;
-                        const bool ok = fi < E;
-                        const int fc = ok ? fi : f;
-                        a0[i] = in0[fc];
-                        a1[i] = TWO ? in1[fc] : 0.f;
-                        dy[i] = ok ? dy_of(fc) : 0.f;
+                        for (int i = 0; i < 4; ++i) {
+                            res[i] = put_lane(res[i], r[i], k, lane);
+                            a0[i] = b0[i];
+                            a1[i] = b1[i];
+                            dy[i] = dyn[i];
+                        }
                     }
-                    U.template bwd4_f32<TWO>(a0, a1, dy, r);
+                } else {
+                    for (int f = f0; f < E && k < 64; f += kStride4, ++k) {
+                        float a0[4], a1[4], dy[4], r[4];
+                        load(f, a0, a1, dy);
+                        U.template bwd4_f32<TWO>(a0, a1, dy, r);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) res[i] = put_lane(res[i], r[i], k, lane);
+                        for (int i = 0; i < 4; ++i) res[i] = put_lane(res[i], r[i], k, lane);
+                    }
                 }
                 const int fl = f0 + kStride4 * lane;
                 if (lane < k) {
@@ -408,6 +444,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                         if (fl + i * W < E) outp[fl + i * W] = res[i];
                 }
             }
+            if constexpr (kPipe) U.fold();
             return;
         }
         constexpr int kStride = 2 * kTrainWaves;
@@ -557,9 +594,10 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     // workgroup gradient: waves add in order (deterministic), then one row per workgroup
     for (int wv = 0; wv < kTrainWaves; ++wv) {
         if (wave == wv) {
-            uv.template flush<true>(s_acc + kV24Ggc1, lane);
-            uc.template flush<false>(s_acc + kV24Ggc2, lane);
-            uo.template flush<false>(s_acc + kV24Mlp, lane);
+            constexpr bool kFolded = kTrainThreads <= 512;      // unit_pass folds per pass
+            uv.template flush<true>(s_acc + kV24Ggc1, lane, kFolded);
+            uc.template flush<false>(s_acc + kV24Ggc2, lane, kFolded);
+            uo.template flush<false>(s_acc + kV24Mlp, lane, kFolded);
         }
         __syncthreads();
     }
@@ -581,6 +619,13 @@ __global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __r
     gw[i] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
+int train_threads_f32() {
+    static int v = [] {
+        const char* e = getenv("GNND_TRAIN_THREADS");
+        return e && atoi(e) == 512 ? 512 : 1024;
+    }();
+    return v;
+}
 // workgroups of the reverse pass: one codeword each up to 1024 (the partial-row count),
 // larger batches loop (each workgroup a fixed, strided set of codewords: deterministic)
 constexpr int64_t kTrainMaxBlocks = 1024;
@@ -621,14 +666,17 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     lossp.ncomp = split ? g->ncomp : 1;
     const size_t lds = train_lds(gk, sizeof(T), lossp.y ? lossp.nl : -1);
     if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
-    auto kern = v24_bwd_kernel<T>;
+    // fp32: 16 waves (128 VGPRs) by default, GNND_TRAIN_THREADS=512 for 8 waves (A/B)
+    const bool w8 = sizeof(T) == 4 && train_threads_f32() == 512;
+    auto kern = w8 ? v24_bwd_kernel<T, 512> : v24_bwd_kernel<T>;
+    const int nthreads = w8 ? 512 : train_threads<T>();
     if (lds > 64 * 1024)
         GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const size_t n = (size_t)iters * B * g->view.E;
     T* base = (T*)tape;
     TapeView<T> tv{base, base + n, base + 2 * n, base + 3 * n};
-    kern<<<(unsigned)blocks, train_threads<T>(), lds, st>>>(
+    kern<<<(unsigned)blocks, nthreads, lds, st>>>(
         gk->view, (const T*)w, (const T*)x, (const T*)out, (const T*)gout, tv, (T*)ws, B, iters,
         split ? g->dcomp : nullptr, (int)cblk, lossp);   // dcomp[0..K): the components' `view`
     GNND_LAUNCH_CHECK();
@@ -881,9 +929,10 @@ adam_kernel(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ m, T* __
 
 // ---------------------------------------------------------------------------------------
 // fused optimizer epilogue of a training step (gnnd_train_update): per parameter i
-//   REDUCE  g_i = fixed-order sum of the reverse pass's per-workgroup rows (16 lanes per
-//           parameter: lane j sums rows j, j+16, ... in order, then a fixed LDS tree), written
-//           to grad (if given); otherwise g_i = grad[i] (an all-reduced gradient)
+//   REDUCE  g_i = fixed-order sum of the reverse pass's per-workgroup rows (a block = 64
+//           parameters x 16 waves: wave w sums rows w, w+16, ... in order with coalesced row
+//           reads, then a fixed LDS tree), written to grad (if given); otherwise g_i = grad[i]
+//           (an all-reduced gradient)
 //   LOSS    block 0 also sums the per-codeword losses in a fixed order -> loss[0]
 //   ADAM    torch.optim.Adam's update (adam_kernel's order) of param/exp_avg/exp_avg_sq, then
 //           the kernel-layout copy of the updated weight (gnnd_prepare_weights' mapping) into
@@ -893,7 +942,7 @@ adam_kernel(T* __restrict__ p, const T* __restrict__ g, T* __restrict__ m, T* __
 // counter.  Nothing else crosses workgroups: one launch replaces grad_reduce, the loss sum,
 // Adam and prepare (four ~5 us launches of the single-rank step).
 // ---------------------------------------------------------------------------------------
-constexpr int kUpdLanes = 16;               // lanes per parameter in the row reduction
+constexpr int kUpdThreads = 1024;           // 16 row groups x 64 parameters per block
 
 // plain packed index i of decoder_v2_4 -> (prepared index, scale) of the fp32 kernel layout
 // (prepare_v24_f32_kernel in gnnd_decode.hip)
@@ -915,18 +964,19 @@ __device__ __forceinline__ int v24_prep_index(int i, float& scale) {
 }
 
 template <typename T>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kUpdThreads)
 train_update_kernel(const T* __restrict__ rows, int nrows, T* __restrict__ grad,
                     const T* __restrict__ loss_b, int64_t nloss, T* __restrict__ loss,
                     T* __restrict__ p, T* __restrict__ m, T* __restrict__ v,
                     double* __restrict__ step, uint32_t* __restrict__ sync, int n, double lr,
                     double b1, double b2, double eps, double wd, T* __restrict__ prepared,
                     int prep_v24_f32) {
-    __shared__ T s_red[256];
+    __shared__ T s_red[kUpdThreads];
     __shared__ double s_t;
     __shared__ T s_coef[2];
-    const int tid = threadIdx.x, j = tid % kUpdLanes, q = tid / kUpdLanes;
-    const int i = blockIdx.x * (256 / kUpdLanes) + q;
+    constexpr int kGroups = kUpdThreads / 64;          // row groups (waves)
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int i = blockIdx.x * 64 + lane;               // this lane's parameter
     const bool adam = p != nullptr;
     if (adam && tid == 0) {                   // bias corrections once per block (double pow)
         s_t = step[0] + 1.0;
@@ -935,28 +985,29 @@ train_update_kernel(const T* __restrict__ rows, int nrows, T* __restrict__ grad,
     }
     T gi = T(0);
     if (rows) {
+        // wave w sums rows w, w + 16, ... of 64 consecutive parameters (coalesced rows),
+        // then a fixed tree over the 16 waves' partials
         T s = T(0);
         if (i < n)
-            for (int r = j; r < nrows; r += kUpdLanes) s += rows[(size_t)r * kV24W + i];
+            for (int r = wv; r < nrows; r += kGroups) s += rows[(size_t)r * kV24W + i];
         s_red[tid] = s;
         __syncthreads();
-        // fixed tree over the 16 lanes of one parameter
-        for (int o = kUpdLanes / 2; o >= 1; o >>= 1) {
-            if (j < o) s_red[tid] += s_red[tid + o];
+        for (int o = kGroups / 2; o >= 1; o >>= 1) {
+            if (wv < o) s_red[tid] += s_red[tid + 64 * o];
             __syncthreads();
         }
-        gi = s_red[q * kUpdLanes];
-        if (grad && j == 0 && i < n) grad[i] = gi;
-    } else if (i < n && j == 0) {
+        gi = s_red[lane];
+        if (grad && wv == 0 && i < n) grad[i] = gi;
+    } else if (i < n && wv == 0) {
         gi = grad[i];
     }
     if (loss_b && blockIdx.x == 0) {          // per-codeword losses, fixed order
         __syncthreads();
         T s = T(0);
-        for (int64_t b = tid; b < nloss; b += 256) s += loss_b[b];
+        for (int64_t b = tid; b < nloss; b += kUpdThreads) s += loss_b[b];
         s_red[tid] = s;
         __syncthreads();
-        for (int o = 128; o >= 1; o >>= 1) {
+        for (int o = kUpdThreads / 2; o >= 1; o >>= 1) {
             if (tid < o) s_red[tid] += s_red[tid + o];
             __syncthreads();
         }
@@ -965,7 +1016,7 @@ train_update_kernel(const T* __restrict__ rows, int nrows, T* __restrict__ grad,
     if (!adam) return;
     __syncthreads();                          // s_t (and every use of step) before arrival
     const double t = s_t;
-    if (j == 0 && i < n) {
+    if (wv == 0 && i < n) {
         const AdamCoef<T> c(s_coef[0], s_coef[1], b1, b2, eps, wd);
         T mi = m[i], vi = v[i];
         const T np = adam_one(c, p[i], gi, mi, vi);
@@ -1104,16 +1155,16 @@ extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64
     if (adam && (!d_exp_avg || !d_exp_avg_sq || !d_step || !d_sync)) return GNND_ERR_INVALID_ARG;
     if (!adam && d_prepared) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
-    const int blocks = (kV24W + 256 / kUpdLanes - 1) / (256 / kUpdLanes);
+    const int blocks = (kV24W + 63) / 64;
     const bool lossb = batch > 0 && d_loss_b;
     if (dtype == GNND_F32)
-        train_update_kernel<float><<<blocks, 256, 0, st>>>(
+        train_update_kernel<float><<<blocks, kUpdThreads, 0, st>>>(
             n_rows ? (const float*)d_rows : nullptr, (int)n_rows, (float*)d_grad,
             lossb ? (const float*)d_loss_b : nullptr, batch, (float*)d_loss, (float*)d_param,
             (float*)d_exp_avg, (float*)d_exp_avg_sq, d_step, d_sync, kV24W, lr, beta1, beta2, eps,
             weight_decay, (float*)d_prepared, 1);
     else
-        train_update_kernel<double><<<blocks, 256, 0, st>>>(
+        train_update_kernel<double><<<blocks, kUpdThreads, 0, st>>>(
             n_rows ? (const double*)d_rows : nullptr, (int)n_rows, (double*)d_grad,
             lossb ? (const double*)d_loss_b : nullptr, batch, (double*)d_loss, (double*)d_param,
             (double*)d_exp_avg, (double*)d_exp_avg_sq, d_step, d_sync, kV24W, lr, beta1, beta2,

@@ -123,7 +123,7 @@ class _GraphedStep:
             return None
         return self._sx, self._sy
 
-    def _run(self, x, y):
+    def _run(self, x, y, copy_loss=True):
         if not self.use_graph:
             return self._eager(x, y).detach().clone()
         if self._g_compute is None:
@@ -157,7 +157,9 @@ class _GraphedStep:
         if self._g_apply is not None:
             self._reduce(self._sloss, self._sgrads)      # eager RCCL between the two graphs
             self._g_apply.replay()
-        return self._sloss.clone()                       # the static buffer is reused
+        # the static buffer is reused by the next replay: a copy unless the caller reads it
+        # before the next step (copy_loss=False skips the one extra copy launch per step)
+        return self._sloss.clone() if copy_loss else self._sloss
 
 
 class Trainer(_GraphedStep):
@@ -359,10 +361,12 @@ class FusedV24Trainer(_GraphedStep):
         else:                                    # the (all-reduced) flat gradient
             ops.train_update('v24', self.flat.dtype, grad=self._gw, **kw)
 
-    def step(self, data, y):
+    def step(self, data, y, copy_loss=True):
+        """One training step; returns the batch loss (copy_loss=False: the graph's static loss
+        buffer itself, valid until the next step)."""
         self.model.train()
         x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
         self._refresh_prepared()
-        out = self._run(x, y)
+        out = self._run(x, y, copy_loss)
         _invalidate(self.model)      # parameters changed on the device (gnnd_train_update)
         return out

@@ -1,9 +1,10 @@
 """The fp64 exp / expm1 / log / tanh / Softplus of the decoders' fp64 paths
 (gnnd_common.h: Taylor exp with a two-part ln2, cancellation-free expm1, atanh-series log,
 tanh via expm1, Softplus as max(x, 0) + log1p(exp(-|x|)), and the table-driven exp / log1p /
-Softplus of the fp64 decoder_v2_4 MLPs) compiled for the HOST with g++
-(the device builtins mapped to exact host equivalents) and compared with glibc over random
-arguments spanning the ranges the decoders feed them: every function within 4 ulp."""
+Softplus) compiled for the HOST with g++ (the device builtins mapped to exact host
+equivalents) and compared with glibc over random arguments spanning the ranges the decoders
+feed them: every function within 4 ulp, except the fp64 decoder_v2_4 MLPs' Softplus
+(softplus_tab_lite), which is held to the absolute error its parity contract needs."""
 import os
 import re
 import shutil
@@ -29,7 +30,7 @@ static double ulp(double a, double b) {
 }
 int main() {
     std::mt19937_64 g(1);
-    double me = 0, ml = 0, mt = 0, mm = 0, ms = 0, mst = 0, met = 0, mlt = 0;
+    double me = 0, ml = 0, mt = 0, mm = 0, ms = 0, mst = 0, met = 0, mlt = 0, msl = 0;
     static double TAB[kFp64TabDoubles];
     for (int i = 0; i < kFp64TabDoubles; ++i) TAB[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
     std::uniform_real_distribution<double> U(-700, 700), L(-300, 300), T(-12, 12), S(-60, 30);
@@ -49,8 +50,10 @@ int main() {
         met = fmax(met, ulp(exp_tab_nonpos(yn, TAB), exp(yn)));
         double uu = (i % 3 == 0) ? exp(-fabs(L(g)) * 0.1) : std::uniform_real_distribution<double>(0, 1)(g);
         mlt = fmax(mlt, ulp(log1p_tab_unit(uu, TAB + kExpTabN), log1p(uu)));
+        double hl = (i % 5) ? S(g) : U(g);
+        msl = fmax(msl, fabs(softplus_tab_lite(hl, TAB) - (hl > 20 ? hl : log1p(exp(hl)))));
     }
-    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f\n", me, ml, mt, mm, ms, mst, met, mlt);
+    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e\n", me, ml, mt, mm, ms, mst, met, mlt, msl);
 }
 '''
 
@@ -71,3 +74,7 @@ def test_fp64_fast_math_ulp(tmp_path):
     errs = dict(zip(['exp', 'log', 'tanh', 'expm1', 'softplus', 'softplus_tab', 'exp_tab',
                      'log1p_tab'], map(float, out)))
     assert all(v <= 4.0 for v in errs.values()), errs
+    # the fp64 decoder_v2_4 MLPs' Softplus (softplus_tab_lite): the relaxed bound DESIGN.md
+    # states — ABSOLUTE error <= 1e-14 over [-700, 700] (the fp64 parity contract is rtol 1e-10
+    # on the decoder outputs; measured 6.2e-15)
+    assert float(out[8]) <= 1e-14, out[8]

@@ -1,0 +1,79 @@
+"""Multi-GPU decode is checkable: data-parallel ranks draw their shards of
+ONE global batch by Philox global codeword offset (bench.py: offset = rank * batch), decode
+them, and all-reduce the hard-decision error counts (gnnd_decision_errors); the result must
+equal a single-process decode of the whole global batch bit for bit.  Two gloo ranks share
+the one GPU here (quantum/error_generate.py:252-278 gen_syn, classical/CGNNI.py:125-147
+Gen_Data: the sampled inputs; classical/CGNNI.py:259-284, quantum/decoder_v2_4.py:272-294:
+the decoders)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CASES = [('cgnni', 'ldpc_648_324', 'f32', 3000), ('v24', 'toric_5', 'f32', 700),
+         ('qbp', 'toric_5', 'f64', 2500)]
+
+
+def _counts(model, code, dtype, B, offset, seed=3):
+    import gnndecode as gd
+    import numpy as np
+    import os
+    from conftest import ROOT
+    dt = torch.float64 if dtype == 'f64' else torch.float32
+    H = gd.codes.get_code(code)
+    dev = torch.device('cuda', 0)
+    T = gd.DEFAULT_ITERS[model]
+    torch.manual_seed(0)
+    m = gd.MODELS[model](T, H).to(dev).eval()
+    wf = os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights', f'{model}_{code}.npz')
+    if os.path.exists(wf):
+        z = np.load(wf)
+        m.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files})
+    g = m.graph(dev)
+    classical = model in ('cgnni', 'cbp')
+    if classical:
+        x, y = gd.data.awgn_batch(H, B, codewords='random', seed=seed, offset=offset, device=dev, dtype=dt)
+        lg = None
+    else:
+        x, y = gd.data.toric_batch(H, B, seed=seed, offset=offset, device=dev, dtype=dt)
+        lg = (torch.as_tensor(gd.codes.toric_logicals(H)) != 0).to(torch.int32)
+    out = gd.ops.decode(g, model, x, T, m.prepared_weights(dt, dev))
+    return gd.ops.decision_errors(g, lg, out, y).cpu()
+
+
+def _worker(rank, world, port, case, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    model, code, dtype, B = case
+    per = B // world
+    c = _counts(model, code, dtype, per, rank * per)
+    dist.all_reduce(c)                       # int64 counts, exact
+    q.put((rank, c.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('case', CASES, ids=[f'{c[0]}-{c[1]}-{c[2]}' for c in CASES])
+def test_two_rank_decode_counts_equal_single_process(case):
+    import socket
+    import torch.multiprocessing as mp
+    sock = socket.socket()
+    sock.bind(('127.0.0.1', 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    model, code, dtype, B = case
+    whole = _counts(model, code, dtype, B, 0).tolist()
+    assert res[0][1] == res[1][1] == whole, (res, whole)
+    assert whole[0] > 0                      # the decoders leave some bit errors at these SNRs/p
