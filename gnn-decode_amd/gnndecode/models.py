@@ -683,14 +683,34 @@ class DecoderV22(_WeightedBP):
         return torch.cat(per + [self.W[t].reshape(-1), self.W_pr[t].reshape(-1),
                                 torch.sigmoid(self.weight).reshape(-1)])
 
+    def fused_ok(self, x, edge_index):
+        """The fused decoder_v2_2 kernel runs on register-resident plans only (its per-layer
+        readout list); a plan that is not resident (utilisation below 0.5, fp64 items beyond
+        the residency budget, GNND_NO_RESIDENT / GNND_NO_F64_RESIDENT) takes the layer path."""
+        if not super().fused_ok(x, edge_index):
+            return False
+        key = ('resident', str(x.device), x.dtype)
+        ok = self._plan_ok.get(key) if hasattr(self, '_plan_ok') else None
+        if ok is None:
+            if not hasattr(self, '_plan_ok'):
+                self._plan_ok = {}
+            plan = ops.decode_plan(self.graph(x.device), self.kind, x.dtype)
+            ok = self._plan_ok[key] = plan['kernel'] == 'decode_resident_kernel'
+        return ok
+
     def forward(self, data):
+        from . import _lib
         x, edge_index = data.x, data.edge_index
         if x.dim() == 1:
             x = x.unsqueeze(1)
         if self.fused_ok(x, edge_index):
             g = self.graph(x.device)
-            out = ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(x.dtype, x.device))
-            return list(out.chunk(self.Nc, 0)) if self.Nc else []
+            try:
+                out = ops.decode(g, self.kind, x, self.Nc, self.prepared_weights(x.dtype, x.device))
+                return list(out.chunk(self.Nc, 0)) if self.Nc else []
+            except _lib.GnndError as e:          # not register-resident after all: layer path
+                if e.status != _lib.ERR_UNSUPPORTED:
+                    raise
         if not x.is_cuda:
             raise RuntimeError('gnndecode runs on the GPU only (HIP/gfx950); move data to cuda')
         self.graph(x.device)

@@ -29,6 +29,9 @@ def main():
     p.add_argument('--lr', type=float, default=1e-3)
     p.add_argument('--seed', type=int, default=0)
     p.add_argument('--out', default=None)
+    # the shipped qgnni_toric_5.npz was trained with decoder_v2_4's weight decay 1e-9
+    # (weights/README.md); quantum/QGNNI.py:294 uses 5e-4 (gnndecode.train.REFERENCE_OPTIM)
+    p.add_argument('--weight-decay', type=float, default=1e-9)
     a = p.parse_args()
     code = f'toric_{a.L}'
     out = a.out or os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights', f'qgnni_{code}.npz')
@@ -49,7 +52,7 @@ def main():
     logical = gd.codes.toric_logicals(H)
     lf = gd.loss.SyndromeLoss(H, logical).to(dev)
     lg = (torch.as_tensor(logical) != 0).to(torch.int32).to(dev)
-    tr = gd.train.Trainer(model, lf, lr=a.lr, graph=True, warmup=2)
+    tr = gd.train.Trainer(model, lf, lr=a.lr, weight_decay=a.weight_decay, graph=True, warmup=2)
     xe, ye = gd.data.toric_batch(H, 8192, seed=10 ** 6, device=dev)
     de = gd.data.make_batch(xe, g)
 
