@@ -123,9 +123,50 @@ def load_pmc(tag):
         return {}
 
 
-# VALU issue capacity: one wave64 VALU instruction per CU per clock (4 SIMDs x one
-# 4-cycle wave64 op); 256 CUs at the 2.4 GHz peak engine clock (MI355X_MICROARCH.md).
-VALU_ISSUE_PER_S = 256 * 2.4e9
+# Issue model: measured issue time of one wave64 instruction per SIMD, by
+# instruction class — tools/micro/issue_cost.hip on this MI355X (8 waves per SIMD, independent
+# chains, clock warmed up; profiles/r03/issue_cost_r03f.txt).  A kernel's issue time is its
+# per-class VALU instruction counts (rocprofv3 SQ_INSTS_VALU_* passes, tools/pmc_classes.sh,
+# committed per codeword as profiles/pmc_classes_<tag>.json) times these costs over the 1 024
+# SIMDs; `issue_frac` = that time / the measured kernel time (<= 1 for a sound model).  FP32
+# FMA/ADD/MUL split into packed and plain forms by SQ_INSTS_VALU_FLOPS_FP32 (a packed op counts
+# twice); unclassified VALU (moves, DPP, selects) at the cheapest measured cost.
+ISSUE_NS = {'pk_f32': 1.90, 'fma_f32': 1.58, 'addmul_f32': 1.04, 'trans_f32': 3.53,
+            'f64': 1.92, 'trans_f64': 6.89, 'int32': 1.22, 'int64': 1.92, 'cvt': 1.22,
+            'other': 1.03}
+N_SIMDS = 256 * 4
+
+
+def load_pmc_classes(tag):
+    path = os.path.join(ROOT, 'profiles', f'pmc_classes_{tag}.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
+def issue_model(cls, codewords, kernel_s):
+    """Issue-time model of one launch over `codewords` from per-codeword class counts."""
+    c = {k[len('SQ_INSTS_VALU_'):] if k != 'SQ_INSTS_VALU' else 'ALL': v * codewords
+         for k, v in cls['per_codeword'].items() if k.startswith('SQ_INSTS_VALU')}
+    g = lambda k: c.get(k, 0.0)
+    fma, addmul = g('FMA_F32'), g('ADD_F32') + g('MUL_F32')
+    scalar_flops = 2 * fma + addmul
+    pk = min(1.0, max(0.0, g('FLOPS_FP32') / scalar_flops - 1.0)) if scalar_flops else 0.0
+    f64 = g('ADD_F64') + g('MUL_F64') + g('FMA_F64')
+    known = fma + addmul + g('TRANS_F32') + f64 + g('TRANS_F64') + g('INT32') + g('INT64') + g('CVT')
+    other = max(0.0, g('ALL') - known)
+    ns = (pk * (fma + addmul) * ISSUE_NS['pk_f32'] +
+          (1 - pk) * (fma * ISSUE_NS['fma_f32'] + addmul * ISSUE_NS['addmul_f32']) +
+          g('TRANS_F32') * ISSUE_NS['trans_f32'] + f64 * ISSUE_NS['f64'] +
+          g('TRANS_F64') * ISSUE_NS['trans_f64'] + g('INT32') * ISSUE_NS['int32'] +
+          g('INT64') * ISSUE_NS['int64'] + g('CVT') * ISSUE_NS['cvt'] + other * ISSUE_NS['other'])
+    t = ns / N_SIMDS * 1e-9
+    return {'issue_model_ms': t * 1e3, 'issue_frac': t / kernel_s, 'packed_fp32_frac': pk,
+            'valu_insts_per_launch': g('ALL'), 'unclassified_valu_frac': other / g('ALL') if g('ALL') else None,
+            'counts_source': f"profiles/pmc_classes_{cls['tag']}.json ({cls['source']})",
+            'costs_ns_per_wave64_inst_per_simd': ISSUE_NS,
+            'costs_source': 'profiles/r03/issue_cost_r03f.txt (tools/micro/issue_cost.hip)'}
 # Transcendental ops (v_exp/v_log/v_rcp_f32): 8 issue cycles per wave64 op per SIMD
 # (MI355X_MICROARCH.md constants; measured 3.5 ns per op per SIMD-wave in
 # tools/micro/issue_mix.hip = 18.7 T/s): 1024 SIMDs x 64 lanes / 8 cycles x 2.4 GHz.
@@ -586,6 +627,12 @@ def decode_run(a, world, rank, dev, cpu='full'):
 
     if rank == 0:
         fl, trans = flops_per_codeword(a.model, g, T)
+        sp_flops = None
+        if a.model == 'v24' and dtype == torch.float64:
+            # fp64 has no hardware exp/log: price each Softplus at the fp64 FLOPs of its
+            # minimal table form (softplus_tab_lite, gnnd_common.h: 11 FMAs + 6 adds/muls = 28)
+            sp_flops = 28
+            fl = fl + sp_flops * trans
         achieved = fl * a.batch / kernel_s / 1e12
         peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
         trans_frac = 2 * trans * a.batch / kernel_s / TRANS_OPS_PER_S
@@ -595,7 +642,7 @@ def decode_run(a, world, rank, dev, cpu='full'):
         tag = f'{a.model}_{a.code}_B{a.batch}_T{T}_{a.dtype}'
         pmc = load_pmc(tag)
         traffic = pmc.get('hbm_bytes_per_launch')
-        valu = (pmc.get('counters_per_dispatch_mean') or {}).get('SQ_INSTS_VALU')
+        cls = load_pmc_classes(f'{a.model}_{a.code}_T{T}_{a.dtype}')
         res = {
             'metric': 'codewords/sec (whole node) at matched BER, T-iter GNN decode',
             'value': world * a.batch * a.steps / elapsed,
@@ -622,13 +669,11 @@ def decode_run(a, world, rank, dev, cpu='full'):
             'roofline': {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
                          'frac': achieved / peak, 'traffic': traffic,
                          'kernel': f"{plan['kernel']}<{a.model}, {a.dtype}>",
-                         # from the committed PMC pass of this workload: wave64 VALU
-                         # instructions per launch / issue capacity over the kernel time
-                         'valu_insts_per_launch': valu,
-                         'valu_issue_frac_at_peak_clock':
-                             valu / (kernel_s * VALU_ISSUE_PER_S) if valu else None,
+                         # per-class VALU counts x measured per-class issue costs (ISSUE_NS)
+                         'issue_model': issue_model(cls, a.batch, kernel_s) if cls else None,
                          'kernel_ms': kernel_s * 1e3,
                          'flops_per_codeword': fl, 'transcendentals_per_codeword': trans,
+                         'softplus_flops_included': sp_flops,
                          # >= 2 hardware transcendental ops per function vs the 8-cycle issue
                          # rate (fp32; fp64 has no hardware transcendentals)
                          'transcendental_op_frac': trans_frac if dtype == torch.float32 else None,

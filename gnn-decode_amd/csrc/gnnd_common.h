@@ -546,11 +546,30 @@ __device__ __forceinline__ double softplus_tab(double x, const double* __restric
 //          series of log1p(t), |t| <= 2^-9 (t^5/5 <= 6e-15 absolute).
 // ~26 fp64 VALU + 2 LDS reads per unit instead of ~33 + 2 (the table pair r_j, l_j is one
 // 16-byte read).
-__device__ __forceinline__ double exp_tab_nonpos_lite(double y, const double* __restrict__ et) {
-    const double tk = __builtin_fma(y, 369.32993046757462, kRoundMagic);   // 256 / ln2
+// a * s + v as ONE VOP3 v_fma_f64 with s in an SGPR pair and v in a (loop-invariant) VGPR pair:
+// gfx9 VOP3 takes no literal and one scalar operand, so hipcc otherwise copies a non-inline
+// constant addend into the accumulator of a v_fmac_f64 before every use (two v_mov_b32)
+__device__ __forceinline__ double fma_vsv(double a, double s, double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(s), "v"(v));
+    return d;
+#else
+    return __builtin_fma(a, s, v);       // host build of this header (tests/test_fastmath_cpu.py)
+#endif
+}
+// e^-|x| for |x| < 2^51 / 369 (no clamp: below -745 the ldexp underflows to 0 exactly); the
+// -|x| is a source modifier of both reduction FMAs
+__device__ __forceinline__ double exp_tab_negabs_lite(double x, const double* __restrict__ et) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double tk;
+    asm("v_fma_f64 %0, -|%1|, %2, %3" : "=v"(tk) : "v"(x), "s"(369.32993046757462), "v"(kRoundMagic));
+#else
+    const double tk = __builtin_fma(-__builtin_fabs(x), 369.32993046757462, kRoundMagic);
+#endif
     const double kd = tk - kRoundMagic;                                // exact
-    const double r = __builtin_fma(-kd, 6.93147180559945309417e-01 / 256, y);
-    double p = __builtin_fma(r, 1.0 / 24, 1.0 / 6);
+    const double r = __builtin_fma(-kd, 6.93147180559945309417e-01 / 256, -__builtin_fabs(x));
+    double p = fma_vsv(r, 1.0 / 24, 1.0 / 6);
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     p = __builtin_fma(p, r, 1.0);
@@ -559,18 +578,26 @@ __device__ __forceinline__ double exp_tab_nonpos_lite(double y, const double* __
 }
 __device__ __forceinline__ double log1p_tab_unit_lite(double u, const double* __restrict__ lt) {
     const double m = 1.0 + u;
-    const int j = round_magic_lo(__builtin_fma(u, 256.0, kRoundMagic));    // rint(256 u): 0..256
+    const int j = round_magic_lo(fma_vsv(u, 256.0, kRoundMagic));      // rint(256 u): 0..256
     const double rj = lt[2 * j], lj = lt[2 * j + 1];
     const double t = __builtin_fma(m, rj, -1.0);
-    double q = __builtin_fma(t, -0.25, 1.0 / 3);
+    double q = fma_vsv(t, -0.25, 1.0 / 3);
     q = __builtin_fma(q, t, -0.5);
     return lj + __builtin_fma(q * t, t, t);
 }
+// max(x, 0) as one v_max_f64 (fmax would canonicalise x first: NaN quieting, one more op)
+__device__ __forceinline__ double relu_f64(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double d;
+    asm("v_max_f64 %0, %1, 0" : "=v"(d) : "v"(x));
+    return d;
+#else
+    return x > 0.0 ? x : 0.0;
+#endif
+}
 __device__ __forceinline__ double softplus_tab_lite(double x, const double* __restrict__ tab) {
-    const double y = -__builtin_fabs(x);
-    const double r = log1p_tab_unit_lite(exp_tab_nonpos_lite(y > -745.0 ? y : -745.0, tab),
-                                         tab + kExpTabN);
-    const double v = __builtin_fmax(x, 0.0) + r;
+    const double r = log1p_tab_unit_lite(exp_tab_negabs_lite(x, tab), tab + kExpTabN);
+    const double v = relu_f64(x) + r;
     return x > 20.0 ? x : v;
 }
 

@@ -246,11 +246,18 @@ struct Mlp10F32 {
 // fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1); the
 // Softplus is the table-driven form at the parity contract's accuracy (softplus_tab_lite;
 // tab = the kernel's LDS copy of kExpTab | kLogTab)
+// the unit's bias into a VGPR pair with ONE v_mov_b64 (its weight stays an SGPR operand of the
+// layer-1 FMA: VOP3 takes one scalar operand)
+__device__ __forceinline__ double vgpr_of(double s) {
+    double d;
+    asm("v_mov_b64 %0, %1" : "=v"(d) : "s"(s));
+    return d;
+}
 __device__ __forceinline__ double mlp128_sp(const double* w, double u, const double* tab) {
     double acc = 0.0;
 #pragma unroll 4
     for (int k = 0; k < 128; ++k) {
-        double h = fma(u, w[k], w[128 + k]);
+        double h = fma_vsv(u, w[k], vgpr_of(w[128 + k]));
         acc = fma(softplus_tab_lite(h, tab), w[256 + k], acc);
     }
     return acc + w[384];
@@ -260,7 +267,7 @@ __device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double
     double acc = 0.0;
 #pragma unroll 4
     for (int k = 0; k < 128; ++k) {
-        double h = fma(u0, w[k], fma(u1, w[128 + k], w[256 + k]));
+        double h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], vgpr_of(w[256 + k])));
         acc = fma(softplus_tab_lite(h, tab), w[384 + k], acc);
     }
     return acc + w[512];
@@ -1679,6 +1686,30 @@ struct Plan {
     const GraphView* dviews = nullptr;   // device [ncomp] views of the plan's kind
 };
 
+// The component split pays while a whole-codeword launch would leave CUs idle: below one
+// codeword per CU (the latency-bound training steps and small decodes).  At larger batches the
+// whole-graph workgroups already fill the chip and the split only doubles the per-codeword
+// fixed costs (measured r03b: toric-7 training step B = 256 0.485 ms split vs 0.449 whole,
+// B = 1024 1.63 vs 1.53; B = 128 0.285 vs 0.397).  GNND_SPLIT_ALWAYS=1 splits at every B.
+int device_cus() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) {
+            (void)hipGetLastError();
+            return 256;
+        }
+        return v;
+    }();
+    return n;
+}
+bool split_pays(int64_t B) {
+    static bool always = [] {
+        const char* e = getenv("GNND_SPLIT_ALWAYS");
+        return e && e[0] == '1';
+    }();
+    return always || B < device_cus();
+}
 // GNND_NO_SPLIT=1: decode split graphs whole (A/B of the component split)
 bool split_disabled() {
     static bool v = [] {
@@ -1836,7 +1867,8 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
 // its own workgroup(s); the plan is made for component 0 (all components share its shape and
 // slot plans) at the launch's B * ncomp component-codewords.
 int plan_for(int model, int dtype, const gnnd_graph* g, Plan* p, int64_t B = INT64_MAX) {
-    if (model == GNND_V24 && g->ncomp > 1 && g->dcomp && !g->nosplit && !split_disabled()) {
+    if (model == GNND_V24 && g->ncomp > 1 && g->dcomp && !g->nosplit && !split_disabled() &&
+        split_pays(B)) {
         const int K = g->ncomp;
         const gnnd_graph* c0 = g->comp[0];
         const int64_t BK = B > INT64_MAX / K ? INT64_MAX : B * K;

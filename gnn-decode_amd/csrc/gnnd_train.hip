@@ -148,12 +148,14 @@ template <typename T> struct Units {
     T gw1a[2], gw1b[2], gb1[2], gw2[2], gb2;
     f32x2 pgw1a[2], pgw1b[2], pgb1[2], pgw2[2];  // fp32 packed path: per-edge-half partials
     float s1a[2], s1b[2], sb1[2];                // fp32: layer 1 in log2 units (x log2 e)
+    float ws1a[2];                               // fp32: W2 s1a (d input with W2 factored out)
     __device__ void zero_packed() {
         zero_pg();
         for (int j = 0; j < 2; ++j) {
             s1a[j] = (float)w1a[j] * kLog2e;
             s1b[j] = (float)w1b[j] * kLog2e;
             sb1[j] = (float)b1[j] * kLog2e;
+            ws1a[j] = (float)w2[j] * s1a[j];
         }
     }
     // fp32: the per-edge-half partials live for one pass over the edges only (zero_pg at its
@@ -161,11 +163,11 @@ template <typename T> struct Units {
     __device__ __forceinline__ void zero_pg() {
         for (int j = 0; j < 2; ++j) pgw1a[j] = pgw1b[j] = pgb1[j] = pgw2[j] = f32x2{0.f, 0.f};
     }
-    __device__ __forceinline__ void fold() {
+    __device__ __forceinline__ void fold() {       // (layer-1 partials carry no W2 factor)
         for (int j = 0; j < 2; ++j) {
-            gw1a[j] += pgw1a[j].x + pgw1a[j].y;
-            gw1b[j] += pgw1b[j].x + pgw1b[j].y;
-            gb1[j] += pgb1[j].x + pgb1[j].y;
+            gw1a[j] += (pgw1a[j].x + pgw1a[j].y) * (float)w2[j];
+            gw1b[j] += (pgw1b[j].x + pgw1b[j].y) * (float)w2[j];
+            gb1[j] += (pgb1[j].x + pgb1[j].y) * (float)w2[j];
             gw2[j] += (pgw2[j].x + pgw2[j].y) * kLn2;
         }
     }
@@ -263,16 +265,20 @@ template <typename T> struct Units {
             const f32x2 z = {__builtin_amdgcn_exp2f(hc.x), __builtin_amdgcn_exp2f(hc.y)};
             const f32x2 z1 = z + 1.f;
             const f32x2 l = {__builtin_amdgcn_logf(z1.x), __builtin_amdgcn_logf(z1.y)};
-            // l + (h - hc): l below the cap, h (to within an ulp) above it; two packed adds
-            // instead of max(h, l) (whose fmaxf form adds NaN-quieting maxes in IEEE mode)
-            const f32x2 sp = l + (h - hc);
+            // sp log2 e = max(h, l): l > h below the cap, h above it (l of the capped
+            // argument); two plain v_max_f32 (fmaxf would add NaN-quieting canonicalisations)
+            f32x2 sp;
+            asm("v_max_f32 %0, %1, %2" : "=v"(sp.x) : "v"(h.x), "v"(l.x));
+            asm("v_max_f32 %0, %1, %2" : "=v"(sp.y) : "v"(h.y), "v"(l.y));
             const f32x2 sg = z * f32x2{__builtin_amdgcn_rcpf(z1.x), __builtin_amdgcn_rcpf(z1.y)};
             pgw2[j] = dy * sp + pgw2[j];
-            const f32x2 dh = (dy * (float)w2[j]) * sg;
+            // dh = dy W2 sg: the lane's constant W2 is factored out of the layer-1 partials
+            // (applied in fold) and into ws1a = W2 s1a for d input: one packed multiply less
+            const f32x2 dh = dy * sg;
             pgw1a[j] = dh * x0 + pgw1a[j];
             if constexpr (TWO) pgw1b[j] = dh * x1 + pgw1b[j];
             pgb1[j] = pgb1[j] + dh;
-            p = dh * s1a[j] + p;             // d input in log2 units (ln 2 below)
+            p = dh * ws1a[j] + p;            // d input in log2 units (ln 2 below)
         }
         gb2 += dya;
         gb2 += dyb;
@@ -309,8 +315,8 @@ template <typename T> struct BwdLoss {
 };
 // Split graphs (views non-null): blocks [k*cblk, (k+1)*cblk) run component k (graph views[k],
 // rows addressed through its GraphView addressing fields) of codewords j, j + cblk, ...
-template <typename T, int kTrainThreads = train_threads<T>()>
-__global__ void __launch_bounds__(kTrainThreads)
+template <typename T, int kTrainThreads = train_threads<T>(), int kMinWaves = 1>
+__global__ void __launch_bounds__(kTrainThreads, kMinWaves)   // kMinWaves: per SIMD
 v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                const T* __restrict__ p, const T* __restrict__ gp, TapeView<T> tape,
                T* __restrict__ gpart, int64_t B, int iters, const GraphView* __restrict__ views,
@@ -396,7 +402,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             // 8-wave workgroups (256 VGPRs per lane): the per-half partials are pass-local and the
             // next step's inputs are read ahead; 16-wave ones (128 VGPRs) keep every MLP's
             // partials resident and read each step's inputs in place (no register spills)
-            constexpr bool kPipe = kTrainThreads <= 512;
+            constexpr bool kPipe = kTrainThreads <= 512 && kMinWaves == 1;
             if constexpr (kPipe) U.zero_pg();
             auto load = [&](int f, float (&a0)[4], float (&a1)[4], float (&dy)[4]) {
 #pragma unroll
@@ -561,40 +567,47 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
         unit_pass(uo, std::false_type{}, s_u, nullptr, [&](int f) { return s_da[f]; }, s_dm);
         __syncthreads();
 
+#ifndef GNND_BWD_EXP
+#define GNND_BWD_EXP 0   // timing experiments only (wrong gradients): 1 no LOO compute,
+#endif                   // 2 no LOO phases or their barriers, 3 no unit passes
         for (int it = iters - 1; it >= 0; --it) {
             stage(it);
             __syncthreads();
             if (it > 0) prefetch(it - 1);
             // A: m^{t+1} = MLP_c(u) s_c + m^t
-            unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; }, s_g);
+            if (GNND_BWD_EXP != 3)
+                unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; }, s_g);
             __syncthreads();
             // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
             for (int f = tid; f < E; f += kTrainThreads) {
                 const int c = (int)(s_evc[f] >> 16);
                 T s = T(0);
-                for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += s_g[s_cedge[k]];
+                if (GNND_BWD_EXP == 0 || GNND_BWD_EXP == 3)
+                    for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += s_g[s_cedge[k]];
                 const T t = s_t[f];
                 s_da[f] = ((s - s_g[f]) * (T(1) - t * t)) / T(2);
             }
-            __syncthreads();
+            if (GNND_BWD_EXP != 2) __syncthreads();
             // C: a = MLP_v(ext, x_v)
-            unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; }, s_g);
+            if (GNND_BWD_EXP != 3)
+                unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; }, s_g);
             __syncthreads();
             // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
             for (int f = tid; f < E; f += kTrainThreads) {
                 const int v = (int)(s_evc[f] & 0xffffu);
                 T s = T(0);
-                for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += s_g[k];
+                if (GNND_BWD_EXP == 0 || GNND_BWD_EXP == 3)
+                    for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += s_g[k];
                 s_dm[f] += s - s_g[f];
             }
-            __syncthreads();
+            if (GNND_BWD_EXP != 2) __syncthreads();
         }
     }
 
     // workgroup gradient: waves add in order (deterministic), then one row per workgroup
     for (int wv = 0; wv < kTrainWaves; ++wv) {
         if (wave == wv) {
-            constexpr bool kFolded = kTrainThreads <= 512;      // unit_pass folds per pass
+            constexpr bool kFolded = kTrainThreads <= 512 && kMinWaves == 1;   // unit_pass folds
             uv.template flush<true>(s_acc + kV24Ggc1, lane, kFolded);
             uc.template flush<false>(s_acc + kV24Ggc2, lane, kFolded);
             uo.template flush<false>(s_acc + kV24Mlp, lane, kFolded);
@@ -619,10 +632,13 @@ __global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __r
     gw[i] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
+// fp32 reverse-pass workgroup shape (GNND_TRAIN_THREADS, A/B): 1024 = 16 waves, one workgroup
+// per CU (default); 512 = 8 waves with 256 VGPRs; 5122 = 8 waves, two workgroups per CU
 int train_threads_f32() {
     static int v = [] {
         const char* e = getenv("GNND_TRAIN_THREADS");
-        return e && atoi(e) == 512 ? 512 : 1024;
+        const int n = e ? atoi(e) : 0;
+        return n == 512 || n == 5122 ? n : 1024;
     }();
     return v;
 }
@@ -631,17 +647,17 @@ int train_threads_f32() {
 constexpr int64_t kTrainMaxBlocks = 1024;
 int64_t train_blocks(int64_t B) { return B < kTrainMaxBlocks ? B : kTrainMaxBlocks; }
 // the reverse pass on a split graph: each component of a codeword in its own workgroup
-bool train_split(const gnnd_graph* g) {
-    return g->ncomp > 1 && g->dcomp && !g->nosplit && !split_disabled();
+bool train_split(const gnnd_graph* g, int64_t B) {
+    return g->ncomp > 1 && g->dcomp && !g->nosplit && !split_disabled() && split_pays(B);
 }
 // workgroups per component and in all (<= kTrainMaxBlocks gradient rows)
 int64_t train_cblk(const gnnd_graph* g, int64_t B) {
-    if (!train_split(g)) return train_blocks(B);
+    if (!train_split(g, B)) return train_blocks(B);
     const int64_t per = kTrainMaxBlocks / g->ncomp;
     return B < per ? B : per;
 }
 int64_t train_rows(const gnnd_graph* g, int64_t B) {
-    return train_split(g) ? train_cblk(g, B) * g->ncomp : train_blocks(B);
+    return train_split(g, B) ? train_cblk(g, B) * g->ncomp : train_blocks(B);
 }
 size_t train_lds(const gnnd_graph* g, int esz, int nl = -1) {   // nl >= 0: fused loss
     const GraphView& v = g->view;
@@ -659,7 +675,7 @@ template <typename T>
 int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* out,
                const void* gout, const void* tape, void* gw, void* ws, int64_t ws_bytes,
                int64_t B, int iters, hipStream_t st, BwdLoss<T> lossp = {}) {
-    const bool split = train_split(g);
+    const bool split = train_split(g, B);
     const gnnd_graph* gk = split ? g->comp[0] : g;        // components share one shape
     const int64_t cblk = train_cblk(g, B), blocks = train_rows(g, B);
     if ((int64_t)blocks * kV24W * (int64_t)sizeof(T) > ws_bytes) return GNND_ERR_INVALID_ARG;
@@ -667,9 +683,11 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     const size_t lds = train_lds(gk, sizeof(T), lossp.y ? lossp.nl : -1);
     if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     // fp32: 16 waves (128 VGPRs) by default, GNND_TRAIN_THREADS=512 for 8 waves (A/B)
-    const bool w8 = sizeof(T) == 4 && train_threads_f32() == 512;
-    auto kern = w8 ? v24_bwd_kernel<T, 512> : v24_bwd_kernel<T>;
-    const int nthreads = w8 ? 512 : train_threads<T>();
+    const int shape = sizeof(T) == 4 ? train_threads_f32() : 0;
+    // (5122: two 8-wave workgroups per CU = 4 waves per SIMD, 128 VGPRs)
+    auto kern = shape == 512 ? v24_bwd_kernel<T, 512> : shape == 5122 ? v24_bwd_kernel<T, 512, 4>
+                                                                       : v24_bwd_kernel<T>;
+    const int nthreads = shape == 512 || shape == 5122 ? 512 : train_threads<T>();
     if (lds > 64 * 1024)
         GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1113,7 +1131,7 @@ extern "C" int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype,
 
 extern "C" int gnnd_train_loss_count(const gnnd_graph* g, int64_t batch, int64_t* h_count) {
     if (!g || batch < 0 || !h_count) return GNND_ERR_INVALID_ARG;
-    *h_count = batch * (train_split(g) ? g->ncomp : 1);
+    *h_count = batch * (train_split(g, batch) ? g->ncomp : 1);
     return GNND_OK;
 }
 

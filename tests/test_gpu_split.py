@@ -2,7 +2,8 @@
 
 The toric code's H is block diagonal (quantum/error_generate.py:39-132: X and Z halves, every
 logical row inside one half), so decoder_v2_4 decodes and trains each component of a codeword
-in its own workgroup.  The components share no edge and the per-edge arithmetic is the same,
+in its own workgroup — below one codeword per CU (split_pays; larger batches fill the chip whole
+and run whole-graph workgroups, so the larger-B cases here check that path's equality too).  The components share no edge and the per-edge arithmetic is the same,
 so the split decode must equal the whole-graph decode BIT FOR BIT (forward outputs and the
 training tape); the reverse pass sums its per-workgroup gradient rows in a different grouping
 (fp rounding only).  Also: the fused optimizer epilogue (gnnd_train_update) against the
@@ -157,7 +158,7 @@ def test_fused_loss_reverse_pass_matches_loss_kernel(dtype, logical_only, split)
     g = m.graph(DEV)
     lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H), logical_only=logical_only).to(DEV)
     assert lf.rows_within_components(2)
-    B = 300
+    B = 100                      # below one codeword per CU: the split applies (split_pays)
     x, y = gd.data.toric_batch(H, B, seed=9, device=DEV, dtype=dtype)
     flat = m.packed_weights().detach().to(dtype).contiguous()
     prep = gd.ops.prepare_weights('v24', flat)
