@@ -538,14 +538,14 @@ __device__ __forceinline__ double softplus_tab(double x, const double* __restric
 }
 
 // The fp64 decoder_v2_4 MLP form: the same tables at the accuracy the fp64 parity contract
-// needs (outputs within rtol 1e-10 of the reference; every Softplus here within 1e-14
+// needs (outputs within rtol 1e-10 of the reference; every Softplus here within 1e-13
 // ABSOLUTE of glibc over the decoders' range, tests/test_fastmath_cpu.py) instead of <= 3 ulp:
 //   exp:   one-part ln2/256 reduction (kd * ulp(ln2/256) <= 2e-16 relative for |y| <= 40;
-//          below that e^y < 5e-18 absolute), degree-4 Taylor (r^5/120 <= 4e-17 relative);
+//          below that e^y < 5e-18 absolute), degree-3 Taylor (r^4/24 <= 1.4e-13 relative);
 //   log1p: m = 1 + u rounded (the dropped rounding error c is <= 1.1e-16 absolute), degree-4
 //          series of log1p(t), |t| <= 2^-9 (t^5/5 <= 6e-15 absolute).
-// ~26 fp64 VALU + 2 LDS reads per unit instead of ~33 + 2 (the table pair r_j, l_j is one
-// 16-byte read).
+// 29 VALU (21 of them fp64) + 2 LDS reads per unit instead of ~37 + 2 (the table pair r_j, l_j
+// is one 16-byte read).
 // a * s + v as ONE VOP3 v_fma_f64 with s in an SGPR pair and v in a (loop-invariant) VGPR pair:
 // gfx9 VOP3 takes no literal and one scalar operand, so hipcc otherwise copies a non-inline
 // constant addend into the accumulator of a v_fmac_f64 before every use (two v_mov_b32)
@@ -569,8 +569,7 @@ __device__ __forceinline__ double exp_tab_negabs_lite(double x, const double* __
 #endif
     const double kd = tk - kRoundMagic;                                // exact
     const double r = __builtin_fma(-kd, 6.93147180559945309417e-01 / 256, -__builtin_fabs(x));
-    double p = fma_vsv(r, 1.0 / 24, 1.0 / 6);
-    p = __builtin_fma(p, r, 0.5);
+    double p = fma_vsv(r, 1.0 / 6, 0.5);                              // degree 3: r^4/24 <= 1.4e-13
     p = __builtin_fma(p, r, 1.0);
     p = __builtin_fma(p, r, 1.0);
     const int k = round_magic_lo(tk);
