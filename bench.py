@@ -123,18 +123,23 @@ def load_pmc(tag):
         return {}
 
 
-# Issue model: measured issue time of one wave64 instruction per SIMD, by
-# instruction class — tools/micro/issue_cost.hip on this MI355X (8 waves per SIMD, independent
-# chains, clock warmed up; profiles/r03/issue_cost_r03f.txt).  A kernel's issue time is its
-# per-class VALU instruction counts (rocprofv3 SQ_INSTS_VALU_* passes, tools/pmc_classes.sh,
-# committed per codeword as profiles/pmc_classes_<tag>.json) times these costs over the 1 024
-# SIMDs; `issue_frac` = that time / the measured kernel time (<= 1 for a sound model).  FP32
-# FMA/ADD/MUL split into packed and plain forms by SQ_INSTS_VALU_FLOPS_FP32 (a packed op counts
-# twice); unclassified VALU (moves, DPP, selects) at the cheapest measured cost.
-ISSUE_NS = {'pk_f32': 1.90, 'fma_f32': 1.58, 'addmul_f32': 1.04, 'trans_f32': 3.53,
-            'f64': 1.92, 'trans_f64': 6.89, 'int32': 1.22, 'int64': 1.92, 'cvt': 1.22,
-            'other': 1.03}
+# Issue model: a kernel's VALU issue time from its per-class instruction
+# counts (rocprofv3 SQ_INSTS_VALU_* passes, tools/pmc_classes.sh; committed per codeword as
+# profiles/pmc_classes_<tag>.json) times each class's issue cycles per wave64 instruction on one
+# SIMD, over the 1 024 SIMDs at the 2.4 GHz peak engine clock; `issue_frac` = that time / the
+# measured kernel time.  Cycles (MI355X_MICROARCH.md constants; ratios confirmed by
+# tools/micro/issue_cost.hip, profiles/r03/issue_cost_r03f.txt): plain VOP2 fp32 / int / move 2,
+# packed fp32 (v_pk_*) 4, fp64 add/mul/fma 4, fp32 transcendental 8, fp64 transcendental 16.
+# The micro measured VOP3-encoded forms (v_fma_f32, v_bfe_u32, v_lshl_add_u64, a VOP3
+# v_cndmask) at up to 2x their VOP2 cost and everything ~1.2x slower in ns than 2.4 GHz cycles,
+# so the model is a LOWER bound on issue time: issue_frac <= 1 for a sound count, and the gap
+# to 1 is issue slack plus VOP3 / clock effects.  FP32 FMA/ADD/MUL are split into packed and
+# plain forms by SQ_INSTS_VALU_FLOPS_FP32 (a packed op counts twice); unclassified VALU
+# (moves, DPP, selects, bit ops) at 2 cycles.
+ISSUE_CYCLES = {'pk_f32': 4, 'fma_f32': 2, 'addmul_f32': 2, 'trans_f32': 8, 'f64': 4,
+                'trans_f64': 16, 'int32': 2, 'int64': 4, 'cvt': 2, 'other': 2}
 N_SIMDS = 256 * 4
+CLOCK_HZ = 2.4e9
 
 
 def load_pmc_classes(tag):
@@ -156,21 +161,20 @@ def issue_model(cls, codewords, kernel_s):
     f64 = g('ADD_F64') + g('MUL_F64') + g('FMA_F64')
     known = fma + addmul + g('TRANS_F32') + f64 + g('TRANS_F64') + g('INT32') + g('INT64') + g('CVT')
     other = max(0.0, g('ALL') - known)
-    ns = (pk * (fma + addmul) * ISSUE_NS['pk_f32'] +
-          (1 - pk) * (fma * ISSUE_NS['fma_f32'] + addmul * ISSUE_NS['addmul_f32']) +
-          g('TRANS_F32') * ISSUE_NS['trans_f32'] + f64 * ISSUE_NS['f64'] +
-          g('TRANS_F64') * ISSUE_NS['trans_f64'] + g('INT32') * ISSUE_NS['int32'] +
-          g('INT64') * ISSUE_NS['int64'] + g('CVT') * ISSUE_NS['cvt'] + other * ISSUE_NS['other'])
-    t = ns / N_SIMDS * 1e-9
+    cy = ISSUE_CYCLES
+    cycles = (pk * (fma + addmul) * cy['pk_f32'] +
+              (1 - pk) * (fma * cy['fma_f32'] + addmul * cy['addmul_f32']) +
+              g('TRANS_F32') * cy['trans_f32'] + f64 * cy['f64'] + g('TRANS_F64') * cy['trans_f64'] +
+              g('INT32') * cy['int32'] + g('INT64') * cy['int64'] + g('CVT') * cy['cvt'] +
+              other * cy['other'])
+    t = cycles / N_SIMDS / CLOCK_HZ
     return {'issue_model_ms': t * 1e3, 'issue_frac': t / kernel_s, 'packed_fp32_frac': pk,
-            'valu_insts_per_launch': g('ALL'), 'unclassified_valu_frac': other / g('ALL') if g('ALL') else None,
+            'valu_insts_per_launch': g('ALL'),
+            'unclassified_valu_frac': other / g('ALL') if g('ALL') else None,
             'counts_source': f"profiles/pmc_classes_{cls['tag']}.json ({cls['source']})",
-            'costs_ns_per_wave64_inst_per_simd': ISSUE_NS,
-            'costs_source': 'profiles/r03/issue_cost_r03f.txt (tools/micro/issue_cost.hip)'}
-# Transcendental ops (v_exp/v_log/v_rcp_f32): 8 issue cycles per wave64 op per SIMD
-# (MI355X_MICROARCH.md constants; measured 3.5 ns per op per SIMD-wave in
-# tools/micro/issue_mix.hip = 18.7 T/s): 1024 SIMDs x 64 lanes / 8 cycles x 2.4 GHz.
-TRANS_OPS_PER_S = 1024 * 64 / 8 * 2.4e9
+            'cycles_per_wave64_inst': ISSUE_CYCLES,
+            'note': 'lower bound on VALU issue time (VOP3 forms and the clock measured up to 2x / '
+                    '1.2x slower, profiles/r03/issue_cost_r03f.txt)'}
 
 
 def cpu_model():
