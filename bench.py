@@ -140,6 +140,10 @@ ISSUE_CYCLES = {'pk_f32': 4, 'fma_f32': 2, 'addmul_f32': 2, 'trans_f32': 8, 'f64
                 'trans_f64': 16, 'int32': 2, 'int64': 4, 'cvt': 2, 'other': 2}
 N_SIMDS = 256 * 4
 CLOCK_HZ = 2.4e9
+# Transcendental ops (v_exp/v_log/v_rcp_f32): 8 issue cycles per wave64 op per SIMD
+# (MI355X_MICROARCH.md constants; measured 3.5 ns per op per SIMD-wave in
+# tools/micro/issue_mix.hip = 18.7 T/s): 1024 SIMDs x 64 lanes / 8 cycles x 2.4 GHz.
+TRANS_OPS_PER_S = N_SIMDS * 64 / ISSUE_CYCLES['trans_f32'] * CLOCK_HZ
 
 
 def load_pmc_classes(tag):
