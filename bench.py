@@ -423,7 +423,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     H = gd.codes.get_code(code)
     torch.manual_seed(a.seed)
     model = gd.MODELS[model_name](T, H).to(dev).to(dtype)
-    fused = model_name == 'v24' and not a.layerwise
+    fused = model_name in ('v24', 'v30') and not a.layerwise
     if model_name == 'v24':
         model.fused_train = fused
     if model_name == 'v22':          # decoder_v2_2's LossFunc: every layer's readout
@@ -436,7 +436,10 @@ def train_run(a, world, rank, dev, cpu='full'):
     parity = None
     if cpu == 'parity' and rank == 0 and model_name == 'v24':
         parity = train_parity(H, model, lf, T, dev, dtype, a.seed)
-    if fused and not a.torch_trainer:
+    if fused and model_name == 'v30':
+        # fwd+tape -> reference LossFunc (torch) -> reverse pass -> [all_reduce] -> Adam
+        tr = gd.train.FusedV30Trainer(model, lf, graph=not a.no_graph, warmup=2)
+    elif fused and not a.torch_trainer:
         # prepare -> fwd+tape -> syndrome loss -> reverse pass -> [all_reduce] -> Adam, one HIP graph
         tr = gd.train.FusedV24Trainer(model, lf, graph=not a.no_graph, warmup=2)
     else:
@@ -455,7 +458,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
-    fused_tr = isinstance(tr, gd.train.FusedV24Trainer)
+    fused_tr = isinstance(tr, (gd.train.FusedV24Trainer, gd.train.FusedV30Trainer))
     for _ in range(a.steps):
         # the loss stays in the step's static buffer (read after the timed region), no copy
         loss = tr.step(data, y, copy_loss=False) if fused_tr else tr.step(data, y)
@@ -470,19 +473,21 @@ def train_run(a, world, rank, dev, cpu='full'):
     if rank == 0:
         step_s = elapsed / a.steps
         roof = None
-        if model_name == 'v24':
+        if model_name in ('v24', 'v30') and fused:
             # training ~ 3x the forward's algorithmic FLOPs: forward, the
             # reverse pass through every MLP (2x); transcendentals: forward Softplus + the
             # backward sigmoid of every unit.  Whole captured step (prepare, forward+tape,
             # loss, reverse pass, Adam) over its wall time per step.
             g = model.graph(dev)
-            fl, trans = flops_per_codeword('v24', g, T)
+            fl, trans = flops_per_codeword(model_name, g, T)
             peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
             achieved = 3 * fl * a.batch / step_s / 1e12
             roof = {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
                     'frac': achieved / peak, 'traffic': None,
-                    'kernel': 'FusedV24Trainer step (HIP graph: gnnd_train_fwd, gnnd_syndrome_loss, '
-                              'gnnd_train_bwd, gnnd_adam_step)',
+                    'kernel': ('FusedV24Trainer step (HIP graph: gnnd_train_fwd, gnnd_syndrome_loss, '
+                               'gnnd_train_bwd, gnnd_adam_step)' if model_name == 'v24' else
+                               'FusedV30Trainer step (HIP graph: gnnd_train_fwd, V30Loss autograd, '
+                               'gnnd_train_bwd_partial, gnnd_train_update)'),
                     'flops_per_sample': 3 * fl, 'transcendentals_per_sample': 2 * trans,
                     'step_ms': step_s * 1e3}
         cpu_res = None
@@ -498,7 +503,9 @@ def train_run(a, world, rank, dev, cpu='full'):
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
                        'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters()),
                        'hip_graph': not a.no_graph,
-                       'path': ('FusedV24Trainer: gnnd_train_fwd/bwd + gnnd_syndrome_loss + gnnd_adam_step'
+                       'path': ('FusedV30Trainer: gnnd_train_fwd/bwd (V30) + V30Loss + gnnd_train_update'
+                                if fused and model_name == 'v30' else
+                                'FusedV24Trainer: gnnd_train_fwd/bwd + gnnd_syndrome_loss + gnnd_adam_step'
                                 if fused and not a.torch_trainer else
                                 'fused gnnd_train_fwd/bwd, torch loss/optimizer' if fused
                                 else 'layer-by-layer propagate ops'),

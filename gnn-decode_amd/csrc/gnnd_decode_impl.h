@@ -364,6 +364,28 @@ struct Mlp10Pair {
         }
         return acc;
     }
+    // N edge pairs at once, unit-major: the N accumulation chains interleave, so no packed
+    // FMA waits on the one just issued (same per-pair operation order: identical bits)
+    template <int N>
+    __device__ __forceinline__ void batch(const f32x2 (&u)[N], f32x2 (&acc)[N]) const {
+        f32x2 h[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
+                : "=v"(h[i]) : "v"(u[i]), "s"(w1b[0]));
+#pragma unroll
+        for (int i = 0; i < N; ++i) acc[i] = pk_fma_sb(h[i], w20b);
+#pragma unroll
+        for (int k = 1; k < 10; ++k) {
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+                asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
+                    : "=v"(h[i]) : "v"(u[i]), "s"(w1b[k]));
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+                acc[i] = (k & 1) ? pk_fma_hi(h[i], w2[k >> 1], acc[i]) : pk_fma_lo(h[i], w2[k >> 1], acc[i]);
+        }
+    }
 };
 
 template <int N, typename F, int I = 0> __device__ __forceinline__ void static_for(F&& f) {
@@ -1367,6 +1389,23 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 if constexpr (kPairBP) Sc2 = f32x2{group_sum_c<G>(csum.x), group_sum_c<G>(csum.y)};
                 T* mba = s_m + cb[qa] * E1;
                 T* mbb = s_m + cb[qb] * E1;
+#ifdef GNND_MLP_BATCH
+                if constexpr (kBase2) {
+                    // the pair's R message MLPs unit-major (Mlp10Pair::batch)
+                    f32x2 u[R], y[R];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) u[r] = Sc - tv[r];
+                    mlp2.template batch<R>(u, y);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        if constexpr (MODEL == GNND_QGNNI) m2[j][r] = __builtin_elementwise_fma(y[r], sc2[j], m2[j][r]);
+                        else m2[j][r] = y[r] + m2[j][r];
+                        mba[GNND_DIDX((int)(ve[qa][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].x;
+                        mbb[GNND_DIDX((int)(ve[qb][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].y;
+                    }
+                    return;
+                }
+#endif
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     m2[j][r] = post2(kProd ? Sc * rcp2(tv[r]) : Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
@@ -1504,6 +1543,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             }
         }
         __syncthreads();
+#ifdef GNND_VAR_PRIO
+        __builtin_amdgcn_s_setprio(GNND_VAR_PRIO);   // latency-bound step first at the arbiter
+#endif
         // variable sums, codeword fastest, variables in degree order (var_ord): a wave's
         // lanes sum 64 / CW variables of (nearly) the same degree for consecutive codewords
         // (odd stride E+1: no bank conflicts).  Edge (index_add) order within a variable;
@@ -1599,6 +1641,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 var_item(b, i, b * E1, b * V);
             }
         }
+#ifdef GNND_VAR_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         __syncthreads();
     }
     if (iters == 0 && MODEL != GNND_V22)        // (V22: zero iterations, empty readout list)
@@ -2016,4 +2061,13 @@ int gnnd_launch_cbp(const gnnd_graph*, int, const void*, const void*, void*, int
 int gnnd_launch_nbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_v10(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_v30(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+// decoder_v3_0 training (gnnd_decode_v30.hip): the forward with its tape
+// ([B][T + 1][2][nslot] states of the plan's slot layout) and the reverse pass to one gradient
+// row [137] per workgroup (gnnd_v30_train_rows of them)
+int64_t gnnd_v30_tape_elems(const gnnd_graph*, int64_t, int);
+int64_t gnnd_v30_train_rows(int64_t);
+int gnnd_launch_v30_tape(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int,
+                         void*, hipStream_t);
+int gnnd_launch_v30_bwd(const gnnd_graph*, int, const void*, const void*, const void*,
+                        const void*, const void*, void*, int64_t, int64_t, int, hipStream_t);
 int gnnd_launch_v22(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

@@ -620,15 +620,16 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
 
 // sum of the per-workgroup rows, fixed order (8 interleaved partial chains, then combined)
 template <typename T>
-__global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __restrict__ gw) {
+__global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __restrict__ gw,
+                                   int n = kV24W) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= kV24W) return;
+    if (i >= n) return;
     T s[8] = {};
     int r = 0;
     for (; r + 8 <= rows; r += 8)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] += gpart[(size_t)(r + j) * kV24W + i];
-    for (int j = 0; r < rows; ++r, ++j) s[j] += gpart[(size_t)r * kV24W + i];
+        for (int j = 0; j < 8; ++j) s[j] += gpart[(size_t)(r + j) * n + i];
+    for (int j = 0; r < rows; ++r, ++j) s[j] += gpart[(size_t)r * n + i];
     gw[i] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
@@ -705,8 +706,14 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
 }
 
 bool train_args_ok(const gnnd_graph* g, int model, int dtype, int64_t B, int32_t iters) {
-    return g && model == GNND_V24 && (dtype == GNND_F32 || dtype == GNND_F64) && B >= 0 &&
-           iters >= 0;
+    return g && (model == GNND_V24 || model == GNND_V30) && (dtype == GNND_F32 || dtype == GNND_F64) &&
+           B >= 0 && iters >= 0;
+}
+// trainable weights of a fused-training model (the packed layout of gnnd.h)
+int train_weights(int model) { return model == GNND_V30 ? kV30Count : kV24W; }
+// gradient rows of the reverse pass
+int64_t model_train_rows(const gnnd_graph* g, int model, int64_t B) {
+    return model == GNND_V30 ? gnnd_v30_train_rows(B) : train_rows(g, B);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1007,7 +1014,7 @@ train_update_kernel(const T* __restrict__ rows, int nrows, T* __restrict__ grad,
         // then a fixed tree over the 16 waves' partials
         T s = T(0);
         if (i < n)
-            for (int r = wv; r < nrows; r += kGroups) s += rows[(size_t)r * kV24W + i];
+            for (int r = wv; r < nrows; r += kGroups) s += rows[(size_t)r * n + i];
         s_red[tid] = s;
         __syncthreads();
         for (int o = kGroups / 2; o >= 1; o >>= 1) {
@@ -1066,7 +1073,8 @@ extern "C" int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, 
                                      int32_t iters, int64_t* h_bytes) {
     if (!train_args_ok(g, model, dtype, batch, iters) || !h_bytes) return GNND_ERR_INVALID_ARG;
     const int64_t esz = dtype == GNND_F64 ? 8 : 4;
-    *h_bytes = esz * batch * g->view.E * (3 * (int64_t)iters + 1);
+    *h_bytes = model == GNND_V30 ? esz * gnnd_v30_tape_elems(g, batch, iters)
+                                 : esz * batch * g->view.E * (3 * (int64_t)iters + 1);
     return GNND_OK;
 }
 
@@ -1076,6 +1084,8 @@ extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const v
     if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
     if (batch == 0) return GNND_OK;
     if (!d_w || !d_x || !d_out || !d_tape) return GNND_ERR_INVALID_ARG;
+    if (model == GNND_V30)
+        return gnnd_launch_v30_tape(g, dtype, d_w, d_x, d_out, batch, iters, d_tape, (hipStream_t)stream);
     return gnnd_launch_v24_tape(g, dtype, d_w, d_x, d_out, batch, iters, d_tape,
                                 (hipStream_t)stream);
 }
@@ -1083,7 +1093,7 @@ extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const v
 extern "C" int gnnd_train_bwd_workspace(const gnnd_graph* g, int model, int dtype,
                                         int64_t batch, int64_t* h_bytes) {
     if (!train_args_ok(g, model, dtype, batch, 0) || !h_bytes) return GNND_ERR_INVALID_ARG;
-    *h_bytes = train_rows(g, batch) * (int64_t)kV24W * (dtype == GNND_F64 ? 8 : 4);
+    *h_bytes = model_train_rows(g, model, batch) * (int64_t)train_weights(model) * (dtype == GNND_F64 ? 8 : 4);
     return GNND_OK;
 }
 
@@ -1096,10 +1106,22 @@ extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const v
     if (!d_w || !d_grad_w) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
     if (batch == 0) {
-        GNND_HIP_CHECK(hipMemsetAsync(d_grad_w, 0, (size_t)kV24W * (dtype == GNND_F64 ? 8 : 4), st));
+        GNND_HIP_CHECK(hipMemsetAsync(d_grad_w, 0, (size_t)train_weights(model) * (dtype == GNND_F64 ? 8 : 4), st));
         return GNND_OK;
     }
     if (!d_x || !d_out || !d_grad_out || !d_tape || !d_workspace) return GNND_ERR_INVALID_ARG;
+    if (model == GNND_V30) {
+        const int rc = gnnd_launch_v30_bwd(g, dtype, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
+                                           workspace_bytes, batch, iters, st);
+        if (rc != GNND_OK) return rc;
+        const int rows = (int)gnnd_v30_train_rows(batch);
+        if (dtype == GNND_F32)
+            grad_reduce_kernel<float><<<1, 256, 0, st>>>((const float*)d_workspace, rows, (float*)d_grad_w, kV30Count);
+        else
+            grad_reduce_kernel<double><<<1, 256, 0, st>>>((const double*)d_workspace, rows, (double*)d_grad_w, kV30Count);
+        GNND_LAUNCH_CHECK();
+        return GNND_OK;
+    }
     if (dtype == GNND_F32)
         return launch_bwd<float>(g, d_w, d_x, d_out, d_grad_out, d_tape, d_grad_w, d_workspace,
                                  workspace_bytes, batch, iters, st);
@@ -1110,7 +1132,7 @@ extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const v
 extern "C" int gnnd_train_bwd_rows(const gnnd_graph* g, int model, int dtype, int64_t batch,
                                    int64_t* h_rows) {
     if (!train_args_ok(g, model, dtype, batch, 0) || !h_rows) return GNND_ERR_INVALID_ARG;
-    *h_rows = batch > 0 ? train_rows(g, batch) : 0;
+    *h_rows = batch > 0 ? model_train_rows(g, model, batch) : 0;
     return GNND_OK;
 }
 
@@ -1122,6 +1144,9 @@ extern "C" int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype,
     if (batch == 0) return GNND_OK;
     if (!d_w || !d_x || !d_out || !d_grad_out || !d_tape || !d_workspace) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
+    if (model == GNND_V30)
+        return gnnd_launch_v30_bwd(g, dtype, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
+                                   workspace_bytes, batch, iters, st);
     if (dtype == GNND_F32)
         return launch_bwd<float>(g, d_w, d_x, d_out, d_grad_out, d_tape, nullptr, d_workspace,
                                  workspace_bytes, batch, iters, st);
@@ -1143,6 +1168,7 @@ extern "C" int gnnd_train_bwd_loss_partial(const gnnd_graph* g, int model, int d
                                            int64_t workspace_bytes, int64_t batch, int32_t iters,
                                            void* stream) {
     if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
+    if (model != GNND_V24) return GNND_ERR_UNSUPPORTED;    // decoder_v2_4's syndrome loss only
     if (n_logical < 0 || n_logical > 32 || (n_logical > 0 && !d_logical_mask)) return GNND_ERR_INVALID_ARG;
     if (batch == 0) return GNND_OK;
     if (!d_w || !d_x || !d_out || !d_y || !d_tape || !d_loss_b || !d_workspace) return GNND_ERR_INVALID_ARG;
@@ -1164,7 +1190,8 @@ extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64
                                  double* d_step, uint32_t* d_sync, double lr, double beta1,
                                  double beta2, double eps, double weight_decay, void* d_prepared,
                                  void* stream) {
-    if (model != GNND_V24 || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
+    if ((model != GNND_V24 && model != GNND_V30) || (dtype != GNND_F32 && dtype != GNND_F64))
+        return GNND_ERR_INVALID_ARG;
     if (n_rows < 0 || batch < 0 || n_rows > 0x7fffffff) return GNND_ERR_INVALID_ARG;
     if (n_rows > 0 && !d_rows) return GNND_ERR_INVALID_ARG;
     if (n_rows == 0 && !d_grad) return GNND_ERR_INVALID_ARG;          // nothing to update from
@@ -1173,19 +1200,21 @@ extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64
     if (adam && (!d_exp_avg || !d_exp_avg_sq || !d_step || !d_sync)) return GNND_ERR_INVALID_ARG;
     if (!adam && d_prepared) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
-    const int blocks = (kV24W + 63) / 64;
+    const int nw = train_weights(model);
+    const int blocks = (nw + 63) / 64;
+    const int prep_f32 = model == GNND_V24 ? 1 : 0;     // V30's kernel layout is the plain one
     const bool lossb = batch > 0 && d_loss_b;
     if (dtype == GNND_F32)
         train_update_kernel<float><<<blocks, kUpdThreads, 0, st>>>(
             n_rows ? (const float*)d_rows : nullptr, (int)n_rows, (float*)d_grad,
             lossb ? (const float*)d_loss_b : nullptr, batch, (float*)d_loss, (float*)d_param,
-            (float*)d_exp_avg, (float*)d_exp_avg_sq, d_step, d_sync, kV24W, lr, beta1, beta2, eps,
-            weight_decay, (float*)d_prepared, 1);
+            (float*)d_exp_avg, (float*)d_exp_avg_sq, d_step, d_sync, nw, lr, beta1, beta2, eps,
+            weight_decay, (float*)d_prepared, prep_f32);
     else
         train_update_kernel<double><<<blocks, kUpdThreads, 0, st>>>(
             n_rows ? (const double*)d_rows : nullptr, (int)n_rows, (double*)d_grad,
             lossb ? (const double*)d_loss_b : nullptr, batch, (double*)d_loss, (double*)d_param,
-            (double*)d_exp_avg, (double*)d_exp_avg_sq, d_step, d_sync, kV24W, lr, beta1, beta2,
+            (double*)d_exp_avg, (double*)d_exp_avg_sq, d_step, d_sync, nw, lr, beta1, beta2,
             eps, weight_decay, (double*)d_prepared, 0);
     GNND_LAUNCH_CHECK();
     return GNND_OK;

@@ -251,7 +251,8 @@ def decode_tile(graph, model, dtype):
 # fused training step (decoder_v2_4): forward with tape + one-launch reverse pass
 # ---------------------------------------------------------------------------------------
 def train_forward(graph, model, x, prepared_weights, iters):
-    """gnnd_train_fwd: the fused decode plus the training tape.  Returns (out, tape)."""
+    """gnnd_train_fwd: the fused decode plus the training tape (models v24, v30).
+    Returns (out, tape)."""
     _require_gpu(x, prepared_weights)
     x = x.contiguous()
     B = x.numel() // graph.N
@@ -260,7 +261,9 @@ def train_forward(graph, model, x, prepared_weights, iters):
     _lib.call('gnnd_train_tape_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
               ctypes.byref(nb))
     tape = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
-    out = torch.empty(B * graph.V, 1, dtype=x.dtype, device=x.device)
+    # v30: the two readout tensors [2][B*N] (gnnd_decode's layout)
+    nout = 2 * B * graph.N if model == 'v30' else B * graph.V
+    out = torch.empty(nout, 1, dtype=x.dtype, device=x.device)
     _lib.call('gnnd_train_fwd', graph.handle, _lib.VARIANT[model], dt, _ptr(prepared_weights),
               _ptr(x), _ptr(out), _ptr(tape), B, int(iters), current_stream(x.device))
     return out, tape

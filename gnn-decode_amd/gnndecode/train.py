@@ -370,3 +370,100 @@ class FusedV24Trainer(_GraphedStep):
         out = self._run(x, y, copy_loss)
         _invalidate(self.model)      # parameters changed on the device (gnnd_train_update)
         return out
+
+
+class FusedV30Trainer(_GraphedStep):
+    """decoder_v3_0 training step (quantum/decoder_v3_0.py:339-356) on the HIP kernels:
+
+        forward with tape (gnnd_train_fwd, model V30: every iteration's edge states before and
+        after ggc1) -> the reference LossFunc (loss.V30Loss) and d loss / d [out0, out1] by
+        torch autograd on the two readout tensors -> reverse pass to per-workgroup gradient
+        rows (gnnd_train_bwd_partial) -> fused epilogue (gnnd_train_update: fixed-order row
+        reduction, Adam, the weights the next forward reads)
+
+    all in one HIP graph (with a collective: split around the all_reduce(SUM) of the flat
+    gradient, as FusedV24Trainer).  The 137 trained parameters (ggc1.mlp1/rnn1, ggc2.mlp2/
+    rnn2, mlp) are re-bound as views of the flat packed buffer; the reference's unused
+    ggc1.mlp2/rnn2 and ggc2.mlp1/rnn1 keep their storage and never change (torch's Adam
+    skips parameters without a gradient).  Adam as the script: lr 3e-4, weight decay 5e-4."""
+
+    def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
+                 group=None, graph=True, warmup=2, force_collective=False):
+        from .models import DecoderV30
+        if not isinstance(model, DecoderV30):
+            raise TypeError('FusedV30Trainer trains decoder_v3_0 (DecoderV30) models')
+        rlr, rwd = REFERENCE_OPTIM['v30']
+        self.model, self.loss_fn = model, loss_fn
+        self.lr = rlr if lr is None else lr
+        self.wd = rwd if weight_decay is None else weight_decay
+        self.betas, self.eps = betas, eps
+        self._init_graph(graph, warmup, group, force_collective)
+        flat = model.packed_weights().detach().clone().contiguous()
+        off = 0
+
+        def bind(p, shape):
+            nonlocal off
+            n = p.numel()
+            p.data = flat[off:off + n].view(shape)
+            off += n
+        # gnnd.h V30 layout: mlp {W1, b1, W2, b2}, GRU {w_ih, w_hh, b_ih, b_hh}
+        mlp = lambda q: (q[0].weight, q[0].bias, q[2].weight, q[2].bias)
+        gru = lambda c: (c.weight_ih, c.weight_hh, c.bias_ih, c.bias_hh)
+        for group in (mlp(model.ggc1.mlp1), gru(model.ggc1.rnn1), mlp(model.ggc2.mlp2),
+                      gru(model.ggc2.rnn2), mlp(model.mlp)):
+            for p in group:
+                bind(p, p.shape)
+        assert off == flat.numel()
+        self.flat = flat
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.step_count = torch.zeros(1, dtype=torch.float64, device=flat.device)
+        self._sync = torch.zeros(1, dtype=torch.int32, device=flat.device)
+        self._loss = torch.zeros((), dtype=flat.dtype, device=flat.device)
+        self._gw = torch.zeros_like(flat)
+        model.graph(flat.device)                 # device graph tables now, never in a capture
+
+    def _loss_grad(self, out, x, y):
+        """The reference LossFunc on [out0, out1] and its gradient w.r.t. both tensors."""
+        o = out.detach().requires_grad_(True)
+        n = o.size(0) // 2
+        with torch.enable_grad():
+            loss = self.loss_fn([o[:n], o[n:]], y, x)
+            (d,) = torch.autograd.grad(loss, o)
+        return loss.detach(), d
+
+    def _compute(self, x, y):
+        m = self.model
+        g = m.graph(x.device)
+        w = self.flat if self.flat.dtype == x.dtype else self.flat.to(x.dtype)
+        out, tape = ops.train_forward(g, 'v30', x, w, m.Nc)
+        loss, d = self._loss_grad(out, x, y)
+        if self.flat.dtype != x.dtype or self._dist():
+            gw = ops.train_backward(g, 'v30', w, x, out, d, tape, m.Nc)
+            self._gw.copy_(gw.to(self.flat.dtype))
+            self._loss.copy_(loss.to(self.flat.dtype))
+            self._pending = None
+            return self._loss, [self._gw]
+        ws, nrows = ops.train_backward_partial(g, 'v30', w, x, out, d, tape, m.Nc)
+        self._pending = (ws, nrows, loss.reshape(1))
+        return self._loss, []
+
+    def _apply(self):
+        kw = dict(param=self.flat, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq,
+                  step=self.step_count, sync=self._sync, lr=self.lr, betas=self.betas,
+                  eps=self.eps, weight_decay=self.wd)
+        if self._pending is not None:            # single rank: rows -> gradient -> Adam
+            ws, nrows, loss1 = self._pending
+            ops.train_update('v30', self.flat.dtype, rows=ws, n_rows=nrows, loss_b=loss1,
+                             loss=self._loss, **kw)
+        else:
+            ops.train_update('v30', self.flat.dtype, grad=self._gw, **kw)
+
+    def step(self, data, y, copy_loss=True):
+        """One training step; returns the batch loss (copy_loss=False: the graph's static loss
+        buffer itself, valid until the next step)."""
+        self.model.train()
+        x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
+        out = self._run(x, y, copy_loss)
+        _invalidate(self.model)
+        return out
