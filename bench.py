@@ -423,7 +423,8 @@ def train_run(a, world, rank, dev, cpu='full'):
     H = gd.codes.get_code(code)
     torch.manual_seed(a.seed)
     model = gd.MODELS[model_name](T, H).to(dev).to(dtype)
-    fused = model_name in ('v24', 'v30') and not a.layerwise
+    fused = (model_name in ('v24', 'v30') or
+             (model_name in ('nbp', 'v22') and dtype == torch.float64)) and not a.layerwise
     if model_name == 'v24':
         model.fused_train = fused
     if model_name == 'v22':          # decoder_v2_2's LossFunc: every layer's readout
@@ -436,7 +437,10 @@ def train_run(a, world, rank, dev, cpu='full'):
     parity = None
     if cpu == 'parity' and rank == 0 and model_name == 'v24':
         parity = train_parity(H, model, lf, T, dev, dtype, a.seed)
-    if fused and model_name == 'v30':
+    if fused and model_name in ('nbp', 'v22'):
+        # packed per-edge weights -> fwd+tape -> syndrome loss -> reverse pass -> Adam (fp64)
+        tr = gd.train.FusedWbpTrainer(model, lf, graph=not a.no_graph, warmup=2)
+    elif fused and model_name == 'v30':
         # fwd+tape -> reference LossFunc (torch) -> reverse pass -> [all_reduce] -> Adam
         tr = gd.train.FusedV30Trainer(model, lf, graph=not a.no_graph, warmup=2)
     elif fused and not a.torch_trainer:
@@ -458,7 +462,8 @@ def train_run(a, world, rank, dev, cpu='full'):
     if dist.is_initialized():
         dist.barrier()
     t0 = time.perf_counter()
-    fused_tr = isinstance(tr, (gd.train.FusedV24Trainer, gd.train.FusedV30Trainer))
+    fused_tr = isinstance(tr, (gd.train.FusedV24Trainer, gd.train.FusedV30Trainer,
+                               gd.train.FusedWbpTrainer))
     for _ in range(a.steps):
         # the loss stays in the step's static buffer (read after the timed region), no copy
         loss = tr.step(data, y, copy_loss=False) if fused_tr else tr.step(data, y)
@@ -473,7 +478,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     if rank == 0:
         step_s = elapsed / a.steps
         roof = None
-        if model_name in ('v24', 'v30') and fused:
+        if model_name in ('v24', 'v30', 'nbp', 'v22') and fused:
             # training ~ 3x the forward's algorithmic FLOPs: forward, the
             # reverse pass through every MLP (2x); transcendentals: forward Softplus + the
             # backward sigmoid of every unit.  Whole captured step (prepare, forward+tape,
@@ -487,7 +492,9 @@ def train_run(a, world, rank, dev, cpu='full'):
                     'kernel': ('FusedV24Trainer step (HIP graph: gnnd_train_fwd, gnnd_syndrome_loss, '
                                'gnnd_train_bwd, gnnd_adam_step)' if model_name == 'v24' else
                                'FusedV30Trainer step (HIP graph: gnnd_train_fwd, V30Loss autograd, '
-                               'gnnd_train_bwd_partial, gnnd_train_update)'),
+                               'gnnd_train_bwd_partial, gnnd_train_update)' if model_name == 'v30' else
+                               'FusedWbpTrainer step (HIP graph: packed weights, gnnd_train_fwd, '
+                               'gnnd_syndrome_loss, gnnd_train_bwd, torch Adam)'),
                     'flops_per_sample': 3 * fl, 'transcendentals_per_sample': 2 * trans,
                     'step_ms': step_s * 1e3}
         cpu_res = None
@@ -505,6 +512,8 @@ def train_run(a, world, rank, dev, cpu='full'):
                        'hip_graph': not a.no_graph,
                        'path': ('FusedV30Trainer: gnnd_train_fwd/bwd (V30) + V30Loss + gnnd_train_update'
                                 if fused and model_name == 'v30' else
+                                'FusedWbpTrainer: gnnd_train_fwd/bwd (weighted BP) + gnnd_syndrome_loss'
+                                if fused and model_name in ('nbp', 'v22') else
                                 'FusedV24Trainer: gnnd_train_fwd/bwd + gnnd_syndrome_loss + gnnd_adam_step'
                                 if fused and not a.torch_trainer else
                                 'fused gnnd_train_fwd/bwd, torch loss/optimizer' if fused

@@ -2070,4 +2070,12 @@ int gnnd_launch_v30_tape(const gnnd_graph*, int, const void*, const void*, void*
                          void*, hipStream_t);
 int gnnd_launch_v30_bwd(const gnnd_graph*, int, const void*, const void*, const void*,
                         const void*, const void*, void*, int64_t, int64_t, int, hipStream_t);
+// weighted-BP training (gnnd_train_wbp.hip, models NBP and V22, fp64): the same tape shape and
+// one gradient row [2 E T + 2 E + 1] per workgroup
+int64_t gnnd_wbp_tape_elems(const gnnd_graph*, int64_t, int);
+int64_t gnnd_wbp_train_rows(int64_t);
+int gnnd_launch_wbp_tape(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int,
+                         void*, hipStream_t);
+int gnnd_launch_wbp_bwd(const gnnd_graph*, int, const void*, const void*, const void*,
+                        const void*, const void*, void*, int64_t, int64_t, int, hipStream_t);
 int gnnd_launch_v22(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

@@ -705,14 +705,21 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     return GNND_OK;
 }
 
+bool is_wbp_train(int model) { return model == GNND_NBP || model == GNND_V22; }
 bool train_args_ok(const gnnd_graph* g, int model, int dtype, int64_t B, int32_t iters) {
-    return g && (model == GNND_V24 || model == GNND_V30) && (dtype == GNND_F32 || dtype == GNND_F64) &&
-           B >= 0 && iters >= 0;
+    if (!g || B < 0 || iters < 0) return false;
+    if (is_wbp_train(model)) return dtype == GNND_F64;       // the scripts' dtype only
+    return (model == GNND_V24 || model == GNND_V30) && (dtype == GNND_F32 || dtype == GNND_F64);
+}
+// per-edge weight tables of the weighted-BP models (gnnd.h NBP / V22 layout)
+int64_t wbp_weights(const gnnd_graph* g, int iters) {
+    return 2 * (int64_t)iters * g->view.E + 2 * (int64_t)g->view.E + 1;
 }
 // trainable weights of a fused-training model (the packed layout of gnnd.h)
 int train_weights(int model) { return model == GNND_V30 ? kV30Count : kV24W; }
 // gradient rows of the reverse pass
 int64_t model_train_rows(const gnnd_graph* g, int model, int64_t B) {
+    if (is_wbp_train(model)) return gnnd_wbp_train_rows(B);
     return model == GNND_V30 ? gnnd_v30_train_rows(B) : train_rows(g, B);
 }
 
@@ -1074,7 +1081,8 @@ extern "C" int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, 
     if (!train_args_ok(g, model, dtype, batch, iters) || !h_bytes) return GNND_ERR_INVALID_ARG;
     const int64_t esz = dtype == GNND_F64 ? 8 : 4;
     *h_bytes = model == GNND_V30 ? esz * gnnd_v30_tape_elems(g, batch, iters)
-                                 : esz * batch * g->view.E * (3 * (int64_t)iters + 1);
+               : is_wbp_train(model) ? esz * gnnd_wbp_tape_elems(g, batch, iters)
+                                     : esz * batch * g->view.E * (3 * (int64_t)iters + 1);
     return GNND_OK;
 }
 
@@ -1086,13 +1094,24 @@ extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const v
     if (!d_w || !d_x || !d_out || !d_tape) return GNND_ERR_INVALID_ARG;
     if (model == GNND_V30)
         return gnnd_launch_v30_tape(g, dtype, d_w, d_x, d_out, batch, iters, d_tape, (hipStream_t)stream);
+    if (is_wbp_train(model))
+        return gnnd_launch_wbp_tape(g, model, d_w, d_x, d_out, batch, iters, d_tape, (hipStream_t)stream);
     return gnnd_launch_v24_tape(g, dtype, d_w, d_x, d_out, batch, iters, d_tape,
                                 (hipStream_t)stream);
+}
+
+extern "C" int gnnd_train_workspace_bytes(const gnnd_graph* g, int model, int dtype,
+                                          int64_t batch, int32_t iters, int64_t* h_bytes) {
+    if (!train_args_ok(g, model, dtype, batch, iters) || !h_bytes) return GNND_ERR_INVALID_ARG;
+    const int64_t n = is_wbp_train(model) ? wbp_weights(g, iters) : train_weights(model);
+    *h_bytes = model_train_rows(g, model, batch) * n * (dtype == GNND_F64 ? 8 : 4);
+    return GNND_OK;
 }
 
 extern "C" int gnnd_train_bwd_workspace(const gnnd_graph* g, int model, int dtype,
                                         int64_t batch, int64_t* h_bytes) {
     if (!train_args_ok(g, model, dtype, batch, 0) || !h_bytes) return GNND_ERR_INVALID_ARG;
+    if (is_wbp_train(model)) return GNND_ERR_UNSUPPORTED;    // depends on iters: the call above
     *h_bytes = model_train_rows(g, model, batch) * (int64_t)train_weights(model) * (dtype == GNND_F64 ? 8 : 4);
     return GNND_OK;
 }
@@ -1105,11 +1124,22 @@ extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const v
     if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
     if (!d_w || !d_grad_w) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
+    const int64_t nw = is_wbp_train(model) ? wbp_weights(g, iters) : train_weights(model);
     if (batch == 0) {
-        GNND_HIP_CHECK(hipMemsetAsync(d_grad_w, 0, (size_t)train_weights(model) * (dtype == GNND_F64 ? 8 : 4), st));
+        GNND_HIP_CHECK(hipMemsetAsync(d_grad_w, 0, (size_t)nw * (dtype == GNND_F64 ? 8 : 4), st));
         return GNND_OK;
     }
     if (!d_x || !d_out || !d_grad_out || !d_tape || !d_workspace) return GNND_ERR_INVALID_ARG;
+    if (is_wbp_train(model)) {
+        const int rc = gnnd_launch_wbp_bwd(g, model, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
+                                           workspace_bytes, batch, iters, st);
+        if (rc != GNND_OK) return rc;
+        if (nw > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
+        grad_reduce_kernel<double><<<(unsigned)((nw + 255) / 256), 256, 0, st>>>(
+            (const double*)d_workspace, (int)gnnd_wbp_train_rows(batch), (double*)d_grad_w, (int)nw);
+        GNND_LAUNCH_CHECK();
+        return GNND_OK;
+    }
     if (model == GNND_V30) {
         const int rc = gnnd_launch_v30_bwd(g, dtype, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
                                            workspace_bytes, batch, iters, st);
@@ -1146,6 +1176,9 @@ extern "C" int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype,
     hipStream_t st = (hipStream_t)stream;
     if (model == GNND_V30)
         return gnnd_launch_v30_bwd(g, dtype, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
+                                   workspace_bytes, batch, iters, st);
+    if (is_wbp_train(model))
+        return gnnd_launch_wbp_bwd(g, model, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
                                    workspace_bytes, batch, iters, st);
     if (dtype == GNND_F32)
         return launch_bwd<float>(g, d_w, d_x, d_out, d_grad_out, d_tape, nullptr, d_workspace,

@@ -53,6 +53,7 @@ SIGNATURES = {
     'gnnd_train_tape_bytes': (_int, [_vp, _int, _int, _i64, _i32, _c_i64p]),
     'gnnd_train_fwd': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _i64, _i32, _vp]),
     'gnnd_train_bwd_workspace': (_int, [_vp, _int, _int, _i64, _c_i64p]),
+    'gnnd_train_workspace_bytes': (_int, [_vp, _int, _int, _i64, _i32, _c_i64p]),
     'gnnd_train_bwd': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32,
                               _vp]),
     'gnnd_train_bwd_rows': (_int, [_vp, _int, _int, _i64, _c_i64p]),

@@ -251,7 +251,7 @@ def decode_tile(graph, model, dtype):
 # fused training step (decoder_v2_4): forward with tape + one-launch reverse pass
 # ---------------------------------------------------------------------------------------
 def train_forward(graph, model, x, prepared_weights, iters):
-    """gnnd_train_fwd: the fused decode plus the training tape (models v24, v30).
+    """gnnd_train_fwd: the fused decode plus the training tape (models v24, v30; nbp, v22 fp64).
     Returns (out, tape)."""
     _require_gpu(x, prepared_weights)
     x = x.contiguous()
@@ -261,8 +261,9 @@ def train_forward(graph, model, x, prepared_weights, iters):
     _lib.call('gnnd_train_tape_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
               ctypes.byref(nb))
     tape = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
-    # v30: the two readout tensors [2][B*N] (gnnd_decode's layout)
-    nout = 2 * B * graph.N if model == 'v30' else B * graph.V
+    # v30: the two readout tensors [2][B*N]; v22: every layer's readout [T][B*V] (gnnd_decode's
+    # layouts)
+    nout = 2 * B * graph.N if model == 'v30' else iters * B * graph.V if model == 'v22' else B * graph.V
     out = torch.empty(nout, 1, dtype=x.dtype, device=x.device)
     _lib.call('gnnd_train_fwd', graph.handle, _lib.VARIANT[model], dt, _ptr(prepared_weights),
               _ptr(x), _ptr(out), _ptr(tape), B, int(iters), current_stream(x.device))
@@ -274,7 +275,8 @@ def train_backward(graph, model, plain_weights, x, out, grad_out, tape, iters):
     B = x.numel() // graph.N
     dt = dtype_code(x.dtype)
     nb = ctypes.c_int64()
-    _lib.call('gnnd_train_bwd_workspace', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nb))
+    _lib.call('gnnd_train_workspace_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
+              ctypes.byref(nb))
     ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
     gw = torch.empty_like(plain_weights)
     grad_out = grad_out.contiguous()
@@ -292,7 +294,8 @@ def train_backward_partial(graph, model, plain_weights, x, out, grad_out, tape, 
     nr = ctypes.c_int64()
     _lib.call('gnnd_train_bwd_rows', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nr))
     nb = ctypes.c_int64()
-    _lib.call('gnnd_train_bwd_workspace', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nb))
+    _lib.call('gnnd_train_workspace_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
+              ctypes.byref(nb))
     if ws is None or ws.numel() < nb.value:
         ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
     grad_out = grad_out.contiguous()
@@ -311,7 +314,8 @@ def train_backward_loss_partial(graph, model, plain_weights, x, out, y, logical_
     nr = ctypes.c_int64()
     _lib.call('gnnd_train_bwd_rows', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nr))
     nb = ctypes.c_int64()
-    _lib.call('gnnd_train_bwd_workspace', graph.handle, _lib.VARIANT[model], dt, B, ctypes.byref(nb))
+    _lib.call('gnnd_train_workspace_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
+              ctypes.byref(nb))
     nl = ctypes.c_int64()
     _lib.call('gnnd_train_loss_count', graph.handle, B, ctypes.byref(nl))
     if ws is None or ws.numel() < nb.value:

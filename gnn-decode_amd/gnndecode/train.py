@@ -467,3 +467,109 @@ class FusedV30Trainer(_GraphedStep):
         out = self._run(x, y, copy_loss)
         _invalidate(self.model)
         return out
+
+
+class FusedWbpTrainer(_GraphedStep):
+    """Weighted-BP training step on the HIP kernels, fp64 (the scripts' dtype):
+    NeuralBP (quantum/neural_BP.py:370-395) and decoder_v2_2 (quantum/decoder_v2_2.py:421-443).
+
+        packed per-edge weights (ONE gather from the flat parameter buffer; V22: the 8 edge-type
+        weights expanded per edge, sigmoid(weight)) -> forward with tape (gnnd_train_fwd) ->
+        syndrome loss and d loss / d out of the readout (gnnd_syndrome_loss; V22: of every
+        layer's readout at once, PerLayerLoss) -> reverse pass to the per-edge weight gradient
+        (gnnd_train_bwd) -> type sums (V22: one [2T+2, E] x [E, 8] GEMM, deterministic) and
+        sigmoid' -> flat gradient -> Adam (gnnd_adam_step)
+
+    ~12 launches in one HIP graph (with a collective: compute and Adam graphs around the
+    all_reduce(SUM) of the flat gradient).  The trained parameters (the source_to_target
+    layers' W, W_p, the readout W / W_pr, and weight / alpha) are re-bound as views of one
+    flat buffer; the target_to_source layers' unused W, W_p keep their storage and never
+    change (torch's Adam skips parameters without a gradient).  Adam as the scripts (NBP
+    lr 3e-4, V22 lr 2e-4, no decay), torch.optim.Adam's update order."""
+
+    def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
+                 group=None, graph=True, warmup=2, force_collective=False):
+        from .models import DecoderV22, NeuralBP
+        if not isinstance(model, (DecoderV22, NeuralBP)):
+            raise TypeError('FusedWbpTrainer trains NeuralBP and DecoderV22 models')
+        rlr, rwd = REFERENCE_OPTIM[model.kind]
+        self.model, self.loss_fn = model, loss_fn
+        self.lr = rlr if lr is None else lr
+        self.wd = rwd if weight_decay is None else weight_decay
+        self.betas, self.eps = betas, eps
+        self._init_graph(graph, warmup, group, force_collective)
+        T = model.Nc
+        v22 = model.kind == 'v22'
+        tail = model.weight if v22 else model.alpha
+        params = ([q for t in range(T) for q in (model.layers[2 * t].W, model.layers[2 * t].W_p)]
+                  + [model.W, model.W_pr if v22 else model.W_p, tail])
+        dev = tail.device
+        flat = torch.cat([q.detach().reshape(-1) for q in params]).contiguous()
+        off = 0
+        for q in params:
+            n = q.numel()
+            q.data = flat[off:off + n].view(q.shape)
+            off += n
+        self.flat, self.params = flat, params
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.step_count = torch.zeros(1, dtype=torch.float64, device=dev)
+        self._grad = torch.zeros_like(flat)
+        E = model.E
+        if v22:
+            # packed position (block k of 2T + 2, edge e) reads flat[8 k + type(e)]
+            types = model.types.to(dev)
+            blocks = torch.arange(2 * T + 2, device=dev).unsqueeze(1)
+            self._gather = (8 * blocks + types.unsqueeze(0)).reshape(-1)
+            self._onehot = torch.nn.functional.one_hot(types, 8).to(torch.float64)   # [E, 8]
+        else:
+            self._gather = None                  # identity: the tables ARE the parameters
+        self._E = E
+        model.graph(dev)                         # device graph tables now, never in a capture
+        getattr(loss_fn, 'inner', loss_fn)._graph(dev)
+
+    def _packed(self):
+        if self._gather is None:
+            return self.flat
+        p = torch.empty(self._gather.numel() + 1, dtype=self.flat.dtype, device=self.flat.device)
+        torch.index_select(self.flat, 0, self._gather, out=p[:-1])
+        torch.sigmoid(self.flat[-1:], out=p[-1:])
+        return p
+
+    def _loss_grad(self, out, y):
+        """Per-codeword losses and d loss / d out of the readout(s)."""
+        m = self.model
+        if m.kind == 'v22':                      # PerLayerLoss(train=True): every layer
+            yy = y.reshape(1, -1).expand(m.Nc, -1).reshape(-1, 1)
+            return self.loss_fn.inner.per_codeword(out, yy)
+        return self.loss_fn.per_codeword(out, y)
+
+    def _compute(self, x, y):
+        m = self.model
+        if x.dtype != torch.float64:
+            raise ValueError('FusedWbpTrainer trains in fp64 (the reference scripts\' dtype)')
+        g = m.graph(x.device)
+        w = self._packed()
+        out, tape = ops.train_forward(g, m.kind, x, w, m.Nc)
+        loss_b, dpred = self._loss_grad(out, y)
+        gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc)
+        if self._gather is None:
+            self._grad.copy_(gw)
+        else:                                    # type sums, then sigmoid'(weight)
+            nb = 2 * m.Nc + 2
+            torch.mm(gw[:-1].view(nb, self._E), self._onehot, out=self._grad[:-1].view(nb, 8))
+            a = w[-1:]
+            torch.mul(gw[-1:], a * (1 - a), out=self._grad[-1:])
+        loss = loss_b.sum()
+        return loss, [self._grad] if self._dist() else []
+
+    def _apply(self):
+        ops.adam_step(self.flat, self._grad, self.exp_avg, self.exp_avg_sq, self.step_count,
+                      self.lr, self.betas, self.eps, self.wd)
+
+    def step(self, data, y, copy_loss=True):
+        self.model.train()
+        x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
+        out = self._run(x, y, copy_loss)
+        _invalidate(self.model)
+        return out

@@ -211,24 +211,32 @@ int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan)
  * gnnd_train_fwd = gnnd_decode (same prepared weights, same output) that also writes the
  * training tape (gnnd_train_tape_bytes bytes of d_tape): per iteration and edge the
  * v->c MLP input, the tanh output and the c->v MLP input, plus the final messages.
- * gnnd_train_bwd turns d loss / d out [B*V] into d loss / d weights [1283] in the PLAIN
+ * gnnd_train_bwd turns d loss / d out [B*V] into d loss / d weights [1283] (V24) in the PLAIN
  * packed layout of gnnd_weights_count (d_w is that plain layout, not the prepared one):
  * reverse mode through all T iterations and the readout in one launch (+ a fixed-order
  * reduction of per-workgroup partials in d_workspace, gnnd_train_bwd_workspace bytes).
- * Only model V24 (quantum/decoder_v2_4.py:260-294); the other models train through
- * gnnd_propagate_*_bwd.                                                                 */
+ * Models: V24 (quantum/decoder_v2_4.py:260-294, fp32/fp64), V30 (quantum/decoder_v3_0.py:
+ * 245-290, fp32/fp64; d_out / d_grad_out are the two readout tensors [2][B*N]), and fp64 NBP
+ * (quantum/neural_BP.py:263-314) and V22 (quantum/decoder_v2_2.py:299-347; d_out /
+ * d_grad_out every layer's readout [T][B*V]) whose gradient is w.r.t. the per-edge tables
+ * of their packed layout (2 E T + 2 E + 1 values).  The other models train through
+ * gnnd_propagate_*_bwd.  gnnd_train_workspace_bytes sizes the workspace of every model
+ * (gnnd_train_bwd_workspace, which has no iteration count, only V24 and V30).             */
 int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, int64_t batch,
                           int32_t iters, int64_t* h_bytes);
 int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
                    void* d_out, void* d_tape, int64_t batch, int32_t iters, void* stream);
 int gnnd_train_bwd_workspace(const gnnd_graph* g, int model, int dtype, int64_t batch,
                              int64_t* h_bytes);
+int gnnd_train_workspace_bytes(const gnnd_graph* g, int model, int dtype, int64_t batch,
+                               int32_t iters, int64_t* h_bytes);
 int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
                    const void* d_out, const void* d_grad_out, const void* d_tape,
                    void* d_grad_w, void* d_workspace, int64_t workspace_bytes, int64_t batch,
                    int32_t iters, void* stream);
 /* The reverse pass without its reduction: leaves gnnd_train_bwd_rows() per-workgroup
- * gradient rows [rows][1283] in d_workspace, for gnnd_train_update to reduce (fused with
+ * gradient rows [rows][n] (n = the model's weights: V24 1283, V30 137, NBP/V22 2ET + 2E + 1)
+ * in d_workspace, for gnnd_train_update (V24, V30) to reduce (fused with
  * the optimizer).  On a split graph (gnnd_graph_components > 1) every component of a
  * codeword runs in its own workgroup.                                                     */
 int gnnd_train_bwd_rows(const gnnd_graph* g, int model, int dtype, int64_t batch,
@@ -255,7 +263,8 @@ int gnnd_train_bwd_loss_partial(const gnnd_graph* g, int model, int dtype, const
  *   n_rows > 0: d_grad[i] = fixed-order sum of the rows (d_grad may be NULL: not stored);
  *   n_rows = 0: the gradient is read from d_grad (e.g. after an all-reduce of it);
  *   d_loss_b [batch] non-NULL: *d_loss = fixed-order sum of the per-codeword losses;
- *   d_param non-NULL: gnnd_adam_step's update of the 1283 plain packed weights (moments
+ *   d_param non-NULL: gnnd_adam_step's update of the plain packed weights (V24 1283, V30 137;
+ *   the V30 kernel layout is the plain one) (moments
  *   d_exp_avg / d_exp_avg_sq, device step count *d_step incremented once), then, if
  *   d_prepared is non-NULL, gnnd_prepare_weights' kernel layout of the updated weights into
  *   d_prepared.  d_sync: one device uint32, zero before the first call (the kernel leaves it
