@@ -633,15 +633,20 @@ __global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __r
     gw[i] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
-// fp32 reverse-pass workgroup shape (GNND_TRAIN_THREADS, A/B): 1024 = 16 waves, one workgroup
-// per CU (default); 512 = 8 waves with 256 VGPRs; 5122 = 8 waves, two workgroups per CU
-int train_threads_f32() {
-    static int v = [] {
+// fp32 reverse-pass workgroup shape: 1024 = 16 waves, one workgroup per CU; 5122 = 8 waves,
+// two workgroups per CU; 2564 = 4 waves, four per CU (all 128 VGPRs, 4 waves per SIMD);
+// 512 = 8 waves with 256 VGPRs.  Default by grid: the 16-wave shape while the workgroups do
+// not fill the CUs twice (B = 128: 0.274 vs 0.284 ms/step for 5122), the two-per-CU shape
+// above (B = 8 192: 9.29 vs 10.09 ms, r03o: independent barriers hide each other's phases).
+// GNND_TRAIN_THREADS forces one (A/B).
+int train_threads_f32(int64_t blocks) {
+    static int forced = [] {
         const char* e = getenv("GNND_TRAIN_THREADS");
         const int n = e ? atoi(e) : 0;
-        return n == 512 || n == 5122 ? n : 1024;
+        return n == 512 || n == 5122 || n == 2564 || n == 1024 ? n : 0;
     }();
-    return v;
+    if (forced) return forced;
+    return blocks >= 2 * (int64_t)device_cus() ? 5122 : 1024;
 }
 // workgroups of the reverse pass: one codeword each up to 1024 (the partial-row count),
 // larger batches loop (each workgroup a fixed, strided set of codewords: deterministic)
@@ -684,11 +689,11 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     const size_t lds = train_lds(gk, sizeof(T), lossp.y ? lossp.nl : -1);
     if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     // fp32: 16 waves (128 VGPRs) by default, GNND_TRAIN_THREADS=512 for 8 waves (A/B)
-    const int shape = sizeof(T) == 4 ? train_threads_f32() : 0;
-    // (5122: two 8-wave workgroups per CU = 4 waves per SIMD, 128 VGPRs)
+    const int shape = sizeof(T) == 4 ? train_threads_f32(blocks) : 0;
+    // (5122: two 8-wave workgroups per CU = 4 waves per SIMD, 128 VGPRs; 2564: four 4-wave ones)
     auto kern = shape == 512 ? v24_bwd_kernel<T, 512> : shape == 5122 ? v24_bwd_kernel<T, 512, 4>
-                                                                       : v24_bwd_kernel<T>;
-    const int nthreads = shape == 512 || shape == 5122 ? 512 : train_threads<T>();
+              : shape == 2564 ? v24_bwd_kernel<T, 256, 4> : v24_bwd_kernel<T>;
+    const int nthreads = shape == 512 || shape == 5122 ? 512 : shape == 2564 ? 256 : train_threads<T>();
     if (lds > 64 * 1024)
         GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

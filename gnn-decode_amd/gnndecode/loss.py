@@ -161,6 +161,39 @@ class V30Loss(torch.nn.Module):
         self.a, self.b = max(H.shape), min(H.shape)
         self.register_buffer('Ht', H.t().contiguous())                      # [C, V]
 
+    def loss_and_grad(self, out, y, x):
+        """(loss, d loss / d out) for the fused trainer, out = [out0; out1] as one [2*B*N]
+        tensor.  The check term is gnnd_syndrome_loss on out0's first B*V rows (column k =
+        rows kV..kV+V-1, the script's stride-V slicing) with every column's y = the first
+        codeword's (`tmp`); the BCE term and its gradient are elementwise on the strided
+        [B, C] views of out1 and x (torch autograd's formulas: BCE' = (1 - s)/(1 - q) - s/q,
+        q = |sin(pi/2 r)|).  None when the BCE rows of neighbouring columns overlap (C > V)."""
+        a, b = self.a, self.b
+        N = a + b
+        B = y.numel() // a
+        if b > a or out.dtype not in (torch.float32, torch.float64) or not out.is_cuda:
+            return None
+        syn_loss = getattr(self, '_syn', {}).get(out.device)
+        if syn_loss is None:                     # the check term: H^T s rows, no logical rows
+            syn_loss = SyndromeLoss(self.Ht.t().cpu(), torch.zeros(0, a)).to(out.device)
+            self._syn = {**getattr(self, '_syn', {}), out.device: syn_loss}
+        o = out.reshape(-1)
+        n = B * N
+        ycols = y.reshape(-1)[:a].to(o.dtype).repeat(B)
+        loss_a, d_a = syn_loss.per_codeword(o[:B * a], ycols)
+        r = o[n:].as_strided((B, b), (a, 1), a)
+        syn = x.reshape(-1).as_strided((B, b), (N, 1), a).to(o.dtype)
+        h = r * math.pi / 2
+        sn = torch.sin(h)
+        q = torch.abs(sn)
+        bce = -1 * (1 - syn).mul(torch.log(1 - q)) - syn.mul(torch.log(q))
+        gq = (1 - syn) / (1 - q) - syn / q
+        gr = gq * torch.sgn(sn) * torch.cos(h) * (math.pi / 2)
+        d = torch.zeros_like(o)
+        d[:B * a] = d_a.reshape(-1)
+        d[n:].as_strided((B, b), (a, 1), a).copy_(gr)
+        return loss_a.sum() + bce.sum(), d.view_as(out)
+
     def forward(self, preds, y, x):
         a, b = self.a, self.b
         N = a + b

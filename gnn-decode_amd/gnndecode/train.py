@@ -424,7 +424,13 @@ class FusedV30Trainer(_GraphedStep):
         model.graph(flat.device)                 # device graph tables now, never in a capture
 
     def _loss_grad(self, out, x, y):
-        """The reference LossFunc on [out0, out1] and its gradient w.r.t. both tensors."""
+        """The reference LossFunc on [out0, out1] and its gradient w.r.t. both tensors: the
+        check term by gnnd_syndrome_loss and the BCE term elementwise (V30Loss.loss_and_grad),
+        or torch autograd on the loss where that does not apply."""
+        lg = getattr(self.loss_fn, 'loss_and_grad', None)
+        res = lg(out, y, x) if lg is not None else None
+        if res is not None:
+            return res[0].detach(), res[1]
         o = out.detach().requires_grad_(True)
         n = o.size(0) // 2
         with torch.enable_grad():
