@@ -1081,6 +1081,9 @@ template <typename T> __device__ __forceinline__ T var_sum_uniform(const T* mp, 
 // (variable, edge) and check feature.  Step 1 therefore touches LDS only to read
 // {S_v, x_v} and to publish m_e in VARIABLE-major order (E + 1 per codeword, the extra
 // slot absorbs padding writes), and step 2 sums contiguous rows with no indirection.
+#ifndef GNND_VAR_PRIO
+#define GNND_VAR_PRIO 2            // s_setprio of the variable-sum step (0: off, A/B builds)
+#endif
 #ifndef GNND_RESIDENT_WAVES
 #define GNND_RESIDENT_WAVES 4      // min waves per SIMD: 4 -> <= 128 VGPRs (tuning builds vary it)
 #endif
@@ -1543,9 +1546,10 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             }
         }
         __syncthreads();
-#ifdef GNND_VAR_PRIO
-        __builtin_amdgcn_s_setprio(GNND_VAR_PRIO);   // latency-bound step first at the arbiter
-#endif
+        // the latency-bound variable-sum step first at the issue arbiter (its LDS read chains
+        // start while other workgroups' waves fill the VALU; BCH CGNNI +0.5 %,
+        // profiles/r03/experiments/headline_mlp_batch_prio_ab_r03l.txt)
+        if constexpr (GNND_VAR_PRIO > 0) __builtin_amdgcn_s_setprio(GNND_VAR_PRIO);
         // variable sums, codeword fastest, variables in degree order (var_ord): a wave's
         // lanes sum 64 / CW variables of (nearly) the same degree for consecutive codewords
         // (odd stride E+1: no bank conflicts).  Edge (index_add) order within a variable;
@@ -1641,9 +1645,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 var_item(b, i, b * E1, b * V);
             }
         }
-#ifdef GNND_VAR_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
+        if constexpr (GNND_VAR_PRIO > 0) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
     }
     if (iters == 0 && MODEL != GNND_V22)        // (V22: zero iterations, empty readout list)

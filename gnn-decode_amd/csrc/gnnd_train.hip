@@ -120,6 +120,25 @@ __device__ __forceinline__ void wave_sum4(f32x2 ab, f32x2 cd, float& ra, float& 
     if (GNND_PL16_MAP == 0) { ra = r0; rc = r1; rb = r2; rd = r3; }
     else { rc = r0; ra = r1; rd = r2; rb = r3; }
 }
+// wave_sum4 without the lane reads: every lane of 16-lane row r ends with the total of the
+// edge kRowEdge[r] (rows {a, c, b, d} under GNND_PL16_MAP 0), for a store by the rows' lanes
+__device__ __forceinline__ float wave_rows4(f32x2 ab, f32x2 cd) {
+    const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_int(ab.x), __float_as_int(ab.y), false, false);
+    const float v1 = __int_as_float(s1[0]) + __int_as_float(s1[1]);
+    const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_int(cd.x), __float_as_int(cd.y), false, false);
+    const float v2 = __int_as_float(s2[0]) + __int_as_float(s2[1]);
+    const auto s3 = __builtin_amdgcn_permlane16_swap(__float_as_int(v1), __float_as_int(v2), false, false);
+    float v = __int_as_float(s3[0]) + __int_as_float(s3[1]);
+    v += __int_as_float(dpp_i<0xB1, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x4E, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x141, 0xf>(__float_as_int(v)));
+    v += __int_as_float(dpp_i<0x140, 0xf>(__float_as_int(v)));
+    return v;
+}
+// edge (0..3 of the step's four) whose total row r of wave_rows4 holds
+__device__ __forceinline__ int row_edge(int row) {
+    return GNND_PL16_MAP == 0 ? (row == 1 ? 2 : row == 2 ? 1 : row) : (row == 0 ? 2 : row == 1 ? 0 : row == 2 ? 3 : 1);
+}
 template <int CTRL, int ROWS> __device__ __forceinline__ double dpp_d(double v) {
     const long long b = __double_as_longlong(v);
     const int lo = dpp_i<CTRL, ROWS>((int)b), hi = dpp_i<CTRL, ROWS>((int)(b >> 32));
@@ -148,14 +167,14 @@ template <typename T> struct Units {
     T gw1a[2], gw1b[2], gb1[2], gw2[2], gb2;
     f32x2 pgw1a[2], pgw1b[2], pgb1[2], pgw2[2];  // fp32 packed path: per-edge-half partials
     float s1a[2], s1b[2], sb1[2];                // fp32: layer 1 in log2 units (x log2 e)
-    float ws1a[2];                               // fp32: W2 s1a (d input with W2 factored out)
+    float ws1a[2];                               // fp32: W2 W1a (d input with W2 factored out)
     __device__ void zero_packed() {
         zero_pg();
         for (int j = 0; j < 2; ++j) {
             s1a[j] = (float)w1a[j] * kLog2e;
             s1b[j] = (float)w1b[j] * kLog2e;
             sb1[j] = (float)b1[j] * kLog2e;
-            ws1a[j] = (float)w2[j] * s1a[j];
+            ws1a[j] = (float)w2[j] * (float)w1a[j];
         }
     }
     // fp32: the per-edge-half partials live for one pass over the edges only (zero_pg at its
@@ -236,8 +255,6 @@ template <typename T> struct Units {
                                              float dyb, float& ra, float& rb) {
         const f32x2 p = bwd2_f32_part<TWO>(xa0, xa1, dya, xb0, xb1, dyb);
         wave_sum2(p.x, p.y, ra, rb);
-        ra *= kLn2;
-        rb *= kLn2;
     }
     // four edges: two pairs' unit work, one shared wave reduction (wave_sum4)
     template <bool TWO>
@@ -246,15 +263,25 @@ template <typename T> struct Units {
         const f32x2 pab = bwd2_f32_part<TWO>(x0[0], x1[0], dy[0], x0[1], x1[1], dy[1]);
         const f32x2 pcd = bwd2_f32_part<TWO>(x0[2], x1[2], dy[2], x0[3], x1[3], dy[3]);
         wave_sum4(pab, pcd, r[0], r[1], r[2], r[3]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) r[i] *= kLn2;
+    }
+    // four CONSECUTIVE edges as two packed pairs {0,1}, {2,3} (the ds_read_b128 inputs of the
+    // unit pass): returns the row-reduced vector of wave_rows4 (every lane of row r holds the
+    // d input total of edge kRowEdge[r])
+    template <bool TWO>
+    __device__ __forceinline__ float bwd4_rows(f32x4 x0, f32x4 x1, f32x4 dy) {
+        const f32x2 pab = bwd2_f32_part2<TWO>(f32x2{x0.x, x0.y}, f32x2{x1.x, x1.y}, f32x2{dy.x, dy.y});
+        const f32x2 pcd = bwd2_f32_part2<TWO>(f32x2{x0.z, x0.w}, f32x2{x1.z, x1.w}, f32x2{dy.z, dy.w});
+        return wave_rows4(pab, pcd);
     }
     // the per-lane unit work of two edges: weight-gradient partials accumulated, returns the
     // lane's d input partials (log2 units) of both edges, to be wave-reduced
     template <bool TWO>
     __device__ __forceinline__ f32x2 bwd2_f32_part(float xa0, float xa1, float dya, float xb0,
                                                    float xb1, float dyb) {
-        const f32x2 x0 = {xa0, xb0}, x1 = {xa1, xb1}, dy = {dya, dyb};
+        return bwd2_f32_part2<TWO>(f32x2{xa0, xb0}, f32x2{xa1, xb1}, f32x2{dya, dyb});
+    }
+    template <bool TWO>
+    __device__ __forceinline__ f32x2 bwd2_f32_part2(f32x2 x0, f32x2 x1, f32x2 dy) {
         f32x2 p = {0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -278,10 +305,10 @@ template <typename T> struct Units {
             pgw1a[j] = dh * x0 + pgw1a[j];
             if constexpr (TWO) pgw1b[j] = dh * x1 + pgw1b[j];
             pgb1[j] = pgb1[j] + dh;
-            p = dh * ws1a[j] + p;            // d input in log2 units (ln 2 below)
+            p = dh * ws1a[j] + p;            // d input (natural units)
         }
-        gb2 += dya;
-        gb2 += dyb;
+        gb2 += dy.x;
+        gb2 += dy.y;
         return p;
     }
     // add this wave's gradients into the workgroup accumulator (packed plain layout)
@@ -341,15 +368,18 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     const int* s_cptr = s_vptr + V + 1;
     const int* s_cedge = s_cptr + C + 1;
     size_t off = ((size_t)nints * 4 + 15) & ~(size_t)15;
+    // per-edge arrays at a 4-aligned stride Ep (the fp32 unit passes read four consecutive
+    // edges with one ds_read_b128; entries E..Ep-1 stay zero: finite inputs, dy = 0)
+    const int Ep = (E + 3) & ~3;
     T* s_dm = (T*)(smem + off);              // [E] d loss / d m (current iteration)
-    T* s_g = s_dm + E;                       // [E] du, then dext
-    T* s_da = s_g + E;                       // [E] d a
-    T* s_u = s_da + E;                       // [E] tape of the iteration: u, t, ext
-    T* s_t = s_u + E;
-    T* s_ext = s_t + E;
-    T* s_xv = s_ext + E;                     // [E] x_{v(e)}  (prior of the edge's variable)
-    T* s_sc = s_xv + E;                      // [E] s_{c(e)}  (syndrome of the edge's check)
-    T* s_acc = s_sc + E;                     // [1283] workgroup gradient accumulator
+    T* s_g = s_dm + Ep;                      // [E] du, then dext
+    T* s_da = s_g + Ep;                      // [E] d a
+    T* s_u = s_da + Ep;                      // [E] tape of the iteration: u, t, ext
+    T* s_t = s_u + Ep;
+    T* s_ext = s_t + Ep;
+    T* s_xv = s_ext + Ep;                    // [E] x_{v(e)}  (prior of the edge's variable)
+    T* s_sc = s_xv + Ep;                     // [E] s_{c(e)}  (syndrome of the edge's check)
+    T* s_acc = s_sc + Ep;                    // [1283] workgroup gradient accumulator
     // fused loss (lossp.y): [V] y + p, p, d loss / d p; [C + nl] row gradients, row terms;
     // int [V] logical masks, [nl] row lengths, [nl][V] row variable lists
     const bool floss = lossp.y != nullptr;
@@ -366,6 +396,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     const int* gtab = (const int*)g.edge_vc;
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     for (int i = tid; i < kV24W; i += kTrainThreads) s_acc[i] = T(0);
+    for (int i = tid; i < 8 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
     if (floss) {
         for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
         __syncthreads();
@@ -393,7 +424,8 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
     // The uniform results of step k go to lane k of two VGPRs (compare + select), stored by the
     // lanes after every 64 steps (no per-step exec-masked lane-0 stores).
-    auto unit_pass = [&](auto& U, auto two_tag, const T* in0, const T* in1, auto dy_of, T* outp) {
+    auto unit_pass = [&](auto& U, auto two_tag, const T* in0, const T* in1, auto dy_of, auto dy4_of,
+                         T* outp) {
         constexpr bool TWO = decltype(two_tag)::value;
         if constexpr (sizeof(T) == 4) {
             // fp32: four edges f + i W (i = 0..3) per wave step, one shared reduction; the next
@@ -435,16 +467,27 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                         }
                     }
                 } else {
-                    for (int f = f0; f < E && k < 64; f += kStride4, ++k) {
-                        float a0[4], a1[4], dy[4], r[4];
-                        load(f, a0, a1, dy);
-                        U.template bwd4_f32<TWO>(a0, a1, dy, r);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) res[i] = put_lane(res[i], r[i], k, lane);
+                    // four CONSECUTIVE edges f..f+3 per wave step (f = 4 (wave + W k)): one
+                    // ds_read_b128 per input array, the pairs {f, f+1}, {f+2, f+3} straight into
+                    // the packed halves; the row-reduced d input stored by one lane per row
+                    // the per-half partials are pass-local here too (zero_pg / fold around the
+                    // pass): only the active MLP's 16 partial VGPRs live, not all three MLPs' 48
+                    const int eo = row_edge(lane >> 4);
+                    U.zero_pg();
+                    for (int f = 4 * f0; f < E; f += 4 * kTrainWaves) {
+                        const f32x4 v0 = *(const f32x4*)(in0 + f);
+                        const f32x4 v1 = TWO ? *(const f32x4*)(in1 + f) : f32x4{0.f, 0.f, 0.f, 0.f};
+                        const float r = U.template bwd4_rows<TWO>(v0, v1, dy4_of(f));
+                        // every lane stores its row's total (16 identical writes per
+                        // address, no exec-masked region inside the hot loop; f + eo < Ep, and
+                        // the padding entries only ever meet dy = 0)
+                        outp[f + eo] = r;
                     }
+                    U.fold();
+                    break;                       // (one pass covers every edge)
                 }
                 const int fl = f0 + kStride4 * lane;
-                if (lane < k) {
+                if (kPipe && lane < k) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         if (fl + i * W < E) outp[fl + i * W] = res[i];
@@ -564,7 +607,12 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
         __syncthreads();
 
         // readout: r_v = sum_e MLP_o(m^T_e) + x_v  ->  dm
-        unit_pass(uo, std::false_type{}, s_u, nullptr, [&](int f) { return s_da[f]; }, s_dm);
+        auto ld4 = [](const T* a, int f) -> f32x4 {
+            if constexpr (sizeof(T) == 4) return *(const f32x4*)(a + f);
+            else return f32x4{0.f, 0.f, 0.f, 0.f};
+        };
+        unit_pass(uo, std::false_type{}, s_u, nullptr, [&](int f) { return s_da[f]; },
+                  [&](int f) { return ld4(s_da, f); }, s_dm);
         __syncthreads();
 
 #ifndef GNND_BWD_EXP
@@ -576,7 +624,8 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             if (it > 0) prefetch(it - 1);
             // A: m^{t+1} = MLP_c(u) s_c + m^t
             if (GNND_BWD_EXP != 3)
-                unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; }, s_g);
+                unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; },
+                          [&](int f) { return ld4(s_dm, f) * ld4(s_sc, f); }, s_g);
             __syncthreads();
             // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
             for (int f = tid; f < E; f += kTrainThreads) {
@@ -590,7 +639,8 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             if (GNND_BWD_EXP != 2) __syncthreads();
             // C: a = MLP_v(ext, x_v)
             if (GNND_BWD_EXP != 3)
-                unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; }, s_g);
+                unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; },
+                          [&](int f) { return ld4(s_da, f); }, s_g);
             __syncthreads();
             // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
             for (int f = tid; f < E; f += kTrainThreads) {
@@ -607,7 +657,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     // workgroup gradient: waves add in order (deterministic), then one row per workgroup
     for (int wv = 0; wv < kTrainWaves; ++wv) {
         if (wave == wv) {
-            constexpr bool kFolded = kTrainThreads <= 512 && kMinWaves == 1;   // unit_pass folds
+            constexpr bool kFolded = true;   // fp32: every unit_pass folds its partials
             uv.template flush<true>(s_acc + kV24Ggc1, lane, kFolded);
             uc.template flush<false>(s_acc + kV24Ggc2, lane, kFolded);
             uo.template flush<false>(s_acc + kV24Mlp, lane, kFolded);
@@ -668,7 +718,7 @@ int64_t train_rows(const gnnd_graph* g, int64_t B) {
 size_t train_lds(const gnnd_graph* g, int esz, int nl = -1) {   // nl >= 0: fused loss
     const GraphView& v = g->view;
     size_t n = (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
-               (size_t)esz * (8 * (size_t)v.E + kV24W);
+               (size_t)esz * (8 * (((size_t)v.E + 3) & ~(size_t)3) + kV24W);
     if (nl >= 0)
         n += (size_t)esz * (3 * (size_t)v.V + 2 * ((size_t)v.C + nl)) +
              4 * ((size_t)v.V + nl + (size_t)nl * v.V);
@@ -1024,9 +1074,20 @@ train_update_kernel(const T* __restrict__ rows, int nrows, T* __restrict__ grad,
     if (rows) {
         // wave w sums rows w, w + 16, ... of 64 consecutive parameters (coalesced rows),
         // then a fixed tree over the 16 waves' partials
+        // (16 rows' loads issued before their adds: the same order, without one dependent
+        // L2 round trip per row)
         T s = T(0);
-        if (i < n)
-            for (int r = wv; r < nrows; r += kGroups) s += rows[(size_t)r * n + i];
+        if (i < n) {
+            int r = wv;
+            for (; r + 15 * kGroups < nrows; r += 16 * kGroups) {
+                T v[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[j] = rows[(size_t)(r + j * kGroups) * n + i];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) s += v[j];
+            }
+            for (; r < nrows; r += kGroups) s += rows[(size_t)r * n + i];
+        }
         s_red[tid] = s;
         __syncthreads();
         for (int o = kGroups / 2; o >= 1; o >>= 1) {
