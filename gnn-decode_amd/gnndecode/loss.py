@@ -166,12 +166,12 @@ class V30Loss(torch.nn.Module):
         tensor.  The check term is gnnd_syndrome_loss on out0's first B*V rows (column k =
         rows kV..kV+V-1, the script's stride-V slicing) with every column's y = the first
         codeword's (`tmp`); the BCE term and its gradient are elementwise on the strided
-        [B, C] views of out1 and x (torch autograd's formulas: BCE' = (1 - s)/(1 - q) - s/q,
+        [B, C] gathers of out1 and x (torch autograd's formulas: BCE' = (1 - s)/(1 - q) - s/q,
         q = |sin(pi/2 r)|).  None when the BCE rows of neighbouring columns overlap (C > V)."""
         a, b = self.a, self.b
         N = a + b
         B = y.numel() // a
-        if b > a or out.dtype not in (torch.float32, torch.float64) or not out.is_cuda:
+        if b > a or out.dtype not in (torch.float32, torch.float64):
             return None
         syn_loss = getattr(self, '_syn', {}).get(out.device)
         if syn_loss is None:                     # the check term: H^T s rows, no logical rows
@@ -181,8 +181,16 @@ class V30Loss(torch.nn.Module):
         n = B * N
         ycols = y.reshape(-1)[:a].to(o.dtype).repeat(B)
         loss_a, d_a = syn_loss.per_codeword(o[:B * a], ycols)
-        r = o[n:].as_strided((B, b), (a, 1), a)
-        syn = x.reshape(-1).as_strided((B, b), (N, 1), a).to(o.dtype)
+        key = (B, out.device)
+        cache = getattr(self, '_bce_idx', {})
+        if key not in cache:                     # (rows of out1, rows of x) of the BCE term
+            k = torch.arange(B, device=out.device).unsqueeze(1)
+            j = torch.arange(b, device=out.device)
+            cache[key] = (n + k * a + a + j, k * N + a + j)
+            self._bce_idx = cache
+        ri, xi = cache[key]
+        r = o[ri]
+        syn = x.reshape(-1)[xi].to(o.dtype)
         h = r * math.pi / 2
         sn = torch.sin(h)
         q = torch.abs(sn)
@@ -191,7 +199,7 @@ class V30Loss(torch.nn.Module):
         gr = gq * torch.sgn(sn) * torch.cos(h) * (math.pi / 2)
         d = torch.zeros_like(o)
         d[:B * a] = d_a.reshape(-1)
-        d[n:].as_strided((B, b), (a, 1), a).copy_(gr)
+        d[ri] = gr                               # (distinct rows: b <= a)
         return loss_a.sum() + bce.sum(), d.view_as(out)
 
     def forward(self, preds, y, x):

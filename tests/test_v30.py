@@ -193,3 +193,28 @@ def test_v30_empty_batch(golden):
     x = torch.empty(0, 1, dtype=torch.float64, device=DEV)
     out = gd.ops.decode(g, 'v30', x, 15, m.prepared_weights(torch.float64, DEV))
     assert out.numel() == 0
+
+
+def test_v30_loss_and_grad_matches_autograd_cpu():
+    """V30Loss.loss_and_grad (the fused trainer's loss: the check term through SyndromeLoss,
+    the BCE term and its gradient by formula, gathered rows of out1 and x) equals torch
+    autograd of the reference LossFunc restatement, on a view with a storage offset (CPU: the
+    check term takes SyndromeLoss's reference formula there)."""
+    import gnndecode as gd
+    H = torch.as_tensor(gd.codes.toric_code(5), dtype=torch.float64)
+    lf = gd.loss.V30Loss(H)
+    a, b = lf.a, lf.b
+    N, B = a + b, 6
+    g = torch.Generator().manual_seed(0)
+    base = torch.rand(2 * B * N + 7, 1, generator=g, dtype=torch.float64) * 0.9 + 0.05
+    out = base[7:]
+    y = (torch.rand(B * a, 1, generator=g) < 0.1).double()
+    x = torch.rand(B * N, 1, generator=g, dtype=torch.float64)
+    x.view(B, N)[:, a:] = (torch.rand(B, b, generator=g) < 0.5).double()
+    n = B * N
+    o = out.detach().clone().requires_grad_(True)
+    ref = lf([o[:n], o[n:]], y, x)
+    (dref,) = torch.autograd.grad(ref, o)
+    loss, d = lf.loss_and_grad(out, y, x)
+    assert abs(loss.item() - ref.item()) <= 1e-12 * abs(ref.item())
+    assert (d - dref).abs().max().item() <= 1e-12 * dref.abs().max().item()
