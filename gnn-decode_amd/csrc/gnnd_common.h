@@ -50,6 +50,54 @@ __device__ __forceinline__ int gnnd_dcheck_idx(int i, int n, int bit) {
 #endif
 
 // ---------------------------------------------------------------------------------------
+// phase timing (timing experiments only, -DGNND_PHASE_PROF): one wave of workgroup 0 sums the
+// shader-clock cycles (s_memtime) spent between consecutive marks and prints the per-phase
+// totals at the end of the launch.  Release builds compile the marks away.
+// ---------------------------------------------------------------------------------------
+struct PhaseProf {
+#ifdef GNND_PHASE_PROF
+    uint64_t acc[12];
+    uint64_t last;
+    bool on;
+    __device__ void start(bool enable) {
+        on = enable;
+        for (int i = 0; i < 12; ++i) acc[i] = 0;
+        last = __builtin_amdgcn_s_memtime();
+    }
+    __device__ __forceinline__ void mark(int i) {
+        if (on) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            acc[i] += t - last;
+            last = t;
+        }
+    }
+    __device__ void report(const char* tag, int n, int iters) {
+        if (on && (threadIdx.x & 63) == 0)
+            printf("PHASE %s iters %d | %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n",
+                   tag, iters, (unsigned long long)acc[0], (unsigned long long)acc[1],
+                   (unsigned long long)acc[2], (unsigned long long)acc[3], (unsigned long long)acc[4],
+                   (unsigned long long)acc[5], (unsigned long long)acc[6], (unsigned long long)acc[7],
+                   (unsigned long long)acc[8], (unsigned long long)acc[9], (unsigned long long)acc[10],
+                   (unsigned long long)acc[11]);
+        (void)n;
+    }
+#endif
+};
+#ifdef GNND_PHASE_PROF
+#define GNND_PPROF(pf) PhaseProf pf
+#define GNND_PSTART(pf, on) pf.start(on)
+#define GNND_PMARK(pf, i) pf.mark(i)
+#define GNND_PREPORT(pf, tag, n, iters) pf.report(tag, n, iters)
+#define GNND_PARG(pf, i) , &pf, i
+#else
+#define GNND_PPROF(pf) do { } while (0)
+#define GNND_PSTART(pf, on) do { } while (0)
+#define GNND_PMARK(pf, i) do { } while (0)
+#define GNND_PREPORT(pf, tag, n, iters) do { } while (0)
+#define GNND_PARG(pf, i)
+#endif
+
+// ---------------------------------------------------------------------------------------
 // host-side graph (owned by libgnnd, device-resident tables built once per H)
 // ---------------------------------------------------------------------------------------
 struct GraphView {            // passed by value to kernels

@@ -403,7 +403,7 @@ template <int N, typename F, int I = 0> __device__ __forceinline__ void static_f
 // (u0 -> W1a', u1 -> W1b').  wg: the MLP's prepared weights in global memory (uniform
 // address: scalar loads; J0 is a template argument so the weight offsets stay compile-time).
 template <int NC, int J0, bool TWO>
-__device__ __forceinline__ f32x2 mlp128_chains(const float* __restrict__ wg, const V24Lin& lin,
+__device__ __forceinline__ f32x2 mlp128_chains(const float* __restrict__ wg, V24Lin lin,
                                                f32x2 u0, f32x2 u1) {
     const f32x2* wb = (const f32x2*)wg;                      // {W1b'_k, b1'_k}
     const f32x2* wa = (const f32x2*)(wg + 256);              // W1a' pairs (TWO)
@@ -441,11 +441,11 @@ __device__ __forceinline__ f32x2 mlp128_chains(const float* __restrict__ wg, con
     else if constexpr (NC == 2) return c[0] + c[1];
     else return c[0];
 }
-__device__ __forceinline__ f32x2 mlp128_sp2(const float* __restrict__ wg, const V24Lin& lin,
+__device__ __forceinline__ f32x2 mlp128_sp2(const float* __restrict__ wg, V24Lin lin,
                                             f32x2 u) {
     return mlp128_chains<8, 0, false>(wg, lin, u, u);
 }
-__device__ __forceinline__ f32x2 mlp128x2_sp2(const float* __restrict__ wg, const V24Lin& lin,
+__device__ __forceinline__ f32x2 mlp128x2_sp2(const float* __restrict__ wg, V24Lin lin,
                                               f32x2 u0, f32x2 u1) {
     return mlp128_chains<8, 0, true>(wg, lin, u0, u1);
 }
@@ -459,9 +459,10 @@ template <int US> constexpr int unit_split_lanes() { return US == 8 ? 128 : GNND
 // (wave-uniform): the wave holds no live work item (its result is never stored) and skips the
 // units, so the SIMDs' issue goes to the live item waves only.
 template <int US, bool TWO>
-__device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, const V24Lin& lin,
+__device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, V24Lin lin,
                                               f32x2 u0, f32x2 u1, int sub, f32x2* buf, int itid,
-                                              bool idle) {
+                                              bool idle, PhaseProf* pf = nullptr, int mk = 0) {
+    (void)pf; (void)mk;
     constexpr int IL = unit_split_lanes<US>();
     f32x2 p = {0.f, 0.f};
     if constexpr (US == 1) {
@@ -482,14 +483,22 @@ __device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, cons
                 default: if constexpr (US == 8) p = mlp128_chains<1, 7, TWO>(wg, lin, u0, u1); break;
             }
         }
+#ifdef GNND_PHASE_PROF
+        if (pf) pf->mark(mk);
+#endif
         buf[sub * IL + itid] = p;
         __syncthreads();
-        if constexpr (US == 2) return buf[itid] + buf[IL + itid];
+        f32x2 r;
+        if constexpr (US == 2) r = buf[itid] + buf[IL + itid];
         else if constexpr (US == 4)
-            return (buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid]);
+            r = (buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid]);
         else
-            return ((buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid])) +
-                   ((buf[4 * IL + itid] + buf[5 * IL + itid]) + (buf[6 * IL + itid] + buf[7 * IL + itid]));
+            r = ((buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid])) +
+                ((buf[4 * IL + itid] + buf[5 * IL + itid]) + (buf[6 * IL + itid] + buf[7 * IL + itid]));
+#ifdef GNND_PHASE_PROF
+        if (pf) pf->mark(mk + 1);
+#endif
+        return r;
     }
 }
 // linear parts, identical in every thread (fixed summation order)
@@ -851,6 +860,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int IC = C * G;               // work items (lanes) per codeword
     const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
     const int nV = nb * V;
+    GNND_PPROF(pf);
+    GNND_PSTART(pf, blockIdx.x == 0 && tid < 64);
     for (int it = 0; it < iters; ++it) {
         for (int f0 = 0; f0 < nItem; f0 += IL) {
             const int f = f0 + itid;
@@ -880,11 +891,13 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     ext[r] = p.s - mv[r];
                     xs[r] = p.x;
                 }
+                GNND_PMARK(pf, 0);
 #pragma unroll
                 for (int r = 0; r < R; r += 2) {
                     const int r1 = r + 1 < R ? r + 1 : r;
                     const f32x2 a = mlp128_split<US, true>(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
-                                                           f32x2{xs[r], xs[r1]}, sub, s_part, itid, widle);
+                                                           f32x2{xs[r], xs[r1]}, sub, s_part, itid, widle
+                                                           GNND_PARG(pf, 1));
                     tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
                     if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
                 }
@@ -961,12 +974,13 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 }
             }
             if constexpr (kV24F32) {
+                GNND_PMARK(pf, 3);
 #pragma unroll
                 for (int r = 0; r < R; r += 2) {
                     const int r1 = r + 1 < R ? r + 1 : r;
                     const f32x2 uu = {Sc - tv[r], Sc - tv[r1]};
                     const f32x2 y = mlp128_split<US, false>(v24.g + kV24Ggc2, v24.l2, uu, uu, sub,
-                                                            s_part + US * IL, itid, widle);
+                                                            s_part + US * IL, itid, widle GNND_PARG(pf, 4));
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
                 }
@@ -983,8 +997,10 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
 #pragma unroll
                 for (int r = 0; r < R; ++r) mb[r] = mn[r];
             }
+            GNND_PMARK(pf, 6);
         }
         __syncthreads();
+        GNND_PMARK(pf, 7);
         if (it + 1 == iters) break;
         for (int f = tid; f < nV; f += NT) {
             const int b = fdiv(f, dV), v = f - b * V;
@@ -994,7 +1010,9 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             else
                 s_sx[f].s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
         }
+        GNND_PMARK(pf, 8);
         __syncthreads();
+        GNND_PMARK(pf, 9);
     }
 
     if constexpr (TAPE) {
@@ -1035,6 +1053,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             out[orow] = M::readout(s + s_sx[f].x, s_w);
         }
     }
+    GNND_PMARK(pf, 10);
+    GNND_PREPORT(pf, TAPE ? "fwd_tape" : "fwd", US, iters);
 }
 
 // HBM storage type of x / out.  GNND_BF16 keeps the inputs and outputs in bf16 (half the

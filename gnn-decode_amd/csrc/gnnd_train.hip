@@ -419,6 +419,8 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     uc.load1(w + kV24Ggc2, lane);
     uo.load1(w + kV24Mlp, lane);
     __syncthreads();
+    GNND_PPROF(pf);
+    GNND_PSTART(pf, blockIdx.x == 0 && tid < 64);
 
     // unit-parallel pass over the codeword's edges, two per wave step:
     // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
@@ -611,9 +613,11 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             if constexpr (sizeof(T) == 4) return *(const f32x4*)(a + f);
             else return f32x4{0.f, 0.f, 0.f, 0.f};
         };
+        GNND_PMARK(pf, 0);
         unit_pass(uo, std::false_type{}, s_u, nullptr, [&](int f) { return s_da[f]; },
                   [&](int f) { return ld4(s_da, f); }, s_dm);
         __syncthreads();
+        GNND_PMARK(pf, 1);
 
 #ifndef GNND_BWD_EXP
 #define GNND_BWD_EXP 0   // timing experiments only (wrong gradients): 1 no LOO compute,
@@ -621,12 +625,15 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
         for (int it = iters - 1; it >= 0; --it) {
             stage(it);
             __syncthreads();
+            GNND_PMARK(pf, 2);
             if (it > 0) prefetch(it - 1);
             // A: m^{t+1} = MLP_c(u) s_c + m^t
             if (GNND_BWD_EXP != 3)
                 unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; },
                           [&](int f) { return ld4(s_dm, f) * ld4(s_sc, f); }, s_g);
+            GNND_PMARK(pf, 3);
             __syncthreads();
+            GNND_PMARK(pf, 4);
             // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
             for (int f = tid; f < E; f += kTrainThreads) {
                 const int c = (int)(s_evc[f] >> 16);
@@ -636,12 +643,16 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                 const T t = s_t[f];
                 s_da[f] = ((s - s_g[f]) * (T(1) - t * t)) / T(2);
             }
+            GNND_PMARK(pf, 5);
             if (GNND_BWD_EXP != 2) __syncthreads();
+            GNND_PMARK(pf, 6);
             // C: a = MLP_v(ext, x_v)
             if (GNND_BWD_EXP != 3)
                 unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; },
                           [&](int f) { return ld4(s_da, f); }, s_g);
+            GNND_PMARK(pf, 7);
             __syncthreads();
+            GNND_PMARK(pf, 8);
             // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
             for (int f = tid; f < E; f += kTrainThreads) {
                 const int v = (int)(s_evc[f] & 0xffffu);
@@ -650,7 +661,9 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                     for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += s_g[k];
                 s_dm[f] += s - s_g[f];
             }
+            GNND_PMARK(pf, 9);
             if (GNND_BWD_EXP != 2) __syncthreads();
+            GNND_PMARK(pf, 10);
         }
     }
 
@@ -666,6 +679,8 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     }
     T* row = gpart + (size_t)blockIdx.x * kV24W;
     for (int i = tid; i < kV24W; i += kTrainThreads) row[i] = s_acc[i];
+    GNND_PMARK(pf, 11);
+    GNND_PREPORT(pf, "bwd", kTrainThreads, iters);
 }
 
 // sum of the per-workgroup rows, fixed order (8 interleaved partial chains, then combined)
