@@ -501,22 +501,26 @@ __device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, V24L
         return r;
     }
 }
-// linear parts, identical in every thread (fixed summation order)
+// linear parts, identical in every thread: a fixed-order 128-term dot product spread over the
+// wave's lanes (lane l: units l and l + 64, then the group_sum_c<64> butterfly, whose result
+// is the same bits in every lane and wave) — one vector-load latency instead of a serial chain
+// of scalar loads and 128 dependent FMAs per thread.  All 64 lanes must call it.
+__device__ __forceinline__ float wave_dot128(const float* __restrict__ a, int sa,
+                                             const float* __restrict__ b, int sb) {
+    const int l = threadIdx.x & 63;
+    const float p = __builtin_fmaf(a[(l + 64) * sa], b[(l + 64) * sb], a[l * sa] * b[l * sb]);
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                         __builtin_bit_cast(int, group_sum_c<64>(p))));
+}
 __device__ __forceinline__ V24Lin v24_lin1(const float* __restrict__ wg) {
-    float a = 0.f, b = 0.f;
-    for (int k = 0; k < 128; ++k) {
-        a = __builtin_fmaf(wg[256 + k], wg[2 * k], a);
-        b = __builtin_fmaf(wg[256 + k], wg[2 * k + 1], b);
-    }
+    const float a = wave_dot128(wg + 256, 1, wg, 2);
+    const float b = wave_dot128(wg + 256, 1, wg + 1, 2);
     return V24Lin{0.5f * a, 0.f, __builtin_fmaf(0.5f, b, wg[384])};
 }
 __device__ __forceinline__ V24Lin v24_lin2(const float* __restrict__ wg) {
-    float a0 = 0.f, a1 = 0.f, b = 0.f;
-    for (int k = 0; k < 128; ++k) {
-        a0 = __builtin_fmaf(wg[384 + k], wg[256 + k], a0);
-        a1 = __builtin_fmaf(wg[384 + k], wg[2 * k], a1);
-        b = __builtin_fmaf(wg[384 + k], wg[2 * k + 1], b);
-    }
+    const float a0 = wave_dot128(wg + 384, 1, wg + 256, 1);
+    const float a1 = wave_dot128(wg + 384, 1, wg, 2);
+    const float b = wave_dot128(wg + 384, 1, wg + 1, 2);
     return V24Lin{0.5f * a0, 0.5f * a1, __builtin_fmaf(0.5f, b, wg[512])};
 }
 struct V24F32 {            // fp32 V24 weights of the streaming kernel
@@ -781,6 +785,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     using M = EdgeMath<MODEL, T>;
     constexpr bool BP = ModelTraits<MODEL>::bp;
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    GNND_PPROF(pf);
+    GNND_PSTART(pf, blockIdx.x == 0 && threadIdx.x < 64);
     int blk = blockIdx.x;
     GraphView g = g0;
     if (views) {                       // uniform: component k of the split graph
@@ -822,18 +828,42 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // not flat ones as through an integer cast of the pointer)
     f32x2* s_part = (f32x2*)(smem + ((((char*)(s_xc + (size_t)CW * C) - smem) + 7) & ~(ptrdiff_t)7));
 
-    for (int i = tid; i < nw; i += NT) s_w[i] = w[i];
-    for (int i = tid; i < nslot; i += NT) s_slot[i] = g.slot_ve[i];   // v | e << 16
-    for (int i = tid; i <= V; i += NT) s_vptr[i] = g.var_ptr[i];
-    for (int i = tid; i < E; i += NT) s_vslot[i] = g.vslot[i];
     const int64_t b0 = (int64_t)blk * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
-    // the tile's rows (whole graph: one contiguous run of nb*N values)
-    for (int i = tid; i < nb * N; i += NT) {
-        int b = fdiv(i, dN), n = i - b * N;
-        const T* xr = x + (size_t)(b0 + b) * g.xs;
-        if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xr[g.xv0 + n]};
-        else s_xc[b * C + n - V] = xr[g.xc0 + n - V];
+    constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
+    // fp32 decoder_v2_4 reads its weights through the scalar cache only (no LDS copy); with
+    // every table and the tile's rows within one element per thread (small batches: one
+    // component-codeword per workgroup) all global loads are issued before any LDS store, so
+    // their latencies overlap instead of one loop after another
+    const bool one = kV24F32 && nslot <= NT && V + 1 <= NT && E <= NT && nb * N <= NT;
+    if (one) {
+        const int i = tid;
+        const uint32_t a_sl = i < nslot ? g.slot_ve[i] : 0u;
+        const int a_vp = i <= V ? g.var_ptr[i] : 0;
+        const int a_vs = i < E ? g.vslot[i] : 0;
+        const int bx = fdiv(i < nb * N ? i : 0, dN), nx = (i < nb * N ? i : 0) - bx * N;
+        const T* xr = x + (size_t)(b0 + bx) * g.xs;
+        const T a_x = i < nb * N ? (nx < V ? xr[g.xv0 + nx] : xr[g.xc0 + nx - V]) : T(0);
+        if (i < nslot) s_slot[i] = a_sl;
+        if (i <= V) s_vptr[i] = a_vp;
+        if (i < E) s_vslot[i] = a_vs;
+        if (i < nb * N) {
+            if (nx < V) s_sx[bx * V + nx] = SumX<T>{T(0), a_x};
+            else s_xc[bx * C + nx - V] = a_x;
+        }
+    } else {
+        if constexpr (!kV24F32)
+            for (int i = tid; i < nw; i += NT) s_w[i] = w[i];
+        for (int i = tid; i < nslot; i += NT) s_slot[i] = g.slot_ve[i];   // v | e << 16
+        for (int i = tid; i <= V; i += NT) s_vptr[i] = g.var_ptr[i];
+        for (int i = tid; i < E; i += NT) s_vslot[i] = g.vslot[i];
+        // the tile's rows (whole graph: one contiguous run of nb*N values)
+        for (int i = tid; i < nb * N; i += NT) {
+            int b = fdiv(i, dN), n = i - b * N;
+            const T* xr = x + (size_t)(b0 + b) * g.xs;
+            if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xr[g.xv0 + n]};
+            else s_xc[b * C + n - V] = xr[g.xc0 + n - V];
+        }
     }
     for (int i = tid; i < nb * nslot; i += NT) s_m[i] = T(0);
     __syncthreads();
@@ -842,7 +872,6 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // no LDS traffic, one SGPR operand per packed FMA.  Broadcast ds_read_b128 of the same
     // weights from LDS costs 4 LDS cycles per 4 floats per wave and saturated the LDS pipe.
     const T* __restrict__ wv = w;
-    constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
     V24F32 v24{(const float*)w, {}, {}, {}};
     if constexpr (kV24F32) {
         v24.l1 = v24_lin2((const float*)w + kV24Ggc1);
@@ -860,8 +889,37 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int IC = C * G;               // work items (lanes) per codeword
     const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
     const int nV = nb * V;
-    GNND_PPROF(pf);
-    GNND_PSTART(pf, blockIdx.x == 0 && tid < 64);
+    // unit-split small batches (one round of items): each lane's slots are fixed for the whole
+    // decode, so it gathers its variables' messages itself (indices and x_v kept in registers,
+    // summed in var_ptr order = var_sum's order: the same S_v bits) and the variable-sum step
+    // and its barrier go (the unit split's barriers order this iteration's gathers before its
+    // message writes)
+    constexpr bool kGath = kV24F32 && US > 1;
+    constexpr int kGDv = 4;
+#ifdef GNND_NO_GATHER
+    const bool gath = false;
+#else
+    const bool gath = kGath && g.max_dv <= kGDv && nItem <= IL;
+#endif
+    int gidx[kGath ? R : 1][kGDv], gcnt[kGath ? R : 1];
+    float gx[kGath ? R : 1];
+    if constexpr (kGath) {
+        if (gath) {
+            const int fc = itid < nItem ? itid : nItem - 1;
+            const int b = fdiv(fc, dItem), rem = fc - b * IC;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t sv = s_slot[rem * R + r];
+                const int v = (int)(sv & 0xffffu);
+                const int k0 = s_vptr[v], ke = s_vptr[v + 1];
+                gcnt[r] = (int)(sv >> 16) != E ? ke - k0 : 0;
+#pragma unroll
+                for (int j = 0; j < kGDv; ++j) gidx[r][j] = b * nslot + s_vslot[min(k0 + j, ke - 1)];
+                gx[r] = s_sx[b * V + v].x;
+            }
+        }
+    }
+    GNND_PMARK(pf, 11);
     for (int it = 0; it < iters; ++it) {
         for (int f0 = 0; f0 < nItem; f0 += IL) {
             const int f = f0 + itid;
@@ -887,6 +945,20 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     const uint32_t sv = sl[r];
                     val[r] = (int)(sv >> 16) != E;
                     mv[r] = mb[r];
+                    if constexpr (kGath) {
+                        if (gath) {
+                            float m[kGDv];
+#pragma unroll
+                            for (int j = 0; j < kGDv; ++j) m[j] = s_m[gidx[r][j]];
+                            float S = 0.f;
+#pragma unroll
+                            for (int j = 0; j < kGDv; ++j)
+                                if (j < gcnt[r]) S += m[j];
+                            ext[r] = S - mv[r];
+                            xs[r] = gx[r];
+                            continue;
+                        }
+                    }
                     const SumX<T> p = sxb[sv & 0xffffu];
                     ext[r] = p.s - mv[r];
                     xs[r] = p.x;
@@ -1002,6 +1074,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
         __syncthreads();
         GNND_PMARK(pf, 7);
         if (it + 1 == iters) break;
+        if (gath) continue;                 // (uniform) the lanes gather S_v themselves
         for (int f = tid; f < nV; f += NT) {
             const int b = fdiv(f, dV), v = f - b * V;
             if constexpr (MODEL == GNND_NBP)   // S_v of the next layer's weighted messages
@@ -1024,7 +1097,26 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     }
     if constexpr (MODEL == GNND_V24) {
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
-        if constexpr (kV24F32) {
+        if constexpr (kV24F32 && US > 1) {
+            // unit split here too: item lane itid evaluates slot pair f0 + 2 itid, the US waves
+            // sharing it a chain group each (same bits as the whole MLP in one lane); the two
+            // partial-sum buffers alternate between rounds (one barrier per round)
+            const int n = nb * nslot;
+            int rb = 0;
+            for (int f0 = 0; f0 < n; f0 += 2 * IL, rb ^= 1) {
+                const int f = f0 + 2 * itid;
+                const bool widle = __builtin_amdgcn_readfirstlane(f0 + 2 * (itid & ~63)) >= n;
+                const int fa = f < n ? f : n - 1;
+                const int f1 = fa + 1 < n ? fa + 1 : fa;
+                const f32x2 m2 = {s_m[fa], s_m[f1]};
+                const f32x2 y = mlp128_split<US, false>(v24.g + kV24Mlp, v24.l3, m2, m2, sub,
+                                                        s_part + rb * US * IL, itid, widle);
+                if (sub == 0 && f < n) {
+                    s_m[f] = y.x;
+                    if (f + 1 < n) s_m[f + 1] = y.y;
+                }
+            }
+        } else if constexpr (kV24F32) {
             const int n = nb * nslot;
             for (int f = 2 * tid; f < n; f += 2 * NT) {
                 const int f1 = f + 1 < n ? f + 1 : f;

@@ -311,7 +311,8 @@ template <typename T> struct Units {
         gb2 += dy.y;
         return p;
     }
-    // add this wave's gradients into the workgroup accumulator (packed plain layout)
+    // store this wave's gradients into its row of the workgroup's per-wave buffer (packed
+    // plain layout; every index of the MLP written by exactly one lane)
     template <bool TWO>
     __device__ void flush(T* acc, int lane, bool folded) {
         if constexpr (sizeof(T) == 4)
@@ -319,12 +320,12 @@ template <typename T> struct Units {
         for (int j = 0; j < 2; ++j) {
             const int k = lane + 64 * j;
             if constexpr (TWO) {
-                acc[k] += gw1a[j]; acc[128 + k] += gw1b[j]; acc[256 + k] += gb1[j]; acc[384 + k] += gw2[j];
+                acc[k] = gw1a[j]; acc[128 + k] = gw1b[j]; acc[256 + k] = gb1[j]; acc[384 + k] = gw2[j];
             } else {
-                acc[k] += gw1a[j]; acc[128 + k] += gb1[j]; acc[256 + k] += gw2[j];
+                acc[k] = gw1a[j]; acc[128 + k] = gb1[j]; acc[256 + k] = gw2[j];
             }
         }
-        if (lane == 0) acc[TWO ? 512 : 384] += gb2;
+        if (lane == 0) acc[TWO ? 512 : 384] = gb2;
     }
 };
 
@@ -347,8 +348,10 @@ __global__ void __launch_bounds__(kTrainThreads, kMinWaves)   // kMinWaves: per 
 v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                const T* __restrict__ p, const T* __restrict__ gp, TapeView<T> tape,
                T* __restrict__ gpart, int64_t B, int iters, const GraphView* __restrict__ views,
-               int cblk, BwdLoss<T> lossp) {
+               int cblk, BwdLoss<T> lossp, int sibs) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    GNND_PPROF(pf);
+    GNND_PSTART(pf, blockIdx.x == 0 && threadIdx.x < 64);
     GraphView g = g0;
     int blk = blockIdx.x, nblk = gridDim.x, comp = 0;
     if (views) {                       // uniform: component k
@@ -379,12 +382,11 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     T* s_ext = s_t + Ep;
     T* s_xv = s_ext + Ep;                    // [E] x_{v(e)}  (prior of the edge's variable)
     T* s_sc = s_xv + Ep;                     // [E] s_{c(e)}  (syndrome of the edge's check)
-    T* s_acc = s_sc + Ep;                    // [1283] workgroup gradient accumulator
     // fused loss (lossp.y): [V] y + p, p, d loss / d p; [C + nl] row gradients, row terms;
     // int [V] logical masks, [nl] row lengths, [nl][V] row variable lists
     const bool floss = lossp.y != nullptr;
     const int nl = floss ? lossp.nl : 0, nr = C + nl;
-    T* s_ls = s_acc + kV24W;
+    T* s_ls = s_sc + Ep;
     T* s_pv = s_ls + V;
     T* s_gpv = s_pv + V;
     T* s_lg = s_gpv + V;
@@ -392,10 +394,21 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     uint32_t* s_lmask = (uint32_t*)(s_lt + nr);
     int* s_lcnt = (int*)(s_lmask + V);
     int* s_lvar = s_lcnt + nl;
+    // sibs (checks and variables of degree <= 4): per edge its check's edges (cedge order) and
+    // its variable's edges (var_ptr order), -1 padded: [E][8] ints built once per launch, so
+    // the leave-one-out phases read their operands in two LDS round trips instead of walking
+    // evc -> ptr -> edge chains
+    // (after the fused-loss arrays when they exist, else right after the per-edge arrays; offset
+    // arithmetic on the __shared__ base keeps ds_* accesses)
+    const char* sib_end = floss ? (const char*)(s_lvar + (size_t)nl * V) : (const char*)s_ls;
+    int* s_sib = (int*)(smem + (((sib_end - smem) + 15) & ~(ptrdiff_t)15));
 
     const int* gtab = (const int*)g.edge_vc;
+    Units<T> uv, uc, uo;                     // ggc1.mlp, ggc2.mlp, mlp
+    uv.load2(w + kV24Ggc1, lane);
+    uc.load1(w + kV24Ggc2, lane);
+    uo.load1(w + kV24Mlp, lane);
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
-    for (int i = tid; i < kV24W; i += kTrainThreads) s_acc[i] = T(0);
     for (int i = tid; i < 8 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
     if (floss) {
         for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
@@ -414,13 +427,22 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             if (lane == 0) s_lcnt[l] = cnt;
         }
     }
-    Units<T> uv, uc, uo;                     // ggc1.mlp, ggc2.mlp, mlp
-    uv.load2(w + kV24Ggc1, lane);
-    uc.load1(w + kV24Ggc2, lane);
-    uo.load1(w + kV24Mlp, lane);
     __syncthreads();
-    GNND_PPROF(pf);
-    GNND_PSTART(pf, blockIdx.x == 0 && tid < 64);
+    if (sibs) {
+        for (int f = tid; f < E; f += kTrainThreads) {
+            const uint32_t vc = s_evc[f];
+            const int c = (int)(vc >> 16), v = (int)(vc & 0xffffu);
+            const int c0 = s_cptr[c], cn = s_cptr[c + 1] - c0;
+            const int v0 = s_vptr[v], vn = s_vptr[v + 1] - v0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s_sib[8 * f + j] = j < cn ? s_cedge[c0 + j] : -1;
+                s_sib[8 * f + 4 + j] = j < vn ? v0 + j : -1;
+            }
+        }
+        __syncthreads();
+    }
+    GNND_PMARK(pf, 12);
 
     // unit-parallel pass over the codeword's edges, two per wave step:
     // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
@@ -561,7 +583,9 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                 s_pv[v] = pv;
                 s_ls[v] = lossp.y[ob + v] + pv;
             }
+            GNND_PMARK(pf, 13);
             __syncthreads();
+            GNND_PMARK(pf, 14);
             const T kPi = T(M_PI);
             for (int r = tid; r < nr; r += kTrainThreads) {
                 T sr = T(0);
@@ -578,6 +602,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                 s_lg[r] = on ? gr : T(0);
                 s_lt[r] = on ? (sn < T(0) ? -sn : sn) : T(0);
             }
+            GNND_PMARK(pf, 15);
             __syncthreads();
             for (int v = tid; v < V; v += kTrainThreads) {
                 T d = T(0);
@@ -636,10 +661,20 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             GNND_PMARK(pf, 4);
             // B: u = S_c(t) - t  ->  dt = S_c(du) - du;  t = tanh(a/2)
             for (int f = tid; f < E; f += kTrainThreads) {
-                const int c = (int)(s_evc[f] >> 16);
                 T s = T(0);
-                if (GNND_BWD_EXP == 0 || GNND_BWD_EXP == 3)
-                    for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += s_g[s_cedge[k]];
+                if (sibs) {           // the same order: the check's edges in cedge order
+                    const int4 cs = *(const int4*)(s_sib + 8 * f);
+                    const T g0 = s_g[cs.x < 0 ? 0 : cs.x], g1 = s_g[cs.y < 0 ? 0 : cs.y];
+                    const T g2 = s_g[cs.z < 0 ? 0 : cs.z], g3 = s_g[cs.w < 0 ? 0 : cs.w];
+                    if (cs.x >= 0) s += g0;
+                    if (cs.y >= 0) s += g1;
+                    if (cs.z >= 0) s += g2;
+                    if (cs.w >= 0) s += g3;
+                } else {
+                    const int c = (int)(s_evc[f] >> 16);
+                    if (GNND_BWD_EXP == 0 || GNND_BWD_EXP == 3)
+                        for (int k = s_cptr[c], ke = s_cptr[c + 1]; k < ke; ++k) s += s_g[s_cedge[k]];
+                }
                 const T t = s_t[f];
                 s_da[f] = ((s - s_g[f]) * (T(1) - t * t)) / T(2);
             }
@@ -655,10 +690,20 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             GNND_PMARK(pf, 8);
             // D: ext = S_v(m) - m  ->  dm += S_v(dext) - dext  (variable edges are contiguous)
             for (int f = tid; f < E; f += kTrainThreads) {
-                const int v = (int)(s_evc[f] & 0xffffu);
                 T s = T(0);
-                if (GNND_BWD_EXP == 0 || GNND_BWD_EXP == 3)
-                    for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += s_g[k];
+                if (sibs) {           // the same order: the variable's edges ascending
+                    const int4 vs = *(const int4*)(s_sib + 8 * f + 4);
+                    const T g0 = s_g[vs.x < 0 ? 0 : vs.x], g1 = s_g[vs.y < 0 ? 0 : vs.y];
+                    const T g2 = s_g[vs.z < 0 ? 0 : vs.z], g3 = s_g[vs.w < 0 ? 0 : vs.w];
+                    if (vs.x >= 0) s += g0;
+                    if (vs.y >= 0) s += g1;
+                    if (vs.z >= 0) s += g2;
+                    if (vs.w >= 0) s += g3;
+                } else {
+                    const int v = (int)(s_evc[f] & 0xffffu);
+                    if (GNND_BWD_EXP == 0 || GNND_BWD_EXP == 3)
+                        for (int k = s_vptr[v], ke = s_vptr[v + 1]; k < ke; ++k) s += s_g[k];
+                }
                 s_dm[f] += s - s_g[f];
             }
             GNND_PMARK(pf, 9);
@@ -667,18 +712,27 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
         }
     }
 
-    // workgroup gradient: waves add in order (deterministic), then one row per workgroup
-    for (int wv = 0; wv < kTrainWaves; ++wv) {
-        if (wave == wv) {
-            constexpr bool kFolded = true;   // fp32: every unit_pass folds its partials
-            uv.template flush<true>(s_acc + kV24Ggc1, lane, kFolded);
-            uc.template flush<false>(s_acc + kV24Ggc2, lane, kFolded);
-            uo.template flush<false>(s_acc + kV24Mlp, lane, kFolded);
-        }
-        __syncthreads();
+    // workgroup gradient: every wave stores its gradients into its own row of a per-wave
+    // buffer (aliasing the per-edge arrays, dead now), then each parameter is summed over the
+    // waves in wave order from 0 (deterministic; the same bits as adding the waves one by one
+    // into a zeroed accumulator) — one barrier instead of one per wave
+    T* s_red = s_dm;                         // [kTrainWaves][kV24W] (train_lds reserves it)
+    __syncthreads();
+    {
+        constexpr bool kFolded = true;       // fp32: every unit_pass folds its partials
+        T* my = s_red + (size_t)wave * kV24W;
+        uv.template flush<true>(my + kV24Ggc1, lane, kFolded);
+        uc.template flush<false>(my + kV24Ggc2, lane, kFolded);
+        uo.template flush<false>(my + kV24Mlp, lane, kFolded);
     }
+    __syncthreads();
     T* row = gpart + (size_t)blockIdx.x * kV24W;
-    for (int i = tid; i < kV24W; i += kTrainThreads) row[i] = s_acc[i];
+    for (int i = tid; i < kV24W; i += kTrainThreads) {
+        T a = T(0);
+#pragma unroll
+        for (int wv = 0; wv < kTrainWaves; ++wv) a += s_red[(size_t)wv * kV24W + i];
+        row[i] = a;
+    }
     GNND_PMARK(pf, 11);
     GNND_PREPORT(pf, "bwd", kTrainThreads, iters);
 }
@@ -730,14 +784,23 @@ int64_t train_cblk(const gnnd_graph* g, int64_t B) {
 int64_t train_rows(const gnnd_graph* g, int64_t B) {
     return train_split(g, B) ? train_cblk(g, B) * g->ncomp : train_blocks(B);
 }
-size_t train_lds(const gnnd_graph* g, int esz, int nl = -1) {   // nl >= 0: fused loss
+// waves: the workgroup's waves (the final per-wave gradient buffer aliases the arrays after
+// the graph tables: [waves][kV24W] values)
+size_t train_lds(const gnnd_graph* g, int esz, int nl = -1, int waves = 0, bool sibs = false) {   // nl >= 0: fused loss
     const GraphView& v = g->view;
-    size_t n = (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15) +
-               (size_t)esz * (8 * (((size_t)v.E + 3) & ~(size_t)3) + kV24W);
+    const size_t tab = ((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15;
+    size_t n = tab + (size_t)esz * 8 * (((size_t)v.E + 3) & ~(size_t)3);
     if (nl >= 0)
         n += (size_t)esz * (3 * (size_t)v.V + 2 * ((size_t)v.C + nl)) +
              4 * ((size_t)v.V + nl + (size_t)nl * v.V);
-    return n;
+    if (sibs) n = ((n + 15) & ~(size_t)15) + 32 * (size_t)v.E;
+    const size_t red = tab + (size_t)esz * waves * kV24W;
+    return n > red ? n : red;
+}
+// the sibling tables of the leave-one-out phases: checks and variables of degree <= 4, and room
+bool train_sibs(const gnnd_graph* g, int esz, int nl, int waves) {
+    const GraphView& v = g->view;
+    return v.max_dc <= 4 && v.max_dv <= 4 && train_lds(g, esz, nl, waves, true) <= 160 * 1024;
 }
 
 // gw == nullptr: leave the per-workgroup partial rows in ws (gnnd_train_bwd_partial);
@@ -751,14 +814,16 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     const int64_t cblk = train_cblk(g, B), blocks = train_rows(g, B);
     if ((int64_t)blocks * kV24W * (int64_t)sizeof(T) > ws_bytes) return GNND_ERR_INVALID_ARG;
     lossp.ncomp = split ? g->ncomp : 1;
-    const size_t lds = train_lds(gk, sizeof(T), lossp.y ? lossp.nl : -1);
-    if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     // fp32: 16 waves (128 VGPRs) by default, GNND_TRAIN_THREADS=512 for 8 waves (A/B)
     const int shape = sizeof(T) == 4 ? train_threads_f32(blocks) : 0;
     // (5122: two 8-wave workgroups per CU = 4 waves per SIMD, 128 VGPRs; 2564: four 4-wave ones)
     auto kern = shape == 512 ? v24_bwd_kernel<T, 512> : shape == 5122 ? v24_bwd_kernel<T, 512, 4>
               : shape == 2564 ? v24_bwd_kernel<T, 256, 4> : v24_bwd_kernel<T>;
     const int nthreads = shape == 512 || shape == 5122 ? 512 : shape == 2564 ? 256 : train_threads<T>();
+    const int nlf = lossp.y ? lossp.nl : -1;
+    const bool sibs = train_sibs(gk, sizeof(T), nlf, nthreads / 64);
+    const size_t lds = train_lds(gk, sizeof(T), nlf, nthreads / 64, sibs);
+    if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     if (lds > 64 * 1024)
         GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -767,7 +832,7 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     TapeView<T> tv{base, base + n, base + 2 * n, base + 3 * n};
     kern<<<(unsigned)blocks, nthreads, lds, st>>>(
         gk->view, (const T*)w, (const T*)x, (const T*)out, (const T*)gout, tv, (T*)ws, B, iters,
-        split ? g->dcomp : nullptr, (int)cblk, lossp);   // dcomp[0..K): the components' `view`
+        split ? g->dcomp : nullptr, (int)cblk, lossp, sibs ? 1 : 0);   // dcomp[0..K): the components' `view`
     GNND_LAUNCH_CHECK();
     if (!gw) return GNND_OK;
     grad_reduce_kernel<T><<<(kV24W + 255) / 256, 256, 0, st>>>((const T*)ws, (int)blocks, (T*)gw);
