@@ -86,6 +86,11 @@ def parse():
                         '(gnndecode/weights/<model>_<code>.npz), else random init')
     p.add_argument('--no-graph', action='store_true',
                    help='train mode: eager steps instead of one captured HIP graph per step')
+    p.add_argument('--launch', default='auto', choices=['auto', 'graph', 'eager'],
+                   help='train mode: auto = eager stream launches for the fused trainers (three '
+                        'kernels per step; a HIP graph replay leaves ~9 us idle between steps on '
+                        'ROCm 7.2, eager launches none: profiles/r03/experiments/'
+                        'train_graph_vs_eager_r03ac.txt), a captured graph for the torch Trainer'),
     p.add_argument('--layerwise', action='store_true',
                    help='train mode: the layer-by-layer operator path instead of the fused '
                         'decoder_v2_4 training kernels')
@@ -437,17 +442,26 @@ def train_run(a, world, rank, dev, cpu='full'):
     parity = None
     if cpu == 'parity' and rank == 0 and model_name == 'v24':
         parity = train_parity(H, model, lf, T, dev, dtype, a.seed)
+    launch = getattr(a, 'launch', 'auto')
+    if a.no_graph:
+        launch = 'eager'
+    fused_v24 = fused and model_name not in ('nbp', 'v22', 'v30') and not a.torch_trainer
+    if launch == 'auto':
+        # the fused V24 step is three kernels: eager stream launches leave no idle time between
+        # steps, graph replays ~9 us (r03ac); the torch Trainer (~80 launches) keeps its graph
+        launch = 'eager' if fused_v24 else 'graph'
+    use_graph = launch == 'graph'
     if fused and model_name in ('nbp', 'v22'):
         # packed per-edge weights -> fwd+tape -> syndrome loss -> reverse pass -> Adam (fp64)
-        tr = gd.train.FusedWbpTrainer(model, lf, graph=not a.no_graph, warmup=2)
+        tr = gd.train.FusedWbpTrainer(model, lf, graph=use_graph, warmup=2)
     elif fused and model_name == 'v30':
         # fwd+tape -> reference LossFunc (torch) -> reverse pass -> [all_reduce] -> Adam
-        tr = gd.train.FusedV30Trainer(model, lf, graph=not a.no_graph, warmup=2)
-    elif fused and not a.torch_trainer:
-        # prepare -> fwd+tape -> syndrome loss -> reverse pass -> [all_reduce] -> Adam, one HIP graph
-        tr = gd.train.FusedV24Trainer(model, lf, graph=not a.no_graph, warmup=2)
+        tr = gd.train.FusedV30Trainer(model, lf, graph=use_graph, warmup=2)
+    elif fused_v24:
+        # fwd+tape (+ fused syndrome loss) -> reverse pass -> [all_reduce] -> fused epilogue
+        tr = gd.train.FusedV24Trainer(model, lf, graph=use_graph, warmup=2)
     else:
-        tr = gd.train.Trainer(model, lf, graph=not a.no_graph, warmup=2)   # captured after 2 eager steps
+        tr = gd.train.Trainer(model, lf, graph=use_graph, warmup=2)   # captured after 2 eager steps
     x, y = gd.data.toric_batch(H, a.batch, seed=a.seed, offset=rank * a.batch, device=dev,
                                dtype=dtype)
     data = gd.data.make_batch(x, model.graph(dev))
@@ -467,6 +481,9 @@ def train_run(a, world, rank, dev, cpu='full'):
     for _ in range(a.steps):
         # the loss stays in the step's static buffer (read after the timed region), no copy
         loss = tr.step(data, y, copy_loss=False) if fused_tr else tr.step(data, y)
+    # host time to issue the K steps (before the final synchronize): close to the wall time
+    # per step means the step is host-bound (the GPU waits between steps)
+    issue_s = time.perf_counter() - t0
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
@@ -504,12 +521,13 @@ def train_run(a, world, rank, dev, cpu='full'):
             'metric': f'training samples/sec (whole node), {model_name} step with RCCL grad all-reduce',
             'value': world * a.batch * a.steps / elapsed, 'unit': 'samples/s', 'n_gpus': world,
             'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3,
+            'host_issue_ms_per_step': issue_s / a.steps * 1e3,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': a.dtype,
             'data': 'synthetic toric errors (on-device sampler, seeded); seeded reference init',
             'config': {'workload': f'{code} {model_name} training step, T={T}, batch={a.batch}/GPU',
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
                        'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters()),
-                       'hip_graph': not a.no_graph,
+                       'hip_graph': use_graph,
                        'path': ('FusedV30Trainer: gnnd_train_fwd/bwd (V30) + V30Loss + gnnd_train_update'
                                 if fused and model_name == 'v30' else
                                 'FusedWbpTrainer: gnnd_train_fwd/bwd (weighted BP) + gnnd_syndrome_loss'

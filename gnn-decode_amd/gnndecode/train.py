@@ -125,7 +125,9 @@ class _GraphedStep:
 
     def _run(self, x, y, copy_loss=True):
         if not self.use_graph:
-            return self._eager(x, y).detach().clone()
+            # (copy_loss=False: the step's loss buffer itself, as for the captured step)
+            out = self._eager(x, y).detach()
+            return out.clone() if copy_loss else out
         if self._g_compute is None:
             if self._eager_steps < self.warmup:
                 s = torch.cuda.Stream()
