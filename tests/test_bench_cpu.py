@@ -64,3 +64,14 @@ def test_issue_model_is_a_lower_bound_on_committed_counts():
     m = bench.issue_model(cls, 65536, 0.469e-3)
     assert 0.5 < m['issue_frac'] <= 1.0, m
     assert bench.TRANS_OPS_PER_S > 0
+
+
+def test_launch_mode_option(monkeypatch):
+    """--launch: auto by default (eager stream launches for the fused trainers, a captured graph
+    for the torch Trainer); --no-graph still forces eager."""
+    import sys
+    monkeypatch.setattr(sys, 'argv', ['bench.py'])
+    a = bench.parse()
+    assert a.launch == 'auto' and not a.no_graph
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--mode', 'train', '--launch', 'graph'])
+    assert bench.parse().launch == 'graph'
