@@ -769,7 +769,50 @@ template <typename T> struct TapeView {
     T* u;     // [iters][B][E]
     T* t;     // [iters][B][E]
     T* mT;    // [B][E]
+    // optional (y non-null): decoder_v2_4's syndrome loss computed in the forward's epilogue
+    // (gnnd_train_fwd_loss: unit-split small batches) -> d loss / d out and the per-codeword
+    // (and component) losses, the same terms and summation orders as the reverse pass's
+    // fused loss (gnnd_train.hip BwdLoss)
+    const T* y;               // [B*V] labels
+    const uint32_t* lmask;    // [V] logical-row bit masks (whole graph's variables)
+    int nl, logical_only, ncomp;
+    T* gp;                    // [B*V] d loss / d out
+    T* loss_b;                // [B * ncomp]
 };
+// wave all-reduce through the row/bank DPP butterfly and lane 63 (the reverse pass's wave_sum:
+// the forward's loss sums use the same operations so the losses are the same bits)
+__device__ __forceinline__ float fwd_wave_sum(float v) {
+    auto mv = [](float x, auto ctl) {
+        constexpr int C = decltype(ctl)::value;
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), C & 0xfff,
+                                                          (C >> 12) & 0xf, 0xf, false));
+    };
+    v += mv(v, std::integral_constant<int, 0xB1 | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x4E | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x141 | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x140 | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x142 | (0xa << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x143 | (0xc << 12)>{});
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ double fwd_wave_sum(double v) {
+    auto mv = [](double x, auto ctl) {
+        constexpr int C = decltype(ctl)::value;
+        const long long b = __double_as_longlong(x);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)b, C & 0xfff, (C >> 12) & 0xf, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), C & 0xfff, (C >> 12) & 0xf, 0xf, false);
+        return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+    };
+    v += mv(v, std::integral_constant<int, 0xB1 | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x4E | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x141 | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x140 | (0xf << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x142 | (0xa << 12)>{});
+    v += mv(v, std::integral_constant<int, 0x143 | (0xc << 12)>{});
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
 // US (unit split, fp32 decoder_v2_4 small batches): US waves share each wave of work items,
 // each evaluating a quarter / half of every 128-hidden MLP's units (mlp128_split), so a
@@ -787,12 +830,13 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     extern __shared__ __attribute__((aligned(16))) char smem[];
     GNND_PPROF(pf);
     GNND_PSTART(pf, blockIdx.x == 0 && threadIdx.x < 64);
-    int blk = blockIdx.x;
+    int blk = blockIdx.x, comp = 0;
     GraphView g = g0;
     if (views) {                       // uniform: component k of the split graph
         const int k = blk / cblk;
         g = views[k];
         blk -= k * cblk;
+        comp = k;
     }
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
@@ -889,6 +933,19 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int IC = C * G;               // work items (lanes) per codeword
     const int nItem = nb * IC;          // a multiple of G: groups never straddle the end
     const int nV = nb * V;
+    // the syndrome loss in the epilogue (gnnd_train_fwd_loss): labels and logical masks of the
+    // first element per thread are loaded now, their latency hidden behind the iterations
+    constexpr bool kFLoss = kV24F32 && TAPE && US > 1;
+    const bool floss = kFLoss && tape.y != nullptr;
+    T ypre = T(0);
+    uint32_t lmpre = 0u;
+    if (floss) {
+        if (tid < nV) {
+            const int b = fdiv(tid, dV), v = tid - b * V;
+            ypre = tape.y[(size_t)(b0 + b) * g.os + g.o0 + v];
+        }
+        if (tid < V && tape.nl > 0) lmpre = tape.lmask[g.o0 + tid];
+    }
     // unit-split small batches (one round of items): each lane's slots are fixed for the whole
     // decode, so it gathers its variables' messages itself (indices and x_v kept in registers,
     // summed in var_ptr order = var_sum's order: the same S_v bits) and the variable-sum step
@@ -1142,7 +1199,66 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             out[orow] = sigmoid_ref(-(s1 + s2));
         } else {
             const T s = var_sum(s_m + b * nslot, s_vslot, s_vptr[v], s_vptr[v + 1]);
-            out[orow] = M::readout(s + s_sx[f].x, s_w);
+            const T pr = M::readout(s + s_sx[f].x, s_w);
+            out[orow] = pr;
+            // (the unit split's partial-sum buffers are free after the readout MLP's barrier)
+            if constexpr (kFLoss)
+                if (floss) ((T*)s_part)[f] = (f < NT ? ypre : tape.y[orow]) + pr;
+        }
+    }
+    if constexpr (kFLoss) {
+        if (floss) {
+            // quantum/decoder_v2_4.py:297-317 on this tile (one component of each codeword when
+            // split): s = y + p; check rows (slot order = cedge order) and logical rows
+            // (variables ascending) -> |sin| terms and d|sin(pi/2 s_r)| / d s_r; d loss / d p_v
+            // over v's edges in var_ptr order, then its logical rows — the reverse pass's fused
+            // loss (gnnd_train.hip) term by term, so d out and the losses are the same bits
+            const int nr = C + tape.nl, GR = G * R;
+            T* s_ls = (T*)s_part;                          // [nb][V] y + p
+            T* s_lg = s_ls + (size_t)nb * V;               // [nb][nr] row gradients
+            T* s_lt = s_lg + (size_t)nb * nr;              // [nb][nr] row terms
+            uint32_t* s_lm = (uint32_t*)(s_lt + (size_t)nb * nr);   // [V]
+            for (int v = tid; v < V; v += NT)
+                s_lm[v] = v < NT ? lmpre : (tape.nl > 0 ? tape.lmask[g.o0 + v] : 0u);
+            __syncthreads();
+            const T kPi = T(M_PI);
+            for (int i = tid; i < nb * nr; i += NT) {
+                const int b = i / nr, r = i - b * nr;
+                T sr = T(0);
+                if (r < C) {
+                    for (int j = 0; j < GR; ++j) {
+                        const uint32_t sv = s_slot[r * GR + j];
+                        if ((int)(sv >> 16) != E) sr += s_ls[b * V + (int)(sv & 0xffffu)];
+                    }
+                } else {
+                    const int l = r - C;
+                    for (int v = 0; v < V; ++v)
+                        if ((s_lm[v] >> l) & 1u) sr += s_ls[b * V + v];
+                }
+                const T xr = sr * kPi / T(2);
+                const T sn = sin(xr);
+                const T gr = (sn > T(0) ? T(1) : sn < T(0) ? T(-1) : T(0)) * cos(xr) * (kPi / T(2));
+                const bool on = r >= C || !tape.logical_only;
+                s_lg[i] = on ? gr : T(0);
+                s_lt[i] = on ? (sn < T(0) ? -sn : sn) : T(0);
+            }
+            __syncthreads();
+            for (int f = tid; f < nV; f += NT) {
+                const int b = fdiv(f, dV), v = f - b * V;
+                T d = T(0);
+                for (int k = s_vptr[v]; k < s_vptr[v + 1]; ++k) d += s_lg[b * nr + s_vslot[k] / GR];
+                const uint32_t m = s_lm[v];
+                for (int l = 0; l < tape.nl; ++l)
+                    if ((m >> l) & 1u) d += s_lg[b * nr + C + l];
+                tape.gp[(size_t)(b0 + b) * g.os + g.o0 + v] = d;
+            }
+            const int wv = tid >> 6, lane = tid & 63;
+            for (int b = wv; b < nb; b += NT / 64) {     // the codeword's loss, fixed order
+                T t = T(0);
+                for (int r = lane; r < nr; r += 64) t += s_lt[b * nr + r];
+                t = fwd_wave_sum(t);
+                if (lane == 0) tape.loss_b[(size_t)(b0 + b) * tape.ncomp + comp] = t;
+            }
         }
     }
     GNND_PMARK(pf, 10);
@@ -2127,9 +2243,21 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
 }
 
 
+// floss (gnnd_train_fwd_loss): the syndrome loss in the forward's epilogue; only fp32 V24
+// unit-split plans (small batches) whose component split matches the reverse pass's
+// (need_ncomp: the reverse pass's components per codeword) and whose partial-sum buffers
+// hold the loss arrays; UNSUPPORTED otherwise (the caller keeps the reverse pass's loss)
+struct FwdLoss {
+    const void* y;
+    const uint32_t* lmask;
+    int nl, logical_only, need_ncomp;
+    void* gp;
+    void* loss_b;
+};
 template <int MODEL, typename T, typename TI = T>
 int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out, int64_t B,
-                    int iters, hipStream_t st, void* tape_base = nullptr) {
+                    int iters, hipStream_t st, void* tape_base = nullptr,
+                    const FwdLoss* floss = nullptr) {
     Plan p;
     int rc = plan_for(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p, B);
     if (rc != GNND_OK) return rc;
@@ -2139,6 +2267,22 @@ int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out
         const size_t n = (size_t)iters * B * g->view.E;
         T* base = (T*)tape_base;
         tape = TapeView<T>{base, base + n, base + 2 * n, base + 3 * n};
+    }
+    if (floss) {
+        if (MODEL != GNND_V24 || sizeof(T) != 4 || !tape_base || p.us < 2 ||
+            p.ncomp != floss->need_ncomp)
+            return GNND_ERR_UNSUPPORTED;
+        const GraphView& v = *p.view;
+        const int il = p.us == 8 ? 128 : GNND_BLOCK;
+        const size_t need = sizeof(T) * (size_t)p.cw * (v.V + 2 * (size_t)(v.C + floss->nl)) + 4 * (size_t)v.V;
+        if (need > (size_t)2 * p.us * il * 8) return GNND_ERR_UNSUPPORTED;
+        tape.y = (const T*)floss->y;
+        tape.lmask = floss->lmask;
+        tape.nl = floss->nl;
+        tape.logical_only = floss->logical_only;
+        tape.ncomp = p.ncomp;
+        tape.gp = (T*)floss->gp;
+        tape.loss_b = (T*)floss->loss_b;
     }
     switch (p.view->R) {
         case 1: return launch_decode<MODEL, T, 1, TI>(p, w, x, out, B, iters, st, tape);
@@ -2168,6 +2312,11 @@ int gnnd_launch_v24(const gnnd_graph*, int, const void*, const void*, void*, int
 // forward with the training tape (gnnd_train.hip)
 int gnnd_launch_v24_tape(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int,
                          void*, hipStream_t);
+// ... with decoder_v2_4's syndrome loss in the epilogue (y, logical masks, n_logical,
+// logical_only, the reverse pass's components per codeword) -> d loss / d out, losses
+int gnnd_launch_v24_tape_loss(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int,
+                              void*, const void*, const uint32_t*, int, int, int, void*, void*,
+                              hipStream_t);
 int gnnd_launch_qgnni(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_qbp(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
 int gnnd_launch_cgnni(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);

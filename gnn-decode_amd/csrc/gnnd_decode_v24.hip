@@ -13,3 +13,12 @@ int gnnd_launch_v24_tape(const gnnd_graph* g, int dtype, const void* w, const vo
     if (dtype == GNND_F32) return launch_decode_r<GNND_V24, float>(g, w, x, out, B, iters, st, tape);
     return launch_decode_r<GNND_V24, double>(g, w, x, out, B, iters, st, tape);
 }
+
+int gnnd_launch_v24_tape_loss(const gnnd_graph* g, int dtype, const void* w, const void* x, void* out,
+                              int64_t B, int iters, void* tape, const void* y, const uint32_t* lmask,
+                              int nl, int logical_only, int need_ncomp, void* gp, void* loss_b,
+                              hipStream_t st) {
+    if (dtype != GNND_F32) return GNND_ERR_UNSUPPORTED;
+    const FwdLoss fl{y, lmask, nl, logical_only, need_ncomp, gp, loss_b};
+    return launch_decode_r<GNND_V24, float>(g, w, x, out, B, iters, st, tape, &fl);
+}

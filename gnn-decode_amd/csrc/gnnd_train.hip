@@ -1246,6 +1246,24 @@ extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const v
                                 (hipStream_t)stream);
 }
 
+extern "C" int gnnd_train_fwd_loss(const gnnd_graph* g, int model, int dtype, const void* d_w,
+                                   const void* d_x, void* d_out, void* d_tape, const void* d_y,
+                                   const uint32_t* d_logical_mask, int32_t n_logical,
+                                   int32_t logical_only, void* d_grad_out, void* d_loss_b,
+                                   int64_t batch, int32_t iters, void* stream) {
+    if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
+    if (model != GNND_V24 || dtype != GNND_F32) return GNND_ERR_UNSUPPORTED;
+    if (n_logical < 0 || n_logical > 32 || (n_logical > 0 && !d_logical_mask)) return GNND_ERR_INVALID_ARG;
+    if (batch == 0) return GNND_OK;
+    if (!d_w || !d_x || !d_out || !d_tape || !d_y || !d_grad_out || !d_loss_b) return GNND_ERR_INVALID_ARG;
+    // the losses' layout is the reverse pass's (gnnd_train_loss_count): the forward must split
+    // a codeword into the same components
+    const int need = train_split(g, batch) ? g->ncomp : 1;
+    return gnnd_launch_v24_tape_loss(g, dtype, d_w, d_x, d_out, batch, iters, d_tape, d_y,
+                                     d_logical_mask, n_logical, logical_only, need, d_grad_out,
+                                     d_loss_b, (hipStream_t)stream);
+}
+
 extern "C" int gnnd_train_workspace_bytes(const gnnd_graph* g, int model, int dtype,
                                           int64_t batch, int32_t iters, int64_t* h_bytes) {
     if (!train_args_ok(g, model, dtype, batch, iters) || !h_bytes) return GNND_ERR_INVALID_ARG;

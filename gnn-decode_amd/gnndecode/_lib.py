@@ -62,6 +62,8 @@ SIGNATURES = {
     'gnnd_train_loss_count': (_int, [_vp, _i64, _c_i64p]),
     'gnnd_train_bwd_loss_partial': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
                                            _vp, _vp, _vp, _i64, _i64, _i32, _vp]),
+    'gnnd_train_fwd_loss': (_int, [_vp, _int, _int, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32,
+                                   _vp, _vp, _i64, _i32, _vp]),
     'gnnd_train_update': (_int, [_int, _int, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
                                  _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                  ctypes.c_double, ctypes.c_double, _vp, _vp]),
@@ -122,6 +124,15 @@ def check(fn_name, status):
 
 def call(fn_name, *args):
     check(fn_name, getattr(get(), fn_name)(*args))
+
+
+def call_or_unsupported(fn_name, *args):
+    """call(), except that GNND_ERR_UNSUPPORTED (nothing launched) returns False."""
+    status = getattr(get(), fn_name)(*args)
+    if status == ERR_UNSUPPORTED:
+        return False
+    check(fn_name, status)
+    return True
 
 
 def exported_symbols():

@@ -270,6 +270,33 @@ def train_forward(graph, model, x, prepared_weights, iters):
     return out, tape
 
 
+def train_forward_loss(graph, model, x, prepared_weights, iters, y, logical_mask, n_logical,
+                       logical_only):
+    """gnnd_train_fwd_loss: train_forward plus decoder_v2_4's syndrome loss in the forward's
+    epilogue.  Returns (out, tape, d loss / d out, per-codeword-and-component losses), or None
+    when the plan does not take it (fp32 V24 unit-split small batches only): then
+    train_backward_loss_partial computes the same loss in the reverse pass."""
+    _require_gpu(x, prepared_weights)
+    x = x.contiguous()
+    B = x.numel() // graph.N
+    dt = dtype_code(x.dtype)
+    nb = ctypes.c_int64()
+    _lib.call('gnnd_train_tape_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
+              ctypes.byref(nb))
+    nl = ctypes.c_int64()
+    _lib.call('gnnd_train_loss_count', graph.handle, B, ctypes.byref(nl))
+    tape = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
+    out = torch.empty(B * graph.V, 1, dtype=x.dtype, device=x.device)
+    gout = torch.empty_like(out)
+    loss_b = torch.empty(max(nl.value, 1), dtype=x.dtype, device=x.device)[:nl.value]
+    y = y.to(x.dtype).contiguous()
+    ok = _lib.call_or_unsupported(
+        'gnnd_train_fwd_loss', graph.handle, _lib.VARIANT[model], dt, _ptr(prepared_weights),
+        _ptr(x), _ptr(out), _ptr(tape), _ptr(y), _ptr(logical_mask), int(n_logical),
+        int(bool(logical_only)), _ptr(gout), _ptr(loss_b), B, int(iters), current_stream(x.device))
+    return (out, tape, gout, loss_b) if ok else None
+
+
 def train_backward(graph, model, plain_weights, x, out, grad_out, tape, iters):
     """gnnd_train_bwd: d loss / d (plain packed weights) from d loss / d out."""
     B = x.numel() // graph.N

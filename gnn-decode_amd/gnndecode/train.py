@@ -17,6 +17,8 @@ eagerly on the same stream between the two replays.  Single-rank runs keep one g
 
 Optimizer settings per model follow the reference scripts (`REFERENCE_OPTIM`).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -244,7 +246,9 @@ class FusedV24Trainer(_GraphedStep):
         forward with tape (gnnd_train_fwd) -> syndrome loss and d loss / d out
         (gnnd_syndrome_loss) -> reverse pass to per-workgroup gradient rows
         (gnnd_train_bwd_partial; with the syndrome loss of a SyndromeLoss computed inside
-        it, gnnd_train_bwd_loss_partial, the loss launch goes too) -> fused epilogue
+        it, gnnd_train_bwd_loss_partial, the loss launch goes too; loss_in_forward=True computes
+        it in the unit-split forward's epilogue instead, gnnd_train_fwd_loss, the same bits,
+        measured slower) -> fused epilogue
         (gnnd_train_update: fixed-order row
         reduction, the batch loss, Adam, and the kernel-layout weights the next forward reads)
 
@@ -261,7 +265,8 @@ class FusedV24Trainer(_GraphedStep):
     `Trainer` (torch.optim.Adam's order; lr 3e-4, weight decay 1e-9 of the reference)."""
 
     def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
-                 group=None, graph=True, warmup=2, force_collective=False, fuse_loss=True):
+                 group=None, graph=True, warmup=2, force_collective=False, fuse_loss=True,
+                 loss_in_forward=None):
         from .models import DecoderV24
         if not isinstance(model, DecoderV24):
             raise TypeError('FusedV24Trainer trains decoder_v2_4 (DecoderV24) models')
@@ -271,6 +276,11 @@ class FusedV24Trainer(_GraphedStep):
         self.wd = rwd if weight_decay is None else weight_decay
         self.betas, self.eps = betas, eps
         self.fuse_loss, self._fuse_ok = fuse_loss, {}
+        # default off: measured 2-4 % slower than the reverse pass's own loss at B = 16 / 128
+        # (profiles/r03/experiments/train_loss_in_forward_ab_r03ae.txt); GNND_LOSS_IN_FORWARD=1
+        # turns it on for A/B runs
+        self.loss_in_forward = (os.environ.get('GNND_LOSS_IN_FORWARD', '0') == '1'
+                                if loss_in_forward is None else loss_in_forward)
         self._init_graph(graph, warmup, group, force_collective)
         flat = model.packed_weights().detach().clone().contiguous()
         off = 0
@@ -333,14 +343,24 @@ class FusedV24Trainer(_GraphedStep):
             self._gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
             self._pending = None
             return loss_b.sum(), [self._gw]
-        out, tape = ops.train_forward(g, m.kind, x, self.prepared, m.Nc)
         lmask = self._fused_loss_mask(g, x.device)
-        if lmask is not None:
+        fl = None
+        if lmask is not None and self.loss_in_forward:
+            # small batches (unit-split forward): the syndrome loss in the forward's epilogue,
+            # the reverse pass reads d loss / d out (same bits as the reverse pass's own loss)
+            fl = ops.train_forward_loss(g, m.kind, x, self.prepared, m.Nc, y, lmask,
+                                        lf.logical_rows.size(0), lf.logical_only)
+        if fl is not None:
+            out, tape, dpred, loss_b = fl
+            ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
+        elif lmask is not None:
+            out, tape = ops.train_forward(g, m.kind, x, self.prepared, m.Nc)
             # the syndrome loss computed inside the reverse pass (no loss launch)
             ws, nrows, loss_b = ops.train_backward_loss_partial(
                 g, m.kind, self.flat, x, out, y, lmask, lf.logical_rows.size(0), lf.logical_only,
                 tape, m.Nc)
         else:
+            out, tape = ops.train_forward(g, m.kind, x, self.prepared, m.Nc)
             loss_b, dpred = lf.per_codeword(out, y)
             ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
         if self._dist():

@@ -259,6 +259,16 @@ int gnnd_train_bwd_loss_partial(const gnnd_graph* g, int model, int dtype, const
                                 int32_t logical_only, const void* d_tape, void* d_loss_b,
                                 void* d_workspace, int64_t workspace_bytes, int64_t batch,
                                 int32_t iters, void* stream);
+/* The same syndrome loss computed in the FORWARD's epilogue instead: gnnd_train_fwd plus
+ * d_grad_out [B*V] = d loss / d out and d_loss_b as above (the same terms and summation
+ * orders, so the same bits), for gnnd_train_bwd_partial(d_grad_out) to consume.  fp32 V24
+ * on its unit-split small-batch plan only (the 16-wave reverse pass then skips its loss
+ * phases); returns GNND_ERR_UNSUPPORTED (nothing launched) otherwise.                       */
+int gnnd_train_fwd_loss(const gnnd_graph* g, int model, int dtype, const void* d_w,
+                        const void* d_x, void* d_out, void* d_tape, const void* d_y,
+                        const uint32_t* d_logical_mask, int32_t n_logical, int32_t logical_only,
+                        void* d_grad_out, void* d_loss_b, int64_t batch, int32_t iters,
+                        void* stream);
 /* Fused optimizer epilogue of a decoder_v2_4 training step (one launch):
  *   n_rows > 0: d_grad[i] = fixed-order sum of the rows (d_grad may be NULL: not stored);
  *   n_rows = 0: the gradient is read from d_grad (e.g. after an all-reduce of it);

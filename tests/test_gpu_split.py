@@ -227,3 +227,72 @@ def test_syndrome_loss_large_code_uses_big_lds_or_falls_back():
         torch.testing.assert_close(p1.grad, p2.grad, rtol=1e-10, atol=1e-12)
         lb, dp = lf.per_codeword(pred, y)
         assert abs(lb.sum().item() - l2.item()) <= 1e-10 * abs(l2.item())
+
+
+@pytest.mark.parametrize('logical_only', [False, True])
+@pytest.mark.parametrize('L,B', [(7, 16), (7, 128), (5, 100)])
+def test_forward_loss_equals_reverse_pass_loss(logical_only, L, B):
+    """gnnd_train_fwd_loss (the syndrome loss in the unit-split forward's epilogue, fp32 small
+    batches) gives the SAME BITS as the reverse pass's fused loss: outputs, per-codeword-and-
+    component losses and the gradient rows of gnnd_train_bwd_partial on its d loss / d out."""
+    import gnndecode as gd
+    H = _toric(L)
+    torch.manual_seed(L + B)
+    T = 6
+    m = gd.MODELS['v24'](T, H).to(DEV).float()
+    g = m.graph(DEV)
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H), logical_only=logical_only).to(DEV)
+    x, y = gd.data.toric_batch(H, B, seed=B, device=DEV, dtype=torch.float32)
+    flat = m.packed_weights().detach().contiguous()
+    prep = gd.ops.prepare_weights('v24', flat)
+    lm, nl = lf.logical_mask(x.device), lf.logical_rows.size(0)
+    r = gd.ops.train_forward_loss(g, 'v24', x, prep, T, y, lm, nl, logical_only)
+    assert r is not None                       # small batch: the unit-split plan takes it
+    out1, tape1, dpred, lb1 = r
+    ws1, n1 = gd.ops.train_backward_partial(g, 'v24', flat, x, out1, dpred, tape1, T)
+    out2, tape2 = gd.ops.train_forward(g, 'v24', x, prep, T)
+    ws2, n2, lb2 = gd.ops.train_backward_loss_partial(g, 'v24', flat, x, out2, y, lm, nl,
+                                                      logical_only, tape2, T)
+    assert torch.equal(out1, out2) and torch.equal(tape1, tape2)
+    assert torch.equal(lb1, lb2)
+    assert n1 == n2
+    nbytes = n1 * flat.numel() * flat.element_size()
+    assert torch.equal(ws1[:nbytes], ws2[:nbytes])
+
+
+def test_forward_loss_declines_large_batches_and_fp64():
+    """Outside the unit-split fp32 plans gnnd_train_fwd_loss launches nothing (None), and the
+    fused trainer keeps the reverse pass's loss (its steps equal loss_in_forward=False)."""
+    import gnndecode as gd
+    H = _toric(5)
+    m = gd.MODELS['v24'](4, H).to(DEV).float()
+    g = m.graph(DEV)
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+    lm, nl = lf.logical_mask(DEV), lf.logical_rows.size(0)
+    x, y = gd.data.toric_batch(H, 4096, seed=3, device=DEV, dtype=torch.float32)
+    prep = gd.ops.prepare_weights('v24', m.packed_weights().detach().contiguous())
+    assert gd.ops.train_forward_loss(g, 'v24', x, prep, 4, y, lm, nl, False) is None
+    m64 = gd.MODELS['v24'](4, H).to(DEV).double()
+    x64, y64 = gd.data.toric_batch(H, 16, seed=3, device=DEV, dtype=torch.float64)
+    p64 = gd.ops.prepare_weights('v24', m64.packed_weights().detach().contiguous())
+    assert gd.ops.train_forward_loss(m64.graph(DEV), 'v24', x64, p64, 4, y64, lm, nl, False) is None
+
+
+def test_fused_trainer_loss_in_forward_steps_equal():
+    import gnndecode as gd
+    H = _toric(7)
+    lg = gd.codes.toric_logicals(H)
+    torch.manual_seed(5)
+    a = gd.MODELS['v24'](4, H).to(DEV).float()
+    b = gd.MODELS['v24'](4, H).to(DEV).float()
+    b.load_state_dict(a.state_dict())
+    ta = gd.train.FusedV24Trainer(a, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=False,
+                                  loss_in_forward=True)
+    tb = gd.train.FusedV24Trainer(b, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=False,
+                                  loss_in_forward=False)
+    for s in range(3):
+        x, y = gd.data.toric_batch(H, 128, seed=30 + s, device=DEV, dtype=torch.float32)
+        data = gd.data.make_batch(x, a.graph(DEV))
+        la, lb = ta.step(data, y), tb.step(data, y)
+        assert torch.equal(la, lb), s
+    assert torch.equal(ta.flat, tb.flat)
