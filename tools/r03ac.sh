@@ -13,7 +13,7 @@ for mode in graph eager; do
   extra=""; [ $mode = eager ] && extra="--no-graph"
   for b in 16 128 1024; do
     timeout -k 10 200 python bench.py --mode train --batch $b --steps 40 --warmup 3 --cpu-seconds 0 $extra > $OUT/b.log 2>&1 || { tail $OUT/b.log; exit 1; }
-    grep '^{' $OUT/b.log | tail -1 | python -c "import json,sys; j=json.loads(sys.stdin.read()); print('$mode train', $b, round(j['ms_per_step'],4))" >> $OUT/ab.txt
+    grep '^{' $OUT/b.log | tail -1 | python -c "import json,sys; j=json.loads(sys.stdin.read()); print('$mode train', $b, round(j['ms_per_step'],4), 'host', round(j.get('host_issue_ms_per_step',0),4))" >> $OUT/ab.txt
   done
 done
 done
