@@ -416,18 +416,82 @@ def sample_main(a, world, rank, dev):
             'cpu_baseline': None}), flush=True)
 
 
+_ONE_RANK_GROUP = []
+
+
+def one_rank_group(dev):
+    """A 1-rank RCCL process group for the collective-inclusive training timing of a plain
+    (non-torchrun) 1-GPU run; created once, destroyed at the end of main()."""
+    if dist.is_initialized():
+        return True
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group('nccl', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1,
+                            device_id=dev)
+    _ONE_RANK_GROUP.append(True)
+    return True
+
+
+def v24_start_weights(model, code):
+    """decoder_v2_4 training starts from the reference's checkpoint, as the script does
+    (quantum/decoder_v2_4.py:322 loads decoder_parameters_epoch1.pkl before its Adam loop).
+    The shipped epoch-67 checkpoint (quantum/new_model/decoder_parameters_epoch67.pkl, converted
+    to weights/v24_toric_5.npz) has L-independent shapes (1 283 parameters), so it loads at any
+    L.  Returns the weight source string."""
+    wfile = os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights', 'v24_toric_5.npz')
+    if not os.path.exists(wfile):
+        return 'random init (seeded): weights/v24_toric_5.npz missing'
+    z = np.load(wfile)                           # plain arrays (allow_pickle off)
+    model.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files})
+    return (f'{os.path.relpath(wfile, ROOT)} (reference epoch-67 checkpoint, trained at L=5, '
+            f'loaded at {code})')
+
+
+def time_train_steps(tr, data, y, steps, fused_tr):
+    """K timed steps bracketed by barrier + synchronize; returns (elapsed max over ranks, host
+    issue seconds, last loss tensor)."""
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        # the loss stays in the step's static buffer (read after the timed region), no copy
+        loss = tr.step(data, y, copy_loss=False) if fused_tr else tr.step(data, y)
+    # host time to issue the K steps (before the final synchronize): close to the wall time
+    # per step means the step is host-bound (the GPU waits between steps)
+    issue_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=y.device)
+    if dist.is_initialized():
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), issue_s, loss
+
+
 def train_run(a, world, rank, dev, cpu='full'):
     """Config 5: decoder_v2_4 training on the toric code (default L=7), each rank a shard of
     size --batch, one flat all_reduce(SUM) of the gradient per step (gnndecode.train).
-    cpu='full': the CPU training baseline; 'parity': the first step's loss against the fp64
-    oracle step on the same batch and weights; 'off'.  Returns the result dict on rank 0."""
+    decoder_v2_4 starts from the reference checkpoint (v24_start_weights).
+    cpu='full' / 'parity': the CPU training baseline (oracle/torch_train.py), and for 'parity'
+    also a K=10-step trajectory of the fused GPU trainer against the oracle's training steps
+    on the same codewords; 'off'.  Returns the result dict on rank 0."""
     code = a.code if a.code.startswith('toric') else 'toric_7'
     model_name = a.model if a.model in ('v24', 'qgnni', 'nbp', 'v10', 'v22', 'v30') else 'v24'
     T = a.iters or gd.DEFAULT_ITERS[model_name]
     dtype = torch.float64 if a.dtype == 'f64' else torch.float32
     H = gd.codes.get_code(code)
     torch.manual_seed(a.seed)
-    model = gd.MODELS[model_name](T, H).to(dev).to(dtype)
+    model = gd.MODELS[model_name](T, H)
+    wsrc = 'seeded reference init'
+    if model_name == 'v24' and a.weights == 'auto':
+        wsrc = v24_start_weights(model, code)
+    model = model.to(dev).to(dtype)
+    init_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
     fused = (model_name in ('v24', 'v30') or
              (model_name in ('nbp', 'v22') and dtype == torch.float64)) and not a.layerwise
     if model_name == 'v24':
@@ -440,8 +504,8 @@ def train_run(a, world, rank, dev, cpu='full'):
         lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
                                   logical_only=(model_name == 'qgnni')).to(dev)
     parity = None
-    if cpu == 'parity' and rank == 0 and model_name == 'v24':
-        parity = train_parity(H, model, lf, T, dev, dtype, a.seed)
+    if cpu == 'parity' and rank == 0 and model_name == 'v24' and fused and not a.torch_trainer:
+        parity = train_trajectory(H, init_state, T, dev, dtype, a.seed)
     launch = getattr(a, 'launch', 'auto')
     if a.no_graph:
         launch = 'eager'
@@ -472,103 +536,137 @@ def train_run(a, world, rank, dev, cpu='full'):
     st = tr.static_inputs()
     if st is not None:
         data.x, y = st
-    torch.cuda.synchronize()
-    if dist.is_initialized():
-        dist.barrier()
-    t0 = time.perf_counter()
     fused_tr = isinstance(tr, (gd.train.FusedV24Trainer, gd.train.FusedV30Trainer,
                                gd.train.FusedWbpTrainer))
-    for _ in range(a.steps):
-        # the loss stays in the step's static buffer (read after the timed region), no copy
-        loss = tr.step(data, y, copy_loss=False) if fused_tr else tr.step(data, y)
-    # host time to issue the K steps (before the final synchronize): close to the wall time
-    # per step means the step is host-bound (the GPU waits between steps)
-    issue_s = time.perf_counter() - t0
-    torch.cuda.synchronize()
-    if dist.is_initialized():
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist.is_initialized():
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed, issue_s, loss = time_train_steps(tr, data, y, a.steps, fused_tr)
+    # the same step with its RCCL all_reduce(SUM) of the flat gradient + loss actually issued:
+    # N > 1 runs already contain it; a 1-GPU run times it on a 1-rank RCCL group
+    # (force_collective), from the same starting weights on the same batch
+    coll = None
+    if fused_v24 and model_name == 'v24':
+        if world > 1:
+            coll = {'ms_per_step': elapsed / a.steps * 1e3, 'note': 'the timed step above (world > 1)'}
+        elif getattr(a, 'collective', True):
+            one_rank_group(dev)
+            m2 = gd.MODELS['v24'](T, H).to(dev).to(dtype)
+            m2.load_state_dict(init_state)
+            tr2 = gd.train.FusedV24Trainer(m2, lf, graph=use_graph, warmup=2, force_collective=True)
+            d2 = gd.data.make_batch(x, m2.graph(dev))
+            for _ in range(a.warmup):
+                tr2.step(d2, y)
+            st2 = tr2.static_inputs()
+            if st2 is not None:
+                d2.x, y2 = st2
+            else:
+                y2 = y
+            el2, iss2, _ = time_train_steps(tr2, d2, y2, a.steps, True)
+            coll = {'ms_per_step': el2 / a.steps * 1e3, 'host_issue_ms_per_step': iss2 / a.steps * 1e3,
+                    'note': 'FusedV24Trainer(force_collective=True) on a 1-rank RCCL group: '
+                            'compute -> gnnd_train_update(rows -> flat gradient, loss) -> ONE '
+                            'all_reduce(SUM) of [gradient | loss] -> gnnd_train_update(Adam)'}
+            del tr2, m2
     if rank == 0:
         step_s = elapsed / a.steps
         roof = None
         if model_name in ('v24', 'v30', 'nbp', 'v22') and fused:
             # training ~ 3x the forward's algorithmic FLOPs: forward, the
             # reverse pass through every MLP (2x); transcendentals: forward Softplus + the
-            # backward sigmoid of every unit.  Whole captured step (prepare, forward+tape,
-            # loss, reverse pass, Adam) over its wall time per step.
+            # backward sigmoid of every unit.  Whole step over its wall time per step.
             g = model.graph(dev)
             fl, trans = flops_per_codeword(model_name, g, T)
             peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
             achieved = 3 * fl * a.batch / step_s / 1e12
             roof = {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
                     'frac': achieved / peak, 'traffic': None,
-                    'kernel': ('FusedV24Trainer step (HIP graph: gnnd_train_fwd, gnnd_syndrome_loss, '
-                               'gnnd_train_bwd, gnnd_adam_step)' if model_name == 'v24' else
-                               'FusedV30Trainer step (HIP graph: gnnd_train_fwd, V30Loss autograd, '
-                               'gnnd_train_bwd_partial, gnnd_train_update)' if model_name == 'v30' else
-                               'FusedWbpTrainer step (HIP graph: packed weights, gnnd_train_fwd, '
-                               'gnnd_syndrome_loss, gnnd_train_bwd, torch Adam)'),
+                    'kernel': train_path_string(tr, model_name, use_graph),
                     'flops_per_sample': 3 * fl, 'transcendentals_per_sample': 2 * trans,
                     'step_ms': step_s * 1e3}
         cpu_res = None
-        if model_name == 'v24' and a.cpu_seconds > 0 and world == 1 and cpu == 'full':
+        if model_name == 'v24' and a.cpu_seconds > 0 and world == 1 and cpu in ('full', 'parity'):
             cpu_res = train_cpu_baseline(H, model, T, x, y, a.batch, a.cpu_seconds)
-        return {
+        res = {
             'metric': f'training samples/sec (whole node), {model_name} step with RCCL grad all-reduce',
             'value': world * a.batch * a.steps / elapsed, 'unit': 'samples/s', 'n_gpus': world,
             'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3,
             'host_issue_ms_per_step': issue_s / a.steps * 1e3,
+            'ms_per_step_with_collective': coll['ms_per_step'] if coll else None,
+            'collective': coll,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': a.dtype,
-            'data': 'synthetic toric errors (on-device sampler, seeded); seeded reference init',
+            'data': f'synthetic toric errors (on-device sampler, seeded); start weights: {wsrc}',
             'config': {'workload': f'{code} {model_name} training step, T={T}, batch={a.batch}/GPU',
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
-                       'last_loss': float(loss), 'params': sum(p.numel() for p in model.parameters()),
+                       'last_loss': float(loss),
+                       'params': sum(p.numel() for p in model.parameters()),
                        'hip_graph': use_graph,
-                       'path': ('FusedV30Trainer: gnnd_train_fwd/bwd (V30) + V30Loss + gnnd_train_update'
-                                if fused and model_name == 'v30' else
-                                'FusedWbpTrainer: gnnd_train_fwd/bwd (weighted BP) + gnnd_syndrome_loss'
-                                if fused and model_name in ('nbp', 'v22') else
-                                'FusedV24Trainer: gnnd_train_fwd/bwd + gnnd_syndrome_loss + gnnd_adam_step'
-                                if fused and not a.torch_trainer else
-                                'fused gnnd_train_fwd/bwd, torch loss/optimizer' if fused
-                                else 'layer-by-layer propagate ops'),
+                       'path': train_path_string(tr, model_name, use_graph),
                        'graph_components': model.graph(dev).components},
             'roofline': roof, 'cpu_baseline': cpu_res, 'parity': parity}
+        return res
     return None
 
 
-def train_parity(H, model, lf, T, dev, dtype, seed, n=64):
-    """Bounded parity sample of the training objective: the fused GPU forward + syndrome loss
-    of the model's initial weights on n seeded codewords, against the reference training step's
-    forward + LossFunc (oracle/torch_train.py V24Step, fp64) on the same codewords."""
+def train_path_string(tr, model_name, use_graph):
+    """What one timed training step launches, from the trainer actually used."""
+    how = 'one captured HIP graph per step' if use_graph else 'eager stream launches'
+    if isinstance(tr, gd.train.FusedV24Trainer):
+        fused_loss = any(tr._fuse_ok.values()) if tr._fuse_ok else False
+        if fused_loss and tr.loss_in_forward:
+            k = 'gnnd_train_fwd_loss (forward + tape + syndrome loss), gnnd_train_bwd_partial'
+        elif fused_loss:
+            k = 'gnnd_train_fwd (forward + tape), gnnd_train_bwd_loss_partial (reverse pass with the syndrome loss)'
+        else:
+            k = 'gnnd_train_fwd, gnnd_syndrome_loss, gnnd_train_bwd_partial'
+        return f'FusedV24Trainer ({how}): {k}, gnnd_train_update (row reduction + loss + Adam + next weights)'
+    if isinstance(tr, gd.train.FusedV30Trainer):
+        return (f'FusedV30Trainer ({how}): gnnd_train_fwd (V30), V30Loss.loss_and_grad, '
+                f'gnnd_train_bwd_partial, gnnd_train_update')
+    if isinstance(tr, gd.train.FusedWbpTrainer):
+        return (f'FusedWbpTrainer ({how}): packed weights, gnnd_train_fwd, gnnd_syndrome_loss, '
+                f'gnnd_train_bwd, gnnd_adam_step')
+    return f'Trainer ({how}): layer-by-layer propagate ops / fused forward, torch loss + Adam'
+
+
+_TRAJ_CACHE = {}
+
+
+def train_trajectory(H, init_state, T, dev, dtype, seed, n=64, K=10):
+    """K training steps of the fused GPU trainer (FusedV24Trainer, eager) against the oracle's
+    reference training step (oracle/torch_train.py V24Step, fp64: forward, LossFunc, backward,
+    Adam lr 3e-4 wd 1e-9) from the same start weights on the same n seeded codewords; every
+    step's two losses and the largest parameter difference after K steps.  Cached per dtype
+    (the trajectory does not depend on the timed batch)."""
+    key = (str(dtype), T, H.shape)
+    if key in _TRAJ_CACHE:
+        return dict(_TRAJ_CACHE[key], cached=True)
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import torch_train
-    w = {k: v.detach().cpu().double().numpy() for k, v in model.state_dict().items()}
     lg = gd.codes.toric_logicals(H)
     N, V = H.shape[0] + H.shape[1], H.shape[0]
     x, y = gd.data.toric_batch(H, n, seed=seed + 7, device=dev, dtype=dtype)
-    was = model.training
-    model.eval()
-    with torch.no_grad():
-        pred = model(gd.data.make_batch(x, model.graph(dev)))
-        loss_gpu = float(lf(pred, y))
-    model.train(was)
+    m = gd.MODELS['v24'](T, H).to(dev).to(dtype)
+    m.load_state_dict(init_state)
+    lf = gd.loss.SyndromeLoss(H, lg).to(dev)
+    tr = gd.train.FusedV24Trainer(m, lf, graph=False)
+    data = gd.data.make_batch(x, m.graph(dev))
+    gpu_losses = [float(tr.step(data, y)) for _ in range(K)]
+    w = {k: v.detach().cpu().double().numpy() for k, v in init_state.items()}
     st = torch_train.V24Step(H, lg, w, T)
+    xs, ys = x.view(-1, N).cpu().double().reshape(-1, 1), y.view(-1, V).cpu().double()
     t0 = time.perf_counter()
-    with torch.no_grad():
-        ref = st.forward(x.view(-1, N).cpu().double().reshape(-1, 1))
-        loss_ref = float(st.loss(ref, y.view(-1, V).cpu().double()))
-    got = pred.view(-1, V).double().cpu()
-    return {'codewords': n, 'loss_gpu': loss_gpu, 'loss_oracle_f64': loss_ref,
-            'loss_rel_err': abs(loss_gpu - loss_ref) / max(1e-30, abs(loss_ref)),
-            'pred_max_abs_err': float((got - ref).abs().max()),
-            'hard_decision_mismatches': int(((got > 0.5) != (ref > 0.5)).sum()),
-            'oracle': 'oracle/torch_train.py V24Step forward + LossFunc (fp64)',
-            'oracle_seconds': time.perf_counter() - t0}
+    ref_losses = [st.step(xs, ys) for _ in range(K)]
+    osec = time.perf_counter() - t0
+    sd = m.state_dict()
+    pdiff = max(float((sd[k].detach().double().cpu() - st.p[k].detach()).abs().max()) for k in st.p)
+    pscale = max(float(st.p[k].detach().abs().max()) for k in st.p)
+    moved = max(float((st.p[k].detach() - torch.as_tensor(w[k])).abs().max()) for k in st.p)
+    rel = [abs(a_ - b_) / max(1e-30, abs(b_)) for a_, b_ in zip(gpu_losses, ref_losses)]
+    res = {'codewords': n, 'steps': K, 'loss_gpu': gpu_losses, 'loss_oracle_f64': ref_losses,
+           'loss_max_rel_err': max(rel), 'param_max_abs_diff': pdiff, 'param_max_abs': pscale,
+           'param_max_abs_change_oracle': moved,
+           'oracle': 'oracle/torch_train.py V24Step (forward + LossFunc + backward + Adam, fp64)',
+           'oracle_seconds': osec}
+    _TRAJ_CACHE[key] = res
+    return res
 
 
 def decode_run(a, world, rank, dev, cpu='full'):
@@ -749,6 +847,13 @@ SUB_CONFIGS = [
                                                           dtype='f32', steps=200, warmup=5)),
     ('config5_toric7_v24_train_global1024', 'train', dict(model='v24', code='toric_7', gbatch=1024,
                                                            dtype='f32', steps=100, warmup=5)),
+    # the reference's own precision (quantum/decoder_v2_4.py:237-243 .double() MLPs, :278 fp64
+    # messages); the f32 entries above are the perf mode
+    ('config5_toric7_v24_train_global128_f64', 'train', dict(model='v24', code='toric_7', gbatch=128,
+                                                              dtype='f64', steps=200, warmup=5)),
+    ('config5_toric7_v24_train_global1024_f64', 'train', dict(model='v24', code='toric_7',
+                                                               gbatch=1024, dtype='f64', steps=50,
+                                                               warmup=3)),
 ]
 
 

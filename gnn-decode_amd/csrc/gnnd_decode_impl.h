@@ -253,24 +253,80 @@ __device__ __forceinline__ double vgpr_of(double s) {
     asm("v_mov_b64 %0, %1" : "=v"(d) : "s"(s));
     return d;
 }
-__device__ __forceinline__ double mlp128_sp(const double* w, double u, const double* tab) {
-    double acc = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < 128; ++k) {
-        double h = fma_vsv(u, w[k], vgpr_of(w[128 + k]));
-        acc = fma(softplus_tab_lite(h, tab), w[256 + k], acc);
+// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
+template <int N, typename F, int I = 0> __device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, F, I + 1>(static_cast<F&&>(f));
     }
-    return acc + w[384];
+}
+// The 128 units are summed in a FIXED order independent of how they are spread over waves:
+// chain j (0..3) accumulates units k = 4i + j (i ascending) from 0, and the MLP value is
+// ((c0 + c1) + (c2 + c3)) + b2.  A call evaluates NC consecutive chains from J0 (NC = 4: the
+// whole MLP; 2 / 1: the half / quarter a unit-split wave owns, mlp128d_split), so every split
+// gives the same bits.  Layouts (plain packed weights): 1-input {W1[128], b1[128], W2[128], b2},
+// 2-input (TWO: u0 -> W1[:, 0], u1 -> W1[:, 1]) {W1a[128], W1b[128], b1[128], W2[128], b2}.
+template <int NC, int J0, bool TWO>
+__device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, double u0, double u1,
+                                                 const double* tab) {
+    constexpr int kB1 = TWO ? 256 : 128, kW2 = TWO ? 384 : 256;
+    double c[NC];
+#pragma unroll
+    for (int jj = 0; jj < NC; ++jj) c[jj] = 0.0;
+    constexpr int kUnroll = 4 / NC;                          // 4 units per loop trip
+#pragma unroll kUnroll
+    for (int i = 0; i < 32; ++i) {
+        static_for<NC>([&](auto jc) {
+            constexpr int jj = decltype(jc)::value;
+            const int k = 4 * i + J0 + jj;
+            double h;
+            if constexpr (TWO) h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], vgpr_of(w[kB1 + k])));
+            else h = fma_vsv(u0, w[k], vgpr_of(w[kB1 + k]));
+            c[jj] = fma(softplus_tab_lite(h, tab), w[kW2 + k], c[jj]);
+        });
+    }
+    if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
+    else if constexpr (NC == 2) return c[0] + c[1];
+    else return c[0];
+}
+__device__ __forceinline__ double mlp128_sp(const double* w, double u, const double* tab) {
+    return mlp128d_chains<4, 0, false>(w, u, u, tab) + w[384];
 }
 __device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double u1,
                                               const double* tab) {
-    double acc = 0.0;
-#pragma unroll 4
-    for (int k = 0; k < 128; ++k) {
-        double h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], vgpr_of(w[256 + k])));
-        acc = fma(softplus_tab_lite(h, tab), w[384 + k], acc);
+    return mlp128d_chains<4, 0, true>(w, u0, u1, tab) + w[512];
+}
+// unit-split evaluation of the fp64 MLPs (decode_kernel US > 1, fp64 decoder_v2_4 small
+// batches): wave `sub` evaluates chain group sub, the US partial sums meet in LDS (buf = [US][256]
+// doubles, one of two buffers used alternately) and combine in the chain tree above.  Every
+// thread of the workgroup must call it (barrier); idle (wave-uniform): no live work item in this
+// wave, the units are skipped.
+template <int US, bool TWO>
+__device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, double u0, double u1,
+                                                int sub, double* buf, int itid, bool idle,
+                                                const double* tab) {
+    constexpr int kB2 = TWO ? 512 : 384;
+    if constexpr (US == 1) {
+        return idle ? 0.0 : mlp128d_chains<4, 0, TWO>(w, u0, u1, tab) + w[kB2];
+    } else {
+        static_assert(US == 2 || US == 4, "fp64 unit split 1, 2 or 4");
+        constexpr int NC = 4 / US, IL = GNND_BLOCK;
+        double p = 0.0;
+        if (!idle) {
+            switch (sub) {
+                case 0: p = mlp128d_chains<NC, 0, TWO>(w, u0, u1, tab); break;
+                case 1: p = mlp128d_chains<NC, NC, TWO>(w, u0, u1, tab); break;
+                case 2: if constexpr (US == 4) p = mlp128d_chains<1, 2, TWO>(w, u0, u1, tab); break;
+                default: if constexpr (US == 4) p = mlp128d_chains<1, 3, TWO>(w, u0, u1, tab); break;
+            }
+        }
+        buf[sub * IL + itid] = p;
+        __syncthreads();
+        double r;
+        if constexpr (US == 2) r = buf[itid] + buf[IL + itid];
+        else r = (buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid]);
+        return r + w[kB2];
     }
-    return acc + w[512];
 }
 
 // fp32 forms: TWO EDGES per call, riding the two halves of packed FMAs (the lane's
@@ -388,12 +444,6 @@ struct Mlp10Pair {
     }
 };
 
-template <int N, typename F, int I = 0> __device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<N, F, I + 1>(static_cast<F&&>(f));
-    }
-}
 // The unit sum in a FIXED order independent of how the units are spread over lanes: chain j
 // (0..7) accumulates units k = 8i + j (i ascending), chain 0 starting from the linear part,
 // and the MLP value is ((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7)).  A call evaluates
@@ -685,8 +735,6 @@ __device__ __forceinline__ f32x2 rcp2(f32x2 v) {
     return f32x2{__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)};
 }
 
-// compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1
-
 template <int MODEL, typename T> struct EdgeMath {
     static constexpr bool BP = ModelTraits<MODEL>::bp;
     static constexpr bool kFastBP = sizeof(T) == 4 && (MODEL == GNND_CBP || MODEL == GNND_QBP);
@@ -842,8 +890,9 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int tid = threadIdx.x;
     constexpr int IL = unit_split_lanes<US>();        // work-item lanes
     constexpr int NT = IL * US;
-    static_assert(US == 1 || (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2),
-                  "unit split: fp32 decoder_v2_4 on one slot pair per lane");
+    static_assert(US == 1 || (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2) ||
+                      (MODEL == GNND_V24 && sizeof(T) == 8 && US <= 4),
+                  "unit split: decoder_v2_4 (fp32: one slot pair per lane; fp64: US <= 4)");
     // work-item lane (0..255) and the wave's unit chunk: waves w = US i + sub share item wave i
     const int sub = US > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) % US) : 0;
     const int itid = US > 1 ? ((tid >> 6) / US) * 64 + (tid & 63) : tid;
@@ -875,6 +924,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int64_t b0 = (int64_t)blk * CW;
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
+    constexpr bool kV24F64 = MODEL == GNND_V24 && sizeof(T) == 8;
+    double* s_pd = (double*)s_part;                        // fp64 unit split: [2][US][256]
     // fp32 decoder_v2_4 reads its weights through the scalar cache only (no LDS copy); with
     // every table and the tile's rows within one element per thread (small batches: one
     // component-codeword per workgroup) all global loads are issued before any LDS store, so
@@ -1046,6 +1097,36 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     cf[r] = T(0);
                     tsum += tv[r];
                 }
+            } else if constexpr (kV24F64) {
+                // the reference dtype: one slot at a time through the fp64 chain-form MLP (unit
+                // split over US waves at small batches; partial-sum buffer = call index & 1)
+                T ext[R], xs[R];
+                bool val[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t sv = sl[r];
+                    val[r] = (int)(sv >> 16) != E;
+                    mv[r] = mb[r];
+                    const SumX<T> p = sxb[GNND_DIDX((int)(sv & 0xffffu), V, GNND_DBG_VAR)];
+                    ext[r] = p.s - mv[r];
+                    xs[r] = p.x;
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const T a = mlp128d_split<US, true>(wv + kV24Ggc1, ext[r], xs[r], sub,
+                                                        s_pd + (r & 1) * US * GNND_BLOCK, itid, widle,
+                                                        s_tab);
+                    tv[r] = val[r] ? tanh_half_fast(a) : T(0);
+                    cf[r] = T(0);
+                    tsum += tv[r];
+                    if constexpr (TAPE) {
+                        if (own && val[r]) {
+                            const size_t row = ((size_t)it * B + b0 + b) * g.es + g.e0 + (int)(sl[r] >> 16);
+                            tape.ext[row] = ext[r];
+                            tape.t[row] = tv[r];
+                        }
+                    }
+                }
             } else if constexpr (WBP) {
                 // v->c with this iteration's per-edge weights, then the BP pre-op
 #pragma unroll
@@ -1112,6 +1193,14 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                                                             s_part + US * IL, itid, widle GNND_PARG(pf, 4));
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
+                }
+            } else if constexpr (kV24F64) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const T y = mlp128d_split<US, false>(wv + kV24Ggc2, Sc - tv[r], Sc - tv[r], sub,
+                                                         s_pd + ((R + r) & 1) * US * GNND_BLOCK, itid,
+                                                         widle, s_tab);
+                    mn[r] = y * sc + mv[r];
                 }
             } else if constexpr (WBP) {
 #pragma unroll
@@ -1180,6 +1269,19 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const f32x2 y = mlp128_sp2(v24.g + kV24Mlp, v24.l3, f32x2{s_m[f], s_m[f1]});
                 s_m[f] = y.x;
                 if (f + 1 < n) s_m[f + 1] = y.y;
+            }
+        } else if constexpr (US > 1) {
+            // fp64 unit split: item lane itid evaluates message f0 + itid, the US waves a chain
+            // group each (the same bits as the whole MLP in one lane)
+            const int n = nb * nslot;
+            int rb = 0;
+            for (int f0 = 0; f0 < n; f0 += IL, rb ^= 1) {
+                const int f = f0 + itid;
+                const bool widle = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= n;
+                const T m = s_m[f < n ? f : n - 1];
+                const T y = mlp128d_split<US, false>(wv + kV24Mlp, m, m, sub,
+                                                     s_pd + rb * US * GNND_BLOCK, itid, widle, s_tab);
+                if (sub == 0 && f < n) s_m[f] = y;   // (lanes read only their own message)
             }
         } else {
             for (int f = tid; f < nb * nslot; f += NT) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f], s_tab);
@@ -2134,6 +2236,18 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
             p->lds = align16(p->lds) + (size_t)2 * us * il * 8 + 8;
         }
     }
+    // fp64 decoder_v2_4 (the reference dtype) the same way: one slot per lane (R <= 2 plans;
+    // toric: G = 4, R = 1), the 128 units of every MLP over US = 4 (B <= 256) / 2 (B <= 512)
+    // waves in four fixed chains (mlp128d_split)
+    if (model == GNND_V24 && dtype == GNND_F64 && n == 1 && g.R <= 2) {
+        const int forced = v24_split_forced();
+        int us = forced ? forced : B <= 256 ? 4 : B <= 512 ? 2 : 1;
+        if (us > 4) us = 4;
+        if (us > 1 && align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8 <= kLdsMax) {
+            p->us = us;
+            p->lds = align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8;
+        }
+    }
     return GNND_OK;
 }
 
@@ -2230,6 +2344,12 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         if constexpr (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2) {
             if (p.us == 8) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 8>, 8)
                                            : go_s(decode_kernel<MODEL, T, R, false, 8>, 8);
+            if (p.us == 4) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 4>, 4)
+                                           : go_s(decode_kernel<MODEL, T, R, false, 4>, 4);
+            if (p.us == 2) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 2>, 2)
+                                           : go_s(decode_kernel<MODEL, T, R, false, 2>, 2);
+        }
+        if constexpr (MODEL == GNND_V24 && sizeof(T) == 8 && R <= 2) {
             if (p.us == 4) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 4>, 4)
                                            : go_s(decode_kernel<MODEL, T, R, false, 4>, 4);
             if (p.us == 2) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 2>, 2)

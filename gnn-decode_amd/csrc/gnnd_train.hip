@@ -505,7 +505,12 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                         // every lane stores its row's total (16 identical writes per
                         // address, no exec-masked region inside the hot loop; f + eo < Ep, and
                         // the padding entries only ever meet dy = 0)
+#ifdef GNND_W2_MASKED_STORE
+                        // r03r experiment form (one lane per row stores under an exec mask)
+                        if ((lane & 15) == 0) outp[f + eo] = r;
+#else
                         outp[f + eo] = r;
+#endif
                     }
                     U.fold();
                     break;                       // (one pass covers every edge)

@@ -36,9 +36,12 @@ def _graph_of(H, device):
     """Cached device graph of H (keyed by content and the resolved device).  A TannerGraph
     passed as H is used as is: no host copy or hashing of H inside a caller's timed loop."""
     from .graph import TannerGraph
-    if isinstance(H, TannerGraph):
-        return H, None
     dev = _resolved(device)
+    if isinstance(H, TannerGraph):
+        if _resolved(H.device) != dev:
+            raise ValueError(f'the TannerGraph passed as H lives on {H.device}, but the batch is '
+                             f'requested on {dev}: pass the graph of that device (or the matrix)')
+        return H, None
     Hn = (np.asarray(H.detach().cpu() if isinstance(H, torch.Tensor) else H) != 0).astype(np.uint8)
     key = (Hn.shape, hash(Hn.tobytes()), str(dev))
     g = _GRAPHS.get(key)

@@ -335,7 +335,9 @@ def train_backward_partial(graph, model, plain_weights, x, out, grad_out, tape, 
 def train_backward_loss_partial(graph, model, plain_weights, x, out, y, logical_mask, n_logical,
                                 logical_only, tape, iters, ws=None):
     """gnnd_train_bwd_loss_partial: the reverse pass with the syndrome loss fused in (no
-    d loss / d out tensor).  Returns (workspace, rows, per-codeword-and-component losses)."""
+    d loss / d out tensor).  Returns (workspace, rows, per-codeword-and-component losses), or
+    None when the graph's tables plus the loss arrays exceed the workgroup's LDS (nothing
+    launched: use the syndrome-loss kernel and train_backward_partial instead)."""
     B = x.numel() // graph.N
     dt = dtype_code(x.dtype)
     nr = ctypes.c_int64()
@@ -349,11 +351,12 @@ def train_backward_loss_partial(graph, model, plain_weights, x, out, y, logical_
         ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=x.device)
     loss_b = torch.empty(max(nl.value, 1), dtype=x.dtype, device=x.device)[:nl.value]
     y = y.to(x.dtype).contiguous()
-    _lib.call('gnnd_train_bwd_loss_partial', graph.handle, _lib.VARIANT[model], dt,
-              _ptr(plain_weights), _ptr(x), _ptr(out), _ptr(y), _ptr(logical_mask), int(n_logical),
-              int(bool(logical_only)), _ptr(tape), _ptr(loss_b), _ptr(ws), nb.value, B, int(iters),
-              current_stream(x.device))
-    return ws, int(nr.value), loss_b
+    ok = _lib.call_or_unsupported(
+        'gnnd_train_bwd_loss_partial', graph.handle, _lib.VARIANT[model], dt,
+        _ptr(plain_weights), _ptr(x), _ptr(out), _ptr(y), _ptr(logical_mask), int(n_logical),
+        int(bool(logical_only)), _ptr(tape), _ptr(loss_b), _ptr(ws), nb.value, B, int(iters),
+        current_stream(x.device))
+    return (ws, int(nr.value), loss_b) if ok else None
 
 
 def train_update(model, dtype, rows=None, n_rows=0, grad=None, loss_b=None, loss=None,

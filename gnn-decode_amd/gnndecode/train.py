@@ -303,15 +303,21 @@ class FusedV24Trainer(_GraphedStep):
         self.exp_avg_sq = torch.zeros_like(flat)
         self.step_count = torch.zeros(1, dtype=torch.float64, device=flat.device)
         self._sync = torch.zeros(1, dtype=torch.int32, device=flat.device)   # gnnd_train_update
-        self._loss = torch.zeros((), dtype=flat.dtype, device=flat.device)
-        self._gw = torch.zeros_like(flat)
+        # flat gradient and batch loss side by side: ONE all_reduce(SUM) carries both
+        self._gbuf = torch.zeros(flat.numel() + 1, dtype=flat.dtype, device=flat.device)
+        self._gw = self._gbuf[:flat.numel()]
+        self._loss = self._gbuf[flat.numel()]
         # kernel-layout weights of the current parameters: written by the fused epilogue after
         # every update, re-prepared here when the parameters change outside the trainer
         self.prepared = ops.prepare_weights('v24', flat)
-        self._prep_version = flat._version
+        self._prep_version = self._param_versions()
         # device graph tables now, never inside a capture
         model.graph(flat.device)
         loss_fn._graph(flat.device)
+
+    def _reduce(self, loss, grads):
+        # _compute returned views of self._gbuf: one RCCL call for the gradient and the loss
+        dist.all_reduce(self._gbuf, op=dist.ReduceOp.SUM, group=self.group)
 
     def _fused_loss_mask(self, g, device):
         """Logical-row masks for the reverse pass's fused loss, or None (loss kernel path):
@@ -327,10 +333,17 @@ class FusedV24Trainer(_GraphedStep):
                                        lf.rows_within_components(g.components))
         return lf.logical_mask(device) if ok else None
 
+    def _param_versions(self):
+        # a parameter re-bound with `p.data = flat[...]` keeps its OWN version counter: an
+        # in-place change through it (load_state_dict, p.copy_) bumps that counter, not the
+        # flat buffer's, so both are tracked
+        return (self.flat._version,) + tuple(p._version for p in self.model.parameters())
+
     def _refresh_prepared(self):
-        if self.flat._version != self._prep_version:
+        v = self._param_versions()
+        if v != self._prep_version:
             self.prepared.copy_(ops.prepare_weights('v24', self.flat))
-            self._prep_version = self.flat._version
+            self._prep_version = v
 
     def _compute(self, x, y):
         m = self.model
@@ -340,9 +353,10 @@ class FusedV24Trainer(_GraphedStep):
             w = self.flat.to(x.dtype)
             out, tape = ops.train_forward(g, m.kind, x, ops.prepare_weights(m.kind, w), m.Nc)
             loss_b, dpred = lf.per_codeword(out, y)
-            self._gw = ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc).to(self.flat.dtype)
+            self._gw.copy_(ops.train_backward(g, m.kind, w, x, out, dpred, tape, m.Nc))
+            self._loss.copy_(loss_b.sum())
             self._pending = None
-            return loss_b.sum(), [self._gw]
+            return self._loss, [self._gw]
         lmask = self._fused_loss_mask(g, x.device)
         fl = None
         if lmask is not None and self.loss_in_forward:
@@ -353,16 +367,22 @@ class FusedV24Trainer(_GraphedStep):
         if fl is not None:
             out, tape, dpred, loss_b = fl
             ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
-        elif lmask is not None:
-            out, tape = ops.train_forward(g, m.kind, x, self.prepared, m.Nc)
-            # the syndrome loss computed inside the reverse pass (no loss launch)
-            ws, nrows, loss_b = ops.train_backward_loss_partial(
-                g, m.kind, self.flat, x, out, y, lmask, lf.logical_rows.size(0), lf.logical_only,
-                tape, m.Nc)
         else:
             out, tape = ops.train_forward(g, m.kind, x, self.prepared, m.Nc)
-            loss_b, dpred = lf.per_codeword(out, y)
-            ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
+            r = None
+            if lmask is not None:
+                # the syndrome loss computed inside the reverse pass (no loss launch); None when
+                # its tables exceed the workgroup's LDS: remembered, the loss kernel path instead
+                r = ops.train_backward_loss_partial(
+                    g, m.kind, self.flat, x, out, y, lmask, lf.logical_rows.size(0), lf.logical_only,
+                    tape, m.Nc)
+                if r is None:
+                    self._fuse_ok[(g.components, str(x.device))] = False
+            if r is not None:
+                ws, nrows, loss_b = r
+            else:
+                loss_b, dpred = lf.per_codeword(out, y)
+                ws, nrows = ops.train_backward_partial(g, m.kind, self.flat, x, out, dpred, tape, m.Nc)
         if self._dist():
             # rows -> flat gradient and batch loss, for the all-reduce
             ops.train_update('v24', x.dtype, rows=ws, n_rows=nrows, grad=self._gw,

@@ -194,19 +194,23 @@ def test_decision_errors_kernel_on_decoder_outputs(golden):
     assert c[2] + c[3] == int(golden('fer_rule')['v24_B32/count'])
 
 
-def test_v24_f32_unit_split_bit_identical():
-    """fp32 decoder_v2_4 small-batch unit split: decode_kernel runs US = 8 (a component-codeword's
-    items fit 128 lanes) or 4 (B*ncomp <= 256), 2 (<= 512) waves per item wave at one codeword
-    per workgroup and US = 1 above, all on the R = 2 slot table below B = 4096 (the toric graph
-    is split into its two components, B*ncomp = 2B).  The 128 hidden units are summed in one
-    fixed chain order
-    (gnnd_decode_impl.h mlp128_chains), so every codeword decodes to the SAME BITS under every
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_v24_unit_split_bit_identical(dtype):
+    """decoder_v2_4 small-batch unit split: decode_kernel runs US = 4 (B*ncomp <= 256), 2
+    (<= 512) waves per item wave at one codeword per workgroup (fp32 also US = 8 when a
+    component-codeword's items fit 128 lanes) and US = 1 above (the toric graph is split into its
+    two components below one codeword per CU, B*ncomp = 2B).  fp32 runs the R = 2 slot table below
+    B = 4096, fp64 (the reference dtype) the default plan (toric: one slot per lane).  The 128
+    hidden units are summed in one fixed chain order (gnnd_decode_impl.h mlp128_chains: 8 chains,
+    mlp128d_chains: 4 chains in fp64), so every codeword decodes to the SAME BITS under every
     split and tile: slices decoded alone (US = 4 / 2) equal the B = 1024 decode (US = 1)."""
     import gnndecode as gd
     w = _shipped('v24_toric_5')
     m, H = _model('v24', 'toric_5', 15, w)
+    if dtype == torch.float64:
+        m = m.double()
     B = 1024
-    x, _ = gd.data.toric_batch(H, B, seed=5, device=DEV, dtype=torch.float32)
+    x, _ = gd.data.toric_batch(H, B, seed=5, device=DEV, dtype=dtype)
     _, full = _decode(m, x)
     full = full.view(B, -1)
     xb = x.view(B, -1)

@@ -478,3 +478,45 @@ def test_graphed_step_with_rccl_collective_one_rank(fused):
             assert torch.equal(b.state_dict()[k], v), k
     finally:
         dist.destroy_process_group()
+
+
+def _v24_checkpoint_model(H, T, dtype):
+    """decoder_v2_4 at the reference's training start: its own checkpoint (the shipped
+    epoch-67 weights, L-independent shapes, converted to weights/v24_toric_5.npz), as
+    quantum/decoder_v2_4.py:322 loads one before its Adam loop."""
+    import os
+    import gnndecode as gd
+    z = np.load(os.path.join(os.path.dirname(gd.__file__), 'weights', 'v24_toric_5.npz'))
+    m = gd.MODELS['v24'](T, H)
+    m.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files})
+    return m.to(DEV).to(dtype).train(), {k: z[k].astype(np.float64) for k in z.files}
+
+
+def test_config5_trajectory_matches_oracle_L7_B128_f64():
+    """Config 5 at the reference's precision and size: 10 fused training steps (forward + tape,
+    reverse pass with the fused syndrome loss, fused Adam epilogue) on toric L=7, B=128, fp64,
+    from the reference checkpoint, against the oracle's restatement of the reference training
+    step (oracle/torch_train.py V24Step: forward, LossFunc, autograd backward, torch Adam lr
+    3e-4 wd 1e-9) on the same codewords.  The loss must move (non-integer, changing) and every
+    step's loss must agree to 1e-9 relative, the parameters after 10 steps to 1e-10."""
+    import gnndecode as gd
+    import torch_train
+    H = gd.codes.toric_code(7)
+    lg = gd.codes.toric_logicals(H)
+    T, B, K = 15, 128, 10
+    m, w = _v24_checkpoint_model(H, T, torch.float64)
+    x, y = gd.data.toric_batch(H, B, seed=2024, device=DEV, dtype=torch.float64)
+    tr = gd.train.FusedV24Trainer(m, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=False)
+    data = gd.data.make_batch(x, m.graph(x.device))
+    got = [float(tr.step(data, y)) for _ in range(K)]
+    st = torch_train.V24Step(H, lg, w, T)
+    N, V = H.shape[0] + H.shape[1], H.shape[0]
+    xs, ys = x.view(-1, N).cpu().reshape(-1, 1), y.view(-1, V).cpu()
+    ref = [st.step(xs, ys) for _ in range(K)]
+    assert len(set(ref)) == K and all(r != round(r) for r in ref), ref     # the loss moves
+    for s, (a, b) in enumerate(zip(got, ref)):
+        assert abs(a - b) <= 1e-9 * abs(b), (s, a, b)
+    sd = m.state_dict()
+    for k, p in st.p.items():
+        d = float((sd[k].detach().cpu() - p.detach()).abs().max())
+        assert d <= 1e-10, (k, d)

@@ -3,6 +3,10 @@
 # Every GPU step runs under its own timeout; a crash/timeout (exit >= 124 or signal) ends the
 # script immediately.  Test failures (pytest exit 1) do not stop the bench.
 # usage: [STEPS="pytest_gpu smoke bench"] tools/gpu_round.sh [tag] [pytest-args...]
+# Steps: pytest_gpu smoke bench sweep prof pmc (defaults) and, on request,
+#   train_prof  rocprofv3 kernel trace of `bench.py --mode train $TRAIN_ARGS`
+#   bench_args  one `bench.py $BENCH_ARGS` line
+#   prof_args   rocprofv3 kernel trace of `bench.py $BENCH_ARGS`
 set -u
 STEPS="${STEPS:-pytest_gpu smoke bench sweep prof pmc}"
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -25,11 +29,14 @@ step() {  # name, timeout, cmd...
 }
 rocm-smi --showproductname > "$OUT/rocm-smi.txt" 2>&1 || true
 lscpu | grep -E "Model name|^CPU\(s\)" > "$OUT/lscpu.txt" 2>&1 || true
-step pytest_gpu 900 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread "$@"
+step pytest_gpu 900 python -u -m pytest tests -m gpu -v -x --timeout 200 --timeout-method thread "$@"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
 step sweep 900 python tools/sweep.py --steps 5
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0
 step pmc 1200 bash tools/pmc.sh "$OUT/pmc"
+step train_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/train_prof" -o run --output-format csv -- python bench.py --mode train ${TRAIN_ARGS:-} --cpu-seconds 0
+step bench_args 600 python bench.py ${BENCH_ARGS:-}
+step prof_args 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_args" -o run --output-format csv -- python bench.py ${BENCH_ARGS:-} --cpu-seconds 0
 case " $STEPS " in *" pmc "*) python tools/pmc_summary.py "$OUT/pmc" cgnni_bch_63_45_B65536_T25_f32 "$OUT/pmc_cgnni_bch_63_45_B65536_T25_f32.json" > "$OUT/pmc_summary.log" 2>&1 || true;; esac
 echo "=== done $(date +%T)"
