@@ -775,6 +775,9 @@ def decode_run(a, world, rank, dev, cpu='full'):
             fl = fl + sp_flops * trans
         achieved = fl * a.batch / kernel_s / 1e12
         peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
+        # SURVEY §8(d)'s algorithmic count (each Softplus one transcendental, no FLOPs): the
+        # fraction without the fp64 Softplus pricing, reported beside it
+        frac_alg = (fl - (sp_flops or 0) * trans) * a.batch / kernel_s / 1e12 / peak
         trans_frac = 2 * trans * a.batch / kernel_s / TRANS_OPS_PER_S
         esz = {torch.float32: 4, torch.float64: 8, torch.bfloat16: 2}[io_dtype]
         io_bytes = (g.N + gd.ops.decode_out_rows(g, a.model, 1, T)) * esz * a.batch
@@ -814,6 +817,7 @@ def decode_run(a, world, rank, dev, cpu='full'):
                          'kernel_ms': kernel_s * 1e3,
                          'flops_per_codeword': fl, 'transcendentals_per_codeword': trans,
                          'softplus_flops_included': sp_flops,
+                         'frac_algorithmic_count': frac_alg,
                          # >= 2 hardware transcendental ops per function vs the 8-cycle issue
                          # rate (fp32; fp64 has no hardware transcendentals)
                          'transcendental_op_frac': trans_frac if dtype == torch.float32 else None,

@@ -266,10 +266,13 @@ template <int N, typename F, int I = 0> __device__ __forceinline__ void static_f
 // whole MLP; 2 / 1: the half / quarter a unit-split wave owns, mlp128d_split), so every split
 // gives the same bits.  Layouts (plain packed weights): 1-input {W1[128], b1[128], W2[128], b2},
 // 2-input (TWO: u0 -> W1[:, 0], u1 -> W1[:, 1]) {W1a[128], W1b[128], b1[128], W2[128], b2}.
+// bl: the MLP's 128 layer-1 biases staged in LDS (a broadcast ds_read_b64 per unit: VOP3 takes
+// one scalar operand, so a bias from SGPRs costs a v_mov_b64 per unit); tab: the Softplus
+// tables in LDS (softplus_fast).
 template <int NC, int J0, bool TWO>
-__device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, double u0, double u1,
-                                                 const double* tab) {
-    constexpr int kB1 = TWO ? 256 : 128, kW2 = TWO ? 384 : 256;
+__device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, const double* bl,
+                                                 double u0, double u1, const double* tab) {
+    constexpr int kW2 = TWO ? 384 : 256;
     double c[NC];
 #pragma unroll
     for (int jj = 0; jj < NC; ++jj) c[jj] = 0.0;
@@ -280,21 +283,18 @@ __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, d
             constexpr int jj = decltype(jc)::value;
             const int k = 4 * i + J0 + jj;
             double h;
-            if constexpr (TWO) h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], vgpr_of(w[kB1 + k])));
-            else h = fma_vsv(u0, w[k], vgpr_of(w[kB1 + k]));
-            c[jj] = fma(softplus_tab_lite(h, tab), w[kW2 + k], c[jj]);
+            if constexpr (TWO) h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], bl[k]));
+            else h = fma_vsv(u0, w[k], bl[k]);
+            c[jj] = fma(softplus_fast(h, tab), w[kW2 + k], c[jj]);
         });
     }
     if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
     else if constexpr (NC == 2) return c[0] + c[1];
     else return c[0];
 }
-__device__ __forceinline__ double mlp128_sp(const double* w, double u, const double* tab) {
-    return mlp128d_chains<4, 0, false>(w, u, u, tab) + w[384];
-}
-__device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double u1,
-                                              const double* tab) {
-    return mlp128d_chains<4, 0, true>(w, u0, u1, tab) + w[512];
+__device__ __forceinline__ double mlp128_sp(const double* w, const double* bl, double u,
+                                            const double* tab) {
+    return mlp128d_chains<4, 0, false>(w, bl, u, u, tab) + w[384];
 }
 // unit-split evaluation of the fp64 MLPs (decode_kernel US > 1, fp64 decoder_v2_4 small
 // batches): wave `sub` evaluates chain group sub, the US partial sums meet in LDS (buf = [US][256]
@@ -302,22 +302,22 @@ __device__ __forceinline__ double mlp128x2_sp(const double* w, double u0, double
 // thread of the workgroup must call it (barrier); idle (wave-uniform): no live work item in this
 // wave, the units are skipped.
 template <int US, bool TWO>
-__device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, double u0, double u1,
-                                                int sub, double* buf, int itid, bool idle,
-                                                const double* tab) {
+__device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, const double* bl,
+                                                double u0, double u1, int sub, double* buf,
+                                                int itid, bool idle, const double* tab) {
     constexpr int kB2 = TWO ? 512 : 384;
     if constexpr (US == 1) {
-        return idle ? 0.0 : mlp128d_chains<4, 0, TWO>(w, u0, u1, tab) + w[kB2];
+        return idle ? 0.0 : mlp128d_chains<4, 0, TWO>(w, bl, u0, u1, tab) + w[kB2];
     } else {
         static_assert(US == 2 || US == 4, "fp64 unit split 1, 2 or 4");
         constexpr int NC = 4 / US, IL = GNND_BLOCK;
         double p = 0.0;
         if (!idle) {
             switch (sub) {
-                case 0: p = mlp128d_chains<NC, 0, TWO>(w, u0, u1, tab); break;
-                case 1: p = mlp128d_chains<NC, NC, TWO>(w, u0, u1, tab); break;
-                case 2: if constexpr (US == 4) p = mlp128d_chains<1, 2, TWO>(w, u0, u1, tab); break;
-                default: if constexpr (US == 4) p = mlp128d_chains<1, 3, TWO>(w, u0, u1, tab); break;
+                case 0: p = mlp128d_chains<NC, 0, TWO>(w, bl, u0, u1, tab); break;
+                case 1: p = mlp128d_chains<NC, NC, TWO>(w, bl, u0, u1, tab); break;
+                case 2: if constexpr (US == 4) p = mlp128d_chains<1, 2, TWO>(w, bl, u0, u1, tab); break;
+                default: if constexpr (US == 4) p = mlp128d_chains<1, 3, TWO>(w, bl, u0, u1, tab); break;
             }
         }
         buf[sub * IL + itid] = p;
@@ -743,9 +743,7 @@ template <int MODEL, typename T> struct EdgeMath {
     __device__ static __forceinline__ T pre(T ext, T xv, const T* __restrict__ wv, T& cc,
                                             const T* tab = nullptr) {
         cc = T(0);
-        if constexpr (MODEL == GNND_V24) {
-            return tanh_half_fast(mlp128x2_sp(wv + kV24Ggc1, ext, xv, tab));
-        } else if constexpr (kFastBP) {
+        if constexpr (kFastBP) {
             const float a = ext + xv;
             cc = a < 0.f ? 1.f : 0.f;          // tanh(clamp(a)/2) < 0 exactly when a < 0
             return bp_log2tanh_f32(a, MODEL == GNND_QBP ? 1e-20f : 1e-7f);
@@ -763,9 +761,7 @@ template <int MODEL, typename T> struct EdgeMath {
     __device__ static __forceinline__ T post(T u, T n2, T sc, T mprev, const Mlp10F32& mlp,
                                              const T* s_w, const T* __restrict__ wv,
                                              const T* tab = nullptr) {
-        if constexpr (MODEL == GNND_V24) {
-            return mlp128_sp(wv + kV24Ggc2, u, tab) * sc + mprev;
-        } else if constexpr (MODEL == GNND_QGNNI || MODEL == GNND_CGNNI) {
+        if constexpr (MODEL == GNND_QGNNI || MODEL == GNND_CGNNI) {
             T y;
             if constexpr (sizeof(T) == 4) y = mlp(u);
             else y = mlp10_relu(s_w + kMlp10Msg, u);
@@ -897,22 +893,29 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int sub = US > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) % US) : 0;
     const int itid = US > 1 ? ((tid >> 6) / US) * 64 + (tid & 63) : tid;
 
+    // fp64 V24: the Softplus tables (gnnd_common.h kExpTab | kLogTab, indexed per lane) at
+    // LDS byte 0, then the three MLPs' layer-1 biases [3][128]
+    constexpr bool kTab = MODEL == GNND_V24 && sizeof(T) == 8;
     T* s_w = (T*)smem;
     size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
+    T* s_tab = nullptr;
+    T* s_bias = nullptr;
+    if constexpr (kTab) {
+        s_tab = (T*)smem;
+        s_bias = s_tab + kFp64TabDoubles;
+        off = (size_t)(kFp64TabDoubles + 3 * 128) * 8;
+        for (int i = tid; i < kFp64TabDoubles; i += NT)
+            s_tab[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
+        for (int i = tid; i < 3 * 128; i += NT) {
+            const int m = i >> 7, k = i & 127;
+            s_bias[i] = w[m == 0 ? kV24Ggc1 + 256 + k : (m == 1 ? kV24Ggc2 : kV24Mlp) + 128 + k];
+        }
+    }
     const int nslot = C * G * R;
     uint32_t* s_slot = (uint32_t*)(smem + off);
     int* s_vptr = (int*)(s_slot + nslot);
     int* s_vslot = s_vptr + V + 1;
     off += (((size_t)nslot + V + 1 + E) * 4 + 15) & ~(size_t)15;
-    // fp64 V24: the Softplus tables (gnnd_common.h kExpTab | kLogTab), indexed per lane
-    constexpr bool kTab = MODEL == GNND_V24 && sizeof(T) == 8;
-    T* s_tab = nullptr;
-    if constexpr (kTab) {
-        s_tab = (T*)(smem + off);
-        off += (size_t)kFp64TabDoubles * 8;
-        for (int i = tid; i < kFp64TabDoubles; i += NT)
-            s_tab[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
-    }
     T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
@@ -1113,7 +1116,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 }
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const T a = mlp128d_split<US, true>(wv + kV24Ggc1, ext[r], xs[r], sub,
+                    const T a = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
                                                         s_pd + (r & 1) * US * GNND_BLOCK, itid, widle,
                                                         s_tab);
                     tv[r] = val[r] ? tanh_half_fast(a) : T(0);
@@ -1197,7 +1200,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             } else if constexpr (kV24F64) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const T y = mlp128d_split<US, false>(wv + kV24Ggc2, Sc - tv[r], Sc - tv[r], sub,
+                    const T y = mlp128d_split<US, false>(wv + kV24Ggc2, s_bias + 128, Sc - tv[r], Sc - tv[r], sub,
                                                          s_pd + ((R + r) & 1) * US * GNND_BLOCK, itid,
                                                          widle, s_tab);
                     mn[r] = y * sc + mv[r];
@@ -1279,12 +1282,12 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const int f = f0 + itid;
                 const bool widle = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= n;
                 const T m = s_m[f < n ? f : n - 1];
-                const T y = mlp128d_split<US, false>(wv + kV24Mlp, m, m, sub,
+                const T y = mlp128d_split<US, false>(wv + kV24Mlp, s_bias + 256, m, m, sub,
                                                      s_pd + rb * US * GNND_BLOCK, itid, widle, s_tab);
                 if (sub == 0 && f < n) s_m[f] = y;   // (lanes read only their own message)
             }
         } else {
-            for (int f = tid; f < nb * nslot; f += NT) s_m[f] = mlp128_sp(wv + kV24Mlp, s_m[f], s_tab);
+            for (int f = tid; f < nb * nslot; f += NT) s_m[f] = mlp128_sp(wv + kV24Mlp, s_bias + 256, s_m[f], s_tab);
         }
         __syncthreads();
     }
@@ -2007,10 +2010,11 @@ int64_t decode_weights_count(int model, int E, int iters) {
     if (model == GNND_V10) return (int64_t)E * iters + 1;
     return weights_count(model);
 }
-// weights staged to LDS by the kernels (the weighted-BP tables are read through the cache)
+// weights staged in LDS by the decode kernels (decoder_v2_4 reads its weights through the scalar
+// cache: none; its fp64 form stages tables and biases, counted in make_plan)
 int lds_weights(int model) {
     const int n = weights_count(model);
-    return n > 0 ? n : 0;
+    return n > 0 && model != GNND_V24 ? n : 0;
 }
 
 constexpr size_t kLdsMax = 160 * 1024;
@@ -2189,7 +2193,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const GraphView& g = !v24f32 ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
-    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)kFp64TabDoubles * 8 : 0;
+    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kFp64TabDoubles + 3 * 128) * 8 : 0;
     const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab;
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;

@@ -10,6 +10,8 @@
 #include <string.h>
 #include <vector>
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
 
 static thread_local int g_last_hip_error = 0;
 
@@ -58,6 +60,109 @@ struct HostTables {
     int lay_off[7] = {0}, layx_off[7] = {0};
     std::vector<int> table;
 };
+
+// GNND_NO_SLOT_SPREAD=1: the x-augmented layouts keep the slot plan's edge order (A/B)
+bool slot_spread_disabled() {
+    static bool v = [] {
+        const char* e = getenv("GNND_NO_SLOT_SPREAD");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+// LDS bank spreading of the register-resident kernel's message stores (decode_resident_kernel
+// on an x-augmented layout for a tile of cw codewords).  Work item f = (c * cw + b) * G + g
+// (check c, codeword b, group lane g); a 32-lane half of a wave is one LDS bank group, and the
+// check step stores slot r of its items with one ds_write_b32 at b * P1 + pos(edge) (padding
+// slots at the spare position P).  Cycles of a group = distinct addresses on its busiest bank
+// (32 banks, MI355X_MICROARCH.md §LDS).  A check's edges may sit in any of its real slots: the
+// variable sums keep edge order and the check sum is the same sum in another order, so each
+// check's edges are redistributed over its slot rows r by a deterministic annealing (fixed
+// seed: the same tables for the same graph) that minimises the summed cycles.  BCH(63,45),
+// cw = 16: 648 -> ~490 store cycles per tile iteration (tools/t_perm.py models the same).
+// slot[c * G * R + k] = v | pos << 16 for k < deg(c); padding (k >= deg) stays trailing.
+void spread_check_slots(int C, int G, int R, int cw, int P, const std::vector<int>& cdeg,
+                        std::vector<int>& slot) {
+    const int GR = G * R, P1 = (P + 1) | 1;
+    const long items = (long)C * cw * G;
+    const int nh = (int)((items + 31) / 32);
+    if (nh <= 0 || cw < 1) return;
+    // group (h, r): lanes f in [32 h, 32 h + 32) of slot row r
+    std::vector<std::vector<int>> cr_groups((size_t)C * R);     // (c, r) -> groups containing it
+    for (int h = 0; h < nh; ++h) {
+        int last = -1;
+        for (int f = 32 * h; f < 32 * h + 32 && f < items; ++f) {
+            const int c = (f / G) / cw;
+            if (c == last) continue;
+            last = c;
+            for (int r = 0; r < R; ++r) cr_groups[(size_t)c * R + r].push_back(h * R + r);
+        }
+    }
+    auto group_cost = [&](int grp) {
+        const int h = grp / R, r = grp % R;
+        int addr[32], n = 0;
+        for (int f = 32 * h; f < 32 * h + 32 && f < items; ++f) {
+            const int gi = f / G, g = f % G, c = gi / cw, b = gi % cw;
+            const int k = g * R + r;
+            const int pos = k < cdeg[c] ? (int)((uint32_t)slot[(size_t)c * GR + k] >> 16) : P;
+            const int a = b * P1 + pos;
+            bool dup = false;
+            for (int i = 0; i < n && !dup; ++i) dup = addr[i] == a;
+            if (!dup) addr[n++] = a;
+        }
+        int cnt[32] = {0}, m = 0;
+        for (int i = 0; i < n; ++i) m = std::max(m, ++cnt[addr[i] & 31]);
+        return m;
+    };
+    std::vector<int> gcost((size_t)nh * R);
+    long cur = 0;
+    for (int i = 0; i < nh * R; ++i) cur += gcost[i] = group_cost(i);
+    const long init_cost = cur;
+    std::vector<int> best = slot;
+    long bestc = cur;
+    uint64_t s = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&](uint64_t n) {
+        s = s * 6364136223846793005ull + 1442695040888963407ull;
+        return (uint64_t)(s >> 33) % n;
+    };
+    const long iters = 40L * C * GR;
+    std::vector<int> touched;
+    for (long it = 0; it < iters; ++it) {
+        const int c = (int)rnd(C), d = cdeg[c];
+        if (d < 2) continue;
+        const int k1 = (int)rnd(d), k2 = (int)rnd(d);
+        if (k1 % R == k2 % R) continue;                  // same slot row: same costs
+        const size_t base = (size_t)c * GR;
+        std::swap(slot[base + k1], slot[base + k2]);
+        touched.clear();
+        for (int r : {k1 % R, k2 % R})
+            for (int grp : cr_groups[(size_t)c * R + r]) touched.push_back(grp);
+        long delta = 0;
+        std::vector<int> nc(touched.size());
+        for (size_t i = 0; i < touched.size(); ++i) {
+            nc[i] = group_cost(touched[i]);
+            delta += nc[i] - gcost[touched[i]];
+        }
+        const double temp = 2.0 * (1.0 - (double)it / iters) + 0.05;
+        const double u = (double)rnd(1u << 30) / (double)(1u << 30);
+        if (delta <= 0 || u < exp(-(double)delta / temp)) {
+            for (size_t i = 0; i < touched.size(); ++i) gcost[touched[i]] = nc[i];
+            cur += delta;
+            if (cur < bestc) { bestc = cur; best = slot; }
+        } else {
+            std::swap(slot[base + k1], slot[base + k2]);
+        }
+    }
+    slot = best;
+    static const bool log = [] {
+        const char* e = getenv("GNND_SLOT_SPREAD_LOG");
+        return e && e[0] == '1';
+    }();
+    if (log) {
+        fprintf(stderr, "gnnd slot spread: C=%d G=%d R=%d cw=%d P1=%d store cycles per tile "
+                        "iteration %ld -> %ld\n", C, G, R, cw, P1, init_cost, bestc);
+    }
+}
 
 int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, int32_t V,
                  int32_t C, HostTables& T) {
@@ -178,6 +283,13 @@ int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, 
             const int e = (int)(sv >> 16);
             if (e < E) L.slot[k] = (int)(sv & 0xffffu) | (epos[e] << 16);
         }
+        // x-augmented layouts of the register-resident fp32 kernel (tiles of cw = 64 / gs
+        // codewords): each check's edges over its slot rows for conflict-free-er message stores
+        if (with_x && gs >= 2 && gs <= 32 && !slot_spread_disabled()) {
+            std::vector<int> cdeg(C);
+            for (int c = 0; c < C; ++c) cdeg[c] = cptr[c + 1] - cptr[c];
+            spread_check_slots(C, plans[1].G, plans[1].R, 64 / gs, pos, cdeg, L.slot);
+        }
     };
     Layout* lays = T.lays;
     Layout* laysx = T.laysx;
@@ -284,11 +396,28 @@ int check_tables(const HostTables& T, int32_t* report) {
                 for (int e = vptr[v]; e < vptr[v + 1]; ++e) epos[e] = pos + (e - vptr[v]);
             }
             if (expect != L.P) ++fails;
+            // the slot table: per check, its edges in some order (the x layouts spread them over
+            // the slot rows, spread_check_slots), each once, as {variable, position}; padding
+            // trailing at the spare position
             const SlotPlan& sp = T.plans[1];
-            for (int k = 0; k < T.nsr; ++k) {
-                const int e = (int)(sp.slot_ve[k] >> 16);
-                const int want = e < E ? epos[e] : L.P;
-                if ((int)((uint32_t)L.slot[k] >> 16) != want) ++fails;
+            const int GR = sp.G * sp.R;
+            std::vector<int> epos_inv(L.P + 1, -1), seen(E, 0);
+            for (int e = 0; e < E; ++e)
+                if (epos[e] >= 0) epos_inv[epos[e]] = e;
+            for (int c = 0; c < C; ++c) {
+                const int deg = cptr[c + 1] - cptr[c];
+                for (int k = 0; k < GR; ++k) {
+                    const uint32_t sl = (uint32_t)L.slot[c * GR + k];
+                    const int pos = (int)(sl >> 16);
+                    if (k >= deg) {
+                        if (pos != L.P) ++fails;
+                        continue;
+                    }
+                    const int e = pos <= L.P ? epos_inv[pos] : -1;
+                    if (e < 0 || (int)(t[e] >> 16) != c || (int)(sl & 0xffffu) != (int)(t[e] & 0xffff) ||
+                        seen[e]++)
+                        ++fails;
+                }
             }
         }
     if (report) {

@@ -31,6 +31,7 @@ static double ulp(double a, double b) {
 int main() {
     std::mt19937_64 g(1);
     double me = 0, ml = 0, mt = 0, mm = 0, ms = 0, mst = 0, met = 0, mlt = 0, msl = 0;
+    long nfast = 0;
     static double TAB[kFp64TabDoubles];
     for (int i = 0; i < kFp64TabDoubles; ++i) TAB[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
     std::uniform_real_distribution<double> U(-700, 700), L(-300, 300), T(-12, 12), S(-60, 30);
@@ -52,8 +53,10 @@ int main() {
         mlt = fmax(mlt, ulp(log1p_tab_unit(uu, TAB + kExpTabN), log1p(uu)));
         double hl = (i % 5) ? S(g) : U(g);
         msl = fmax(msl, fabs(softplus_tab_lite(hl, TAB) - (hl > 20 ? hl : log1p(exp(hl)))));
+        const double hf = (i % 7 == 0) ? 20.0 + (i % 11) * 1e-15 - 5e-15 : hl;   // around the threshold
+        nfast += softplus_fast(hf, TAB) != softplus_tab_lite(hf, TAB);
     }
-    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e\n", me, ml, mt, mm, ms, mst, met, mlt, msl);
+    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %ld\n", me, ml, mt, mm, ms, mst, met, mlt, msl, nfast);
 }
 '''
 
@@ -78,3 +81,6 @@ def test_fp64_fast_math_ulp(tmp_path):
     # states — ABSOLUTE error <= 1e-13 over [-700, 700] (the fp64 parity contract is rtol 1e-10
     # on the decoder outputs; measured 7e-14, the degree-3 exp polynomial's r^4/24)
     assert float(out[8]) <= 1e-13, out[8]
+    # softplus_fast (the decode kernel's form: byte-offset table indices, the threshold in the
+    # exponent) computes softplus_tab_lite's values bit for bit
+    assert int(out[9]) == 0, out[9]
