@@ -125,8 +125,9 @@ void spread_check_slots(int C, int G, int R, int cw, int P, const std::vector<in
         s = s * 6364136223846793005ull + 1442695040888963407ull;
         return (uint64_t)(s >> 33) % n;
     };
-    const long iters = 40L * C * GR;
-    std::vector<int> touched;
+    // (bounded: graph creation stays in the milliseconds for the framework's codes)
+    const long iters = std::min(20L * C * GR, 20000L);
+    std::vector<int> touched, nc;
     for (long it = 0; it < iters; ++it) {
         const int c = (int)rnd(C), d = cdeg[c];
         if (d < 2) continue;
@@ -138,7 +139,7 @@ void spread_check_slots(int C, int G, int R, int cw, int P, const std::vector<in
         for (int r : {k1 % R, k2 % R})
             for (int grp : cr_groups[(size_t)c * R + r]) touched.push_back(grp);
         long delta = 0;
-        std::vector<int> nc(touched.size());
+        nc.resize(touched.size());
         for (size_t i = 0; i < touched.size(); ++i) {
             nc[i] = group_cost(touched[i]);
             delta += nc[i] - gcost[touched[i]];
@@ -285,7 +286,8 @@ int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, 
         }
         // x-augmented layouts of the register-resident fp32 kernel (tiles of cw = 64 / gs
         // codewords): each check's edges over its slot rows for conflict-free-er message stores
-        if (with_x && gs >= 2 && gs <= 32 && !slot_spread_disabled()) {
+        // (group sizes the register-resident kernel instantiates: G <= 16)
+        if (with_x && gs >= 2 && gs <= 32 && plans[1].G <= 16 && !slot_spread_disabled()) {
             std::vector<int> cdeg(C);
             for (int c = 0; c < C; ++c) cdeg[c] = cptr[c + 1] - cptr[c];
             spread_check_slots(C, plans[1].G, plans[1].R, 64 / gs, pos, cdeg, L.slot);
