@@ -2466,3 +2466,12 @@ int gnnd_launch_wbp_tape(const gnnd_graph*, int, const void*, const void*, void*
 int gnnd_launch_wbp_bwd(const gnnd_graph*, int, const void*, const void*, const void*,
                         const void*, const void*, void*, int64_t, int64_t, int, hipStream_t);
 int gnnd_launch_v22(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int, hipStream_t);
+// CGNNI / QGNNI training (gnnd_train_gnn.hip): the forward with its tape ([B][T][nslot] tanh
+// outputs of the view's slot plan, then [B][V] readout inputs) and the reverse pass to one
+// gradient row [62] per workgroup (gnnd_gnn_train_rows of them)
+int64_t gnnd_gnn_tape_elems(const gnnd_graph*, int64_t, int);
+int64_t gnnd_gnn_train_rows(int64_t);
+int gnnd_launch_gnn_tape(const gnnd_graph*, int, int, const void*, const void*, void*, int64_t, int,
+                         void*, hipStream_t);
+int gnnd_launch_gnn_bwd(const gnnd_graph*, int, int, const void*, const void*, const void*,
+                        const void*, void*, int64_t, int64_t, int, hipStream_t);

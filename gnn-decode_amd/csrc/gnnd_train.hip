@@ -846,20 +846,24 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
 }
 
 bool is_wbp_train(int model) { return model == GNND_NBP || model == GNND_V22; }
+// the 10-hidden-unit GNN decoders (CGNNI, QGNNI): gnnd_train_gnn.hip
+bool is_gnn_train(int model) { return model == GNND_CGNNI || model == GNND_QGNNI; }
 bool train_args_ok(const gnnd_graph* g, int model, int dtype, int64_t B, int32_t iters) {
     if (!g || B < 0 || iters < 0) return false;
     if (is_wbp_train(model)) return dtype == GNND_F64;       // the scripts' dtype only
-    return (model == GNND_V24 || model == GNND_V30) && (dtype == GNND_F32 || dtype == GNND_F64);
+    return (model == GNND_V24 || model == GNND_V30 || is_gnn_train(model)) &&
+           (dtype == GNND_F32 || dtype == GNND_F64);
 }
 // per-edge weight tables of the weighted-BP models (gnnd.h NBP / V22 layout)
 int64_t wbp_weights(const gnnd_graph* g, int iters) {
     return 2 * (int64_t)iters * g->view.E + 2 * (int64_t)g->view.E + 1;
 }
 // trainable weights of a fused-training model (the packed layout of gnnd.h)
-int train_weights(int model) { return model == GNND_V30 ? kV30Count : kV24W; }
+int train_weights(int model) { return model == GNND_V30 ? kV30Count : is_gnn_train(model) ? 62 : kV24W; }
 // gradient rows of the reverse pass
 int64_t model_train_rows(const gnnd_graph* g, int model, int64_t B) {
     if (is_wbp_train(model)) return gnnd_wbp_train_rows(B);
+    if (is_gnn_train(model)) return gnnd_gnn_train_rows(B);
     return model == GNND_V30 ? gnnd_v30_train_rows(B) : train_rows(g, B);
 }
 
@@ -1233,6 +1237,7 @@ extern "C" int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, 
     const int64_t esz = dtype == GNND_F64 ? 8 : 4;
     *h_bytes = model == GNND_V30 ? esz * gnnd_v30_tape_elems(g, batch, iters)
                : is_wbp_train(model) ? esz * gnnd_wbp_tape_elems(g, batch, iters)
+               : is_gnn_train(model) ? esz * gnnd_gnn_tape_elems(g, batch, iters)
                                      : esz * batch * g->view.E * (3 * (int64_t)iters + 1);
     return GNND_OK;
 }
@@ -1247,6 +1252,9 @@ extern "C" int gnnd_train_fwd(const gnnd_graph* g, int model, int dtype, const v
         return gnnd_launch_v30_tape(g, dtype, d_w, d_x, d_out, batch, iters, d_tape, (hipStream_t)stream);
     if (is_wbp_train(model))
         return gnnd_launch_wbp_tape(g, model, d_w, d_x, d_out, batch, iters, d_tape, (hipStream_t)stream);
+    if (is_gnn_train(model))
+        return gnnd_launch_gnn_tape(g, model, dtype, d_w, d_x, d_out, batch, iters, d_tape,
+                                    (hipStream_t)stream);
     return gnnd_launch_v24_tape(g, dtype, d_w, d_x, d_out, batch, iters, d_tape,
                                 (hipStream_t)stream);
 }
@@ -1309,6 +1317,18 @@ extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const v
         GNND_LAUNCH_CHECK();
         return GNND_OK;
     }
+    if (is_gnn_train(model)) {
+        const int rc = gnnd_launch_gnn_bwd(g, model, dtype, d_w, d_x, d_grad_out, d_tape, d_workspace,
+                                           workspace_bytes, batch, iters, st);
+        if (rc != GNND_OK) return rc;
+        const int rows = (int)gnnd_gnn_train_rows(batch);
+        if (dtype == GNND_F32)
+            grad_reduce_kernel<float><<<1, 256, 0, st>>>((const float*)d_workspace, rows, (float*)d_grad_w, 62);
+        else
+            grad_reduce_kernel<double><<<1, 256, 0, st>>>((const double*)d_workspace, rows, (double*)d_grad_w, 62);
+        GNND_LAUNCH_CHECK();
+        return GNND_OK;
+    }
     if (model == GNND_V30) {
         const int rc = gnnd_launch_v30_bwd(g, dtype, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
                                            workspace_bytes, batch, iters, st);
@@ -1348,6 +1368,9 @@ extern "C" int gnnd_train_bwd_partial(const gnnd_graph* g, int model, int dtype,
                                    workspace_bytes, batch, iters, st);
     if (is_wbp_train(model))
         return gnnd_launch_wbp_bwd(g, model, d_w, d_x, d_out, d_grad_out, d_tape, d_workspace,
+                                   workspace_bytes, batch, iters, st);
+    if (is_gnn_train(model))
+        return gnnd_launch_gnn_bwd(g, model, dtype, d_w, d_x, d_grad_out, d_tape, d_workspace,
                                    workspace_bytes, batch, iters, st);
     if (dtype == GNND_F32)
         return launch_bwd<float>(g, d_w, d_x, d_out, d_grad_out, d_tape, nullptr, d_workspace,
@@ -1392,7 +1415,8 @@ extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64
                                  double* d_step, uint32_t* d_sync, double lr, double beta1,
                                  double beta2, double eps, double weight_decay, void* d_prepared,
                                  void* stream) {
-    if ((model != GNND_V24 && model != GNND_V30) || (dtype != GNND_F32 && dtype != GNND_F64))
+    if ((model != GNND_V24 && model != GNND_V30 && !is_gnn_train(model)) ||
+        (dtype != GNND_F32 && dtype != GNND_F64))
         return GNND_ERR_INVALID_ARG;
     if (n_rows < 0 || batch < 0 || n_rows > 0x7fffffff) return GNND_ERR_INVALID_ARG;
     if (n_rows > 0 && !d_rows) return GNND_ERR_INVALID_ARG;
@@ -1404,7 +1428,8 @@ extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64
     hipStream_t st = (hipStream_t)stream;
     const int nw = train_weights(model);
     const int blocks = (nw + 63) / 64;
-    const int prep_f32 = model == GNND_V24 ? 1 : 0;     // V30's kernel layout is the plain one
+    // V30's, CGNNI's and QGNNI's kernel layouts are the plain one
+    const int prep_f32 = model == GNND_V24 ? 1 : 0;
     const bool lossb = batch > 0 && d_loss_b;
     if (dtype == GNND_F32)
         train_update_kernel<float><<<blocks, kUpdThreads, 0, st>>>(

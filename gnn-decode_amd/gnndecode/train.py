@@ -517,6 +517,112 @@ class FusedV30Trainer(_GraphedStep):
         return out
 
 
+class FusedGnnTrainer(_GraphedStep):
+    """Training step of the 10-hidden-unit GNN decoders on the HIP kernels:
+    CGNNI (classical/CGNNI.py:314-338, fp32) and QGNNI (quantum/QGNNI.py:294-320, fp64):
+
+        forward with tape (gnnd_train_fwd, models CGNNI / QGNNI: every iteration's tanh outputs
+        and the readout inputs) -> the reference LossFunc and d loss / d pred (QGNNI: the
+        logical |sin| loss on gnnd_syndrome_loss; CGNNI: the script's BCE + syndrome loss by
+        torch autograd on the B*V predictions) -> reverse pass to per-workgroup gradient rows
+        (gnnd_train_bwd_partial) -> fused epilogue (gnnd_train_update: fixed-order row
+        reduction, Adam)
+
+    one HIP graph per step (with a collective: split around the all_reduce(SUM) of the flat
+    gradient, as FusedV24Trainer).  The 62 trained parameters (the c->v message MLP: CGNNI
+    ggc2.mlp2, QGNNI ggc2.mlp; the readout mlp) are re-bound as views of the flat packed
+    buffer (gnnd.h layout); the reference's unused MLPs (ggc1's, CGNNI's ggc2.mlp1 and GRU)
+    keep their storage and never change (torch's Adam skips parameters without a gradient).
+    Adam as the scripts: lr 3e-4, weight decay 5e-4."""
+
+    def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
+                 group=None, graph=True, warmup=2, force_collective=False):
+        from .models import CGNNI, QGNNI
+        if not isinstance(model, (CGNNI, QGNNI)):
+            raise TypeError('FusedGnnTrainer trains CGNNI and QGNNI models')
+        rlr, rwd = REFERENCE_OPTIM[model.kind]
+        self.model, self.loss_fn = model, loss_fn
+        self.lr = rlr if lr is None else lr
+        self.wd = rwd if weight_decay is None else weight_decay
+        self.betas, self.eps = betas, eps
+        self._init_graph(graph, warmup, group, force_collective)
+        flat = model.packed_weights().detach().clone().contiguous()
+        msg = model.ggc2.mlp2 if model.kind == 'cgnni' else model.ggc2.mlp
+        off = 0
+        for seq in (msg, model.mlp):
+            for p in (seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias):
+                n = p.numel()
+                p.data = flat[off:off + n].view(p.shape)
+                off += n
+        assert off == flat.numel() == 62
+        self.flat = flat
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.step_count = torch.zeros(1, dtype=torch.float64, device=flat.device)
+        self._sync = torch.zeros(1, dtype=torch.int32, device=flat.device)
+        self._gbuf = torch.zeros(flat.numel() + 1, dtype=flat.dtype, device=flat.device)
+        self._gw = self._gbuf[:flat.numel()]
+        self._loss = self._gbuf[flat.numel()]
+        model.graph(flat.device)                 # device graph tables now, never in a capture
+        g = getattr(loss_fn, '_graph', None)
+        if g is not None:
+            g(flat.device)
+
+    def _reduce(self, loss, grads):
+        dist.all_reduce(self._gbuf, op=dist.ReduceOp.SUM, group=self.group)
+        if self.model.kind == 'cgnni':
+            # CGNNI's LossFunc is a MEAN over the batch (classical/CGNNI.py:302-303): with equal
+            # shards the global-batch gradient and loss are the average over the ranks
+            self._gbuf.div_(dist.get_world_size(self.group))
+
+    def _loss_grad(self, out, y):
+        """(per-codeword (or batch) losses, d loss / d pred)."""
+        pc = getattr(self.loss_fn, 'per_codeword', None)
+        if pc is not None:                       # SyndromeLoss: one gnnd_syndrome_loss launch
+            return pc(out, y)
+        o = out.detach().requires_grad_(True)
+        with torch.enable_grad():
+            loss = self.loss_fn(o, y, train=True) if self.model.kind == 'cgnni' else self.loss_fn(o, y)
+            (d,) = torch.autograd.grad(loss, o)
+        return loss.detach().reshape(1), d
+
+    def _compute(self, x, y):
+        m = self.model
+        g = m.graph(x.device)
+        w = self.flat if self.flat.dtype == x.dtype else self.flat.to(x.dtype)
+        out, tape = ops.train_forward(g, m.kind, x, w, m.Nc)
+        loss_b, d = self._loss_grad(out, y)
+        if self.flat.dtype != x.dtype or self._dist():
+            gw = ops.train_backward(g, m.kind, w, x, out, d, tape, m.Nc)
+            self._gw.copy_(gw)
+            self._loss.copy_(loss_b.sum())
+            self._pending = None
+            return self._loss, [self._gw]
+        ws, nrows = ops.train_backward_partial(g, m.kind, w, x, out, d, tape, m.Nc)
+        self._pending = (ws, nrows, loss_b)
+        return self._loss, []
+
+    def _apply(self):
+        kw = dict(param=self.flat, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq,
+                  step=self.step_count, sync=self._sync, lr=self.lr, betas=self.betas,
+                  eps=self.eps, weight_decay=self.wd)
+        if self._pending is not None:            # single rank: rows -> gradient -> Adam
+            ws, nrows, loss_b = self._pending
+            ops.train_update(self.model.kind, self.flat.dtype, rows=ws, n_rows=nrows, loss_b=loss_b,
+                             loss=self._loss, **kw)
+        else:
+            ops.train_update(self.model.kind, self.flat.dtype, grad=self._gw, **kw)
+
+    def step(self, data, y, copy_loss=True):
+        """One training step; returns the batch loss (copy_loss=False: the step's static loss
+        buffer itself, valid until the next step)."""
+        self.model.train()
+        x = data.x if data.x.dim() == 2 else data.x.unsqueeze(1)
+        out = self._run(x, y, copy_loss)
+        _invalidate(self.model)
+        return out
+
+
 class FusedWbpTrainer(_GraphedStep):
     """Weighted-BP training step on the HIP kernels, fp64 (the scripts' dtype):
     NeuralBP (quantum/neural_BP.py:370-395) and decoder_v2_2 (quantum/decoder_v2_2.py:421-443).
