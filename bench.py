@@ -480,8 +480,9 @@ def train_run(a, world, rank, dev, cpu='full'):
     cpu='full' / 'parity': the CPU training baseline (oracle/torch_train.py), and for 'parity'
     also a K=10-step trajectory of the fused GPU trainer against the oracle's training steps
     on the same codewords; 'off'.  Returns the result dict on rank 0."""
-    code = a.code if a.code.startswith('toric') else 'toric_7'
-    model_name = a.model if a.model in ('v24', 'qgnni', 'nbp', 'v10', 'v22', 'v30') else 'v24'
+    model_name = a.model if a.model in ('v24', 'qgnni', 'nbp', 'v10', 'v22', 'v30', 'cgnni') else 'v24'
+    classical = model_name == 'cgnni'       # classical/CGNNI.py trains on a classical code
+    code = a.code if (a.code.startswith('toric') or classical) else 'toric_7'
     T = a.iters or gd.DEFAULT_ITERS[model_name]
     dtype = torch.float64 if a.dtype == 'f64' else torch.float32
     H = gd.codes.get_code(code)
@@ -492,7 +493,7 @@ def train_run(a, world, rank, dev, cpu='full'):
         wsrc = v24_start_weights(model, code)
     model = model.to(dev).to(dtype)
     init_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    fused = (model_name in ('v24', 'v30') or
+    fused = (model_name in ('v24', 'v30', 'qgnni', 'cgnni') or
              (model_name in ('nbp', 'v22') and dtype == torch.float64)) and not a.layerwise
     if model_name == 'v24':
         model.fused_train = fused
@@ -500,6 +501,8 @@ def train_run(a, world, rank, dev, cpu='full'):
         lf = gd.loss.PerLayerLoss(H, gd.codes.toric_logicals(H)).to(dev)
     elif model_name == 'v30':        # decoder_v3_0's LossFunc (two-output readout)
         lf = gd.loss.V30Loss(H).to(dev)
+    elif classical:                  # classical/CGNNI.py LossFunc (BCE + syndrome term)
+        lf = gd.loss.ClassicalLoss(H).to(dev)
     else:
         lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H),
                                   logical_only=(model_name == 'qgnni')).to(dev)
@@ -509,7 +512,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     launch = getattr(a, 'launch', 'auto')
     if a.no_graph:
         launch = 'eager'
-    fused_v24 = fused and model_name not in ('nbp', 'v22', 'v30') and not a.torch_trainer
+    fused_v24 = fused and model_name == 'v24' and not a.torch_trainer
     if launch == 'auto':
         # the fused V24 step is three kernels: eager stream launches leave no idle time between
         # steps, graph replays ~9 us (r03ac); the torch Trainer (~80 launches) keeps its graph
@@ -521,13 +524,21 @@ def train_run(a, world, rank, dev, cpu='full'):
     elif fused and model_name == 'v30':
         # fwd+tape -> reference LossFunc (torch) -> reverse pass -> [all_reduce] -> Adam
         tr = gd.train.FusedV30Trainer(model, lf, graph=use_graph, warmup=2)
+    elif fused and model_name in ('qgnni', 'cgnni'):
+        # fwd+tape -> reference LossFunc -> reverse pass -> [all_reduce] -> fused epilogue
+        tr = gd.train.FusedGnnTrainer(model, lf, graph=use_graph, warmup=2)
     elif fused_v24:
         # fwd+tape (+ fused syndrome loss) -> reverse pass -> [all_reduce] -> fused epilogue
         tr = gd.train.FusedV24Trainer(model, lf, graph=use_graph, warmup=2)
     else:
-        tr = gd.train.Trainer(model, lf, graph=use_graph, warmup=2)   # captured after 2 eager steps
-    x, y = gd.data.toric_batch(H, a.batch, seed=a.seed, offset=rank * a.batch, device=dev,
-                               dtype=dtype)
+        loss = (lambda p, yy: lf(p, yy, train=True)) if classical else lf
+        tr = gd.train.Trainer(model, loss, graph=use_graph, warmup=2)   # captured after 2 eager steps
+    if classical:                    # random codewords under AWGN (Gen_Data.AWGN)
+        x, y = gd.data.awgn_batch(H, a.batch, codewords='random', seed=a.seed, offset=rank * a.batch,
+                                  device=dev, dtype=dtype)
+    else:
+        x, y = gd.data.toric_batch(H, a.batch, seed=a.seed, offset=rank * a.batch, device=dev,
+                                   dtype=dtype)
     data = gd.data.make_batch(x, model.graph(dev))
     for _ in range(a.warmup):
         tr.step(data, y)
@@ -537,7 +548,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     if st is not None:
         data.x, y = st
     fused_tr = isinstance(tr, (gd.train.FusedV24Trainer, gd.train.FusedV30Trainer,
-                               gd.train.FusedWbpTrainer))
+                               gd.train.FusedWbpTrainer, gd.train.FusedGnnTrainer))
     elapsed, issue_s, loss = time_train_steps(tr, data, y, a.steps, fused_tr)
     # the same step with its RCCL all_reduce(SUM) of the flat gradient + loss actually issued:
     # N > 1 runs already contain it; a 1-GPU run times it on a 1-rank RCCL group
@@ -568,7 +579,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     if rank == 0:
         step_s = elapsed / a.steps
         roof = None
-        if model_name in ('v24', 'v30', 'nbp', 'v22') and fused:
+        if model_name in ('v24', 'v30', 'nbp', 'v22', 'qgnni', 'cgnni') and fused:
             # training ~ 3x the forward's algorithmic FLOPs: forward, the
             # reverse pass through every MLP (2x); transcendentals: forward Softplus + the
             # backward sigmoid of every unit.  Whole step over its wall time per step.
@@ -592,7 +603,8 @@ def train_run(a, world, rank, dev, cpu='full'):
             'ms_per_step_with_collective': coll['ms_per_step'] if coll else None,
             'collective': coll,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': a.dtype,
-            'data': f'synthetic toric errors (on-device sampler, seeded); start weights: {wsrc}',
+            'data': (f'synthetic {"AWGN random codewords" if classical else "toric errors"} '
+                     f'(on-device sampler, seeded); start weights: {wsrc}'),
             'config': {'workload': f'{code} {model_name} training step, T={T}, batch={a.batch}/GPU',
                        'global_batch': a.batch * world, 'parallelism': f'dp{world}',
                        'last_loss': float(loss),
@@ -620,6 +632,9 @@ def train_path_string(tr, model_name, use_graph):
     if isinstance(tr, gd.train.FusedV30Trainer):
         return (f'FusedV30Trainer ({how}): gnnd_train_fwd (V30), V30Loss.loss_and_grad, '
                 f'gnnd_train_bwd_partial, gnnd_train_update')
+    if isinstance(tr, gd.train.FusedGnnTrainer):
+        return (f'FusedGnnTrainer ({how}): gnnd_train_fwd ({model_name}), the reference LossFunc '
+                f'and d loss / d pred, gnnd_train_bwd_partial, gnnd_train_update')
     if isinstance(tr, gd.train.FusedWbpTrainer):
         return (f'FusedWbpTrainer ({how}): packed weights, gnnd_train_fwd, gnnd_syndrome_loss, '
                 f'gnnd_train_bwd, gnnd_adam_step')

@@ -129,6 +129,12 @@ struct GraphView {            // passed by value to kernels
     // The identity layout (vgroup 1) is var_ord with positions = edge ids, spare = E.
     const uint2* vlay;        // [V]
     int vgroup, spare, P1;
+    // T layout of the fp32 resident kernel (x-augmented layouts, gnnd_graph::rlayx): T_v of
+    // codeword b sits at LDS row b * ts + tpos(v), tpos in the high half of vlay[i].y (its low
+    // half is the first message position) and in the low half of slot_ve (instead of v);
+    // placed for bank-conflict-free-er gathers (gnnd_graph.hip place_t_rows).  Identity
+    // elsewhere: ts = V, tpos(v) = v.
+    int ts;
     // where this graph's rows sit in the caller's batch layout.  A whole graph: identity
     // (xs = N, xv0 = 0, xc0 = V, os = V, o0 = 0, es = E, e0 = 0).  A COMPONENT of a split
     // graph (gnnd_graph::comp) addresses its slice of the parent codeword's rows: variable v

@@ -1459,6 +1459,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     const int V = g.V, C = g.C, E = g.E, N = g.N;
     const int E1 = g.P1;                  // message positions per codeword (layout stride)
     const int spare = g.spare;            // position padding slots and idle items write
+    // T layout: codeword b's T_v at b * TS + tpos(v) (tpos in the slot tables' low halves and
+    // vlay .y's high half; gnnd_graph.hip place_t_rows); {S_v, x_v} rows stay b * V + v
+    const int TS = kTX ? g.ts : V;
     const int tid = threadIdx.x;
 
     T* s_w = (T*)smem;
@@ -1471,7 +1474,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     // kTX: [CW][V] T_v in place of {S_v, x_v}; x_v lives in the message layout
     // (gnnd_graph::rlayx: the last position of each variable's run)
     float* s_t = (float*)s_sx;
-    if constexpr (kTX) s_xc = (T*)(s_t + (size_t)CW * V);
+    if constexpr (kTX) s_xc = (T*)(s_t + (size_t)CW * TS);
 
     for (int i = tid; i < nw; i += GNND_BLOCK) s_w[i] = w[i];
     for (int i = tid; i < V; i += GNND_BLOCK) s_vord[i] = g.vlay[i];
@@ -1480,13 +1483,13 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     const TI* xg = x + b0 * N;
     for (int i = tid; i < nb * N; i += GNND_BLOCK) {
         int b = fdiv(i, dN), n = i - b * N;
-        T xv = io_ld(xg[i]);
         if (n < V) {
-            const T xs = kBase2 ? xv * T(kLog2e) : xv;
-            if constexpr (kTX) s_t[b * V + n] = xs;     // T = 0 + x
-            else s_sx[b * V + n] = SumX<T>{T(0), xs};
+            if constexpr (!kTX) {                       // (T layout: below, in var_ord order)
+                const T xv = io_ld(xg[i]);
+                s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
+            }
         } else {
-            s_xc[b * C + n - V] = xv;
+            s_xc[b * C + n - V] = io_ld(xg[i]);
         }
     }
     // padded layouts: the positions past a variable's degree are read by the variable sums
@@ -1495,12 +1498,16 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         for (int i = tid; i < CW * E1; i += GNND_BLOCK) s_m[i] = T(0);
     __syncthreads();
     if constexpr (kTX) {
-        // x_v into the last position of its run (after the padded messages: S + 0 + x_v)
+        // T_v = 0 + x_v at its T row, and x_v into the last position of its message run (after
+        // the padded messages: S + 0 + x_v)
         for (int i = tid; i < nb * V; i += GNND_BLOCK) {
             const int b = fdiv(i, dV), j = i - b * V;
             const uint2 o = s_vord[j];
             const int v = GNND_DIDX((int)(o.x & 0xffffu), V, GNND_DBG_VAR);
-            s_m[b * E1 + GNND_DIDX((int)o.y + (int)(o.x >> 16) - 1, E1, GNND_DBG_LDS_POS)] = s_t[b * V + v];
+            const T xv = io_ld(xg[b * N + v]);
+            const T xs = kBase2 ? xv * T(kLog2e) : xv;
+            s_t[b * TS + GNND_DIDX((int)(o.y >> 16), TS, GNND_DBG_VAR)] = xs;
+            s_m[b * E1 + GNND_DIDX((int)(o.y & 0xffffu) + (int)(o.x >> 16) - 1, E1, GNND_DBG_LDS_POS)] = xs;
         }
         __syncthreads();
     }
@@ -1572,7 +1579,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     const bool vfixed = GNND_BLOCK % CW == 0;
     const int vb = tid % CW, vi0 = tid / CW, vstep = GNND_BLOCK / CW;
     const bool vact = vb < nb;
-    const int vmbase = vb * E1, vsbase = vb * V;
+    const int vmbase = vb * E1, vsbase = vb * V, vtbase = vb * TS;
     // a wave covers 64 / CW consecutive var_ord entries per step: uniform when the layout
     // pads each such group to one degree (weighted BP keeps the identity layout: its
     // per-edge weight tables are indexed by edge id)
@@ -1650,7 +1657,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             auto pre2 = [&](uint32_t sa, uint32_t sb, int ca, int cbb, f32x2 mprev, int ra, int rb,
                             f32x2& cc) {
                 if constexpr (kTX)
-                    return pre2t(f32x2{s_t[ca * V + (int)(sa & 0xffffu)], s_t[cbb * V + (int)(sb & 0xffffu)]},
+                    return pre2t(f32x2{s_t[ca * TS + (int)(sa & 0xffffu)], s_t[cbb * TS + (int)(sb & 0xffffu)]},
                                  sa, sb, mprev, ra, rb, cc);
                 else
                     return pre2v(s_sx[ca * V + (int)(sa & 0xffffu)], s_sx[cbb * V + (int)(sb & 0xffffu)],
@@ -1665,8 +1672,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             auto load_pair = [&](int j, PX (&px)[R]) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const int ia = cb[2 * j] * V + GNND_DIDX((int)(ve[2 * j][r] & 0xffffu), V, GNND_DBG_VAR);
-                    const int ib = cb[2 * j + 1] * V + GNND_DIDX((int)(ve[2 * j + 1][r] & 0xffffu), V, GNND_DBG_VAR);
+                    // (T layout: row stride TS, the slot's low half is tpos(v))
+                    const int ia = cb[2 * j] * TS + GNND_DIDX((int)(ve[2 * j][r] & 0xffffu), TS, GNND_DBG_VAR);
+                    const int ib = cb[2 * j + 1] * TS + GNND_DIDX((int)(ve[2 * j + 1][r] & 0xffffu), TS, GNND_DBG_VAR);
                     if constexpr (kTX) {
                         px[r] = f32x2{s_t[ia], s_t[ib]};
                     } else {
@@ -1891,7 +1899,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         // the variable step's result for variable v of codeword b (sum s of its messages):
         // last iteration -> readout (GNN T layout: s = S' base-2 scaled, S + x = s ln2 + x);
         // otherwise the check step's operand (T_v = s + x_v, or S_v of {S_v, x_v})
-        auto var_out = [&](int b, int sbase, int v, T s) {
+        auto var_out = [&](int b, int sbase, int tbase, int v, int tp, T s) {
             if (last) {
                 T r;
                 if constexpr (kTX && kBase2) r = s * kLn2;          // (S' + x') ln2 = S + x
@@ -1899,23 +1907,25 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 else r = s + (kBase2 ? io_ld(xg[b * N + v]) : s_sx[sbase + v].x);
                 out[b0 * V + sbase + v] = io_st<TI>(M::readout(r, s_w));
             } else if constexpr (kTX) {
-                s_t[sbase + v] = s;                                   // T_v = S_v + x_v
+                s_t[tbase + tp] = s;                                  // T_v = S_v + x_v
+                (void)v;
             } else {
                 s_sx[sbase + v].s = s;
             }
         };
-        // one variable-item (codeword b, degree-order index i); mbase = b (E+1), sbase = b V
-        auto var_item = [&](int b, int i, int mbase, int sbase) {
+        // one variable-item (codeword b, degree-order index i); mbase = b E1, sbase = b V,
+        // tbase = b TS
+        auto var_item = [&](int b, int i, int mbase, int sbase, int tbase) {
             const uint2 o = s_vord[i];
             const int v = (int)(o.x & 0xffffu), dv = (int)(o.x >> 16);
-            const T* mp = s_m + mbase + (int)o.y;
+            const T* mp = s_m + mbase + (int)(o.y & 0xffffu);
             if constexpr (MODEL == GNND_V22) {
                 // decoder_v2_2.py:333-347: the check step publishes raw messages (identity
                 // layout: positions = edge ids); the variable step forms the next layer's
                 // S'_v = sum_e m_e W_{t+1}[e] (its v->c input, as in neural_BP) and the
                 // iteration's readout sigmoid(-(sum_e m_e W[e] + sum_e x_v W_pr[e])), every
                 // sum in edge (index_add) order
-                const int e0 = (int)o.y;
+                const int e0 = (int)(o.y & 0xffffu);
                 const T xv = s_sx[sbase + v].x;
                 T sn = T(0), so = T(0), s2 = T(0);
                 for (int k = 0; k < dv; ++k) {
@@ -1945,12 +1955,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 if (last) {   // + sum_v(x_v W_p)  (neural_BP.py:307-312)
                     const T xv = s_sx[sbase + v].x;
                     T s2 = T(0);
-                    for (int j = 0; j < dv; ++j) s2 += xv * ww.out_p((int)o.y + j);
+                    for (int j = 0; j < dv; ++j) s2 += xv * ww.out_p((int)(o.y & 0xffffu) + j);
                     out[b0 * V + sbase + v] = io_st<TI>(sigmoid_ref(-(s + s2)));
                     return;
                 }
             }
-            var_out(b, sbase, v, s);
+            var_out(b, sbase, tbase, v, (int)(o.y >> 16), s);
         };
         if (vuni) {
             // padded layout (GraphView::vlay): the wave's vgroup variables share one padded
@@ -1962,20 +1972,21 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     const uint2 o = s_vord[i];
                     const int dp = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));
                     const int v = (int)(o.x & 0xffffu);
-                    GNND_DCHECK(v < V && (int)o.y + dp <= E1, GNND_DBG_LDS_POS);
-                    var_out(vb, vsbase, v, var_sum_uniform(s_m + vmbase + (int)o.y, dp));
+                    GNND_DCHECK(v < V && (int)(o.y & 0xffffu) + dp <= E1, GNND_DBG_LDS_POS);
+                    var_out(vb, vsbase, vtbase, v, (int)(o.y >> 16),
+                            var_sum_uniform(s_m + vmbase + (int)(o.y & 0xffffu), dp));
                 }
         } else if (vfixed) {
             // CW divides 256: f = tid + k 256 keeps f mod CW, so the lane's codeword and its
             // LDS bases are loop-invariant (no per-item division or 32-bit multiplies: those
             // are quarter-rate and cost as much as the sums themselves)
             if (vact)
-                for (int i = vi0; i < V; i += vstep) var_item(vb, i, vmbase, vsbase);
+                for (int i = vi0; i < V; i += vstep) var_item(vb, i, vmbase, vsbase, vtbase);
         } else {
             for (int f = tid; f < V * CW; f += GNND_BLOCK) {
                 const int i = fdiv(f, dItem), b = f - i * CW;
                 if (b >= nb) continue;
-                var_item(b, i, b * E1, b * V);
+                var_item(b, i, b * E1, b * V, b * TS);
             }
         }
         if constexpr (GNND_VAR_PRIO > 0) __builtin_amdgcn_s_setprio(0);
@@ -2153,9 +2164,10 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         // [CW][C].  Pick (CW, Q) with Q in kResidentQ maximising lane utilisation
         // CW*IC / (Q*256), ties to the larger tile.
         const size_t fixed = wb + align16((size_t)g.V * 8);
-        auto lds_of = [&](int cw) {     // messages, then {S_v, x_v} (T layout: T_v), x_c
-            return fixed + esz * (((size_t)cw * lay_of(cw)->P1 + 1) & ~(size_t)1) +
-                   esz * ((size_t)cw * ((tx ? 1 : 2) * (size_t)g.V + g.C));
+        auto lds_of = [&](int cw) {     // messages, then {S_v, x_v} (T layout: T_v rows), x_c
+            const GraphView* l = lay_of(cw);
+            return fixed + esz * (((size_t)cw * l->P1 + 1) & ~(size_t)1) +
+                   esz * ((size_t)cw * (tx ? (size_t)l->ts : 2 * (size_t)g.V) + (size_t)cw * g.C);
         };
         const bool tx_ok = !tx || gr->rlayx[0].vlay != nullptr;   // else: streaming kernel
         int best = 0, bestq = 0;

@@ -49,6 +49,8 @@ struct Layout {
     bool ok = false;
     int P = 0;
     std::vector<int> vlay, slot;     // [2V] {v | dpad << 16, pos}, [nsr] v | pos << 16
+    int ts = 0;                      // x layouts: T row stride and positions (place_t_rows);
+    std::vector<int> tpos;           // vlay .y high half and slot low half hold tpos(v)
 };
 // everything gnnd_graph_create uploads, built on the host (also checked by
 // gnnd_graph_validate_host without a device)
@@ -162,6 +164,150 @@ void spread_check_slots(int C, int G, int R, int cw, int P, const std::vector<in
     if (log) {
         fprintf(stderr, "gnnd slot spread: C=%d G=%d R=%d cw=%d P1=%d store cycles per tile "
                         "iteration %ld -> %ld\n", C, G, R, cw, P1, init_cost, bestc);
+    }
+}
+
+// GNND_NO_TPERM=1: the x layouts keep T rows in variable order (ts = V, tpos(v) = v) (A/B)
+bool tperm_disabled() {
+    static bool v = [] {
+        const char* e = getenv("GNND_NO_TPERM");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+// Placement of the resident fp32 kernel's T rows (T_v of codeword b at b * ts + tpos(v)) for
+// a tile of cw codewords, after spread_check_slots fixed the slot rows: the check step gathers
+// T_v of slot row r with one ds_read_b32 per item round (lanes f = (c * cw + b) * G + g), the
+// variable step writes T_v of 256 / cw consecutive var_ord entries x cw codewords per row of
+// lanes (lane t: codeword t % cw, entry t / cw).  Cycles of a 32-lane group = distinct
+// addresses on its busiest bank.  For each candidate stride (V, and the next ones = 8, 24, 16
+// mod 32 and odd) a deterministic annealing over the positions (swaps, moves into free
+// positions) minimises the summed cycles; the best stride wins (ties: the smaller).
+// BCH(63,45), cw = 16: gathers 432 -> ~350, writes ~63 -> ~70 cycles per tile iteration.
+void place_t_rows(int C, int G, int R, int cw, int V, const std::vector<int>& vord,
+                  const std::vector<int>& cdeg, const std::vector<int>& slot, int& ts_out,
+                  std::vector<int>& tpos_out) {
+    const int GR = G * R;
+    const long items = (long)C * cw * G;
+    const int nh = (int)((items + 31) / 32);
+    // groups: (stride b, variable) lanes; gathers then variable-step writes
+    std::vector<std::vector<std::pair<int, int>>> grp;
+    for (int h = 0; h < nh; ++h)
+        for (int r = 0; r < R; ++r) {
+            std::vector<std::pair<int, int>> L;
+            for (int f = 32 * h; f < 32 * h + 32 && f < items; ++f) {
+                const int gi = f / G, g = f % G, c = gi / cw, b = gi % cw, k = g * R + r;
+                const int v = k < cdeg[c] ? (slot[(size_t)c * GR + k] & 0xffff) : 0;
+                L.push_back({b, v});
+            }
+            grp.push_back(L);
+        }
+    if (cw <= 32 && 256 % cw == 0) {
+        const int per = 256 / cw;                       // var_ord entries per block row
+        for (int i0 = 0; i0 < V; i0 += per)
+            for (int h = 0; h < 8; ++h) {               // 8 half-waves of the 256 lanes
+                std::vector<std::pair<int, int>> L;
+                for (int t = 32 * h; t < 32 * h + 32; ++t) {
+                    const int i = i0 + t / cw;
+                    if (i < V) L.push_back({t % cw, vord[i]});
+                }
+                if (!L.empty()) grp.push_back(L);
+            }
+    }
+    const int ng = (int)grp.size();
+    std::vector<std::vector<int>> of_var(V);
+    for (int q = 0; q < ng; ++q) {
+        int last = -1;
+        std::vector<int> vs;
+        for (auto& bv : grp[q]) vs.push_back(bv.second);
+        std::sort(vs.begin(), vs.end());
+        for (int v : vs)
+            if (v != last) { of_var[v].push_back(q); last = v; }
+    }
+    auto cost_of = [&](int q, int ts, const std::vector<int>& tp) {
+        int addr[32], n = 0;
+        for (auto& bv : grp[q]) {
+            const int a = bv.first * ts + tp[bv.second];
+            bool dup = false;
+            for (int i = 0; i < n && !dup; ++i) dup = addr[i] == a;
+            if (!dup) addr[n++] = a;
+        }
+        int cnt[32] = {0}, m = 0;
+        for (int i = 0; i < n; ++i) m = std::max(m, ++cnt[addr[i] & 31]);
+        return m;
+    };
+    std::vector<int> cands = {V};
+    for (int want : {8, 24, 1}) {
+        int t = V + 1;
+        while (want == 1 ? (t % 2 == 0) : (t % 32 != want)) ++t;
+        cands.push_back(t);
+    }
+    long best_total = -1;
+    for (int ts : cands) {
+        std::vector<int> tp(V), pos_owner(ts, -1);
+        for (int v = 0; v < V; ++v) { tp[v] = v; pos_owner[v] = v; }
+        std::vector<int> gc(ng);
+        long cur = 0;
+        for (int q = 0; q < ng; ++q) cur += gc[q] = cost_of(q, ts, tp);
+        long bestc = cur;
+        std::vector<int> best = tp;
+        uint64_t s = 0x2545F4914F6CDD1Dull ^ (uint64_t)ts;
+        auto rnd = [&](uint64_t n) {
+            s = s * 6364136223846793005ull + 1442695040888963407ull;
+            return (uint64_t)(s >> 33) % n;
+        };
+        const long iters = std::min(40L * V, 10000L);
+        std::vector<int> touched, nc;
+        for (long it = 0; it < iters; ++it) {
+            const int a = (int)rnd(V);
+            const int p2 = (int)rnd(ts);                 // target position: swap with its owner
+            const int b = pos_owner[p2];
+            if (b == a) continue;
+            const int pa = tp[a];
+            tp[a] = p2;
+            if (b >= 0) tp[b] = pa;
+            touched.clear();
+            for (int q : of_var[a]) touched.push_back(q);
+            if (b >= 0) for (int q : of_var[b]) touched.push_back(q);
+            std::sort(touched.begin(), touched.end());
+            touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+            long delta = 0;
+            nc.resize(touched.size());
+            for (size_t i = 0; i < touched.size(); ++i) {
+                nc[i] = cost_of(touched[i], ts, tp);
+                delta += nc[i] - gc[touched[i]];
+            }
+            const double temp = 2.0 * (1.0 - (double)it / iters) + 0.05;
+            const double u = (double)rnd(1u << 30) / (double)(1u << 30);
+            if (delta <= 0 || u < exp(-(double)delta / temp)) {
+                for (size_t i = 0; i < touched.size(); ++i) gc[touched[i]] = nc[i];
+                cur += delta;
+                pos_owner[p2] = a;
+                pos_owner[pa] = b;
+                if (cur < bestc) { bestc = cur; best = tp; }
+            } else {
+                tp[a] = pa;
+                if (b >= 0) tp[b] = p2;
+            }
+        }
+        if (best_total < 0 || bestc < best_total) {
+            best_total = bestc;
+            ts_out = ts;
+            tpos_out = best;
+        }
+    }
+    static const bool log = [] {
+        const char* e = getenv("GNND_SLOT_SPREAD_LOG");
+        return e && e[0] == '1';
+    }();
+    if (log) {
+        std::vector<int> id(V);
+        for (int v = 0; v < V; ++v) id[v] = v;
+        long c0 = 0;
+        for (int q = 0; q < ng; ++q) c0 += cost_of(q, V, id);
+        fprintf(stderr, "gnnd t rows: C=%d G=%d R=%d cw=%d gather+write cycles per tile iteration "
+                        "%ld (ts = V) -> %ld (ts = %d)\n", C, G, R, cw, c0, best_total, ts_out);
     }
 }
 
@@ -287,10 +433,26 @@ int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, 
         // x-augmented layouts of the register-resident fp32 kernel (tiles of cw = 64 / gs
         // codewords): each check's edges over its slot rows for conflict-free-er message stores
         // (group sizes the register-resident kernel instantiates: G <= 16)
-        if (with_x && gs >= 2 && gs <= 32 && plans[1].G <= 16 && !slot_spread_disabled()) {
+        // (tiles the plan can take: cw * C * G items within kResidentQ's largest 12 per lane)
+        const bool tile_ok = (long)(64 / gs) * C * plans[1].G <= 12L * 256;
+        if (with_x && gs >= 2 && gs <= 32 && plans[1].G <= 16 && tile_ok && !slot_spread_disabled()) {
             std::vector<int> cdeg(C);
             for (int c = 0; c < C; ++c) cdeg[c] = cptr[c + 1] - cptr[c];
             spread_check_slots(C, plans[1].G, plans[1].R, 64 / gs, pos, cdeg, L.slot);
+        }
+        L.ts = V;
+        L.tpos.resize(V);
+        for (int v = 0; v < V; ++v) L.tpos[v] = v;
+        if (with_x && gs >= 2 && gs <= 32 && plans[1].G <= 16 && tile_ok && !tperm_disabled()) {
+            std::vector<int> cdeg(C), vo(V);
+            for (int c = 0; c < C; ++c) cdeg[c] = cptr[c + 1] - cptr[c];
+            for (int j = 0; j < V; ++j) vo[j] = L.vlay[2 * j] & 0xffff;
+            place_t_rows(C, plans[1].G, plans[1].R, 64 / gs, V, vo, cdeg, L.slot, L.ts, L.tpos);
+        }
+        if (with_x) {       // positions travel in 16 bits: ts <= 65535
+            for (int j = 0; j < V; ++j) L.vlay[2 * j + 1] |= L.tpos[L.vlay[2 * j] & 0xffff] << 16;
+            for (int k = 0; k < nsr; ++k)
+                L.slot[k] = (L.slot[k] & ~0xffff) | L.tpos[L.slot[k] & 0xffff];
         }
     };
     Layout* lays = T.lays;
@@ -385,9 +547,21 @@ int check_tables(const HostTables& T, int32_t* report) {
             ++nlay;
             std::vector<int> owner(L.P + 1, -1), epos(E, -1);
             int expect = 0;
+            // x layouts: T row positions, a one-to-one map into [0, ts)
+            const bool tx = x != 0;
+            const int ts = tx ? L.ts : V;
+            if (tx) {
+                std::vector<int> used(ts > 0 ? ts : 1, 0);
+                if ((int)L.tpos.size() != V || ts < V || ts > 65535) ++fails;
+                else
+                    for (int v = 0; v < V; ++v)
+                        if (L.tpos[v] < 0 || L.tpos[v] >= ts || used[L.tpos[v]]++) ++fails;
+            }
+            auto tp = [&](int v) { return tx && (int)L.tpos.size() == V ? L.tpos[v] : v; };
             for (int j = 0; j < V; ++j) {
                 const int v = L.vlay[2 * j] & 0xffff, dpad = (int)((uint32_t)L.vlay[2 * j] >> 16);
-                const int pos = L.vlay[2 * j + 1];
+                const int pos = L.vlay[2 * j + 1] & 0xffff;
+                if (((uint32_t)L.vlay[2 * j + 1] >> 16) != (uint32_t)(tx ? tp(v) : 0)) ++fails;
                 const int deg = vptr[v + 1] - vptr[v];
                 if (pos != expect || dpad < deg + x || pos + dpad > L.P) { ++fails; continue; }
                 expect = pos + dpad;
@@ -416,7 +590,7 @@ int check_tables(const HostTables& T, int32_t* report) {
                         continue;
                     }
                     const int e = pos <= L.P ? epos_inv[pos] : -1;
-                    if (e < 0 || (int)(t[e] >> 16) != c || (int)(sl & 0xffffu) != (int)(t[e] & 0xffff) ||
+                    if (e < 0 || (int)(t[e] >> 16) != c || (int)(sl & 0xffffu) != tp((int)(t[e] & 0xffff)) ||
                         seen[e]++)
                         ++fails;
                 }
@@ -479,6 +653,7 @@ int create_single(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
     gv.chk_edge = d + E + V + 1 + C + 1;
     gv.var_ord = (const uint2*)(d + ord_off);
     gv.xs = V + C; gv.xv0 = 0; gv.xc0 = V; gv.os = V; gv.o0 = 0; gv.es = E; gv.e0 = 0;
+    gv.ts = V;
     g->ncomp = 1;
     g->rview = gv;
     g->pview = gv;
@@ -509,6 +684,7 @@ int create_single(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
             lv.slot_ve = (const uint32_t*)(d + o + 2 * V);
             lv.spare = L.P;
             lv.P1 = (L.P + 1) | 1;          // odd codeword stride, spare slot included
+            lv.ts = x ? L.ts : V;
         }
     }
     *out = g;

@@ -219,8 +219,11 @@ int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan)
  * 245-290, fp32/fp64; d_out / d_grad_out are the two readout tensors [2][B*N]), and fp64 NBP
  * (quantum/neural_BP.py:263-314) and V22 (quantum/decoder_v2_2.py:299-347; d_out /
  * d_grad_out every layer's readout [T][B*V]) whose gradient is w.r.t. the per-edge tables
- * of their packed layout (2 E T + 2 E + 1 values).  The other models train through
- * gnnd_propagate_*_bwd.  gnnd_train_workspace_bytes sizes the workspace of every model
+ * of their packed layout (2 E T + 2 E + 1 values), CGNNI (classical/CGNNI.py:248-284) and
+ * QGNNI (quantum/QGNNI.py:217-252), fp32/fp64, gradient w.r.t. their 62 packed weights (the
+ * forward writes its own tape: every iteration's tanh outputs and the readout inputs; d_out
+ * is its prediction, not gnnd_decode's register-resident one bit for bit).  The other models
+ * train through gnnd_propagate_*_bwd.  gnnd_train_workspace_bytes sizes the workspace of every model
  * (gnnd_train_bwd_workspace, which has no iteration count, only V24 and V30).             */
 int gnnd_train_tape_bytes(const gnnd_graph* g, int model, int dtype, int64_t batch,
                           int32_t iters, int64_t* h_bytes);
@@ -235,8 +238,9 @@ int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const void* d_w, c
                    void* d_grad_w, void* d_workspace, int64_t workspace_bytes, int64_t batch,
                    int32_t iters, void* stream);
 /* The reverse pass without its reduction: leaves gnnd_train_bwd_rows() per-workgroup
- * gradient rows [rows][n] (n = the model's weights: V24 1283, V30 137, NBP/V22 2ET + 2E + 1)
- * in d_workspace, for gnnd_train_update (V24, V30) to reduce (fused with
+ * gradient rows [rows][n] (n = the model's weights: V24 1283, V30 137, CGNNI/QGNNI 62,
+ * NBP/V22 2ET + 2E + 1) in d_workspace, for gnnd_train_update (V24, V30, CGNNI, QGNNI) to
+ * reduce (fused with
  * the optimizer).  On a split graph (gnnd_graph_components > 1) every component of a
  * codeword runs in its own workgroup.                                                     */
 int gnnd_train_bwd_rows(const gnnd_graph* g, int model, int dtype, int64_t batch,
@@ -273,8 +277,8 @@ int gnnd_train_fwd_loss(const gnnd_graph* g, int model, int dtype, const void* d
  *   n_rows > 0: d_grad[i] = fixed-order sum of the rows (d_grad may be NULL: not stored);
  *   n_rows = 0: the gradient is read from d_grad (e.g. after an all-reduce of it);
  *   d_loss_b [batch] non-NULL: *d_loss = fixed-order sum of the per-codeword losses;
- *   d_param non-NULL: gnnd_adam_step's update of the plain packed weights (V24 1283, V30 137;
- *   the V30 kernel layout is the plain one) (moments
+ *   d_param non-NULL: gnnd_adam_step's update of the plain packed weights (V24 1283, V30 137,
+ *   CGNNI/QGNNI 62; the V30, CGNNI and QGNNI kernel layouts are the plain one) (moments
  *   d_exp_avg / d_exp_avg_sq, device step count *d_step incremented once), then, if
  *   d_prepared is non-NULL, gnnd_prepare_weights' kernel layout of the updated weights into
  *   d_prepared.  d_sync: one device uint32, zero before the first call (the kernel leaves it
