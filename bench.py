@@ -72,7 +72,8 @@ def parse():
                    help='decode mode: untimed seconds of steps before the W warm-up steps '
                         '(GPU clocks ramp over the first tens of ms of load; the K timed '
                         'steps then measure the steady state)')
-    p.add_argument('--model', default='cgnni', choices=list(gd.MODELS))
+    p.add_argument('--model', default=None, choices=list(gd.MODELS),
+                   help='default: cgnni (decode: the headline), v24 (--mode train: config 5)')
     p.add_argument('--code', default='bch_63_45')
     p.add_argument('--batch', type=int, default=65536, help='codewords per GPU')
     p.add_argument('--iters', type=int, default=None)
@@ -899,6 +900,8 @@ def sub_config_results(a, world, rank, dev):
 
 def main():
     a = parse()
+    if a.model is None:
+        a.model = 'v24' if a.mode == 'train' else 'cgnni'
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))

@@ -520,3 +520,27 @@ def test_config5_trajectory_matches_oracle_L7_B128_f64():
     for k, p in st.p.items():
         d = float((sd[k].detach().cpu() - p.detach()).abs().max())
         assert d <= 1e-10, (k, d)
+
+
+def test_fused_v24_trainer_sees_weights_loaded_after_construction():
+    """load_state_dict (or any in-place parameter edit) after FusedV24Trainer was built: the next
+    step must run on the loaded weights.  The parameters are views of the trainer's flat buffer
+    that keep their own version counters, so the trainer tracks those."""
+    import gnndecode as gd
+    H = gd.codes.toric_code(5)
+    lg = gd.codes.toric_logicals(H)
+    torch.manual_seed(21)
+    a = gd.MODELS['v24'](5, H).to(DEV)
+    other = gd.MODELS['v24'](5, H).to(DEV)            # different (seeded) weights
+    ta = gd.train.FusedV24Trainer(a, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=False)
+    a.load_state_dict(other.state_dict())
+    b = gd.MODELS['v24'](5, H).to(DEV)
+    b.load_state_dict(other.state_dict())
+    tb = gd.train.FusedV24Trainer(b, gd.loss.SyndromeLoss(H, lg).to(DEV), graph=False)
+    x, y = gd.data.toric_batch(H, 32, seed=9, device=DEV)
+    for _ in range(2):
+        la = float(ta.step(gd.data.make_batch(x, a.graph(x.device)), y))
+        lb = float(tb.step(gd.data.make_batch(x, b.graph(x.device)), y))
+        assert la == lb, (la, lb)
+    for k, v in b.state_dict().items():
+        assert torch.equal(a.state_dict()[k], v), k

@@ -7,6 +7,7 @@
 #   train_prof  rocprofv3 kernel trace of `bench.py --mode train $TRAIN_ARGS`
 #   bench_args  one `bench.py $BENCH_ARGS` line
 #   prof_args   rocprofv3 kernel trace of `bench.py $BENCH_ARGS`
+#   pmc_args    tools/pmc.sh passes of `bench.py $BENCH_ARGS`, summarised as $PMC_TAG
 set -u
 STEPS="${STEPS:-pytest_gpu smoke bench sweep prof pmc}"
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
@@ -38,5 +39,7 @@ step pmc 1200 bash tools/pmc.sh "$OUT/pmc"
 step train_prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/train_prof" -o run --output-format csv -- python bench.py --mode train ${TRAIN_ARGS:-} --cpu-seconds 0
 step bench_args 600 python bench.py ${BENCH_ARGS:-}
 step prof_args 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_args" -o run --output-format csv -- python bench.py ${BENCH_ARGS:-} --cpu-seconds 0
+step pmc_args 1200 bash tools/pmc.sh "$OUT/pmc_args" ${BENCH_ARGS:-}
+case " $STEPS " in *" pmc_args "*) python tools/pmc_summary.py "$OUT/pmc_args" "${PMC_TAG:-args}" "$OUT/pmc_${PMC_TAG:-args}.json" > "$OUT/pmc_args_summary.log" 2>&1 || true;; esac
 case " $STEPS " in *" pmc "*) python tools/pmc_summary.py "$OUT/pmc" cgnni_bch_63_45_B65536_T25_f32 "$OUT/pmc_cgnni_bch_63_45_B65536_T25_f32.json" > "$OUT/pmc_summary.log" 2>&1 || true;; esac
 echo "=== done $(date +%T)"
