@@ -34,15 +34,21 @@ namespace {
 
 // threads per workgroup: 16 waves (4 per SIMD) in fp32 (128 VGPRs), 8 in fp64 (169 VGPRs)
 template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
+// LDS bytes of the Softplus tables the fp64 reverse pass stages ahead of its graph tables
+template <typename T> constexpr size_t bwd_tab_bytes() { return sizeof(T) == 8 ? (size_t)kFp64TabDoubles * 8 : 0; }
 constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 
 // softplus and its derivative at h (natural units).  fp64 without libm (the forward's
 // scheme, gnnd_common.h): e = e^-|h| in (0, 1], sp = max(h, 0) + log1p(e),
 // sg = sigmoid(h) = (h >= 0 ? 1 : e) / (1 + e) with a Newton-refined v_rcp_f64; above the
 // threshold sp = h, sg = 1 (torch's Softplus backward)
-__device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg) {
-    const double e = exp_nonpos_f64(-__builtin_fabs(h));
-    const double r = log1p_unit_f64(e);
+// tab: the forward's Softplus tables in LDS (kExpTab | kLogTab): the same table-driven e^-|h|
+// and log1p as the fp64 forward (softplus_tab_lite: within 1e-13 absolute of glibc) instead of
+// the libm-accuracy series (~20 fp64 ops less per unit and edge); sigmoid by a Newton-refined
+// v_rcp_f64 as before
+__device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg, const double* tab) {
+    const double e = exp_tab_negabs_lite(h, tab);
+    const double r = log1p_tab_unit_lite(e, tab + kExpTabN);
     const double d = 1.0 + e;
     double rc = __builtin_amdgcn_rcp(d);
     rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
@@ -54,7 +60,7 @@ __device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg) {
     sp = big ? h : (h > 0.0 ? h + r : r);
     sg = big ? 1.0 : q;
 }
-__device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg) {
+__device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg, const float*) {
     if (h > 20.f) { sp = h; sg = 1.f; return; }
     const float z = __builtin_amdgcn_exp2f(h * kLog2e);
     const float z1 = 1.f + z;
@@ -212,7 +218,8 @@ template <typename T> struct Units {
     // (independent chains for the scheduler); returns d y / d u0 per edge (wave-reduced,
     // uniform).  An edge with dy = 0 contributes nothing (masked tail).
     template <bool TWO>
-    __device__ __forceinline__ void bwd2(T xa0, T xa1, T dya, T xb0, T xb1, T dyb, T& ra, T& rb) {
+    __device__ __forceinline__ void bwd2(T xa0, T xa1, T dya, T xb0, T xb1, T dyb, T& ra, T& rb,
+                                         const T* tab) {
         if constexpr (sizeof(T) == 4) {
             bwd2_f32<TWO>(xa0, xa1, dya, xb0, xb1, dyb, ra, rb);
             return;
@@ -225,8 +232,8 @@ template <typename T> struct Units {
             ha = ha + b1[j];
             hb = hb + b1[j];
             T spa, sga, spb, sgb;
-            sp_and_grad(ha, spa, sga);
-            sp_and_grad(hb, spb, sgb);
+            sp_and_grad(ha, spa, sga, tab);
+            sp_and_grad(hb, spb, sgb, tab);
             gw2[j] += dya * spa;
             gw2[j] += dyb * spb;
             const T dha = (dya * w2[j]) * sga, dhb = (dyb * w2[j]) * sgb;
@@ -364,13 +371,16 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     constexpr int kTrainWaves = kTrainThreads / 64;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: edge loops on SALU
-    int* s_tab = (int*)smem;
+    // fp64: the forward's Softplus tables (kExpTab | kLogTab) at LDS byte 0 (sp_and_grad)
+    constexpr size_t kTabB = bwd_tab_bytes<T>();
+    T* s_ftab = (T*)smem;
+    int* s_tab = (int*)(smem + kTabB);
     const int nints = graph_table_ints(V, C, E);
     const uint32_t* s_evc = (const uint32_t*)s_tab;
     const int* s_vptr = s_tab + E;
     const int* s_cptr = s_vptr + V + 1;
     const int* s_cedge = s_cptr + C + 1;
-    size_t off = ((size_t)nints * 4 + 15) & ~(size_t)15;
+    size_t off = kTabB + (((size_t)nints * 4 + 15) & ~(size_t)15);
     // per-edge arrays at a 4-aligned stride Ep (the fp32 unit passes read four consecutive
     // edges with one ds_read_b128; entries E..Ep-1 stay zero: finite inputs, dy = 0)
     const int Ep = (E + 3) & ~3;
@@ -409,6 +419,9 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     uc.load1(w + kV24Ggc2, lane);
     uo.load1(w + kV24Mlp, lane);
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
+    if constexpr (kTabB > 0)
+        for (int i = tid; i < kFp64TabDoubles; i += kTrainThreads)
+            s_ftab[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
     for (int i = tid; i < 8 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
     if (floss) {
         for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
@@ -535,7 +548,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                 const int fb = has2 ? f2 : f;
                 T ra, rb;
                 U.template bwd2<TWO>(in0[f], TWO ? in1[f] : T(0), dy_of(f), in0[fb],
-                                     TWO ? in1[fb] : T(0), has2 ? dy_of(fb) : T(0), ra, rb);
+                                     TWO ? in1[fb] : T(0), has2 ? dy_of(fb) : T(0), ra, rb, s_ftab);
                 resa = put_lane(resa, ra, k, lane);
                 resb = put_lane(resb, rb, k, lane);
             }
@@ -793,7 +806,8 @@ int64_t train_rows(const gnnd_graph* g, int64_t B) {
 // the graph tables: [waves][kV24W] values)
 size_t train_lds(const gnnd_graph* g, int esz, int nl = -1, int waves = 0, bool sibs = false) {   // nl >= 0: fused loss
     const GraphView& v = g->view;
-    const size_t tab = ((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15;
+    const size_t tab = (esz == 8 ? bwd_tab_bytes<double>() : 0) +
+                       (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15);
     size_t n = tab + (size_t)esz * 8 * (((size_t)v.E + 3) & ~(size_t)3);
     if (nl >= 0)
         n += (size_t)esz * (3 * (size_t)v.V + 2 * ((size_t)v.C + nl)) +
