@@ -161,6 +161,29 @@ __device__ __forceinline__ double wave_sum(double v) {
     const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+// fp64 wave_rows4: the same lane folds on both 32-bit halves of every value, then the row
+// DPP chain in fp64 (21 VALU for four edges' totals; two six-step wave_sum chains per edge pair
+// were ~40 dependent ops per pair)
+__device__ __forceinline__ double pl32_fold(double a, double b) {
+    const long long ia = __double_as_longlong(a), ib = __double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((int)ia, (int)ib, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((int)(ia >> 32), (int)(ib >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | (unsigned)lo[0]) +
+           __longlong_as_double(((long long)hi[1] << 32) | (unsigned)lo[1]);
+}
+__device__ __forceinline__ double wave_rows4(double a, double b, double c, double d) {
+    const double v1 = pl32_fold(a, b), v2 = pl32_fold(c, d);
+    const long long i1 = __double_as_longlong(v1), i2 = __double_as_longlong(v2);
+    const auto lo = __builtin_amdgcn_permlane16_swap((int)i1, (int)i2, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((int)(i1 >> 32), (int)(i2 >> 32), false, false);
+    double v = __longlong_as_double(((long long)hi[0] << 32) | (unsigned)lo[0]) +
+               __longlong_as_double(((long long)hi[1] << 32) | (unsigned)lo[1]);
+    v += dpp_d<0xB1, 0xf>(v);
+    v += dpp_d<0x4E, 0xf>(v);
+    v += dpp_d<0x141, 0xf>(v);
+    v += dpp_d<0x140, 0xf>(v);
+    return v;
+}
 
 // v with lane k replaced by the uniform value x (compare + select)
 template <typename T> __device__ __forceinline__ T put_lane(T v, T x, int k, int lane) {
@@ -249,6 +272,35 @@ template <typename T> struct Units {
         gb2 += dyb;
         ra = wave_sum(pa);
         rb = wave_sum(pb);
+    }
+    // fp64: four CONSECUTIVE edges per wave step (the fp32 unit pass's shape): eight independent
+    // Softplus/sigmoid evaluations per lane, weight gradients summed over the four edges as a
+    // tree, the four d inputs row-reduced by one wave_rows4 (every lane of row r ends with the
+    // total of edge row_edge(r))
+    template <bool TWO>
+    __device__ __forceinline__ double bwd4_rows_f64(const double (&x0)[4], const double (&x1)[4],
+                                                    const double (&dy)[4], const double* tab) {
+        double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            double sp[4], sg[4], dh[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double h = x0[i] * w1a[j];
+                if constexpr (TWO) h = h + x1[i] * w1b[j];
+                h = h + b1[j];
+                sp_and_grad(h, sp[i], sg[i], tab);
+                dh[i] = (dy[i] * w2[j]) * sg[i];
+                p[i] += dh[i] * w1a[j];
+            }
+            gw2[j] += (dy[0] * sp[0] + dy[1] * sp[1]) + (dy[2] * sp[2] + dy[3] * sp[3]);
+            gw1a[j] += (dh[0] * x0[0] + dh[1] * x0[1]) + (dh[2] * x0[2] + dh[3] * x0[3]);
+            if constexpr (TWO)
+                gw1b[j] += (dh[0] * x1[0] + dh[1] * x1[1]) + (dh[2] * x1[2] + dh[3] * x1[3]);
+            gb1[j] += (dh[0] + dh[1]) + (dh[2] + dh[3]);
+        }
+        gb2 += (dy[0] + dy[1]) + (dy[2] + dy[3]);
+        return wave_rows4(p[0], p[1], p[2], p[3]);
     }
     // fp32: edges a and b ride the two halves of every packed op (v_pk_fma/mul/add_f32 with
     // the lane's weights broadcast); the weight gradients accumulate per half (pg*) and are
@@ -538,6 +590,24 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             if constexpr (kPipe) U.fold();
             return;
         }
+#ifndef GNND_BWD_F64_PAIRS
+        if constexpr (sizeof(T) == 8) {
+            // fp64: four consecutive edges f..f+3 per wave step (f = 4 (wave + W k)); padding
+            // entries E..Ep-1 are zero inputs with dy = 0, and every lane stores its row's total
+            const int eo = row_edge(lane >> 4);
+            for (int f = 4 * wave; f < E; f += 4 * kTrainWaves) {
+                double a0[4], a1[4], dy[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    a0[i] = in0[f + i];
+                    a1[i] = TWO ? in1[f + i] : 0.0;
+                    dy[i] = dy_of(f + i);
+                }
+                outp[f + eo] = U.template bwd4_rows_f64<TWO>(a0, a1, dy, s_ftab);
+            }
+            return;
+        }
+#endif
         constexpr int kStride = 2 * kTrainWaves;
         for (int f0 = wave; f0 < E; f0 += 64 * kStride) {
             T resa = T(0), resb = T(0);
