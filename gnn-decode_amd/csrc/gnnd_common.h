@@ -677,6 +677,25 @@ __device__ __forceinline__ double softplus_fast(double x, const double* __restri
     return relu_f64(x) + log1p_tab_unit_lite(u, tab + kExpTabN);
 }
 
+// e^-|x| with torch's Softplus threshold in the exponent: x > 20 -> exactly 0 (softplus_fast's
+// first half; the fp64 reverse pass, gnnd_train.hip sp_and_grad)
+__device__ __forceinline__ double exp_negabs_thr(double x, const double* __restrict__ tab) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double tk;
+    asm("v_fma_f64 %0, -|%1|, %2, %3" : "=v"(tk) : "v"(x), "s"(369.32993046757462), "v"(kRoundMagic));
+#else
+    const double tk = __builtin_fma(-__builtin_fabs(x), 369.32993046757462, kRoundMagic);
+#endif
+    const double kd = tk - kRoundMagic;                                // exact
+    const double r = __builtin_fma(-kd, 6.93147180559945309417e-01 / 256, -__builtin_fabs(x));
+    double p = fma_vsv(r, 1.0 / 6, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    p = __builtin_fma(p, r, 1.0);
+    const int k = round_magic_lo(tk);
+    const int e = x > 20.0 ? -2048 : (k >> 8);
+    return __builtin_ldexp(tab[k & (kExpTabN - 1)] * p, e);
+}
+
 template <typename T> __device__ __forceinline__ T sigmoid_ref(T x) {
     return T(1) / (T(1) + g_exp(-x));
 }

@@ -43,22 +43,64 @@ constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 // sg = sigmoid(h) = (h >= 0 ? 1 : e) / (1 + e) with a Newton-refined v_rcp_f64; above the
 // threshold sp = h, sg = 1 (torch's Softplus backward)
 // tab: the forward's Softplus tables in LDS (kExpTab | kLogTab): the same table-driven e^-|h|
-// and log1p as the fp64 forward (softplus_tab_lite: within 1e-13 absolute of glibc) instead of
-// the libm-accuracy series (~20 fp64 ops less per unit and edge); sigmoid by a Newton-refined
-// v_rcp_f64 as before
+// and log1p as the fp64 forward (softplus_fast: within 1e-13 absolute of glibc), torch's
+// threshold folded into the exponent of e (h > 20: e = 0 exactly, so log1p(e) = 0, sp = relu(h)
+// = h and 1 / (1 + e) = 1 = sg with no selects on the results); sigmoid from a Newton-refined
+// v_rcp_f64 of the 1 + e the log1p already formed
 __device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg, const double* tab) {
-    const double e = exp_tab_negabs_lite(h, tab);
+    const double e = exp_negabs_thr(h, tab);
     const double r = log1p_tab_unit_lite(e, tab + kExpTabN);
     const double d = 1.0 + e;
     double rc = __builtin_amdgcn_rcp(d);
     rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
     rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
-    const double num = h >= 0.0 ? 1.0 : e;
-    double q = num * rc;
-    q = __builtin_fma(__builtin_fma(-q, d, num), rc, q);               // num / d, ~0.5 ulp
-    const bool big = h > 20.0;
-    sp = big ? h : (h > 0.0 ? h + r : r);
-    sg = big ? 1.0 : q;
+    sp = relu_f64(h) + r;
+    sg = (h >= 0.0 ? 1.0 : e) * rc;
+}
+// sp_and_grad of N independent arguments, stage by stage: all N exp-table reads are issued
+// before the first is used, then all N log-table reads (a per-argument chain waits out two LDS
+// round trips back to back: hipcc scheduled the chains one after another, lgkmcnt(0) after each
+// read)
+template <int N>
+__device__ __forceinline__ void sp_and_grad_n(const double (&h)[N], double (&sp)[N],
+                                              double (&sg)[N], const double* tab) {
+    double p[N], tv[N], e[N], rj[N], lj[N];
+    int ex[N], ia[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        double tk;
+        asm("v_fma_f64 %0, -|%1|, %2, %3" : "=v"(tk) : "v"(h[i]), "s"(369.32993046757462), "v"(kRoundMagic));
+        const double kd = tk - kRoundMagic;
+        const double r = __builtin_fma(-kd, 6.93147180559945309417e-01 / 256, -__builtin_fabs(h[i]));
+        double q = fma_vsv(r, 1.0 / 6, 0.5);
+        q = __builtin_fma(q, r, 1.0);
+        p[i] = __builtin_fma(q, r, 1.0);
+        const int k = round_magic_lo(tk);
+        ex[i] = h[i] > 20.0 ? -2048 : (k >> 8);
+        ia[i] = k & (kExpTabN - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) tv[i] = tab[ia[i]];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        e[i] = __builtin_ldexp(tv[i] * p[i], ex[i]);
+        ia[i] = round_magic_lo(fma_vsv(e[i], 256.0, kRoundMagic));      // rint(256 e): 0..256
+    }
+    const double* lt = tab + kExpTabN;
+#pragma unroll
+    for (int i = 0; i < N; ++i) { rj[i] = lt[2 * ia[i]]; lj[i] = lt[2 * ia[i] + 1]; }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const double d = 1.0 + e[i];
+        const double t = __builtin_fma(d, rj[i], -1.0);
+        double q = fma_vsv(t, -0.25, 1.0 / 3);
+        q = __builtin_fma(q, t, -0.5);
+        sp[i] = relu_f64(h[i]) + (lj[i] + __builtin_fma(q * t, t, t));
+        double rc = __builtin_amdgcn_rcp(d);
+        rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
+        rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
+        sg[i] = (h[i] >= 0.0 ? 1.0 : e[i]) * rc;
+    }
 }
 __device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg, const float*) {
     if (h > 20.f) { sp = h; sg = 1.f; return; }
@@ -161,6 +203,9 @@ __device__ __forceinline__ double wave_sum(double v) {
     const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+#ifndef GNND_BWD_F64_STAGE
+#define GNND_BWD_F64_STAGE 8      // fp64 reverse pass: Softplus chains per LDS stage (A/B: 4, 1)
+#endif
 // fp64 wave_rows4: the same lane folds on both 32-bit halves of every value, then the row
 // DPP chain in fp64 (21 VALU for four edges' totals; two six-step wave_sum chains per edge pair
 // were ~40 dependent ops per pair)
@@ -281,15 +326,43 @@ template <typename T> struct Units {
     __device__ __forceinline__ double bwd4_rows_f64(const double (&x0)[4], const double (&x1)[4],
                                                     const double (&dy)[4], const double* tab) {
         double p[4] = {0.0, 0.0, 0.0, 0.0};
+#if GNND_BWD_F64_STAGE == 8
+        double h8[8], sp8[8], sg8[8];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            double sp[4], sg[4], dh[4];
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 double h = x0[i] * w1a[j];
                 if constexpr (TWO) h = h + x1[i] * w1b[j];
-                h = h + b1[j];
-                sp_and_grad(h, sp[i], sg[i], tab);
+                h8[4 * j + i] = h + b1[j];
+            }
+        sp_and_grad_n<8>(h8, sp8, sg8, tab);
+#endif
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            double sp[4], sg[4], dh[4];
+#if GNND_BWD_F64_STAGE == 8
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { sp[i] = sp8[4 * j + i]; sg[i] = sg8[4 * j + i]; }
+#elif GNND_BWD_F64_STAGE == 4
+            double hh[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double h = x0[i] * w1a[j];
+                if constexpr (TWO) h = h + x1[i] * w1b[j];
+                hh[i] = h + b1[j];
+            }
+            sp_and_grad_n<4>(hh, sp, sg, tab);
+#else
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double h = x0[i] * w1a[j];
+                if constexpr (TWO) h = h + x1[i] * w1b[j];
+                sp_and_grad(h + b1[j], sp[i], sg[i], tab);
+            }
+#endif
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
                 dh[i] = (dy[i] * w2[j]) * sg[i];
                 p[i] += dh[i] * w1a[j];
             }
