@@ -244,8 +244,8 @@ struct Mlp10F32 {
 };
 
 // fp64 reference forms: Linear(1,128)/Linear(2,128) -> Softplus -> Linear(128,1); the
-// Softplus is the table-driven form at the parity contract's accuracy (softplus_tab_lite;
-// tab = the kernel's LDS copy of kExpTab | kLogTab)
+// Softplus is the table-driven form at the parity contract's accuracy (softplus_v24: the one-read
+// kSpTab polynomial; tab = the kernel's LDS copy of its table)
 // the unit's bias into a VGPR pair with ONE v_mov_b64 (its weight stays an SGPR operand of the
 // layer-1 FMA: VOP3 takes one scalar operand)
 __device__ __forceinline__ double vgpr_of(double s) {
@@ -268,7 +268,7 @@ template <int N, typename F, int I = 0> __device__ __forceinline__ void static_f
 // 2-input (TWO: u0 -> W1[:, 0], u1 -> W1[:, 1]) {W1a[128], W1b[128], b1[128], W2[128], b2}.
 // bl: the MLP's 128 layer-1 biases staged in LDS (a broadcast ds_read_b64 per unit: VOP3 takes
 // one scalar operand, so a bias from SGPRs costs a v_mov_b64 per unit); tab: the Softplus
-// tables in LDS (softplus_fast).
+// table in LDS (softplus_v24).
 template <int NC, int J0, bool TWO>
 __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, const double* bl,
                                                  double u0, double u1, const double* tab) {
@@ -285,7 +285,7 @@ __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, c
             double h;
             if constexpr (TWO) h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], bl[k]));
             else h = fma_vsv(u0, w[k], bl[k]);
-            c[jj] = fma(softplus_fast(h, tab), w[kW2 + k], c[jj]);
+            c[jj] = fma(softplus_v24(h, tab), w[kW2 + k], c[jj]);
         });
     }
     if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
@@ -893,8 +893,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int sub = US > 1 ? __builtin_amdgcn_readfirstlane((tid >> 6) % US) : 0;
     const int itid = US > 1 ? ((tid >> 6) / US) * 64 + (tid & 63) : tid;
 
-    // fp64 V24: the Softplus tables (gnnd_common.h kExpTab | kLogTab, indexed per lane) at
-    // LDS byte 0, then the three MLPs' layer-1 biases [3][128]
+    // fp64 V24: the Softplus table (gnnd_common.h kSpTab, indexed per lane) at LDS byte 0,
+    // then the three MLPs' layer-1 biases [3][128]
     constexpr bool kTab = MODEL == GNND_V24 && sizeof(T) == 8;
     T* s_w = (T*)smem;
     size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
@@ -902,10 +902,9 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     T* s_bias = nullptr;
     if constexpr (kTab) {
         s_tab = (T*)smem;
-        s_bias = s_tab + kFp64TabDoubles;
-        off = (size_t)(kFp64TabDoubles + 3 * 128) * 8;
-        for (int i = tid; i < kFp64TabDoubles; i += NT)
-            s_tab[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
+        s_bias = s_tab + kV24F64TabDoubles;
+        off = (size_t)(kV24F64TabDoubles + 3 * 128) * 8;
+        for (int i = tid; i < kV24F64TabDoubles; i += NT) s_tab[i] = v24_f64_tab_entry(i);
         for (int i = tid; i < 3 * 128; i += NT) {
             const int m = i >> 7, k = i & 127;
             s_bias[i] = w[m == 0 ? kV24Ggc1 + 256 + k : (m == 1 ? kV24Ggc2 : kV24Mlp) + 128 + k];
@@ -2034,6 +2033,10 @@ constexpr int kResidentRegBudget = 88;          // Q * (2R + 2) state VGPRs (<= 
 
 // LDS budget per workgroup: 40 KiB -> 4 workgroups (16 waves) per CU.  GNND_LDS_TARGET
 // (bytes) overrides it for tuning sweeps; GNND_NO_RESIDENT=1 forces the streaming kernel.
+bool lds_target_set() {                // GNND_LDS_TARGET given (A/B): it overrides every budget
+    static const bool v = getenv("GNND_LDS_TARGET") != nullptr;
+    return v;
+}
 size_t lds_target() {
     static size_t v = [] {
         const char* e = getenv("GNND_LDS_TARGET");
@@ -2112,6 +2115,16 @@ bool split_disabled() {
 }
 
 // GNND_V24_SPLIT=1|2|4|8 forces the fp32 decoder_v2_4 unit split (A/B); default by batch
+// GNND_V24F64_US=2|4: fp64 decoder_v2_4 large batches (several codewords per workgroup) with
+// the MLP units split over US waves as well (A/B; default 1)
+int v24f64_us_big() {
+    static int v = [] {
+        const char* e = getenv("GNND_V24F64_US");
+        const int n = e ? atoi(e) : 0;
+        return n == 2 || n == 4 ? n : 1;
+    }();
+    return v;
+}
 int v24_split_forced() {
     static int v = [] {
         const char* e = getenv("GNND_V24_SPLIT");
@@ -2205,11 +2218,22 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const GraphView& g = !v24f32 ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
-    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kFp64TabDoubles + 3 * 128) * 8 : 0;
+    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kV24F64TabDoubles + 3 * 128) * 8 : 0;
     const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab;
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
-    size_t n = fixed + per >= target ? 1 : (target - fixed) / per;
+    // fp64 decoder_v2_4 stages its 32.8 KB Softplus table per workgroup: a third of the CU's LDS
+    // per workgroup (3 per CU; toric-5: 4 codewords, 3 full item rounds).  Same-box A/B
+    // (profiles/r04/experiments/v24_f64_shapes_ab_r04g.txt): 2.24 M cw/s vs 1.96 M at 80 KB
+    // (2 per CU), 2.17 M with the units split over 2 waves, 1.74 M over 4
+#ifndef GNND_V24F64_LDS
+#define GNND_V24F64_LDS (GNND_F64_SPTAB ? (kLdsMax / 3) & ~(size_t)15 : 0)
+#endif
+    const size_t tgt = model == GNND_V24 && dtype == GNND_F64 && GNND_V24F64_LDS && !lds_target_set()
+                           ? (size_t)GNND_V24F64_LDS : target;
+    const int us_big = model == GNND_V24 && dtype == GNND_F64 && g.R <= 2 ? v24f64_us_big() : 1;
+    const size_t bufb = us_big > 1 ? (size_t)2 * us_big * GNND_BLOCK * 8 + 8 : 0;
+    size_t n = fixed + bufb + per >= tgt ? 1 : (tgt - fixed - bufb) / per;
     if (n > 64) n = 64;
     // step-1 lane utilisation: the tile's C*G work items run in rounds of 256 lanes; among
     // tiles down to half the LDS-limited size take the one wasting the fewest lanes (ties:
@@ -2255,9 +2279,9 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     // fp64 decoder_v2_4 (the reference dtype) the same way: one slot per lane (R <= 2 plans;
     // toric: G = 4, R = 1), the 128 units of every MLP over US = 4 (B <= 256) / 2 (B <= 512)
     // waves in four fixed chains (mlp128d_split)
-    if (model == GNND_V24 && dtype == GNND_F64 && n == 1 && g.R <= 2) {
+    if (model == GNND_V24 && dtype == GNND_F64 && (n == 1 || us_big > 1) && g.R <= 2) {
         const int forced = v24_split_forced();
-        int us = forced ? forced : B <= 256 ? 4 : B <= 512 ? 2 : 1;
+        int us = forced ? forced : n > 1 ? us_big : B <= 256 ? 4 : B <= 512 ? 2 : 1;
         if (us > 4) us = 4;
         if (us > 1 && align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8 <= kLdsMax) {
             p->us = us;

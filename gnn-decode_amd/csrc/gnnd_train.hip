@@ -35,7 +35,7 @@ namespace {
 // threads per workgroup: 16 waves (4 per SIMD) in fp32 (128 VGPRs), 8 in fp64 (169 VGPRs)
 template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
 // LDS bytes of the Softplus tables the fp64 reverse pass stages ahead of its graph tables
-template <typename T> constexpr size_t bwd_tab_bytes() { return sizeof(T) == 8 ? (size_t)kFp64TabDoubles * 8 : 0; }
+template <typename T> constexpr size_t bwd_tab_bytes() { return sizeof(T) == 8 ? (size_t)kV24F64TabDoubles * 8 : 0; }
 constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 
 // softplus and its derivative at h (natural units).  fp64 without libm (the forward's
@@ -48,6 +48,13 @@ constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 // = h and 1 / (1 + e) = 1 = sg with no selects on the results); sigmoid from a Newton-refined
 // v_rcp_f64 of the 1 + e the log1p already formed
 __device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg, const double* tab) {
+#if GNND_F64_SPTAB
+    const SpIdx q = sp_index(h);
+    const SpEntry e = sp_entry(tab, q.j);
+    sp = relu_f64(h) + sp_poly(q.r, e.f0, e.s);
+    const double sa = sig_poly(q.r, e.s);
+    sg = h >= 0.0 ? 1.0 - sa : sa;
+#else
     const double e = exp_negabs_thr(h, tab);
     const double r = log1p_tab_unit_lite(e, tab + kExpTabN);
     const double d = 1.0 + e;
@@ -56,6 +63,7 @@ __device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg, co
     rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
     sp = relu_f64(h) + r;
     sg = (h >= 0.0 ? 1.0 : e) * rc;
+#endif
 }
 // sp_and_grad of N independent arguments, stage by stage: all N exp-table reads are issued
 // before the first is used, then all N log-table reads (a per-argument chain waits out two LDS
@@ -64,6 +72,21 @@ __device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg, co
 template <int N>
 __device__ __forceinline__ void sp_and_grad_n(const double (&h)[N], double (&sp)[N],
                                               double (&sg)[N], const double* tab) {
+#if GNND_F64_SPTAB
+    // the one-read table (gnnd_common.h softplus_sp / sig_poly): all N 16-byte reads first
+    SpIdx q[N];
+    SpEntry e[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) q[i] = sp_index(h[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = sp_entry(tab, q[i].j);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        sp[i] = relu_f64(h[i]) + sp_poly(q[i].r, e[i].f0, e[i].s);
+        const double sa = sig_poly(q[i].r, e[i].s);
+        sg[i] = h[i] >= 0.0 ? 1.0 - sa : sa;
+    }
+#else
     double p[N], tv[N], e[N], rj[N], lj[N];
     int ex[N], ia[N];
 #pragma unroll
@@ -101,6 +124,7 @@ __device__ __forceinline__ void sp_and_grad_n(const double (&h)[N], double (&sp)
         rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
         sg[i] = (h[i] >= 0.0 ? 1.0 : e[i]) * rc;
     }
+#endif
 }
 __device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg, const float*) {
     if (h > 20.f) { sp = h; sg = 1.f; return; }
@@ -496,7 +520,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     constexpr int kTrainWaves = kTrainThreads / 64;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: edge loops on SALU
-    // fp64: the forward's Softplus tables (kExpTab | kLogTab) at LDS byte 0 (sp_and_grad)
+    // fp64: the forward's Softplus table (kSpTab) at LDS byte 0 (sp_and_grad_n)
     constexpr size_t kTabB = bwd_tab_bytes<T>();
     T* s_ftab = (T*)smem;
     int* s_tab = (int*)(smem + kTabB);
@@ -545,8 +569,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     uo.load1(w + kV24Mlp, lane);
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     if constexpr (kTabB > 0)
-        for (int i = tid; i < kFp64TabDoubles; i += kTrainThreads)
-            s_ftab[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
+        for (int i = tid; i < kV24F64TabDoubles; i += kTrainThreads) s_ftab[i] = v24_f64_tab_entry(i);
     for (int i = tid; i < 8 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
     if (floss) {
         for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
