@@ -56,12 +56,13 @@ __device__ __forceinline__ int gnnd_dcheck_idx(int i, int n, int bit) {
 // ---------------------------------------------------------------------------------------
 struct PhaseProf {
 #ifdef GNND_PHASE_PROF
-    uint64_t acc[16];
+    static constexpr int kN = 20;
+    uint64_t acc[kN];
     uint64_t last;
     bool on;
     __device__ void start(bool enable) {
         on = enable;
-        for (int i = 0; i < 16; ++i) acc[i] = 0;
+        for (int i = 0; i < kN; ++i) acc[i] = 0;
         last = __builtin_amdgcn_s_memtime();
     }
     __device__ __forceinline__ void mark(int i) {
@@ -73,13 +74,14 @@ struct PhaseProf {
     }
     __device__ void report(const char* tag, int n, int iters) {
         if (on && (threadIdx.x & 63) == 0)
-            printf("PHASE %s iters %d | %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n",
+            printf("PHASE %s iters %d | %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n",
                    tag, iters, (unsigned long long)acc[0], (unsigned long long)acc[1],
                    (unsigned long long)acc[2], (unsigned long long)acc[3], (unsigned long long)acc[4],
                    (unsigned long long)acc[5], (unsigned long long)acc[6], (unsigned long long)acc[7],
                    (unsigned long long)acc[8], (unsigned long long)acc[9], (unsigned long long)acc[10],
                    (unsigned long long)acc[11], (unsigned long long)acc[12], (unsigned long long)acc[13],
-                   (unsigned long long)acc[14], (unsigned long long)acc[15]);
+                   (unsigned long long)acc[14], (unsigned long long)acc[15], (unsigned long long)acc[16],
+                   (unsigned long long)acc[17], (unsigned long long)acc[18], (unsigned long long)acc[19]);
         (void)n;
     }
 #endif

@@ -815,6 +815,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             s_u[f] = tape.mT[(size_t)b * g.es + g.e0 + f];
             s_da[f] = -((gv * (T(1) - pv)) * pv);     // p = sigmoid(-r)
         }
+        GNND_PMARK(pf, 19);
         __syncthreads();
 
         // readout: r_v = sum_e MLP_o(m^T_e) + x_v  ->  dm
@@ -902,6 +903,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     // into a zeroed accumulator) — one barrier instead of one per wave
     T* s_red = s_dm;                         // [kTrainWaves][kV24W] (train_lds reserves it)
     __syncthreads();
+    GNND_PMARK(pf, 16);
     {
         constexpr bool kFolded = true;       // fp32: every unit_pass folds its partials
         T* my = s_red + (size_t)wave * kV24W;
@@ -909,7 +911,9 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
         uc.template flush<false>(my + kV24Ggc2, lane, kFolded);
         uo.template flush<false>(my + kV24Mlp, lane, kFolded);
     }
+    GNND_PMARK(pf, 17);
     __syncthreads();
+    GNND_PMARK(pf, 18);
     T* row = gpart + (size_t)blockIdx.x * kV24W;
     for (int i = tid; i < kV24W; i += kTrainThreads) {
         T a = T(0);
