@@ -687,8 +687,8 @@ def train_trajectory(H, init_state, T, dev, dtype, seed, n=64, K=10):
 
 def decode_run(a, world, rank, dev, cpu='full'):
     """One decode workload (a.model / a.code / a.batch per GPU / a.dtype): K timed launches,
-    BER/FER, roofline; cpu='full' times the oracle (1 thread + all cores), 'parity' only a
-    bounded 1-thread oracle sample for matched-BER parity, 'off' none.  Returns the result
+    BER/FER, roofline; cpu='full' times the oracle (1 thread + all cores), 'parity' a bounded
+    oracle sample (1 thread, with matched-BER parity, + a short all-cores leg), 'off' none.  Returns the result
     dict on rank 0 (None elsewhere)."""
     T = a.iters or gd.DEFAULT_ITERS[a.model]
     # bf16: storage type of x / out only (classical models); weights and arithmetic fp32
@@ -844,7 +844,7 @@ def decode_run(a, world, rank, dev, cpu='full'):
             # the oracle decodes the same (for bf16: widened) inputs in fp32
             res['cpu_baseline'] = cpu_baseline(a.model, H, state, x.to(dtype), pred, labels, g, T,
                                                a.cpu_seconds, out_bf16=io_dtype == torch.bfloat16,
-                                               all_cores_leg=cpu == 'full',
+                                               all_cores_leg=cpu in ('full', 'parity'),
                                                chunk=512 if cpu == 'full' else 128)
         else:
             res['cpu_baseline'] = None

@@ -11,7 +11,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 CASES = [('cgnni', 'ldpc_648_324', 'f32', 3000), ('v24', 'toric_5', 'f32', 700),
-         ('qbp', 'toric_5', 'f64', 2500)]
+         ('v24', 'toric_5', 'f64', 700), ('qbp', 'toric_5', 'f64', 2500)]
 
 
 def _counts(model, code, dtype, B, offset, seed=3):
