@@ -35,45 +35,20 @@ namespace {
 // threads per workgroup: 16 waves (4 per SIMD) in fp32 (128 VGPRs), 8 in fp64 (169 VGPRs)
 template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
 // LDS bytes of the Softplus tables the fp64 reverse pass stages ahead of its graph tables
-template <typename T> constexpr size_t bwd_tab_bytes() { return sizeof(T) == 8 ? (size_t)kV24F64TabDoubles * 8 : 0; }
+template <typename T> constexpr size_t bwd_tab_bytes() { return sizeof(T) == 8 ? (size_t)kSpTabDoubles * 8 : 0; }
 constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 
-// softplus and its derivative at h (natural units).  fp64 without libm (the forward's
-// scheme, gnnd_common.h): e = e^-|h| in (0, 1], sp = max(h, 0) + log1p(e),
-// sg = sigmoid(h) = (h >= 0 ? 1 : e) / (1 + e) with a Newton-refined v_rcp_f64; above the
-// threshold sp = h, sg = 1 (torch's Softplus backward)
-// tab: the forward's Softplus tables in LDS (kExpTab | kLogTab): the same table-driven e^-|h|
-// and log1p as the fp64 forward (softplus_fast: within 1e-13 absolute of glibc), torch's
-// threshold folded into the exponent of e (h > 20: e = 0 exactly, so log1p(e) = 0, sp = relu(h)
-// = h and 1 / (1 + e) = 1 = sg with no selects on the results); sigmoid from a Newton-refined
-// v_rcp_f64 of the 1 + e the log1p already formed
-__device__ __forceinline__ void sp_and_grad(double h, double& sp, double& sg, const double* tab) {
-#if GNND_F64_SPTAB
-    const SpIdx q = sp_index(h);
-    const SpEntry e = sp_entry(tab, q.j);
-    sp = relu_f64(h) + sp_poly(q.r, e.f0, e.s);
-    const double sa = sig_poly(q.r, e.s);
-    sg = h >= 0.0 ? 1.0 - sa : sa;
-#else
-    const double e = exp_negabs_thr(h, tab);
-    const double r = log1p_tab_unit_lite(e, tab + kExpTabN);
-    const double d = 1.0 + e;
-    double rc = __builtin_amdgcn_rcp(d);
-    rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
-    rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
-    sp = relu_f64(h) + r;
-    sg = (h >= 0.0 ? 1.0 : e) * rc;
-#endif
-}
-// sp_and_grad of N independent arguments, stage by stage: all N exp-table reads are issued
-// before the first is used, then all N log-table reads (a per-argument chain waits out two LDS
-// round trips back to back: hipcc scheduled the chains one after another, lgkmcnt(0) after each
-// read)
+// fp64 Softplus and its derivative at N arguments h from the kSpTab entries (gnnd_common.h
+// sp_index / sp_poly / sig_poly; the reverse pass stages the table whichever form its forward
+// used), all N 16-byte reads issued before the first use (hipcc otherwise schedules the chains
+// one after another, lgkmcnt(0) after each read):
+//   sph = |h|/2 + ln(1 + e^-|h|) = softplus(h) - h/2  (the linear h/2 part is summed once per
+//         wave, Units::sx*, instead of a max + add per unit),
+//   sg  = sigmoid(h) = 1 - s(|h|) (h >= 0) or s(|h|).
+// Above torch's threshold (h > 20) the zero entry gives sph = h/2 (softplus = h) and sg = 1.
 template <int N>
-__device__ __forceinline__ void sp_and_grad_n(const double (&h)[N], double (&sp)[N],
-                                              double (&sg)[N], const double* tab) {
-#if GNND_F64_SPTAB
-    // the one-read table (gnnd_common.h softplus_sp / sig_poly): all N 16-byte reads first
+__device__ __forceinline__ void sph_and_grad_n(const double (&h)[N], double (&sph)[N],
+                                               double (&sg)[N], const double* tab) {
     SpIdx q[N];
     SpEntry e[N];
 #pragma unroll
@@ -82,49 +57,10 @@ __device__ __forceinline__ void sp_and_grad_n(const double (&h)[N], double (&sp)
     for (int i = 0; i < N; ++i) e[i] = sp_entry(tab, q[i].j);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        sp[i] = relu_f64(h[i]) + sp_poly(q[i].r, e[i].f0, e[i].s);
+        sph[i] = __builtin_fma(__builtin_fabs(h[i]), 0.5, sp_poly(q[i].r, e[i].f0, e[i].s));
         const double sa = sig_poly(q[i].r, e[i].s);
         sg[i] = h[i] >= 0.0 ? 1.0 - sa : sa;
     }
-#else
-    double p[N], tv[N], e[N], rj[N], lj[N];
-    int ex[N], ia[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        double tk;
-        asm("v_fma_f64 %0, -|%1|, %2, %3" : "=v"(tk) : "v"(h[i]), "s"(369.32993046757462), "v"(kRoundMagic));
-        const double kd = tk - kRoundMagic;
-        const double r = __builtin_fma(-kd, 6.93147180559945309417e-01 / 256, -__builtin_fabs(h[i]));
-        double q = fma_vsv(r, 1.0 / 6, 0.5);
-        q = __builtin_fma(q, r, 1.0);
-        p[i] = __builtin_fma(q, r, 1.0);
-        const int k = round_magic_lo(tk);
-        ex[i] = h[i] > 20.0 ? -2048 : (k >> 8);
-        ia[i] = k & (kExpTabN - 1);
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) tv[i] = tab[ia[i]];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        e[i] = __builtin_ldexp(tv[i] * p[i], ex[i]);
-        ia[i] = round_magic_lo(fma_vsv(e[i], 256.0, kRoundMagic));      // rint(256 e): 0..256
-    }
-    const double* lt = tab + kExpTabN;
-#pragma unroll
-    for (int i = 0; i < N; ++i) { rj[i] = lt[2 * ia[i]]; lj[i] = lt[2 * ia[i] + 1]; }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const double d = 1.0 + e[i];
-        const double t = __builtin_fma(d, rj[i], -1.0);
-        double q = fma_vsv(t, -0.25, 1.0 / 3);
-        q = __builtin_fma(q, t, -0.5);
-        sp[i] = relu_f64(h[i]) + (lj[i] + __builtin_fma(q * t, t, t));
-        double rc = __builtin_amdgcn_rcp(d);
-        rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
-        rc = __builtin_fma(__builtin_fma(-d, rc, 1.0), rc, rc);
-        sg[i] = (h[i] >= 0.0 ? 1.0 : e[i]) * rc;
-    }
-#endif
 }
 __device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg, const float*) {
     if (h > 20.f) { sp = h; sg = 1.f; return; }
@@ -227,9 +163,6 @@ __device__ __forceinline__ double wave_sum(double v) {
     const int lo = __builtin_amdgcn_readlane((int)b, 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-#ifndef GNND_BWD_F64_STAGE
-#define GNND_BWD_F64_STAGE 8      // fp64 reverse pass: Softplus chains per LDS stage (A/B: 4, 1)
-#endif
 // fp64 wave_rows4: the same lane folds on both 32-bit halves of every value, then the row
 // DPP chain in fp64 (21 VALU for four edges' totals; two six-step wave_sum chains per edge pair
 // were ~40 dependent ops per pair)
@@ -263,6 +196,10 @@ template <typename T> __device__ __forceinline__ T put_lane(T v, T x, int k, int
 template <typename T> struct Units {
     T w1a[2], w1b[2], b1[2], w2[2];         // w1b only for the 2-input MLP
     T gw1a[2], gw1b[2], gb1[2], gw2[2], gb2;
+    // fp64: layer-1 gradients accumulate WITHOUT the W2 factor (applied at flush), d input
+    // through w2w1a = W2 W1a, and the linear half of relu(h) in dW2 as the per-wave sums
+    // sx0 = sum dy u0, sx1 = sum dy u1 (with gb2 = sum dy): dW2 += (W1a sx0 + W1b sx1 + b1 gb2)/2
+    T w2w1a[2], sx0, sx1;
     f32x2 pgw1a[2], pgw1b[2], pgb1[2], pgw2[2];  // fp32 packed path: per-edge-half partials
     float s1a[2], s1b[2], sb1[2];                // fp32: layer 1 in log2 units (x log2 e)
     float ws1a[2];                               // fp32: W2 W1a (d input with W2 factored out)
@@ -294,7 +231,8 @@ template <typename T> struct Units {
             w1a[j] = w[k]; w1b[j] = T(0); b1[j] = w[128 + k]; w2[j] = w[256 + k];
             gw1a[j] = gw1b[j] = gb1[j] = gw2[j] = T(0);
         }
-        gb2 = T(0);
+        gb2 = sx0 = sx1 = T(0);
+        for (int j = 0; j < 2; ++j) w2w1a[j] = w2[j] * w1a[j];
         zero_packed();
     }
     __device__ void load2(const T* __restrict__ w, int lane) {    // {W1a, W1b, b1, W2, b2}
@@ -303,44 +241,9 @@ template <typename T> struct Units {
             w1a[j] = w[k]; w1b[j] = w[128 + k]; b1[j] = w[256 + k]; w2[j] = w[384 + k];
             gw1a[j] = gw1b[j] = gb1[j] = gw2[j] = T(0);
         }
-        gb2 = T(0);
+        gb2 = sx0 = sx1 = T(0);
+        for (int j = 0; j < 2; ++j) w2w1a[j] = w2[j] * w1a[j];
         zero_packed();
-    }
-    // backward of y = sum_k W2_k sp(W1a_k u0 (+ W1b_k u1) + b1_k) + b2 at two edges a, b
-    // (independent chains for the scheduler); returns d y / d u0 per edge (wave-reduced,
-    // uniform).  An edge with dy = 0 contributes nothing (masked tail).
-    template <bool TWO>
-    __device__ __forceinline__ void bwd2(T xa0, T xa1, T dya, T xb0, T xb1, T dyb, T& ra, T& rb,
-                                         const T* tab) {
-        if constexpr (sizeof(T) == 4) {
-            bwd2_f32<TWO>(xa0, xa1, dya, xb0, xb1, dyb, ra, rb);
-            return;
-        }
-        T pa = T(0), pb = T(0);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            T ha = xa0 * w1a[j], hb = xb0 * w1a[j];
-            if constexpr (TWO) { ha = ha + xa1 * w1b[j]; hb = hb + xb1 * w1b[j]; }
-            ha = ha + b1[j];
-            hb = hb + b1[j];
-            T spa, sga, spb, sgb;
-            sp_and_grad(ha, spa, sga, tab);
-            sp_and_grad(hb, spb, sgb, tab);
-            gw2[j] += dya * spa;
-            gw2[j] += dyb * spb;
-            const T dha = (dya * w2[j]) * sga, dhb = (dyb * w2[j]) * sgb;
-            gw1a[j] += dha * xa0;
-            gw1a[j] += dhb * xb0;
-            if constexpr (TWO) { gw1b[j] += dha * xa1; gw1b[j] += dhb * xb1; }
-            gb1[j] += dha;
-            gb1[j] += dhb;
-            pa += dha * w1a[j];
-            pb += dhb * w1a[j];
-        }
-        gb2 += dya;
-        gb2 += dyb;
-        ra = wave_sum(pa);
-        rb = wave_sum(pb);
     }
     // fp64: four CONSECUTIVE edges per wave step (the fp32 unit pass's shape): eight independent
     // Softplus/sigmoid evaluations per lane, weight gradients summed over the four edges as a
@@ -350,8 +253,7 @@ template <typename T> struct Units {
     __device__ __forceinline__ double bwd4_rows_f64(const double (&x0)[4], const double (&x1)[4],
                                                     const double (&dy)[4], const double* tab) {
         double p[4] = {0.0, 0.0, 0.0, 0.0};
-#if GNND_BWD_F64_STAGE == 8
-        double h8[8], sp8[8], sg8[8];
+        double h8[8], sph8[8], sg8[8];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -360,35 +262,15 @@ template <typename T> struct Units {
                 if constexpr (TWO) h = h + x1[i] * w1b[j];
                 h8[4 * j + i] = h + b1[j];
             }
-        sp_and_grad_n<8>(h8, sp8, sg8, tab);
-#endif
+        sph_and_grad_n<8>(h8, sph8, sg8, tab);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            double sp[4], sg[4], dh[4];
-#if GNND_BWD_F64_STAGE == 8
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { sp[i] = sp8[4 * j + i]; sg[i] = sg8[4 * j + i]; }
-#elif GNND_BWD_F64_STAGE == 4
-            double hh[4];
+            const double* sp = sph8 + 4 * j;
+            double dh[4];                         // d y / d h without the W2 factor
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                double h = x0[i] * w1a[j];
-                if constexpr (TWO) h = h + x1[i] * w1b[j];
-                hh[i] = h + b1[j];
-            }
-            sp_and_grad_n<4>(hh, sp, sg, tab);
-#else
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double h = x0[i] * w1a[j];
-                if constexpr (TWO) h = h + x1[i] * w1b[j];
-                sp_and_grad(h + b1[j], sp[i], sg[i], tab);
-            }
-#endif
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                dh[i] = (dy[i] * w2[j]) * sg[i];
-                p[i] += dh[i] * w1a[j];
+                dh[i] = dy[i] * sg8[4 * j + i];
+                p[i] += dh[i] * w2w1a[j];
             }
             gw2[j] += (dy[0] * sp[0] + dy[1] * sp[1]) + (dy[2] * sp[2] + dy[3] * sp[3]);
             gw1a[j] += (dh[0] * x0[0] + dh[1] * x0[1]) + (dh[2] * x0[2] + dh[3] * x0[3]);
@@ -397,6 +279,8 @@ template <typename T> struct Units {
             gb1[j] += (dh[0] + dh[1]) + (dh[2] + dh[3]);
         }
         gb2 += (dy[0] + dy[1]) + (dy[2] + dy[3]);
+        sx0 += (dy[0] * x0[0] + dy[1] * x0[1]) + (dy[2] * x0[2] + dy[3] * x0[3]);
+        if constexpr (TWO) sx1 += (dy[0] * x1[0] + dy[1] * x1[1]) + (dy[2] * x1[2] + dy[3] * x1[3]);
         return wave_rows4(p[0], p[1], p[2], p[3]);
     }
     // fp32: edges a and b ride the two halves of every packed op (v_pk_fma/mul/add_f32 with
@@ -471,8 +355,16 @@ template <typename T> struct Units {
     // plain layout; every index of the MLP written by exactly one lane)
     template <bool TWO>
     __device__ void flush(T* acc, int lane, bool folded) {
-        if constexpr (sizeof(T) == 4)
+        if constexpr (sizeof(T) == 4) {
             if (!folded) fold();
+        } else {
+            for (int j = 0; j < 2; ++j) {             // the factored-out W2 and relu's linear half
+                gw1a[j] *= w2[j];
+                gw1b[j] *= w2[j];
+                gb1[j] *= w2[j];
+                gw2[j] += (w1a[j] * sx0 + w1b[j] * sx1 + b1[j] * gb2) * 0.5;
+            }
+        }
         for (int j = 0; j < 2; ++j) {
             const int k = lane + 64 * j;
             if constexpr (TWO) {
@@ -569,7 +461,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     uo.load1(w + kV24Mlp, lane);
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     if constexpr (kTabB > 0)
-        for (int i = tid; i < kV24F64TabDoubles; i += kTrainThreads) s_ftab[i] = v24_f64_tab_entry(i);
+        for (int i = tid; i < kSpTabDoubles; i += kTrainThreads) s_ftab[i] = kSpTab[i];
     for (int i = tid; i < 8 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
     if (floss) {
         for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
@@ -686,7 +578,6 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             if constexpr (kPipe) U.fold();
             return;
         }
-#ifndef GNND_BWD_F64_PAIRS
         if constexpr (sizeof(T) == 8) {
             // fp64: four consecutive edges f..f+3 per wave step (f = 4 (wave + W k)); padding
             // entries E..Ep-1 are zero inputs with dy = 0, and every lane stores its row's total
@@ -700,28 +591,6 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                     dy[i] = dy_of(f + i);
                 }
                 outp[f + eo] = U.template bwd4_rows_f64<TWO>(a0, a1, dy, s_ftab);
-            }
-            return;
-        }
-#endif
-        constexpr int kStride = 2 * kTrainWaves;
-        for (int f0 = wave; f0 < E; f0 += 64 * kStride) {
-            T resa = T(0), resb = T(0);
-            int k = 0;
-            for (int f = f0; f < E && k < 64; f += kStride, ++k) {
-                const int f2 = f + kTrainWaves;
-                const bool has2 = f2 < E;
-                const int fb = has2 ? f2 : f;
-                T ra, rb;
-                U.template bwd2<TWO>(in0[f], TWO ? in1[f] : T(0), dy_of(f), in0[fb],
-                                     TWO ? in1[fb] : T(0), has2 ? dy_of(fb) : T(0), ra, rb, s_ftab);
-                resa = put_lane(resa, ra, k, lane);
-                resb = put_lane(resb, rb, k, lane);
-            }
-            const int fl = f0 + kStride * lane;
-            if (lane < k) {
-                outp[fl] = resa;
-                if (fl + kTrainWaves < E) outp[fl + kTrainWaves] = resb;
             }
         }
     };
