@@ -292,6 +292,43 @@ __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, c
     else if constexpr (NC == 2) return c[0] + c[1];
     else return c[0];
 }
+// the unit-split form's weights (US > 1): each MLP's units staged in LDS CHAIN-major (unit
+// k = 4 i + j at entry 32 j + i, {W1a, W1b, b1, W2} per entry), so a wave's chain reads
+// consecutive entries as broadcast ds_read_b128s — from global memory a chain's units are
+// 4 apart, one scalar load and one wait per weight (measured: 11 lgkmcnt(0) waits per 4 units)
+struct WcmEntry {
+    double w1a, w1b, b1, w2;
+};
+template <int NC, int J0, bool TWO>
+__device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u0, double u1,
+                                                    const double* tab) {
+    constexpr int UT = 4, NU = 32 * NC;       // units per stage (NC divides UT), per call
+    static_assert(UT % NC == 0, "stage holds whole chain groups");
+    double c[NC];
+#pragma unroll
+    for (int jj = 0; jj < NC; ++jj) c[jj] = 0.0;
+#pragma unroll 2
+    for (int t0 = 0; t0 < NU; t0 += UT) {
+        WcmEntry e[UT];
+        double h[UT];
+        SpIdx q[UT];
+        SpEntry t[UT];
+#pragma unroll
+        for (int s = 0; s < UT; ++s) e[s] = wl[(J0 + s % NC) * 32 + t0 / NC + s / NC];
+#pragma unroll
+        for (int s = 0; s < UT; ++s) {
+            h[s] = TWO ? fma(u0, e[s].w1a, fma(u1, e[s].w1b, e[s].b1)) : fma(u0, e[s].w1a, e[s].b1);
+            q[s] = sp_index(h[s]);
+        }
+#pragma unroll
+        for (int s = 0; s < UT; ++s) t[s] = sp_entry(tab, q[s].j);
+#pragma unroll
+        for (int s = 0; s < UT; ++s)
+            c[s % NC] = fma(relu_f64(h[s]) + sp_poly(q[s].r, t[s].f0, t[s].s), e[s].w2, c[s % NC]);
+    }
+    if constexpr (NC == 2) return c[0] + c[1];
+    else return c[0];
+}
 __device__ __forceinline__ double mlp128_sp(const double* w, const double* bl, double u,
                                             const double* tab) {
     return mlp128d_chains<4, 0, false>(w, bl, u, u, tab) + w[384];
@@ -304,7 +341,8 @@ __device__ __forceinline__ double mlp128_sp(const double* w, const double* bl, d
 template <int US, bool TWO>
 __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, const double* bl,
                                                 double u0, double u1, int sub, double* buf,
-                                                int itid, bool idle, const double* tab) {
+                                                int itid, bool idle, const double* tab,
+                                                const WcmEntry* wl = nullptr) {
     constexpr int kB2 = TWO ? 512 : 384;
     if constexpr (US == 1) {
         return idle ? 0.0 : mlp128d_chains<4, 0, TWO>(w, bl, u0, u1, tab) + w[kB2];
@@ -313,12 +351,21 @@ __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, co
         constexpr int NC = 4 / US, IL = GNND_BLOCK;
         double p = 0.0;
         if (!idle) {
+#if GNND_F64_SPTAB
+            switch (sub) {
+                case 0: p = mlp128d_chains_cm<NC, 0, TWO>(wl, u0, u1, tab); break;
+                case 1: p = mlp128d_chains_cm<NC, NC, TWO>(wl, u0, u1, tab); break;
+                case 2: if constexpr (US == 4) p = mlp128d_chains_cm<1, 2, TWO>(wl, u0, u1, tab); break;
+                default: if constexpr (US == 4) p = mlp128d_chains_cm<1, 3, TWO>(wl, u0, u1, tab); break;
+            }
+#else
             switch (sub) {
                 case 0: p = mlp128d_chains<NC, 0, TWO>(w, bl, u0, u1, tab); break;
                 case 1: p = mlp128d_chains<NC, NC, TWO>(w, bl, u0, u1, tab); break;
                 case 2: if constexpr (US == 4) p = mlp128d_chains<1, 2, TWO>(w, bl, u0, u1, tab); break;
                 default: if constexpr (US == 4) p = mlp128d_chains<1, 3, TWO>(w, bl, u0, u1, tab); break;
             }
+#endif
         }
         buf[sub * IL + itid] = p;
         __syncthreads();
@@ -928,6 +975,20 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
     constexpr bool kV24F64 = MODEL == GNND_V24 && sizeof(T) == 8;
     double* s_pd = (double*)s_part;                        // fp64 unit split: [2][US][256]
+    // fp64 unit split: the three MLPs' chain-major weights [3][128] (16-byte aligned) after it
+    WcmEntry* s_wcm = (WcmEntry*)(smem + ((((char*)(s_pd + 2 * US * GNND_BLOCK) - smem) + 15) & ~(ptrdiff_t)15));
+    if constexpr (MODEL == GNND_V24 && sizeof(T) == 8 && US > 1 && GNND_F64_SPTAB) {
+        for (int i = tid; i < 3 * 128; i += NT) {     // entry 32 j + i of MLP m: unit k = 4 i + j
+            const int m = i >> 7, pos = i & 127, k = 4 * (pos & 31) + (pos >> 5);
+            const T* wm = w + (m == 0 ? kV24Ggc1 : m == 1 ? kV24Ggc2 : kV24Mlp);
+            WcmEntry e;
+            e.w1a = wm[k];
+            e.w1b = m == 0 ? wm[128 + k] : 0.0;
+            e.b1 = wm[(m == 0 ? 256 : 128) + k];
+            e.w2 = wm[(m == 0 ? 384 : 256) + k];
+            s_wcm[i] = e;
+        }
+    }
     // fp32 decoder_v2_4 reads its weights through the scalar cache only (no LDS copy); with
     // every table and the tile's rows within one element per thread (small batches: one
     // component-codeword per workgroup) all global loads are issued before any LDS store, so
@@ -1117,7 +1178,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 for (int r = 0; r < R; ++r) {
                     const T a = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
                                                         s_pd + (r & 1) * US * GNND_BLOCK, itid, widle,
-                                                        s_tab);
+                                                        s_tab, s_wcm);
                     tv[r] = val[r] ? tanh_half_fast(a) : T(0);
                     cf[r] = T(0);
                     tsum += tv[r];
@@ -1201,7 +1262,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 for (int r = 0; r < R; ++r) {
                     const T y = mlp128d_split<US, false>(wv + kV24Ggc2, s_bias + 128, Sc - tv[r], Sc - tv[r], sub,
                                                          s_pd + ((R + r) & 1) * US * GNND_BLOCK, itid,
-                                                         widle, s_tab);
+                                                         widle, s_tab, s_wcm + 128);
                     mn[r] = y * sc + mv[r];
                 }
             } else if constexpr (WBP) {
@@ -1282,7 +1343,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const bool widle = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= n;
                 const T m = s_m[f < n ? f : n - 1];
                 const T y = mlp128d_split<US, false>(wv + kV24Mlp, s_bias + 256, m, m, sub,
-                                                     s_pd + rb * US * GNND_BLOCK, itid, widle, s_tab);
+                                                     s_pd + rb * US * GNND_BLOCK, itid, widle, s_tab,
+                                                     s_wcm + 256);
                 if (sub == 0 && f < n) s_m[f] = y;   // (lanes read only their own message)
             }
         } else {
@@ -2283,9 +2345,11 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         const int forced = v24_split_forced();
         int us = forced ? forced : n > 1 ? us_big : B <= 256 ? 4 : B <= 512 ? 2 : 1;
         if (us > 4) us = 4;
-        if (us > 1 && align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8 <= kLdsMax) {
+        // (+ the chain-major weights of the three MLPs, 16-byte aligned: mlp128d_chains_cm)
+        const size_t wcm = GNND_F64_SPTAB ? (size_t)3 * 128 * sizeof(WcmEntry) + 16 : 0;
+        if (us > 1 && align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8 + wcm <= kLdsMax) {
             p->us = us;
-            p->lds = align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8;
+            p->lds = align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8 + wcm;
         }
     }
     return GNND_OK;
