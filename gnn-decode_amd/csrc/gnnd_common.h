@@ -1800,6 +1800,21 @@ __device__ __forceinline__ double softplus_v24(double x, const double* __restric
     if (GNND_F64_SPTAB) return softplus_sp(x, tab);
     return softplus_fast(x, tab);
 }
+// softplus(x) - x/2 = |x|/2 + ln(1 + e^-|x|) with the one-read table (one FMA instead of relu's
+// max + add; the linear x/2 is summed per MLP: decode_kernel mlp_lin); the exp + log1p form
+// (GNND_F64_SPTAB 0) keeps the whole value
+#ifndef GNND_F64_LINFOLD
+#define GNND_F64_LINFOLD GNND_F64_SPTAB   // 0: whole Softplus per unit, no per-MLP linear part (A/B)
+#endif
+__device__ __forceinline__ double softplus_v24_half(double x, const double* __restrict__ tab) {
+    if (!GNND_F64_LINFOLD) return softplus_v24(x, tab);
+    if (GNND_F64_SPTAB) {
+        const SpIdx q = sp_index(x);
+        const SpEntry e = sp_entry(tab, q.j);
+        return __builtin_fma(__builtin_fabs(x), 0.5, sp_poly(q.r, e.f0, e.s));
+    }
+    return softplus_fast(x, tab);
+}
 
 template <typename T> __device__ __forceinline__ T sigmoid_ref(T x) {
     return T(1) / (T(1) + g_exp(-x));

@@ -285,7 +285,7 @@ __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, c
             double h;
             if constexpr (TWO) h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], bl[k]));
             else h = fma_vsv(u0, w[k], bl[k]);
-            c[jj] = fma(softplus_v24(h, tab), w[kW2 + k], c[jj]);
+            c[jj] = fma(softplus_v24_half(h, tab), w[kW2 + k], c[jj]);
         });
     }
     if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
@@ -323,15 +323,26 @@ __device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u
 #pragma unroll
         for (int s = 0; s < UT; ++s) t[s] = sp_entry(tab, q[s].j);
 #pragma unroll
-        for (int s = 0; s < UT; ++s)
-            c[s % NC] = fma(relu_f64(h[s]) + sp_poly(q[s].r, t[s].f0, t[s].s), e[s].w2, c[s % NC]);
+        for (int s = 0; s < UT; ++s) {
+            const double g = sp_poly(q[s].r, t[s].f0, t[s].s);
+            c[s % NC] = fma(GNND_F64_LINFOLD ? __builtin_fma(__builtin_fabs(h[s]), 0.5, g) : relu_f64(h[s]) + g,
+                            e[s].w2, c[s % NC]);
+        }
     }
     if constexpr (NC == 2) return c[0] + c[1];
     else return c[0];
 }
+// the linear half of the MLP's relu terms (softplus_v24_half leaves out h/2):
+// sum_k W2_k h_k / 2 = u0 A + u1 B + C, ln = {A, B, C} staged per MLP (decode_kernel prologue);
+// added after the fixed chain tree, before b2, in every split (the same bits)
+template <bool TWO>
+__device__ __forceinline__ double mlp_lin(const double* ln, double u0, double u1) {
+    if (!GNND_F64_LINFOLD) return 0.0;
+    return TWO ? fma(u0, ln[0], fma(u1, ln[1], ln[2])) : fma(u0, ln[0], ln[2]);
+}
 __device__ __forceinline__ double mlp128_sp(const double* w, const double* bl, double u,
-                                            const double* tab) {
-    return mlp128d_chains<4, 0, false>(w, bl, u, u, tab) + w[384];
+                                            const double* tab, const double* ln) {
+    return (mlp128d_chains<4, 0, false>(w, bl, u, u, tab) + mlp_lin<false>(ln, u, u)) + w[384];
 }
 // unit-split evaluation of the fp64 MLPs (decode_kernel US > 1, fp64 decoder_v2_4 small
 // batches): wave `sub` evaluates chain group sub, the US partial sums meet in LDS (buf = [US][256]
@@ -342,10 +353,10 @@ template <int US, bool TWO>
 __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, const double* bl,
                                                 double u0, double u1, int sub, double* buf,
                                                 int itid, bool idle, const double* tab,
-                                                const WcmEntry* wl = nullptr) {
+                                                const double* ln, const WcmEntry* wl = nullptr) {
     constexpr int kB2 = TWO ? 512 : 384;
     if constexpr (US == 1) {
-        return idle ? 0.0 : mlp128d_chains<4, 0, TWO>(w, bl, u0, u1, tab) + w[kB2];
+        return idle ? 0.0 : (mlp128d_chains<4, 0, TWO>(w, bl, u0, u1, tab) + mlp_lin<TWO>(ln, u0, u1)) + w[kB2];
     } else {
         static_assert(US == 2 || US == 4, "fp64 unit split 1, 2 or 4");
         constexpr int NC = 4 / US, IL = GNND_BLOCK;
@@ -372,7 +383,7 @@ __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, co
         double r;
         if constexpr (US == 2) r = buf[itid] + buf[IL + itid];
         else r = (buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid]);
-        return r + w[kB2];
+        return (r + mlp_lin<TWO>(ln, u0, u1)) + w[kB2];
     }
 }
 
@@ -947,10 +958,28 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
     T* s_tab = nullptr;
     T* s_bias = nullptr;
+    T* s_lin = nullptr;        // [3][4] {A, B, C, 0} per MLP (mlp_lin), after the biases
     if constexpr (kTab) {
         s_tab = (T*)smem;
         s_bias = s_tab + kV24F64TabDoubles;
-        off = (size_t)(kV24F64TabDoubles + 3 * 128) * 8;
+        s_lin = s_bias + 3 * 128;
+        off = (size_t)(kV24F64TabDoubles + 3 * 128 + 12) * 8;
+        if (tid < 64) {            // wave 0: fixed-order 128-term dot products (same in every block)
+            for (int m = 0; m < 3; ++m) {
+                const T* wm = w + (m == 0 ? kV24Ggc1 : m == 1 ? kV24Ggc2 : kV24Mlp);
+                const int o2 = m == 0 ? 384 : 256;
+                for (int q = 0; q < 3; ++q) {
+                    const int oa = q == 0 ? 0 : q == 1 ? 128 : (m == 0 ? 256 : 128);
+                    T v = T(0);
+                    if (q != 1 || m == 0) {
+                        const T pl = fma(wm[o2 + tid + 64], wm[oa + tid + 64], wm[o2 + tid] * wm[oa + tid]);
+                        v = group_sum_c<64>(pl) * T(0.5);
+                    }
+                    if (tid == 0) s_lin[4 * m + q] = v;
+                }
+                if (tid == 0) s_lin[4 * m + 3] = T(0);
+            }
+        }
         for (int i = tid; i < kV24F64TabDoubles; i += NT) s_tab[i] = v24_f64_tab_entry(i);
         for (int i = tid; i < 3 * 128; i += NT) {
             const int m = i >> 7, k = i & 127;
@@ -1178,7 +1207,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 for (int r = 0; r < R; ++r) {
                     const T a = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
                                                         s_pd + (r & 1) * US * GNND_BLOCK, itid, widle,
-                                                        s_tab, s_wcm);
+                                                        s_tab, s_lin, s_wcm);
                     tv[r] = val[r] ? tanh_half_fast(a) : T(0);
                     cf[r] = T(0);
                     tsum += tv[r];
@@ -1262,7 +1291,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 for (int r = 0; r < R; ++r) {
                     const T y = mlp128d_split<US, false>(wv + kV24Ggc2, s_bias + 128, Sc - tv[r], Sc - tv[r], sub,
                                                          s_pd + ((R + r) & 1) * US * GNND_BLOCK, itid,
-                                                         widle, s_tab, s_wcm + 128);
+                                                         widle, s_tab, s_lin + 4, s_wcm + 128);
                     mn[r] = y * sc + mv[r];
                 }
             } else if constexpr (WBP) {
@@ -1344,11 +1373,11 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const T m = s_m[f < n ? f : n - 1];
                 const T y = mlp128d_split<US, false>(wv + kV24Mlp, s_bias + 256, m, m, sub,
                                                      s_pd + rb * US * GNND_BLOCK, itid, widle, s_tab,
-                                                     s_wcm + 256);
+                                                     s_lin + 8, s_wcm + 256);
                 if (sub == 0 && f < n) s_m[f] = y;   // (lanes read only their own message)
             }
         } else {
-            for (int f = tid; f < nb * nslot; f += NT) s_m[f] = mlp128_sp(wv + kV24Mlp, s_bias + 256, s_m[f], s_tab);
+            for (int f = tid; f < nb * nslot; f += NT) s_m[f] = mlp128_sp(wv + kV24Mlp, s_bias + 256, s_m[f], s_tab, s_lin + 8);
         }
         __syncthreads();
     }
@@ -2280,7 +2309,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const GraphView& g = !v24f32 ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
-    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kV24F64TabDoubles + 3 * 128) * 8 : 0;
+    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kV24F64TabDoubles + 3 * 128 + 12) * 8 : 0;
     const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab;
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
