@@ -2320,8 +2320,12 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
 #ifndef GNND_V24F64_LDS
 #define GNND_V24F64_LDS (GNND_F64_SPTAB ? (kLdsMax / 3) & ~(size_t)15 : 0)
 #endif
-    const size_t tgt = model == GNND_V24 && dtype == GNND_F64 && GNND_V24F64_LDS && !lds_target_set()
-                           ? (size_t)GNND_V24F64_LDS : target;
+    size_t tgt = model == GNND_V24 && dtype == GNND_F64 && GNND_V24F64_LDS && !lds_target_set()
+                     ? (size_t)GNND_V24F64_LDS : target;
+    // (larger graphs, e.g. toric-7 at 7 KB per codeword: where a third of the LDS holds fewer
+    // than two codewords, half of it: 2 workgroups per CU, several codewords each)
+    if (tgt == (size_t)GNND_V24F64_LDS && tgt != target && fixed + 2 * per > tgt)
+        tgt = (kLdsMax / 2) & ~(size_t)15;
     const int us_big = model == GNND_V24 && dtype == GNND_F64 && g.R <= 2 ? v24f64_us_big() : 1;
     const size_t bufb = us_big > 1 ? (size_t)2 * us_big * GNND_BLOCK * 8 + 8 : 0;
     size_t n = fixed + bufb + per >= tgt ? 1 : (tgt - fixed - bufb) / per;
