@@ -225,6 +225,27 @@ template <typename T> struct Units {
             gw2[j] += (pgw2[j].x + pgw2[j].y) * kLn2;
         }
     }
+    // fp32: the per-lane constants a unit pass reads (s1a, s1b, sb1, ws1a, W2) parked in LDS
+    // between passes ([10][64] floats per MLP, identical in every wave: wave 0 writes them), so
+    // only the active MLP's stay in registers (the 16-wave reverse pass holds 128 VGPRs)
+    __device__ void park(float* sp, int lane) const {
+        for (int j = 0; j < 2; ++j) {
+            sp[(0 + j) * 64 + lane] = s1a[j];
+            sp[(2 + j) * 64 + lane] = s1b[j];
+            sp[(4 + j) * 64 + lane] = sb1[j];
+            sp[(6 + j) * 64 + lane] = ws1a[j];
+            sp[(8 + j) * 64 + lane] = (float)w2[j];
+        }
+    }
+    __device__ __forceinline__ void unpark(const float* sp, int lane) {
+        for (int j = 0; j < 2; ++j) {
+            s1a[j] = sp[(0 + j) * 64 + lane];
+            s1b[j] = sp[(2 + j) * 64 + lane];
+            sb1[j] = sp[(4 + j) * 64 + lane];
+            ws1a[j] = sp[(6 + j) * 64 + lane];
+            w2[j] = (T)sp[(8 + j) * 64 + lane];
+        }
+    }
     __device__ void load1(const T* __restrict__ w, int lane) {    // {W1, b1, W2, b2}
         for (int j = 0; j < 2; ++j) {
             const int k = lane + 64 * j;
@@ -412,6 +433,10 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     constexpr int kTrainWaves = kTrainThreads / 64;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: edge loops on SALU
+#ifndef GNND_BWD_PARK
+#define GNND_BWD_PARK 1
+#endif
+    constexpr bool kParkF32 = sizeof(T) == 4 && GNND_BWD_PARK;
     // fp64: the forward's Softplus table (kSpTab) at LDS byte 0 (sp_and_grad_n)
     constexpr size_t kTabB = bwd_tab_bytes<T>();
     T* s_ftab = (T*)smem;
@@ -453,12 +478,23 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     // arithmetic on the __shared__ base keeps ds_* accesses)
     const char* sib_end = floss ? (const char*)(s_lvar + (size_t)nl * V) : (const char*)s_ls;
     int* s_sib = (int*)(smem + (((sib_end - smem) + 15) & ~(ptrdiff_t)15));
+    // fp32: the three MLPs' parked pass constants [3][10][64] after the sibling tables (or where
+    // they would start; train_lds reserves it; dead before the gradient flush reuses the space)
+    float* s_wp = (float*)(smem + (((((const char*)s_sib - smem) + (sibs ? 32 * (ptrdiff_t)E : 0)) + 15) &
+                                   ~(ptrdiff_t)15));
 
     const int* gtab = (const int*)g.edge_vc;
     Units<T> uv, uc, uo;                     // ggc1.mlp, ggc2.mlp, mlp
     uv.load2(w + kV24Ggc1, lane);
     uc.load1(w + kV24Ggc2, lane);
     uo.load1(w + kV24Mlp, lane);
+    if constexpr (kParkF32) {
+        if (wave == 0) {
+            uv.park(s_wp, lane);
+            uc.park(s_wp + 640, lane);
+            uo.park(s_wp + 1280, lane);
+        }
+    }
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     if constexpr (kTabB > 0)
         for (int i = tid; i < kSpTabDoubles; i += kTrainThreads) s_ftab[i] = kSpTab[i];
@@ -693,6 +729,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             else return f32x4{0.f, 0.f, 0.f, 0.f};
         };
         GNND_PMARK(pf, 0);
+        if constexpr (kParkF32) uo.unpark(s_wp + 1280, lane);
         unit_pass(uo, std::false_type{}, s_u, nullptr, [&](int f) { return s_da[f]; },
                   [&](int f) { return ld4(s_da, f); }, s_dm);
         __syncthreads();
@@ -708,8 +745,11 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             if (it > 0) prefetch(it - 1);
             // A: m^{t+1} = MLP_c(u) s_c + m^t
             if (GNND_BWD_EXP != 3)
+            {
+                if constexpr (kParkF32) uc.unpark(s_wp + 640, lane);
                 unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; },
                           [&](int f) { return ld4(s_dm, f) * ld4(s_sc, f); }, s_g);
+            }
             GNND_PMARK(pf, 3);
             __syncthreads();
             GNND_PMARK(pf, 4);
@@ -737,8 +777,11 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             GNND_PMARK(pf, 6);
             // C: a = MLP_v(ext, x_v)
             if (GNND_BWD_EXP != 3)
+            {
+                if constexpr (kParkF32) uv.unpark(s_wp, lane);
                 unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; },
                           [&](int f) { return ld4(s_da, f); }, s_g);
+            }
             GNND_PMARK(pf, 7);
             __syncthreads();
             GNND_PMARK(pf, 8);
@@ -852,6 +895,7 @@ size_t train_lds(const gnnd_graph* g, int esz, int nl = -1, int waves = 0, bool 
         n += (size_t)esz * (3 * (size_t)v.V + 2 * ((size_t)v.C + nl)) +
              4 * ((size_t)v.V + nl + (size_t)nl * v.V);
     if (sibs) n = ((n + 15) & ~(size_t)15) + 32 * (size_t)v.E;
+    if (esz == 4) n = ((n + 15) & ~(size_t)15) + (size_t)3 * 10 * 64 * 4;   // parked constants
     const size_t red = tab + (size_t)esz * waves * kV24W;
     return n > red ? n : red;
 }
