@@ -1766,7 +1766,13 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     const int ia = cb[2 * j] * TS + GNND_DIDX((int)(ve[2 * j][r] & 0xffffu), TS, GNND_DBG_VAR);
                     const int ib = cb[2 * j + 1] * TS + GNND_DIDX((int)(ve[2 * j + 1][r] & 0xffffu), TS, GNND_DBG_VAR);
                     if constexpr (kTX) {
+#ifdef GNND_DIAG_TV_LINEAR
+                        // diagnostic build only (wrong results): lane-linear, conflict-free T reads
+                        (void)ia; (void)ib;
+                        px[r] = f32x2{s_t[(int)(threadIdx.x & 63)], s_t[64 + (int)(threadIdx.x & 63)]};
+#else
                         px[r] = f32x2{s_t[ia], s_t[ib]};
+#endif
                     } else {
                         px[r][0] = s_sx[ia];
                         px[r][1] = s_sx[ib];
@@ -1843,8 +1849,15 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     m2[j][r] = post2(kProd ? Sc * rcp2(tv[r]) : Sc - tv[r], Sc2 - cv[r], sc2[j], m2[j][r]);
+#ifdef GNND_DIAG_MSG_LINEAR
+                    // diagnostic build only (wrong results): lane-linear, conflict-free message writes
+                    (void)mba; (void)mbb;
+                    s_m[(int)(threadIdx.x & 63)] = m2[j][r].x * wnext(ve[qa][r]);
+                    s_m[64 + (int)(threadIdx.x & 63)] = m2[j][r].y * wnext(ve[qb][r]);
+#else
                     mba[GNND_DIDX((int)(ve[qa][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].x * wnext(ve[qa][r]);
                     mbb[GNND_DIDX((int)(ve[qb][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].y * wnext(ve[qb][r]);
+#endif
                 }
             };
             // one item with its slots in pairs (the same per-edge arithmetic as pair_step:
@@ -1997,7 +2010,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 else r = s + (kBase2 ? io_ld(xg[b * N + v]) : s_sx[sbase + v].x);
                 out[b0 * V + sbase + v] = io_st<TI>(M::readout(r, s_w));
             } else if constexpr (kTX) {
+#ifdef GNND_DIAG_VAR_LINEAR
+                s_t[(int)(threadIdx.x & 63)] = s;
+                (void)tbase; (void)tp;
+#else
                 s_t[tbase + tp] = s;                                  // T_v = S_v + x_v
+#endif
                 (void)v;
             } else {
                 s_sx[sbase + v].s = s;
@@ -2008,7 +2026,13 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         auto var_item = [&](int b, int i, int mbase, int sbase, int tbase) {
             const uint2 o = s_vord[i];
             const int v = (int)(o.x & 0xffffu), dv = (int)(o.x >> 16);
+#ifdef GNND_DIAG_VAR_LINEAR
+            // diagnostic build only (wrong results): lane-linear, conflict-free message-run reads
+            const T* mp = s_m + (int)(threadIdx.x & 63);
+            (void)mbase;
+#else
             const T* mp = s_m + mbase + (int)(o.y & 0xffffu);
+#endif
             if constexpr (MODEL == GNND_V22) {
                 // decoder_v2_2.py:333-347: the check step publishes raw messages (identity
                 // layout: positions = edge ids); the variable step forms the next layer's
