@@ -662,7 +662,8 @@ def train_trajectory(H, init_state, T, dev, dtype, seed, n=64, K=10):
     m = gd.MODELS['v24'](T, H).to(dev).to(dtype)
     m.load_state_dict(init_state)
     lf = gd.loss.SyndromeLoss(H, lg).to(dev)
-    tr = gd.train.FusedV24Trainer(m, lf, graph=False)
+    # (rank 0 alone runs this check: LOCAL, so an N-rank job's trainer issues no collective)
+    tr = gd.train.FusedV24Trainer(m, lf, graph=False, group=gd.train.LOCAL)
     data = gd.data.make_batch(x, m.graph(dev))
     gpu_losses = [float(tr.step(data, y)) for _ in range(K)]
     w = {k: v.detach().cpu().double().numpy() for k, v in init_state.items()}

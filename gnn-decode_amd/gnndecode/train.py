@@ -64,7 +64,14 @@ def flat_grads(params):
                       for p in params])
 
 
+# group=LOCAL: a trainer of this process alone, never issuing a collective even inside an
+# initialised N-rank job (e.g. a check one rank runs on its own: bench.py's trajectory parity)
+LOCAL = 'local'
+
+
 def _collective(group, force):
+    if group is LOCAL or group == LOCAL:
+        return False
     if not dist.is_available() or not dist.is_initialized():
         return False
     return force or dist.get_world_size(group) > 1

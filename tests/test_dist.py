@@ -91,3 +91,37 @@ def test_two_rank_training_equals_full_batch():
         assert flat.tolist() == res[0][2]     # ranks bitwise equal
         assert torch.allclose(flat, ref_flat, rtol=1e-12, atol=1e-13)
         assert all(abs(a - b) <= 1e-10 * max(1, abs(b)) for a, b in zip(losses, ref_losses))
+
+
+def _local_worker(rank, world, port, B, steps, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    if rank == 0:
+        # a check rank 0 runs on its own inside the 2-rank job (bench.py's trajectory parity):
+        # group=LOCAL, so its steps issue no collective (the other rank is not in them)
+        model = _Toy()
+        tr = train.Trainer(model, _sum_loss, lr=1e-2, group=train.LOCAL)
+        x, y = _data(B)
+        losses = [float(tr.step(x, y)) for _ in range(steps)]
+        q.put((rank, losses))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_local_trainer_in_a_multi_rank_job_issues_no_collective():
+    B, steps, world = 10, 3, 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_worker, args=(r, world, port, B, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rank, losses = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    model = _Toy()
+    tr = train.Trainer(model, _sum_loss, lr=1e-2)
+    x, y = _data(B)
+    assert losses == [float(tr.step(x, y)) for _ in range(steps)]
+    assert not train._collective(train.LOCAL, True)
