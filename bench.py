@@ -906,13 +906,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # (GNND_BENCH_BACKEND=gloo: a rehearsal of the N-rank flow with several ranks on one GPU,
+    # which RCCL refuses; ranks then share the visible GPUs round-robin)
+    backend = os.environ.get('GNND_BENCH_BACKEND', 'nccl')
+    if backend != 'nccl':
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1 or 'TORCHELASTIC_RUN_ID' in os.environ:
         # any torchrun launch (also --nproc-per-node 1) brings up RCCL, so the N>1 code path is
         # the one a 1-GPU torchrun run exercises; bind the communicator to this rank's GPU
         # (barriers then never touch GPU 0)
-        dist.init_process_group('nccl', device_id=dev)
+        dist.init_process_group(backend, device_id=dev)
     res = None
     if a.mode == 'train':
         res = train_run(a, world, rank, dev, cpu='full')
