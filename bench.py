@@ -436,6 +436,14 @@ def one_rank_group(dev):
     return True
 
 
+def drop_one_rank_group():
+    """Destroy the 1-rank group right after the collective timing, so later configs are timed
+    without a barrier / all_reduce inside their timed region."""
+    if _ONE_RANK_GROUP and dist.is_initialized():
+        dist.destroy_process_group()
+        _ONE_RANK_GROUP.clear()
+
+
 def v24_start_weights(model, code):
     """decoder_v2_4 training starts from the reference's checkpoint, as the script does
     (quantum/decoder_v2_4.py:322 loads decoder_parameters_epoch1.pkl before its Adam loop).
@@ -451,27 +459,37 @@ def v24_start_weights(model, code):
             f'loaded at {code})')
 
 
+TIMED_NS = [0, 0]       # monotonic-ns window of the last time_train_steps call
+
+
 def time_train_steps(tr, data, y, steps, fused_tr):
     """K timed steps bracketed by barrier + synchronize; returns (elapsed max over ranks, host
     issue seconds, last loss tensor)."""
     torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    mono0 = time.monotonic_ns()
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(steps):
         # the loss stays in the step's static buffer (read after the timed region), no copy
         loss = tr.step(data, y, copy_loss=False) if fused_tr else tr.step(data, y)
+    ev1.record()
     # host time to issue the K steps (before the final synchronize): close to the wall time
     # per step means the step is host-bound (the GPU waits between steps)
     issue_s = time.perf_counter() - t0
     torch.cuda.synchronize()
+    TIMED_NS[:] = [mono0, time.monotonic_ns()]
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # GPU time of the K steps on the stream the trainers launch on (torch's current stream)
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
     t = torch.tensor([elapsed], dtype=torch.float64, device=y.device)
     if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item()), issue_s, loss
+    return float(t.item()), issue_s, loss, gpu_s
 
 
 def train_run(a, world, rank, dev, cpu='full'):
@@ -550,7 +568,8 @@ def train_run(a, world, rank, dev, cpu='full'):
         data.x, y = st
     fused_tr = isinstance(tr, (gd.train.FusedV24Trainer, gd.train.FusedV30Trainer,
                                gd.train.FusedWbpTrainer, gd.train.FusedGnnTrainer))
-    elapsed, issue_s, loss = time_train_steps(tr, data, y, a.steps, fused_tr)
+    elapsed, issue_s, loss, gpu_s = time_train_steps(tr, data, y, a.steps, fused_tr)
+    timed_ns = list(TIMED_NS)
     # the same step with its RCCL all_reduce(SUM) of the flat gradient + loss actually issued:
     # N > 1 runs already contain it; a 1-GPU run times it on a 1-rank RCCL group
     # (force_collective), from the same starting weights on the same batch
@@ -571,12 +590,13 @@ def train_run(a, world, rank, dev, cpu='full'):
                 d2.x, y2 = st2
             else:
                 y2 = y
-            el2, iss2, _ = time_train_steps(tr2, d2, y2, a.steps, True)
+            el2, iss2, _, _ = time_train_steps(tr2, d2, y2, a.steps, True)
             coll = {'ms_per_step': el2 / a.steps * 1e3, 'host_issue_ms_per_step': iss2 / a.steps * 1e3,
                     'note': 'FusedV24Trainer(force_collective=True) on a 1-rank RCCL group: '
                             'compute -> gnnd_train_update(rows -> flat gradient, loss) -> ONE '
                             'all_reduce(SUM) of [gradient | loss] -> gnnd_train_update(Adam)'}
             del tr2, m2
+            drop_one_rank_group()
     if rank == 0:
         step_s = elapsed / a.steps
         roof = None
@@ -592,7 +612,9 @@ def train_run(a, world, rank, dev, cpu='full'):
                     'frac': achieved / peak, 'traffic': None,
                     'kernel': train_path_string(tr, model_name, use_graph),
                     'flops_per_sample': 3 * fl, 'transcendentals_per_sample': 2 * trans,
-                    'step_ms': step_s * 1e3}
+                    'step_ms': step_s * 1e3,
+                    # event-timed GPU time per step (all the step's kernels, same stream)
+                    'kernel_ms': gpu_s / a.steps * 1e3}
         cpu_res = None
         if model_name == 'v24' and a.cpu_seconds > 0 and world == 1 and cpu in ('full', 'parity'):
             cpu_res = train_cpu_baseline(H, model, T, x, y, a.batch, a.cpu_seconds)
@@ -600,6 +622,7 @@ def train_run(a, world, rank, dev, cpu='full'):
             'metric': f'training samples/sec (whole node), {model_name} step with RCCL grad all-reduce',
             'value': world * a.batch * a.steps / elapsed, 'unit': 'samples/s', 'n_gpus': world,
             'steps': a.steps, 'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3,
+            'timed_region_ns': timed_ns,
             'host_issue_ms_per_step': issue_s / a.steps * 1e3,
             'ms_per_step_with_collective': coll['ms_per_step'] if coll else None,
             'collective': coll,
@@ -742,12 +765,14 @@ def decode_run(a, world, rank, dev, cpu='full'):
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    mono0 = time.monotonic_ns()           # the profiler's clock: tools/prof_vs_line.py windows
     t0 = time.perf_counter()
     ev0.record()
     for _ in range(a.steps):
         step()
     ev1.record()
     torch.cuda.synchronize()
+    mono1 = time.monotonic_ns()
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
@@ -808,7 +833,7 @@ def decode_run(a, world, rank, dev, cpu='full'):
             'value': world * a.batch * a.steps / elapsed,
             'unit': 'codewords/s',
             'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup, 'prewarm_s': a.prewarm_s,
-            'ms_per_step': elapsed / a.steps * 1e3,
+            'ms_per_step': elapsed / a.steps * 1e3, 'timed_region_ns': [mono0, mono1],
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': a.dtype, 'data': 'synthetic (on-device AWGN/toric sampler, seeded); ' +
                                       ('trained weights' if trained else 'random-init weights'),
@@ -875,11 +900,18 @@ SUB_CONFIGS = [
     ('config5_toric7_v24_train_global1024_f64', 'train', dict(model='v24', code='toric_7',
                                                                gbatch=1024, dtype='f64', steps=50,
                                                                warmup=3)),
+    # per-GPU batch 16 = the reference's global 128 over 8 GPUs: t1(128) / (8 t1(16)) is the
+    # strong-scaling efficiency at the reference's batch (scaling_efficiency_global128)
+    ('config5_toric7_v24_train_b16', 'train', dict(model='v24', code='toric_7', batch=16,
+                                                   dtype='f32', steps=200, warmup=5)),
+    ('config5_toric7_v24_train_b16_f64', 'train', dict(model='v24', code='toric_7', batch=16,
+                                                       dtype='f64', steps=200, warmup=5)),
 ]
 
 
 def sub_config_results(a, world, rank, dev):
     out = {}
+    traj_done = set()
     for name, mode, ov in SUB_CONFIGS:
         sa = argparse.Namespace(**vars(a))
         for k, v in ov.items():
@@ -888,15 +920,174 @@ def sub_config_results(a, world, rank, dev):
         sa.cpu_seconds = min(a.cpu_seconds, 2.0)
         t0 = time.perf_counter()
         if mode == 'train':
-            sa.batch = max(1, sa.gbatch // world)
+            # global-batch entries split the batch over the ranks; per-GPU entries keep it
+            sa.batch = max(1, sa.gbatch // world) if 'gbatch' in ov else sa.batch
             sa.no_graph = sa.layerwise = sa.torch_trainer = False
-            r = train_run(sa, world, rank, dev, cpu='parity')
+            # the 10-step trajectory against the oracle runs once per dtype (it does not
+            # depend on the timed batch); later entries of that dtype time the CPU leg only
+            cpu = 'parity' if sa.dtype not in traj_done else 'full'
+            traj_done.add(sa.dtype)
+            r = train_run(sa, world, rank, dev, cpu=cpu)
         else:
             r = decode_run(sa, world, rank, dev, cpu='parity')
         if rank == 0:
             r['wall_s'] = time.perf_counter() - t0
             out[name] = r
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# The driver keeps only the last 8 KB of a run's stdout (+ stderr): the JSON line it parses must
+# fit with room to spare.  The full record (every field above) goes to a file; stdout carries a
+# compact line holding, per config, the value, the roofline, the CPU baseline and a parity
+# summary.
+LINE_LIMIT = 6144
+
+
+def _r(v, sig=5):
+    """Round a float to `sig` significant digits (ints, None and strings pass through)."""
+    if isinstance(v, float) and math.isfinite(v) and v != 0.0:
+        return float(f'{v:.{sig}g}')
+    return v
+
+
+def _pick(d, keys, sig=5):
+    if not d:
+        return None
+    return {k: _r(d[k], sig) for k in keys if k in d and d[k] is not None}
+
+
+def compact_parity(r):
+    """Parity summary of one result: decode = oracle sample (bits compared, hard-decision
+    mismatches, max abs error); train = the 10-step trajectory vs the fp64 oracle."""
+    cb = r.get('cpu_baseline') or {}
+    if 'parity_bits_compared' in cb:
+        return {'bits': cb['parity_bits_compared'], 'mismatches': cb['parity_hard_decision_mismatches'],
+                'max_abs_err': _r(cb['parity_max_abs_err'], 3)}
+    p = r.get('parity')
+    if p:
+        return {'steps': p['steps'], 'codewords': p['codewords'],
+                'loss_max_rel_err': _r(p['loss_max_rel_err'], 3),
+                'param_max_abs_diff': _r(p['param_max_abs_diff'], 3)}
+    return None
+
+
+def compact_entry(r, top=False):
+    """The driver-line form of one result dict (decode or train)."""
+    keys = ['value', 'unit', 'ms_per_step', 'steps', 'dtype']
+    if top:
+        keys = ['metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+                'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'data']
+    e = {k: _r(r[k], 7) if k == 'value' else _r(r[k]) for k in keys if k in r}
+    c = r.get('config') or {}
+    if top:
+        e['config'] = _pick(c, ['workload', 'code', 'model', 'iters', 'global_batch', 'parallelism',
+                                'hard_decision_error_rate', 'frame_error_rate',
+                                'channel_hard_decision_error_rate'], 4)
+    else:
+        e['workload'] = c.get('workload')
+        if 'ms_per_step_with_collective' in r:
+            e['ms_per_step_with_collective'] = _r(r['ms_per_step_with_collective'])
+        if 'hard_decision_error_rate' in c:
+            e['ber'] = _r(c['hard_decision_error_rate'], 4)
+    rf = r.get('roofline') or {}
+    roof = _pick(rf, (['bound', 'achieved', 'peak', 'unit', 'frac', 'traffic', 'kernel_ms',
+                       'frac_algorithmic_count', 'hbm_io_frac', 'kernel'] if top else
+                      ['frac', 'achieved', 'peak', 'traffic', 'kernel_ms', 'frac_algorithmic_count']), 4)
+    if roof is not None:
+        roof.setdefault('traffic', None)
+        im = rf.get('issue_model')
+        if im:
+            roof['issue_frac'] = _r(im['issue_frac'], 3)
+    e['roofline'] = roof
+    cb = r.get('cpu_baseline')
+    e['cpu_baseline'] = _pick(cb, ['value', 'unit', 'cores', 'kind', 'value_1_thread', 'sample',
+                                   'cpu_model'] if top else ['value', 'value_1_thread', 'cores'], 4)
+    e['parity'] = compact_parity(r)
+    return e
+
+
+def strong_scaling(cfgs):
+    """Strong-scaling efficiency of config 5 at the reference's global batch of 128 over 8 GPUs
+    from this 1-GPU line: t1(128) / (8 t1(16)) per dtype (collective excluded; with it, the
+    collective-inclusive step times).  Only meaningful on a 1-GPU run."""
+    out = {}
+    for dt in ('', '_f64'):
+        a = cfgs.get('config5_toric7_v24_train_global128' + dt)
+        b = cfgs.get('config5_toric7_v24_train_b16' + dt)
+        if not a or not b or a.get('n_gpus') != 1:
+            continue
+        e = {'t1_128_ms': _r(a['ms_per_step'], 4), 't1_16_ms': _r(b['ms_per_step'], 4),
+             'eff_8gpu': _r(a['ms_per_step'] / (8 * b['ms_per_step']), 3)}
+        if a.get('ms_per_step_with_collective') and b.get('ms_per_step_with_collective'):
+            e['eff_8gpu_with_collective'] = _r(a['ms_per_step_with_collective'] /
+                                               (8 * b['ms_per_step_with_collective']), 3)
+        out['f64' if dt else 'f32'] = e
+    return out or None
+
+
+def driver_line(res, full_path=None, limit=LINE_LIMIT):
+    """Compact JSON line for stdout; asserts it fits `limit` bytes (optional detail is
+    dropped first)."""
+    line = compact_entry(res, top=True)
+    if res.get('dist') is not None:
+        dd = res['dist']
+        # [rank, device, PCI bus] per rank, the hosts once
+        line['dist'] = {'backend': dd['backend'], 'world_size': dd['world_size'],
+                        'ranks': [[q['rank'], q['device'], q.get('pci_bus')] for q in dd['ranks']],
+                        'hosts': sorted({q.get('host') for q in dd['ranks']})}
+    if res.get('scaling_efficiency_global128') is not None:
+        line['scaling_efficiency_global128'] = res['scaling_efficiency_global128']
+    if res.get('configs'):
+        line['configs'] = {n: compact_entry(r) for n, r in res['configs'].items()}
+    if full_path:
+        line['full_record'] = full_path
+    s = json.dumps(line, separators=(',', ':'))
+    # shed optional detail until the line fits (never the contract fields)
+    for drop in (('cpu_baseline', 'sample'), ('cpu_baseline', 'cpu_model'), ('roofline', 'kernel'),
+                 ('data',)):
+        if len(s) <= limit:
+            break
+        d = line
+        for k in drop[:-1]:
+            d = d.get(k) or {}
+        d.pop(drop[-1], None)
+        s = json.dumps(line, separators=(',', ':'))
+    assert len(s) <= limit, f'bench line {len(s)} bytes > {limit}'
+    return s
+
+
+def rank_map(dev):
+    """Backend, world size and every rank's device, gathered to all ranks:
+    an N-GPU line shows that the backend saw N ranks on N distinct GPUs."""
+    import socket
+    me = {'rank': dist.get_rank() if dist.is_initialized() else 0,
+          'device': dev.index if dev.type == 'cuda' else -1,
+          'host': socket.gethostname()[:24]}
+    if dev.type == 'cuda':
+        try:
+            me['pci_bus'] = torch.cuda.get_device_properties(dev).pci_bus_id
+        except Exception:
+            pass
+    if not dist.is_initialized():
+        return {'backend': None, 'world_size': 1, 'ranks': [me]}
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, me)
+    return {'backend': str(dist.get_backend()), 'world_size': dist.get_world_size(),
+            'ranks': ranks}
+
+
+def write_full_record(res):
+    """The full record (every nested field) under gpurun_out/ (merged back by gpurun; scratch on
+    the driver's box) or $GNND_BENCH_FULL."""
+    path = os.environ.get('GNND_BENCH_FULL', os.path.join('gpurun_out', 'bench_full.json'))
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, 'w') as f:
+            json.dump(res, f, indent=1)
+        return path
+    except OSError:
+        return None
 
 
 def main():
@@ -919,6 +1110,7 @@ def main():
         # (barriers then never touch GPU 0)
         dist.init_process_group(backend, device_id=dev)
     res = None
+    ranks = rank_map(dev)
     if a.mode == 'train':
         res = train_run(a, world, rank, dev, cpu='full')
     elif a.mode == 'sample':
@@ -931,8 +1123,10 @@ def main():
             sub = sub_config_results(a, world, rank, dev)
             if rank == 0:
                 res['configs'] = sub
+                res['scaling_efficiency_global128'] = strong_scaling(sub)
     if rank == 0 and res is not None:
-        print(json.dumps(res), flush=True)
+        res['dist'] = ranks
+        print(driver_line(res, write_full_record(res)), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

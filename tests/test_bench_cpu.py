@@ -75,3 +75,87 @@ def test_launch_mode_option(monkeypatch):
     assert a.launch == 'auto' and not a.no_graph
     monkeypatch.setattr(sys, 'argv', ['bench.py', '--mode', 'train', '--launch', 'graph'])
     assert bench.parse().launch == 'graph'
+
+
+def _full_size_record():
+    """The round-4 default run's full record (20 KB, every nested field), widened to the round-5
+    config list and an 8-rank job: the largest line the driver can see."""
+    import json
+    import os
+    r = json.load(open(os.path.join(os.path.dirname(bench.__file__), 'profiles', 'r04',
+                                    'bench_r04ad.json')))
+    c = r['configs']
+    c['config5_toric7_v24_train_b16'] = dict(c['config5_toric7_v24_train_global128'])
+    c['config5_toric7_v24_train_b16_f64'] = dict(c['config5_toric7_v24_train_global128_f64'])
+    r['scaling_efficiency_global128'] = bench.strong_scaling(c)
+    r['dist'] = {'backend': 'nccl', 'world_size': 8,
+                 'ranks': [{'rank': i, 'device': i, 'host': 'h' * 24, 'pci_bus': 10 + i}
+                           for i in range(8)]}
+    return r
+
+
+def test_driver_line_fits_and_keeps_every_config():
+    """the stdout line stays <= 6 KB (the driver keeps the last 8 KB of
+    stdout + stderr) and still carries value, roofline, cpu_baseline and parity per config."""
+    import json
+    r = _full_size_record()
+    assert len(json.dumps(r)) > 15000                 # the uncompacted record would not fit
+    s = bench.driver_line(r, 'gpurun_out/bench_full.json')
+    assert len(s) <= bench.LINE_LIMIT
+    line = json.loads(s)
+    for k in ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+              'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'config', 'roofline',
+              'cpu_baseline'):
+        assert k in line, k
+    for k in ('bound', 'achieved', 'peak', 'unit', 'frac', 'traffic'):
+        assert k in line['roofline'], k
+    for k in ('value', 'unit', 'cores', 'kind'):
+        assert k in line['cpu_baseline'], k
+    assert set(line['configs']) == set(r['configs'])
+    for name, e in line['configs'].items():
+        assert e['value'] > 0 and e['ms_per_step'] > 0, name
+        assert e['roofline']['frac'] > 0 and 'traffic' in e['roofline'], name
+        assert e['cpu_baseline']['value'] > 0, name
+        assert e['parity'], name
+    assert line['dist']['world_size'] == 8 and len(line['dist']['ranks']) == 8
+    assert line['scaling_efficiency_global128']['f32']['eff_8gpu'] > 0
+    # a line over the limit sheds optional detail, never a contract field, and asserts
+    tight = bench.driver_line(r, None, limit=len(s) - 50)
+    assert len(tight) <= len(s) - 50 and 'cpu_baseline' in json.loads(tight)
+
+
+def _rank_map_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    # a CPU stand-in for "this rank's GPU": device index = rank
+    m = bench.rank_map(torch.device('cpu'))
+    q.put((rank, m))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank_map_gathers_every_rank_gloo():
+    """every rank's entry reaches every rank (all_gather_object), with the
+    backend and world size as the process group reports them."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_map_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, m in res:
+        assert m['backend'] == 'gloo' and m['world_size'] == 2
+        assert [q_['rank'] for q_ in m['ranks']] == [0, 1]
+    assert res[0][1] == res[1][1]
+    single = bench.rank_map(torch.device('cpu'))
+    assert single['world_size'] == 1 and single['ranks'][0]['rank'] == 0

@@ -33,6 +33,14 @@ lscpu | grep -E "Model name|^CPU\(s\)" > "$OUT/lscpu.txt" 2>&1 || true
 step pytest_gpu 900 python -u -m pytest tests -m gpu -v -x --timeout 200 --timeout-method thread "$@"
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
+# the driver's own command, then the same command under rocprofv3 (kernel trace of the run whose
+# line it annotates; tools/prof_vs_line.py windows the trace by each config's timed region)
+export GNND_BENCH_FULL="$OUT/bench_default_full.json"
+step bench_default 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+export GNND_BENCH_FULL="$OUT/prof_default_full.json"
+step prof_default 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
+case " $STEPS " in *" prof_default "*) python tools/prof_vs_line.py "$OUT"/prof_default/*/run_kernel_trace.csv "$OUT/prof_default_full.json" "$OUT/prof_vs_line.json" > "$OUT/prof_vs_line.txt" 2>&1 || true;; esac
+unset GNND_BENCH_FULL
 step sweep 900 python tools/sweep.py --steps 5
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0
 step pmc 1200 bash tools/pmc.sh "$OUT/pmc"
