@@ -5,7 +5,9 @@
 #include <math.h>
 #include "../../include/gnnd.h"
 
-#define GNND_BLOCK 256
+#ifndef GNND_BLOCK
+#define GNND_BLOCK 256            // threads per decode workgroup (tuning variants: -DGNND_BLOCK=128)
+#endif
 
 // ---------------------------------------------------------------------------------------
 // debug build (make debug -> gnndecode/libgnnd_debug.so, -DGNND_DEBUG): the kernels check

@@ -39,7 +39,7 @@ export GNND_BENCH_FULL="$OUT/bench_default_full.json"
 step bench_default 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
 export GNND_BENCH_FULL="$OUT/prof_default_full.json"
 step prof_default 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_default" -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5
-case " $STEPS " in *" prof_default "*) python tools/prof_vs_line.py "$OUT"/prof_default/*/run_kernel_trace.csv "$OUT/prof_default_full.json" "$OUT/prof_vs_line.json" > "$OUT/prof_vs_line.txt" 2>&1 || true;; esac
+case " $STEPS " in *" prof_default "*) python tools/prof_vs_line.py "$OUT"/prof_default/run_kernel_trace.csv "$OUT/prof_default_full.json" "$OUT/prof_vs_line.json" > "$OUT/prof_vs_line.txt" 2>&1 || true;; esac
 unset GNND_BENCH_FULL
 step sweep 900 python tools/sweep.py --steps 5
 step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-seconds 0
