@@ -513,7 +513,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     model = model.to(dev).to(dtype)
     init_state = {k: v.detach().clone() for k, v in model.state_dict().items()}
     fused = (model_name in ('v24', 'v30', 'qgnni', 'cgnni') or
-             (model_name in ('nbp', 'v22') and dtype == torch.float64)) and not a.layerwise
+             (model_name in ('nbp', 'v22', 'v10') and dtype == torch.float64)) and not a.layerwise
     if model_name == 'v24':
         model.fused_train = fused
     if model_name == 'v22':          # decoder_v2_2's LossFunc: every layer's readout
@@ -537,7 +537,7 @@ def train_run(a, world, rank, dev, cpu='full'):
         # steps, graph replays ~9 us (r03ac); the torch Trainer (~80 launches) keeps its graph
         launch = 'eager' if fused_v24 else 'graph'
     use_graph = launch == 'graph'
-    if fused and model_name in ('nbp', 'v22'):
+    if fused and model_name in ('nbp', 'v22', 'v10'):
         # packed per-edge weights -> fwd+tape -> syndrome loss -> reverse pass -> Adam (fp64)
         tr = gd.train.FusedWbpTrainer(model, lf, graph=use_graph, warmup=2)
     elif fused and model_name == 'v30':
@@ -600,7 +600,7 @@ def train_run(a, world, rank, dev, cpu='full'):
     if rank == 0:
         step_s = elapsed / a.steps
         roof = None
-        if model_name in ('v24', 'v30', 'nbp', 'v22', 'qgnni', 'cgnni') and fused:
+        if model_name in ('v24', 'v30', 'nbp', 'v22', 'v10', 'qgnni', 'cgnni') and fused:
             # training ~ 3x the forward's algorithmic FLOPs: forward, the
             # reverse pass through every MLP (2x); transcendentals: forward Softplus + the
             # backward sigmoid of every unit.  Whole step over its wall time per step.

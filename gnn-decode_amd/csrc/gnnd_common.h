@@ -1758,13 +1758,15 @@ __device__ __forceinline__ SpIdx sp_index(double x) {
     return q;
 }
 // ln(1 + e^-a) from the entry {f0, s} at offset r (the Taylor polynomial above, Horner form
-// f0 + r (-s + t r (1/2 + r (B + r A))), B = (2s - 1)/6, A = (1 - 6t)/24: 8 VALU)
+// f0 + r (-s + u (1/2 + r (B + r A))), u = t r, B = (2s - 1)/6, A = (1 - 6t)/24: 8 VALU, the
+// r A term spread as r/24 - u/4 so no operand needs a register copy (A = 1/24 - t/4 as an
+// accumulating FMA had the constant 1/24 copied into its destination first, one v_mov_b64)
 __device__ __forceinline__ double sp_poly(double r, double f0, double s) {
     const double t = __builtin_fma(-s, s, s);
     const double u = t * r;
-    const double a = __builtin_fma(t, -0.25, 1.0 / 24);
     const double b = __builtin_fma(s, 1.0 / 3, -1.0 / 6);
-    double p = __builtin_fma(a, r, b);
+    double p = __builtin_fma(r, 1.0 / 24, b);
+    p = __builtin_fma(u, -0.25, p);
     p = __builtin_fma(p, r, 0.5);
     return __builtin_fma(__builtin_fma(u, p, -s), r, f0);
 }
@@ -1780,11 +1782,15 @@ __device__ __forceinline__ double softplus_sp(double x, const double* __restrict
     const SpEntry e = sp_entry(st, q.j);
     return relu_f64(x) + sp_poly(q.r, e.f0, e.s);
 }
-// sigmoid(-a) = 1/(1 + e^a) about the same entry, degree 3 (remainder < 3e-11; the fp64
-// reverse pass's Softplus derivative): s - u (1 + r (b2 + r a2))
+// sigmoid(-a) = 1/(1 + e^a) about the same entry, degree 4 (the fp64 reverse pass's Softplus
+// derivative, as accurate as the forward's softplus_sp: remainder r^5 s^(5) / 120 < 1e-13):
+// with t = s (1 - s), s' = -t, s'' = t (1 - 2s), s''' = -t (1 - 6t), s'''' = t (1 - 2s)(1 - 12t),
+// s - t r (1 + r (b2 + r (a2 + r c2))), b2 = s - 1/2, a2 = 1/6 - t, c2 = b2 (1/12 - t)
 __device__ __forceinline__ double sig_poly(double r, double s) {
     const double t = __builtin_fma(-s, s, s);
-    const double p = __builtin_fma(__builtin_fma(1.0 / 6 - t, r, s - 0.5), r, 1.0);
+    const double b2 = s - 0.5;
+    const double c2 = b2 * (1.0 / 12 - t);
+    const double p = __builtin_fma(__builtin_fma(__builtin_fma(c2, r, 1.0 / 6 - t), r, b2), r, 1.0);
     return __builtin_fma(-(t * r), p, s);
 }
 

@@ -466,6 +466,40 @@ struct Mlp10Pair {
         }
     }
     __device__ __forceinline__ f32x2 operator()(f32x2 u) const {
+#ifdef GNND_MLP_ONEASM
+        // the whole MLP as ONE asm block: hipcc's hazard recognizer assumes an op_sel dst
+        // forwarding hazard between consecutive inline-asm VALU blocks and puts an s_nop 0
+        // before every one that reads the previous block's result (one per unit); inside a block
+        // the packed FMAs are ordinary interlocked VALU dependencies (no trans ops, no DPP, no
+        // dst op_sel).  Layer 1 of unit k+1 is issued before unit k's layer-2 FMA (same
+        // accumulation order: b2, then units 0..9 — identical bits).
+        f32x2 acc, h0, h1;
+        asm("v_pk_fma_f32 %1, %3, %4, %4 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %2, %3, %5, %5 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %1, %14, %14 op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+            "v_pk_fma_f32 %1, %3, %6, %6 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %2, %15, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %2, %3, %7, %7 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %1, %16, %0 op_sel_hi:[1,0,1]\n\t"
+            "v_pk_fma_f32 %1, %3, %8, %8 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %2, %16, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %2, %3, %9, %9 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %1, %17, %0 op_sel_hi:[1,0,1]\n\t"
+            "v_pk_fma_f32 %1, %3, %10, %10 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %2, %17, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %2, %3, %11, %11 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %1, %18, %0 op_sel_hi:[1,0,1]\n\t"
+            "v_pk_fma_f32 %1, %3, %12, %12 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %2, %18, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+            "v_pk_fma_f32 %2, %3, %13, %13 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+            "v_pk_fma_f32 %0, %1, %19, %0 op_sel_hi:[1,0,1]\n\t"
+            "v_pk_fma_f32 %0, %2, %19, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+            : "=&v"(acc), "=&v"(h0), "=&v"(h1)
+            : "v"(u), "s"(w1b[0]), "s"(w1b[1]), "s"(w1b[2]), "s"(w1b[3]), "s"(w1b[4]),
+              "s"(w1b[5]), "s"(w1b[6]), "s"(w1b[7]), "s"(w1b[8]), "s"(w1b[9]), "s"(w20b),
+              "s"(w2[0]), "s"(w2[1]), "s"(w2[2]), "s"(w2[3]), "s"(w2[4]));
+        return acc;
+#else
         f32x2 h, acc;
         asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
             : "=v"(h) : "v"(u), "s"(w1b[0]));
@@ -477,6 +511,7 @@ struct Mlp10Pair {
             acc = (k & 1) ? pk_fma_hi(h, w2[k >> 1], acc) : pk_fma_lo(h, w2[k >> 1], acc);
         }
         return acc;
+#endif
     }
     // N edge pairs at once, unit-major: the N accumulation chains interleave, so no packed
     // FMA waits on the one just issued (same per-pair operation order: identical bits)
@@ -2614,10 +2649,11 @@ int gnnd_launch_v30_tape(const gnnd_graph*, int, const void*, const void*, void*
                          void*, hipStream_t);
 int gnnd_launch_v30_bwd(const gnnd_graph*, int, const void*, const void*, const void*,
                         const void*, const void*, void*, int64_t, int64_t, int, hipStream_t);
-// weighted-BP training (gnnd_train_wbp.hip, models NBP and V22, fp64): the same tape shape and
+// weighted-BP training (gnnd_train_wbp.hip, models NBP, V22 and V10, fp64): the same tape shape and
 // one gradient row [2 E T + 2 E + 1] per workgroup
 int64_t gnnd_wbp_tape_elems(const gnnd_graph*, int64_t, int);
 int64_t gnnd_wbp_train_rows(int64_t);
+int64_t gnnd_wbp_weights(const gnnd_graph*, int, int);
 int gnnd_launch_wbp_tape(const gnnd_graph*, int, const void*, const void*, void*, int64_t, int,
                          void*, hipStream_t);
 int gnnd_launch_wbp_bwd(const gnnd_graph*, int, const void*, const void*, const void*,

@@ -942,7 +942,7 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     return GNND_OK;
 }
 
-bool is_wbp_train(int model) { return model == GNND_NBP || model == GNND_V22; }
+bool is_wbp_train(int model) { return model == GNND_NBP || model == GNND_V22 || model == GNND_V10; }
 // the 10-hidden-unit GNN decoders (CGNNI, QGNNI): gnnd_train_gnn.hip
 bool is_gnn_train(int model) { return model == GNND_CGNNI || model == GNND_QGNNI; }
 bool train_args_ok(const gnnd_graph* g, int model, int dtype, int64_t B, int32_t iters) {
@@ -951,9 +951,9 @@ bool train_args_ok(const gnnd_graph* g, int model, int dtype, int64_t B, int32_t
     return (model == GNND_V24 || model == GNND_V30 || is_gnn_train(model)) &&
            (dtype == GNND_F32 || dtype == GNND_F64);
 }
-// per-edge weight tables of the weighted-BP models (gnnd.h NBP / V22 layout)
-int64_t wbp_weights(const gnnd_graph* g, int iters) {
-    return 2 * (int64_t)iters * g->view.E + 2 * (int64_t)g->view.E + 1;
+// per-edge weight tables of the weighted-BP models (gnnd.h NBP / V22 / V10 layouts)
+int64_t wbp_weights(const gnnd_graph* g, int model, int iters) {
+    return gnnd_wbp_weights(g, model, iters);
 }
 // trainable weights of a fused-training model (the packed layout of gnnd.h)
 int train_weights(int model) { return model == GNND_V30 ? kV30Count : is_gnn_train(model) ? 62 : kV24W; }
@@ -1377,7 +1377,7 @@ extern "C" int gnnd_train_fwd_loss(const gnnd_graph* g, int model, int dtype, co
 extern "C" int gnnd_train_workspace_bytes(const gnnd_graph* g, int model, int dtype,
                                           int64_t batch, int32_t iters, int64_t* h_bytes) {
     if (!train_args_ok(g, model, dtype, batch, iters) || !h_bytes) return GNND_ERR_INVALID_ARG;
-    const int64_t n = is_wbp_train(model) ? wbp_weights(g, iters) : train_weights(model);
+    const int64_t n = is_wbp_train(model) ? wbp_weights(g, model, iters) : train_weights(model);
     *h_bytes = model_train_rows(g, model, batch) * n * (dtype == GNND_F64 ? 8 : 4);
     return GNND_OK;
 }
@@ -1398,7 +1398,7 @@ extern "C" int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const v
     if (!train_args_ok(g, model, dtype, batch, iters)) return GNND_ERR_INVALID_ARG;
     if (!d_w || !d_grad_w) return GNND_ERR_INVALID_ARG;
     hipStream_t st = (hipStream_t)stream;
-    const int64_t nw = is_wbp_train(model) ? wbp_weights(g, iters) : train_weights(model);
+    const int64_t nw = is_wbp_train(model) ? wbp_weights(g, model, iters) : train_weights(model);
     if (batch == 0) {
         GNND_HIP_CHECK(hipMemsetAsync(d_grad_w, 0, (size_t)nw * (dtype == GNND_F64 ? 8 : 4), st));
         return GNND_OK;

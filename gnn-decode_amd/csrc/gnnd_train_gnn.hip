@@ -269,14 +269,22 @@ int launch_gnn(const gnnd_graph* gr, const void* w, const void* x, void* out, co
     const int nslot = g.C * g.G * g.R;
     const int64_t blocks = gnnd_gnn_train_rows(B);
     const size_t lds = gnn_lds<T>(g.V, g.C, g.E, nslot);
-    if (lds > 64 * 1024) return GNND_ERR_UNSUPPORTED;
+    // dynamic LDS up to the CU's 160 KB (fp64 LDPC-648 needs ~76 KB) together with the reverse
+    // pass's static s_red rows; above the 64 KB default the kernel's limit is raised first
+    constexpr size_t kStaticBwd = sizeof(T) * (kGnnThreads / 64) * kGnnW;
+    if (lds + (fwd ? 0 : kStaticBwd) > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     if (fwd) {
-        gnn_train_fwd_kernel<MODEL, T, R><<<(unsigned)blocks, kGnnThreads, lds, st>>>(
-            g, (const T*)w, (const T*)x, (T*)out, (T*)tape, B, iters);
+        auto k = gnn_train_fwd_kernel<MODEL, T, R>;
+        if (lds > 64 * 1024)
+            GNND_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        k<<<(unsigned)blocks, kGnnThreads, lds, st>>>(g, (const T*)w, (const T*)x, (T*)out, (T*)tape, B, iters);
     } else {
         if (blocks * kGnnW * (int64_t)sizeof(T) > rows_bytes) return GNND_ERR_INVALID_ARG;
-        gnn_train_bwd_kernel<MODEL, T, R><<<(unsigned)blocks, kGnnThreads, lds, st>>>(
-            g, (const T*)w, (const T*)x, (const T*)dout, (const T*)tape, (T*)rows, B, iters);
+        auto k = gnn_train_bwd_kernel<MODEL, T, R>;
+        if (lds > 64 * 1024)
+            GNND_HIP_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        k<<<(unsigned)blocks, kGnnThreads, lds, st>>>(g, (const T*)w, (const T*)x, (const T*)dout,
+                                                      (const T*)tape, (T*)rows, B, iters);
     }
     GNND_LAUNCH_CHECK();
     return GNND_OK;

@@ -3,6 +3,11 @@
 //   NBP  quantum/neural_BP.py:95-160, 263-314 (readout after the last layer)
 //   V22  quantum/decoder_v2_2.py:120-160, 272-347 (a readout after EVERY layer; the script's
 //        8 edge-type weights arrive expanded per edge, gnnd.h V22 layout)
+//   V10  quantum/decoder_v1_0.py:97-133, 236-313 (the check-side layer's W scales the whole
+//        v->c argument; plain readout): a_e = ((S_v(m) - m_e) + x_v) W_t[e], W_t = w[tE + e],
+//        alpha = w[TE]; readout r_v = S_v(m) + x_v.  The tape keeps the unweighted argument
+//        z_e = (S_v(m) - m_e) + x_v; the reverse pass takes d W_t[e] = g_a z_e and carries
+//        g_z = g_a W_t[e] into the variable leave-one-out (unit message weight).
 // fp64 only (both scripts train in double).  Per layer t (packed weights w: W_t = w[2tE + e],
 // Wp_t = w[(2t+1)E + e], W_out = w[2TE + e], W_pr = w[2TE + E + e], alpha = w[2TE + 2E]):
 //   a_e  = (S_v(m W_t) - m_e W_t[e]) + x_v Wp_t[e]                          (v -> c)
@@ -33,6 +38,13 @@ struct WbpLayout {          // packed per-edge weight tables (gnnd.h NBP / V22)
     __device__ __forceinline__ int out_p(int e) const { return 2 * T * E + E + e; }
     __device__ __forceinline__ int alpha() const { return 2 * T * E + 2 * E; }
 };
+struct V10Layout {          // gnnd.h V10: the check-side layers' W, then alpha
+    int E, T;
+    __device__ __forceinline__ int chk(int t, int e) const { return t * E + e; }
+    __device__ __forceinline__ int alpha() const { return T * E; }
+};
+// kernel kinds: the readout and weight placement of each script
+enum WbpKind { kWbpNbp = 0, kWbpV22 = 1, kWbpV10 = 2 };
 
 constexpr int kWbpThreads = GNND_BLOCK;
 
@@ -43,12 +55,14 @@ __host__ __device__ constexpr size_t wbp_lds(int V, int C, int E, int nslot) {
 }
 
 // forward with tape: tape[b][t][0][slot] = m entering layer t, tape[b][t][1][slot] = a_e of
-// layer t; tape[b][T][0][slot] = the final states.  out: PER_LAYER [T][B][V], else [B][V].
-template <int R, bool PER_LAYER>
+// layer t (V10: the unweighted z_e); tape[b][T][0][slot] = the final states.  out: PER_LAYER
+// [T][B][V], else [B][V].
+template <int R, int KIND>
 __global__ void __launch_bounds__(kWbpThreads)
 wbp_train_fwd_kernel(GraphView g, const double* __restrict__ w, const double* __restrict__ x,
                      double* __restrict__ out, double* __restrict__ tape, int64_t B, int iters) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr bool PER_LAYER = KIND == kWbpV22, V10 = KIND == kWbpV10;
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
     const int nslot = C * G * R, IC = C * G;
@@ -56,14 +70,15 @@ wbp_train_fwd_kernel(GraphView g, const double* __restrict__ w, const double* __
     int* s_vptr = (int*)(s_slot + nslot);
     int* s_vslot = s_vptr + V + 1;
     double* s_m = (double*)(smem + wbp_a16(((size_t)nslot + V + 1 + E) * 4));   // [nslot] states
-    double* s_sv = s_m + nslot;          // [V] S_v(m W_t)
+    double* s_sv = s_m + nslot;          // [V] S_v(m W_t) (V10: S_v(m))
     double* s_xv = s_sv + V;
     double* s_xc = s_xv + V;
     for (int i = tid; i < nslot; i += kWbpThreads) s_slot[i] = g.slot_ve[i];
     for (int i = tid; i <= V; i += kWbpThreads) s_vptr[i] = g.var_ptr[i];
     for (int i = tid; i < E; i += kWbpThreads) s_vslot[i] = g.vslot[i];
     const WbpLayout L{E, iters};
-    const double alpha = w[L.alpha()];
+    const V10Layout L10{E, iters};
+    const double alpha = w[V10 ? L10.alpha() : L.alpha()];
     const size_t tstride = 2 * (size_t)nslot;
 
     for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
@@ -92,8 +107,15 @@ wbp_train_fwd_kernel(GraphView g, const double* __restrict__ w, const double* __
                     const bool valid = e != E;
                     const int ec = valid ? e : 0;
                     mr[r] = s_m[s0 + r];
-                    const double a = (s_sv[v] - mr[r] * w[L.msg(it, ec)]) + s_xv[v] * w[L.prior(it, ec)];
-                    if (act) { tt[s0 + r] = mr[r]; tt[nslot + s0 + r] = a; }
+                    double a;
+                    if constexpr (V10) {     // decode_resident_kernel's V10 order
+                        const double z = (s_sv[v] - mr[r]) + s_xv[v];
+                        a = z * w[L10.chk(it, ec)];
+                        if (act) { tt[s0 + r] = mr[r]; tt[nslot + s0 + r] = z; }
+                    } else {
+                        a = (s_sv[v] - mr[r] * w[L.msg(it, ec)]) + s_xv[v] * w[L.prior(it, ec)];
+                        if (act) { tt[s0 + r] = mr[r]; tt[nslot + s0 + r] = a; }
+                    }
                     double cc;
                     const double l = wbp_L(a, cc);
                     tv[r] = valid ? l : 0.0;
@@ -117,6 +139,13 @@ wbp_train_fwd_kernel(GraphView g, const double* __restrict__ w, const double* __
             for (int v = tid; v < V; v += kWbpThreads) {
                 const int k0 = s_vptr[v], k1 = s_vptr[v + 1];
                 const double xv = s_xv[v];
+                if constexpr (V10) {         // S_v(m), then the readout sigmoid(-(S_v + x_v))
+                    double sn = 0.0;
+                    for (int k = k0; k < k1; ++k) sn += s_m[s_vslot[k]];
+                    if (last) out[b * V + v] = sigmoid_ref(-(sn + xv));
+                    s_sv[v] = sn;
+                    continue;
+                }
                 double so = 0.0, s2 = 0.0, sn = 0.0;
                 for (int k = k0; k < k1; ++k) {
                     const double mk = s_m[s_vslot[k]];
@@ -133,20 +162,23 @@ wbp_train_fwd_kernel(GraphView g, const double* __restrict__ w, const double* __
         if (iters == 0 && !PER_LAYER)
             for (int v = tid; v < V; v += kWbpThreads) {
                 double s2 = 0.0;
-                for (int k = s_vptr[v]; k < s_vptr[v + 1]; ++k) s2 += s_xv[v] * w[L.out_p(k)];
+                if constexpr (V10) s2 = s_xv[v];
+                else
+                    for (int k = s_vptr[v]; k < s_vptr[v + 1]; ++k) s2 += s_xv[v] * w[L.out_p(k)];
                 out[b * V + v] = sigmoid_ref(-s2);
             }
     }
 }
 
-// reverse pass: d loss / d out -> one gradient row [2TE + 2E + 1] per workgroup
-template <int R, bool PER_LAYER>
+// reverse pass: d loss / d out -> one gradient row [2TE + 2E + 1] (V10: [TE + 1]) per workgroup
+template <int R, int KIND>
 __global__ void __launch_bounds__(kWbpThreads)
 wbp_train_bwd_kernel(GraphView g, const double* __restrict__ w, const double* __restrict__ x,
                      const double* __restrict__ out, const double* __restrict__ dout,
                      const double* __restrict__ tape, double* __restrict__ rows, int64_t B,
                      int iters) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr bool PER_LAYER = KIND == kWbpV22, V10 = KIND == kWbpV10;
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
     const int nslot = C * G * R, IC = C * G;
@@ -163,8 +195,10 @@ wbp_train_bwd_kernel(GraphView g, const double* __restrict__ w, const double* __
     for (int i = tid; i <= V; i += kWbpThreads) s_vptr[i] = g.var_ptr[i];
     for (int i = tid; i < E; i += kWbpThreads) s_vslot[i] = g.vslot[i];
     const WbpLayout L{E, iters};
-    const int P = L.alpha() + 1;
-    const double alpha = w[L.alpha()];
+    const V10Layout L10{E, iters};
+    const int ialpha = V10 ? L10.alpha() : L.alpha();
+    const int P = ialpha + 1;
+    const double alpha = w[ialpha];
     const double hi = 1 - 1e-15;
     const size_t tstride = 2 * (size_t)nslot;
     double* row = rows + (size_t)blockIdx.x * P;
@@ -210,14 +244,19 @@ wbp_train_bwd_kernel(GraphView g, const double* __restrict__ w, const double* __
                     double Gv = s_G[s0 + r];
                     if (ro && ok[r]) {
                         const double gr = s_gr[vv[r]];
-                        Gv += w[L.out_w(ec)] * gr;
-                        if (act) {
-                            row[L.out_w(ec)] += tn[s0 + r] * gr;
-                            row[L.out_p(ec)] += s_xv[vv[r]] * gr;
+                        if constexpr (V10) {
+                            Gv += gr;                  // r_v = S_v(m) + x_v: unit weights
+                        } else {
+                            Gv += w[L.out_w(ec)] * gr;
+                            if (act) {
+                                row[L.out_w(ec)] += tn[s0 + r] * gr;
+                                row[L.out_p(ec)] += s_xv[vv[r]] * gr;
+                            }
                         }
                     }
                     Gm[r] = ok[r] ? Gv : 0.0;
-                    a[r] = tt[nslot + s0 + r];
+                    // (V10: the forward's a = z W_t[e], the same product)
+                    a[r] = V10 ? tt[nslot + s0 + r] * w[L10.chk(t, ec)] : tt[nslot + s0 + r];
                     th[r] = g_tanh(a[r] / 2.0);
                     cf[r] = th[r] < 0.0 ? 1.0 : 0.0;
                     cl[r] = g_clamp(fabs(th[r]), 1e-20, 1e10);
@@ -254,9 +293,16 @@ wbp_train_bwd_kernel(GraphView g, const double* __restrict__ w, const double* __
                     const double gt = th[r] > 0.0 ? gabs : th[r] < 0.0 ? -gabs : 0.0;
                     const double ga = ok[r] ? (gt * (1.0 - th[r] * th[r])) / 2.0 : 0.0;
                     if (act) {
-                        s_ga[sl] = ga;
                         s_G[sl] = Gm[r] * alpha;                     // residual m^t alpha
-                        if (ok[r]) row[L.prior(t, ee[r])] += s_xv[vv[r]] * ga;
+                        if constexpr (V10) {
+                            // a = z W_t[e]: d W_t[e] = g_a z, d z = g_a W_t[e]
+                            const int ec = ok[r] ? ee[r] : 0;
+                            s_ga[sl] = ga * w[L10.chk(t, ec)];
+                            if (ok[r]) row[L10.chk(t, ee[r])] += tt[nslot + sl] * ga;
+                        } else {
+                            s_ga[sl] = ga;
+                            if (ok[r]) row[L.prior(t, ee[r])] += s_xv[vv[r]] * ga;
+                        }
                     }
                 }
             }
@@ -268,13 +314,18 @@ wbp_train_bwd_kernel(GraphView g, const double* __restrict__ w, const double* __
             }
             __syncthreads();
             // a_e = (S_v(m W_t) - m_e W_t[e]) + ...:  d / d (m W_t)[e] = S_v(g_a) - g_a[e]
+            // (V10: z_e = (S_v(m) - m_e) + x_v:  d / d m_e = S_v(g_z) - g_z[e])
             for (int i = tid; i < nslot; i += kWbpThreads) {
                 const uint32_t sv = s_slot[i];
                 const int e = (int)(sv >> 16);
                 if (e == E) continue;
                 const double gmw = s_gs[sv & 0xffffu] - s_ga[i];
-                row[L.msg(t, e)] += tt[i] * gmw;
-                s_G[i] += w[L.msg(t, e)] * gmw;
+                if constexpr (V10) {
+                    s_G[i] += gmw;
+                } else {
+                    row[L.msg(t, e)] += tt[i] * gmw;
+                    s_G[i] += w[L.msg(t, e)] * gmw;
+                }
             }
         }
     }
@@ -287,7 +338,7 @@ wbp_train_bwd_kernel(GraphView g, const double* __restrict__ w, const double* __
     if (tid == 0) {
         double s = 0.0;
         for (int k = 0; k < kWbpThreads / 64; ++k) s += s_al[k];
-        row[L.alpha()] = s;
+        row[ialpha] = s;
     }
 }
 
@@ -300,15 +351,17 @@ int launch_wbp(const gnnd_graph* gr, int model, const void* w, const void* x, vo
     const int64_t blocks = gnnd_wbp_train_rows(B);
     const size_t lds = wbp_lds(g.V, g.C, g.E, nslot);
     if (lds > 64 * 1024) return GNND_ERR_UNSUPPORTED;
-    const bool per = model == GNND_V22;
+    const int kind = model == GNND_V22 ? kWbpV22 : model == GNND_V10 ? kWbpV10 : kWbpNbp;
     if (fwd) {
-        auto k = per ? wbp_train_fwd_kernel<R, true> : wbp_train_fwd_kernel<R, false>;
+        auto k = kind == kWbpV22 ? wbp_train_fwd_kernel<R, kWbpV22>
+               : kind == kWbpV10 ? wbp_train_fwd_kernel<R, kWbpV10> : wbp_train_fwd_kernel<R, kWbpNbp>;
         k<<<(unsigned)blocks, kWbpThreads, lds, st>>>(g, (const double*)w, (const double*)x,
                                                        (double*)out, (double*)tape, B, iters);
     } else {
-        const int64_t P = 2 * (int64_t)iters * g.E + 2 * (int64_t)g.E + 1;
+        const int64_t P = gnnd_wbp_weights(gr, model, iters);
         if (blocks * P * 8 > rows_bytes) return GNND_ERR_INVALID_ARG;
-        auto k = per ? wbp_train_bwd_kernel<R, true> : wbp_train_bwd_kernel<R, false>;
+        auto k = kind == kWbpV22 ? wbp_train_bwd_kernel<R, kWbpV22>
+               : kind == kWbpV10 ? wbp_train_bwd_kernel<R, kWbpV10> : wbp_train_bwd_kernel<R, kWbpNbp>;
         k<<<(unsigned)blocks, kWbpThreads, lds, st>>>(g, (const double*)w, (const double*)x,
                                                        (const double*)out, (const double*)dout,
                                                        (const double*)tape, (double*)rows, B, iters);
@@ -335,6 +388,11 @@ int64_t gnnd_wbp_tape_elems(const gnnd_graph* g, int64_t B, int iters) {
     return B * (int64_t)(iters + 1) * 2 * ((int64_t)g->view.C * g->view.G * g->view.R);
 }
 int64_t gnnd_wbp_train_rows(int64_t B) { return B < 1024 ? B : 1024; }
+// trainable values of a weighted-BP model's packed tables (gnnd.h NBP / V22 / V10 layouts)
+int64_t gnnd_wbp_weights(const gnnd_graph* g, int model, int iters) {
+    const int64_t E = g->view.E;
+    return model == GNND_V10 ? (int64_t)iters * E + 1 : 2 * (int64_t)iters * E + 2 * E + 1;
+}
 int gnnd_launch_wbp_tape(const gnnd_graph* g, int model, const void* w, const void* x, void* out,
                          int64_t B, int iters, void* tape, hipStream_t st) {
     if (!tape) return GNND_ERR_INVALID_ARG;

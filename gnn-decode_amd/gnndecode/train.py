@@ -567,20 +567,30 @@ class FusedGnnTrainer(_GraphedStep):
         self.exp_avg_sq = torch.zeros_like(flat)
         self.step_count = torch.zeros(1, dtype=torch.float64, device=flat.device)
         self._sync = torch.zeros(1, dtype=torch.int32, device=flat.device)
-        self._gbuf = torch.zeros(flat.numel() + 1, dtype=flat.dtype, device=flat.device)
+        # [gradient | loss | codewords of this rank] (the count weights CGNNI's mean, _reduce)
+        self._gbuf = torch.zeros(flat.numel() + 2, dtype=flat.dtype, device=flat.device)
         self._gw = self._gbuf[:flat.numel()]
         self._loss = self._gbuf[flat.numel()]
+        self._gl = self._gbuf[:flat.numel() + 1]
+        self._count = self._gbuf[flat.numel() + 1]
+        self._nb = 0
         model.graph(flat.device)                 # device graph tables now, never in a capture
         g = getattr(loss_fn, '_graph', None)
         if g is not None:
             g(flat.device)
 
     def _reduce(self, loss, grads):
-        dist.all_reduce(self._gbuf, op=dist.ReduceOp.SUM, group=self.group)
         if self.model.kind == 'cgnni':
-            # CGNNI's LossFunc is a MEAN over the batch (classical/CGNNI.py:302-303): with equal
-            # shards the global-batch gradient and loss are the average over the ranks
-            self._gbuf.div_(dist.get_world_size(self.group))
+            # CGNNI's LossFunc is a MEAN over the batch (classical/CGNNI.py:302-303): each rank's
+            # mean gradient and loss weighted by its codeword count, summed, divided by the
+            # global count -- the full-batch mean for any shard sizes (shard_bounds of an odd
+            # global batch gives unequal shards)
+            self._gl.mul_(float(self._nb))
+            self._count.fill_(float(self._nb))
+            dist.all_reduce(self._gbuf, op=dist.ReduceOp.SUM, group=self.group)
+            self._gl.div_(self._count)
+        else:
+            dist.all_reduce(self._gbuf, op=dist.ReduceOp.SUM, group=self.group)
 
     def _loss_grad(self, out, y):
         """(per-codeword (or batch) losses, d loss / d pred)."""
@@ -598,6 +608,7 @@ class FusedGnnTrainer(_GraphedStep):
         g = m.graph(x.device)
         w = self.flat if self.flat.dtype == x.dtype else self.flat.to(x.dtype)
         out, tape = ops.train_forward(g, m.kind, x, w, m.Nc)
+        self._nb = out.shape[0] // g.V           # codewords of this rank's shard
         loss_b, d = self._loss_grad(out, y)
         if self.flat.dtype != x.dtype or self._dist():
             gw = ops.train_backward(g, m.kind, w, x, out, d, tape, m.Nc)
@@ -632,7 +643,8 @@ class FusedGnnTrainer(_GraphedStep):
 
 class FusedWbpTrainer(_GraphedStep):
     """Weighted-BP training step on the HIP kernels, fp64 (the scripts' dtype):
-    NeuralBP (quantum/neural_BP.py:370-395) and decoder_v2_2 (quantum/decoder_v2_2.py:421-443).
+    NeuralBP (quantum/neural_BP.py:370-395), decoder_v2_2 (quantum/decoder_v2_2.py:421-443)
+    and decoder_v1_0 (quantum/decoder_v1_0.py:377-403: the check-side layers' W and alpha).
 
         packed per-edge weights (ONE gather from the flat parameter buffer; V22: the 8 edge-type
         weights expanded per edge, sigmoid(weight)) -> forward with tape (gnnd_train_fwd) ->
@@ -650,9 +662,9 @@ class FusedWbpTrainer(_GraphedStep):
 
     def __init__(self, model, loss_fn, lr=None, weight_decay=None, betas=(0.9, 0.999), eps=1e-8,
                  group=None, graph=True, warmup=2, force_collective=False):
-        from .models import DecoderV22, NeuralBP
-        if not isinstance(model, (DecoderV22, NeuralBP)):
-            raise TypeError('FusedWbpTrainer trains NeuralBP and DecoderV22 models')
+        from .models import DecoderV10, DecoderV22, NeuralBP
+        if not isinstance(model, (DecoderV10, DecoderV22, NeuralBP)):
+            raise TypeError('FusedWbpTrainer trains NeuralBP, DecoderV22 and DecoderV10 models')
         rlr, rwd = REFERENCE_OPTIM[model.kind]
         self.model, self.loss_fn = model, loss_fn
         self.lr = rlr if lr is None else lr
@@ -662,8 +674,13 @@ class FusedWbpTrainer(_GraphedStep):
         T = model.Nc
         v22 = model.kind == 'v22'
         tail = model.weight if v22 else model.alpha
-        params = ([q for t in range(T) for q in (model.layers[2 * t].W, model.layers[2 * t].W_p)]
-                  + [model.W, model.W_pr if v22 else model.W_p, tail])
+        if model.kind == 'v10':
+            # decoder_v1_0: only the target_to_source layers' W enter the forward
+            # (quantum/decoder_v1_0.py:246-247); the source_to_target layers' W never change
+            params = [model.layers[2 * t + 1].W for t in range(T)] + [model.alpha]
+        else:
+            params = ([q for t in range(T) for q in (model.layers[2 * t].W, model.layers[2 * t].W_p)]
+                      + [model.W, model.W_pr if v22 else model.W_p, tail])
         dev = tail.device
         flat = torch.cat([q.detach().reshape(-1) for q in params]).contiguous()
         off = 0

@@ -217,9 +217,10 @@ int gnnd_decode_plan(const gnnd_graph* g, int model, int dtype, int32_t* h_plan)
  * reduction of per-workgroup partials in d_workspace, gnnd_train_bwd_workspace bytes).
  * Models: V24 (quantum/decoder_v2_4.py:260-294, fp32/fp64), V30 (quantum/decoder_v3_0.py:
  * 245-290, fp32/fp64; d_out / d_grad_out are the two readout tensors [2][B*N]), and fp64 NBP
- * (quantum/neural_BP.py:263-314) and V22 (quantum/decoder_v2_2.py:299-347; d_out /
- * d_grad_out every layer's readout [T][B*V]) whose gradient is w.r.t. the per-edge tables
- * of their packed layout (2 E T + 2 E + 1 values), CGNNI (classical/CGNNI.py:248-284) and
+ * (quantum/neural_BP.py:263-314), V22 (quantum/decoder_v2_2.py:299-347; d_out /
+ * d_grad_out every layer's readout [T][B*V]) and V10 (quantum/decoder_v1_0.py:263-313)
+ * whose gradient is w.r.t. the per-edge tables of their packed layout (NBP/V22 2 E T + 2 E + 1
+ * values, V10 E T + 1), CGNNI (classical/CGNNI.py:248-284) and
  * QGNNI (quantum/QGNNI.py:217-252), fp32/fp64, gradient w.r.t. their 62 packed weights (the
  * forward writes its own tape: every iteration's tanh outputs and the readout inputs; d_out
  * is its prediction, not gnnd_decode's register-resident one bit for bit).  The other models
@@ -239,7 +240,7 @@ int gnnd_train_bwd(const gnnd_graph* g, int model, int dtype, const void* d_w, c
                    int32_t iters, void* stream);
 /* The reverse pass without its reduction: leaves gnnd_train_bwd_rows() per-workgroup
  * gradient rows [rows][n] (n = the model's weights: V24 1283, V30 137, CGNNI/QGNNI 62,
- * NBP/V22 2ET + 2E + 1) in d_workspace, for gnnd_train_update (V24, V30, CGNNI, QGNNI) to
+ * NBP/V22 2ET + 2E + 1, V10 ET + 1) in d_workspace, for gnnd_train_update (V24, V30, CGNNI, QGNNI) to
  * reduce (fused with
  * the optimizer).  On a split graph (gnnd_graph_components > 1) every component of a
  * codeword runs in its own workgroup.                                                     */

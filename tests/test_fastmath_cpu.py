@@ -94,6 +94,6 @@ def test_fp64_fast_math_ulp(tmp_path):
     assert int(out[9]) == 0, out[9]
     # softplus_sp (one 16-byte table read, degree-4 Taylor about a_j = j/64): <= 5e-14 absolute
     # over the decoders' range (measured 3.1e-14), torch's threshold exact; its sigmoid
-    # (sig_poly, the reverse pass's derivative) <= 1e-10 absolute
+    # (sig_poly, the reverse pass's derivative, degree 4 since r05) <= 1e-13 absolute
     assert float(out[10]) <= 5e-14, out[10]
-    assert float(out[11]) <= 1e-10, out[11]
+    assert float(out[11]) <= 1e-13, out[11]

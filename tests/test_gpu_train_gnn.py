@@ -120,7 +120,7 @@ def test_fused_qgnni_large_batch_equals_sum_of_chunks():
     assert (gfull - gsum).abs().max().item() <= 1e-10 * gsum.abs().max().item()
 
 
-def _dp_worker(rank, world, port, q, model):
+def _dp_worker(rank, world, port, q, model, odd=False):
     import os
     import torch.distributed as dist
     import gnndecode as gd
@@ -138,6 +138,9 @@ def _dp_worker(rank, world, port, q, model):
     N, V = H.shape[0] + H.shape[1], H.shape[0]
     x = torch.from_numpy(z['x']).to(DEV).double().view(-1, N)
     y = torch.from_numpy(z['y']).to(DEV).double().view(-1, V)
+    if odd:                                  # an odd global batch: unequal shards
+        n = x.size(0) - 1 if x.size(0) % 2 == 0 else x.size(0)
+        x, y = x[:n], y[:n]
     s, e = gd.train.shard_bounds(x.size(0), rank, world)
     xs, ys = x[s:e].reshape(-1, 1).contiguous(), y[s:e].reshape(-1, 1).contiguous()
     tr = gd.train.FusedGnnTrainer(m, lf, graph=False)
@@ -147,11 +150,13 @@ def _dp_worker(rank, world, port, q, model):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('model', ['qgnni', 'cgnni'])
-def test_two_rank_fused_gnn_training_equals_full_batch(golden, model):
+@pytest.mark.parametrize('model,odd', [('qgnni', False), ('cgnni', False), ('cgnni', True)])
+def test_two_rank_fused_gnn_training_equals_full_batch(golden, model, odd):
     """Data-parallel FusedGnnTrainer: 2 gloo ranks on the one GPU, each half of the batch, one
-    all_reduce of [gradient | loss] per step (SUM for QGNNI's summed loss, the average for
-    CGNNI's mean loss) -> the single-process full-batch parameters and losses (fp64)."""
+    all_reduce of [gradient | loss] per step (SUM for QGNNI's summed loss; for CGNNI's mean loss
+    each rank's mean weighted by its shard size, so an odd global batch -- unequal shards --
+    still gives the full-batch mean) -> the single-process full-batch parameters and losses
+    (fp64)."""
     import socket
     import torch.multiprocessing as mp
     import gnndecode as gd
@@ -161,7 +166,7 @@ def test_two_rank_fused_gnn_training_equals_full_batch(golden, model):
     sock.close()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, model)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, model, odd)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(2)])
@@ -170,6 +175,11 @@ def test_two_rank_fused_gnn_training_equals_full_batch(golden, model):
         assert p.exitcode == 0
     fx = 'train_cgnni_bch' if model == 'cgnni' else 'train_qgnni_L4'
     z, m, lf, H, x, y = _setup(golden, fx, model, ('bch', None) if model == 'cgnni' else ('toric', 4), f64=True)
+    if odd:
+        N, V = H.shape[0] + H.shape[1], H.shape[0]
+        n = x.numel() // N
+        n = n - 1 if n % 2 == 0 else n
+        x, y = x[:n * N].contiguous(), y[:n * V].contiguous()
     tr = gd.train.FusedGnnTrainer(m, lf, graph=False)
     ref_losses = [float(tr.step(gd.data.make_batch(x, m.graph(x.device)), y)) for _ in range(2)]
     ref = tr.flat.double().cpu()
