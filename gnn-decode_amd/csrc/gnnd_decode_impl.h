@@ -414,10 +414,17 @@ __device__ __forceinline__ f32x2 softplus_tail2(f32x2 hs) {   // |hs|/2 + log2(1
     e.y = __builtin_amdgcn_exp2f(-fabsf(hs.y));
     e = e + f32x2{1.0f, 1.0f};
     // |hs| as a source modifier of one v_fma_f32 per value (hipcc otherwise materialises
-    // |hs| with v_and and packs the FMA: one extra VALU op per pair)
+    // |hs| with v_and and packs the FMA: one extra VALU op per pair).  The two v_log_f32 and the
+    // two FMAs in ONE asm block, interleaved, so each FMA reads its log result with one
+    // instruction in between: the compiler's TRANS -> VALU-use wait state does not cover an
+    // inline-asm consumer, and an FMA placed right after its v_log reads a stale value
+    // (tools/trans_hazard_check.py)
     float tx, ty;
-    asm("v_fma_f32 %0, |%1|, 0.5, %2" : "=v"(tx) : "v"(hs.x), "v"(__builtin_amdgcn_logf(e.x)));
-    asm("v_fma_f32 %0, |%1|, 0.5, %2" : "=v"(ty) : "v"(hs.y), "v"(__builtin_amdgcn_logf(e.y)));
+    asm("v_log_f32 %0, %2\n\t"
+        "v_log_f32 %1, %3\n\t"
+        "v_fma_f32 %0, |%4|, 0.5, %0\n\t"
+        "v_fma_f32 %1, |%5|, 0.5, %1"
+        : "=&v"(tx), "=&v"(ty) : "v"(e.x), "v"(e.y), "v"(hs.x), "v"(hs.y));
     return f32x2{tx, ty};
 }
 // {u0 wb.x + wb.y, u1 wb.x + wb.y}: one SGPR pair as multiplier (lo) and addend (hi)
@@ -642,6 +649,92 @@ __device__ __forceinline__ f32x2 mlp128_split(const float* __restrict__ wg, V24L
         if (pf) pf->mark(mk + 1);
 #endif
         return r;
+    }
+}
+// Unit-PAIR form of the fp32 MLPs (decode_kernel on an R = 1 slot plan, the small batches of
+// the training steps): ONE edge per lane and the two halves of every packed op carrying two
+// hidden units, k = 8i + 2p and k + 1 — chains 2p and 2p + 1 of the fixed order above, each
+// half accumulating its chain exactly as mlp128_chains does for one edge (same FMA per edge and
+// unit, chain 0 from the linear part), and pair p's value c.x + c.y = c[2p] + c[2p + 1] enters
+// the same tree: every form gives the same bits.  With a toric component's 192 edges on 192
+// lanes the unit split's item waves are FULL (the edge-pair form puts 96 pairs on 128 lanes).
+// Weights: the workgroup's LDS copy in pair-major order (UpairLds, staged from the prepared
+// layout): entry e = 16 p + i holds {W'_k, W'_k+1, b'_k, b'_k+1} (2-input: the W1b' weights),
+// then [64] {w2'_k, w2'_k+1} and (2-input) [64] {W1a'_k, W1a'_k+1}: broadcast LDS reads, every
+// operand of the packed FMAs a VGPR pair (the SGPR pairs of the edge-pair form hold one unit).
+struct UpairLds {
+    static constexpr int kL1 = 0, kW2 = 256, kWA = 384;          // float offsets in an MLP block
+    static constexpr int kMlp0 = 0, kMlp1 = 512, kMlp2 = 896, kFloats = 1280;   // ggc1, ggc2, mlp
+};
+template <int NP, int P0, bool TWO>
+__device__ __forceinline__ float mlp128_upair(const float* wl, V24Lin lin, float u0, float u1) {
+    const f32x4* l1 = (const f32x4*)(wl + UpairLds::kL1);
+    const f32x2* w2 = (const f32x2*)(wl + UpairLds::kW2);
+    const f32x2* wa = (const f32x2*)(wl + UpairLds::kWA);
+    const f32x2 U0 = {u0, u0}, U1 = {u1, u1};
+    f32x2 c[NP];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) c[q] = f32x2{0.f, 0.f};
+    if constexpr (P0 == 0)
+        c[0].x = TWO ? __builtin_fmaf(u0, lin.a0, __builtin_fmaf(u1, lin.a1, lin.b))
+                     : __builtin_fmaf(u0, lin.a0, lin.b);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const int e = (P0 + q) * 16 + i;
+            const f32x4 L = l1[e];
+            const f32x2 w = {L.x, L.y}, b = {L.z, L.w};
+            f32x2 h;
+            if constexpr (TWO) h = __builtin_elementwise_fma(U0, wa[e], __builtin_elementwise_fma(U1, w, b));
+            else h = __builtin_elementwise_fma(U0, w, b);
+            c[q] = __builtin_elementwise_fma(softplus_tail2(h), w2[e], c[q]);
+        }
+    }
+    if constexpr (NP == 4)
+        return ((c[0].x + c[0].y) + (c[1].x + c[1].y)) + ((c[2].x + c[2].y) + (c[3].x + c[3].y));
+    else if constexpr (NP == 2) return (c[0].x + c[0].y) + (c[1].x + c[1].y);
+    else return c[0].x + c[0].y;
+}
+// unit-split evaluation of the unit-pair form (as mlp128_split: wave `sub` evaluates pairs
+// [sub NP, (sub + 1) NP), the partials meet in buf = [US][IL] floats, one of two buffers used
+// alternately; every thread must call it; idle waves skip the units)
+template <int US, bool TWO>
+__device__ __forceinline__ float mlp128_upair_split(const float* wl, V24Lin lin, float u0, float u1,
+                                                    int sub, float* buf, int itid, bool idle) {
+    constexpr int IL = GNND_BLOCK;
+    if constexpr (US == 1) {
+        return idle ? 0.f : mlp128_upair<4, 0, TWO>(wl, lin, u0, u1);
+    } else {
+        static_assert(US == 2 || US == 4, "unit-pair split 1, 2 or 4");
+        constexpr int NP = 4 / US;
+        float p = 0.f;
+        if (!idle) {
+            switch (sub) {
+                case 0: p = mlp128_upair<NP, 0, TWO>(wl, lin, u0, u1); break;
+                case 1: p = mlp128_upair<NP, NP, TWO>(wl, lin, u0, u1); break;
+                case 2: if constexpr (US == 4) p = mlp128_upair<1, 2, TWO>(wl, lin, u0, u1); break;
+                default: if constexpr (US == 4) p = mlp128_upair<1, 3, TWO>(wl, lin, u0, u1); break;
+            }
+        }
+        buf[sub * IL + itid] = p;
+        __syncthreads();
+        if constexpr (US == 2) return buf[itid] + buf[IL + itid];
+        else return (buf[itid] + buf[IL + itid]) + (buf[2 * IL + itid] + buf[3 * IL + itid]);
+    }
+}
+// stage the three MLPs' pair-major LDS blocks from the prepared fp32 V24 weights (gnnd_decode.hip
+// prepare_v24_f32_kernel layout): one entry per thread (workgroups have >= 256 threads)
+__device__ __forceinline__ void stage_upair(const float* __restrict__ w, float* s, int tid) {
+    if (tid < 3 * 64) {
+        const int idx = tid;
+        const int m = idx >> 6, e = idx & 63, k = 8 * (e & 15) + 2 * (e >> 4);
+        const float* src = w + (m == 0 ? kV24Ggc1 : m == 1 ? kV24Ggc2 : kV24Mlp);
+        float* d = s + (m == 0 ? UpairLds::kMlp0 : m == 1 ? UpairLds::kMlp1 : UpairLds::kMlp2);
+        ((f32x4*)(d + UpairLds::kL1))[e] = f32x4{src[2 * k], src[2 * k + 2], src[2 * k + 1], src[2 * k + 3]};
+        const int o2 = m == 0 ? 384 : 256;
+        ((f32x2*)(d + UpairLds::kW2))[e] = f32x2{src[o2 + k], src[o2 + k + 1]};
+        if (m == 0) ((f32x2*)(d + UpairLds::kWA))[e] = f32x2{src[256 + k], src[256 + k + 1]};
     }
 }
 // linear parts, identical in every thread: a fixed-order 128-term dot product spread over the
@@ -1038,6 +1131,11 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
     constexpr bool kV24F64 = MODEL == GNND_V24 && sizeof(T) == 8;
+    // fp32 V24 on the R = 1 slot plan (B <= 4096): the unit-pair MLPs (mlp128_upair), their
+    // pair-major weights staged in LDS after the unit split's partial-sum buffers
+    constexpr bool kUP = kV24F32 && R == 1 && US <= 4;
+    float* s_up = (float*)(smem + ((((char*)(s_part + (US > 1 ? 2 * US * IL : 0))) - smem) + 15 & ~(ptrdiff_t)15));
+    if constexpr (kUP) stage_upair((const float*)w, s_up, tid);
     double* s_pd = (double*)s_part;                        // fp64 unit split: [2][US][256]
     // fp64 unit split: the three MLPs' chain-major weights [3][128] (16-byte aligned) after it
     WcmEntry* s_wcm = (WcmEntry*)(smem + ((((char*)(s_pd + 2 * US * GNND_BLOCK) - smem) + 15) & ~(ptrdiff_t)15));
@@ -1199,14 +1297,21 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     xs[r] = p.x;
                 }
                 GNND_PMARK(pf, 0);
+                if constexpr (kUP) {
+                    // one edge per lane, two hidden units per packed op
+                    const float a = mlp128_upair_split<US, true>(s_up + UpairLds::kMlp0, v24.l1, ext[0], xs[0],
+                                                                 sub, (float*)s_part, itid, widle);
+                    tv[0] = val[0] ? tanh_half_fast(a) : 0.f;
+                } else {
 #pragma unroll
-                for (int r = 0; r < R; r += 2) {
-                    const int r1 = r + 1 < R ? r + 1 : r;
-                    const f32x2 a = mlp128_split<US, true>(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
-                                                           f32x2{xs[r], xs[r1]}, sub, s_part, itid, widle
-                                                           GNND_PARG(pf, 1));
-                    tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
-                    if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
+                    for (int r = 0; r < R; r += 2) {
+                        const int r1 = r + 1 < R ? r + 1 : r;
+                        const f32x2 a = mlp128_split<US, true>(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
+                                                               f32x2{xs[r], xs[r1]}, sub, s_part, itid, widle
+                                                               GNND_PARG(pf, 1));
+                        tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
+                        if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
+                    }
                 }
                 if constexpr (TAPE) {
 #pragma unroll
@@ -1310,7 +1415,13 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     if (own && e != E) tape.u[((size_t)it * B + b0 + b) * g.es + g.e0 + e] = Sc - tv[r];
                 }
             }
-            if constexpr (kV24F32) {
+            if constexpr (kUP) {
+                GNND_PMARK(pf, 3);
+                const float u = Sc - tv[0];
+                const float y = mlp128_upair_split<US, false>(s_up + UpairLds::kMlp1, v24.l2, u, u, sub,
+                                                              (float*)(s_part + US * IL), itid, widle);
+                mn[0] = y * sc + mv[0];
+            } else if constexpr (kV24F32) {
                 GNND_PMARK(pf, 3);
 #pragma unroll
                 for (int r = 0; r < R; r += 2) {
@@ -1370,7 +1481,20 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     }
     if constexpr (MODEL == GNND_V24) {
         // per-edge MLP_o(m_e), then variable sums (decoder_v2_4.py:291-292)
-        if constexpr (kV24F32 && US > 1) {
+        if constexpr (kUP) {
+            // unit pairs: item lane itid evaluates message f0 + itid (the US waves sharing it a
+            // pair group each); the two partial-sum buffers alternate between rounds
+            const int n = nb * nslot;
+            int rb = 0;
+            for (int f0 = 0; f0 < n; f0 += IL, rb ^= 1) {
+                const int f = f0 + itid;
+                const bool widle = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= n;
+                const float m = s_m[f < n ? f : n - 1];
+                const float y = mlp128_upair_split<US, false>(s_up + UpairLds::kMlp2, v24.l3, m, m, sub,
+                                                              (float*)(s_part + rb * US * IL), itid, widle);
+                if (sub == 0 && f < n) s_m[f] = y;
+            }
+        } else if constexpr (kV24F32 && US > 1) {
             // unit split here too: item lane itid evaluates slot pair f0 + 2 itid, the US waves
             // sharing it a chain group each (same bits as the whole MLP in one lane); the two
             // partial-sum buffers alternate between rounds (one barrier per round)
@@ -2275,6 +2399,15 @@ int v24f64_us_big() {
     }();
     return v;
 }
+// GNND_V24_UPAIR=0: fp32 decoder_v2_4 small batches on the R = 2 edge-pair plan (A/B of the
+// unit-pair MLPs)
+bool v24_upair_disabled() {
+    static bool v = [] {
+        const char* e = getenv("GNND_V24_UPAIR");
+        return e && e[0] == '0';
+    }();
+    return v;
+}
 int v24_split_forced() {
     static int v = [] {
         const char* e = getenv("GNND_V24_SPLIT");
@@ -2365,11 +2498,16 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     // (small batches: the R = 2 plan puts one edge pair per lane and the most lanes on a
     // codeword — the training step's latency-bound forward)
     const bool v24f32 = model == GNND_V24 && dtype == GNND_F32;
+    // (B <= 4096 with a one-slot plan, toric: G = 4, R = 1): one edge per lane through the
+    // unit-pair MLPs (mlp128_upair) — a component's edges fill whole item waves
+    const bool upair = v24f32 && B <= 4096 && gr->view.R == 1 && !v24_upair_disabled();
     const GraphView& g = !v24f32 ? gr->view
+                         : upair ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
     const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kV24F64TabDoubles + 3 * 128 + 12) * 8 : 0;
-    const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab;
+    const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab +
+                         (upair ? (size_t)UpairLds::kFloats * 4 + 16 : 0);
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     // fp64 decoder_v2_4 stages its 32.8 KB Softplus table per workgroup: a third of the CU's LDS
@@ -2423,7 +2561,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         // (US = 8 measured slower than 4 on the split toric-7 step, r03c: 0.283 vs 0.276 ms at
         // B = 128 -- the per-item overhead repeats in every split wave; forced only)
         int us = forced ? forced : B <= 256 ? 4 : B <= 512 ? 2 : 1;
-        if (us == 8 && !fit128) us = 4;
+        if (us == 8 && (!fit128 || upair)) us = 4;      // (unit pairs: US <= 4)
         const size_t il = us == 8 ? 128 : GNND_BLOCK;
         if (us > 1 && align16(p->lds) + (size_t)2 * us * il * 8 + 8 <= kLdsMax) {
             p->us = us;
