@@ -1793,6 +1793,16 @@ __device__ __forceinline__ double sig_poly(double r, double s) {
     const double p = __builtin_fma(__builtin_fma(__builtin_fma(c2, r, 1.0 / 6 - t), r, b2), r, 1.0);
     return __builtin_fma(-(t * r), p, s);
 }
+// the same polynomial centred: d = 1/2 - s(a_j + r) = (1/2 - s) + t r P, so that the sigmoid of
+// the signed argument h is 1/2 + copysign(d, h) (one FMA, a sign copy and an add instead of
+// 1 - s, a compare and a 64-bit select: the degree-4 term costs nothing)
+__device__ __forceinline__ double sig_half_poly(double r, double s) {
+    const double t = __builtin_fma(-s, s, s);
+    const double b2 = s - 0.5;
+    const double c2 = b2 * (1.0 / 12 - t);
+    const double p = __builtin_fma(__builtin_fma(__builtin_fma(c2, r, 1.0 / 6 - t), r, b2), r, 1.0);
+    return __builtin_fma(t * r, p, -b2);
+}
 
 // The fp64 decoder_v2_4 MLPs' Softplus table in LDS: GNND_F64_SPTAB 1 (default) the one-read
 // kSpTab form (softplus_sp), 0 the exp + log1p tables (softplus_fast; A/B builds)

@@ -44,7 +44,7 @@ constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 // one after another, lgkmcnt(0) after each read):
 //   sph = |h|/2 + ln(1 + e^-|h|) = softplus(h) - h/2  (the linear h/2 part is summed once per
 //         wave, Units::sx*, instead of a max + add per unit),
-//   sg  = sigmoid(h) = 1 - s(|h|) (h >= 0) or s(|h|).
+//   sg  = sigmoid(h) = 1 - s(|h|) (h >= 0) or s(|h|), as 1/2 + copysign(1/2 - s(|h|), h).
 // Above torch's threshold (h > 20) the zero entry gives sph = h/2 (softplus = h) and sg = 1.
 template <int N>
 __device__ __forceinline__ void sph_and_grad_n(const double (&h)[N], double (&sph)[N],
@@ -58,8 +58,8 @@ __device__ __forceinline__ void sph_and_grad_n(const double (&h)[N], double (&sp
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         sph[i] = __builtin_fma(__builtin_fabs(h[i]), 0.5, sp_poly(q[i].r, e[i].f0, e[i].s));
-        const double sa = sig_poly(q[i].r, e[i].s);
-        sg[i] = h[i] >= 0.0 ? 1.0 - sa : sa;
+        // sigmoid(h) = 1/2 + copysign(1/2 - s(|h|), h)
+        sg[i] = 0.5 + __builtin_copysign(sig_half_poly(q[i].r, e[i].s), h[i]);
     }
 }
 __device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg, const float*) {
@@ -412,12 +412,16 @@ template <typename T> struct BwdLoss {
 };
 // Split graphs (views non-null): blocks [k*cblk, (k+1)*cblk) run component k (graph views[k],
 // rows addressed through its GraphView addressing fields) of codewords j, j + cblk, ...
-template <typename T, int kTrainThreads = train_threads<T>(), int kMinWaves = 1>
+template <typename T, int kTrainThreads = train_threads<T>(), int kMinWaves = 1, bool kSibs = true>
 __global__ void __launch_bounds__(kTrainThreads, kMinWaves)   // kMinWaves: per SIMD
 v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                const T* __restrict__ p, const T* __restrict__ gp, TapeView<T> tape,
                T* __restrict__ gpart, int64_t B, int iters, const GraphView* __restrict__ views,
-               int cblk, BwdLoss<T> lossp, int sibs) {
+               int cblk, BwdLoss<T> lossp, int) {
+    // kSibs: the sibling tables (checks and variables of degree <= 4) and the leave-one-out
+    // phases folded into per-wave prologues; a compile-time switch so each instantiation keeps
+    // one iteration loop (two loops in one kernel spilled the 16-wave shape's registers)
+    constexpr bool sibs = kSibs;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     GNND_PPROF(pf);
     GNND_PSTART(pf, blockIdx.x == 0 && threadIdx.x < 64);
@@ -458,11 +462,12 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     T* s_ext = s_t + Ep;
     T* s_xv = s_ext + Ep;                    // [E] x_{v(e)}  (prior of the edge's variable)
     T* s_sc = s_xv + Ep;                     // [E] s_{c(e)}  (syndrome of the edge's check)
+    T* s_ge = s_sc + Ep;                     // [E] dext (sibling path: pass C's output)
     // fused loss (lossp.y): [V] y + p, p, d loss / d p; [C + nl] row gradients, row terms;
     // int [V] logical masks, [nl] row lengths, [nl][V] row variable lists
     const bool floss = lossp.y != nullptr;
     const int nl = floss ? lossp.nl : 0, nr = C + nl;
-    T* s_ls = s_sc + Ep;
+    T* s_ls = s_ge + Ep;
     T* s_pv = s_ls + V;
     T* s_gpv = s_pv + V;
     T* s_lg = s_gpv + V;
@@ -498,7 +503,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     if constexpr (kTabB > 0)
         for (int i = tid; i < kSpTabDoubles; i += kTrainThreads) s_ftab[i] = kSpTab[i];
-    for (int i = tid; i < 8 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
+    for (int i = tid; i < 9 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
     if (floss) {
         for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
         __syncthreads();
@@ -738,6 +743,65 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
 #ifndef GNND_BWD_EXP
 #define GNND_BWD_EXP 0   // timing experiments only (wrong gradients): 1 no LOO compute,
 #endif                   // 2 no LOO phases or their barriers, 3 no unit passes
+        // With the sibling tables the two leave-one-out phases need no edge-parallel phase and
+        // no barrier of their own: each wave first forms, lane-parallel, the values of the edges
+        // its own unit-pass steps will read (phase D's dm += S_v(dext) - dext before pass A,
+        // phase B's da = ((S_c(du) - du)(1 - t^2)) / 2 before pass C), and LDS keeps a wave's
+        // accesses in order, so its unit pass sees them.  du and dext live in separate buffers
+        // (s_g, and s_da's twin s_ge) so a prologue never reads what another wave's pass of the
+        // same phase writes.  The same operations in the same order as the phases: bit-identical.
+        if constexpr (sibs) {
+            // the unit pass's edge set of this wave: four consecutive edges per step (fp32
+            // 16-wave shape, fp64) or edges = wave mod W (fp32 pipelined 8-wave shape)
+            constexpr bool kPipeSet = sizeof(T) == 4 && kTrainThreads <= 512 && kMinWaves == 1;
+            auto my_edge = [&](int j) -> int {
+                return kPipeSet ? wave + kTrainWaves * j : 4 * (wave + kTrainWaves * (j >> 2)) + (j & 3);
+            };
+            for (int it = iters - 1; it >= 0; --it) {
+                stage(it);
+                __syncthreads();
+                if (it > 0) prefetch(it - 1);
+                if (it < iters - 1) {          // D of the previous step, for this wave's edges
+                    for (int j = lane;; j += 64) {
+                        const int f = my_edge(j);
+                        if (f >= E) break;
+                        T sv = T(0);
+                        const int4 vs = *(const int4*)(s_sib + 8 * f + 4);
+                        const T g0 = s_ge[vs.x < 0 ? 0 : vs.x], g1 = s_ge[vs.y < 0 ? 0 : vs.y];
+                        const T g2 = s_ge[vs.z < 0 ? 0 : vs.z], g3 = s_ge[vs.w < 0 ? 0 : vs.w];
+                        if (vs.x >= 0) sv += g0;
+                        if (vs.y >= 0) sv += g1;
+                        if (vs.z >= 0) sv += g2;
+                        if (vs.w >= 0) sv += g3;
+                        s_dm[f] += sv - s_ge[f];
+                    }
+                }
+                // A: m^{t+1} = MLP_c(u) s_c + m^t
+                if constexpr (kParkF32) uc.unpark(s_wp + 640, lane);
+                unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; },
+                          [&](int f) { return ld4(s_dm, f) * ld4(s_sc, f); }, s_g);
+                __syncthreads();
+                for (int j = lane;; j += 64) {   // B, for this wave's edges
+                    const int f = my_edge(j);
+                    if (f >= E) break;
+                    T sc = T(0);
+                    const int4 cs = *(const int4*)(s_sib + 8 * f);
+                    const T g0 = s_g[cs.x < 0 ? 0 : cs.x], g1 = s_g[cs.y < 0 ? 0 : cs.y];
+                    const T g2 = s_g[cs.z < 0 ? 0 : cs.z], g3 = s_g[cs.w < 0 ? 0 : cs.w];
+                    if (cs.x >= 0) sc += g0;
+                    if (cs.y >= 0) sc += g1;
+                    if (cs.z >= 0) sc += g2;
+                    if (cs.w >= 0) sc += g3;
+                    const T t = s_t[f];
+                    s_da[f] = ((sc - s_g[f]) * (T(1) - t * t)) / T(2);
+                }
+                // C: a = MLP_v(ext, x_v)
+                if constexpr (kParkF32) uv.unpark(s_wp, lane);
+                unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; },
+                          [&](int f) { return ld4(s_da, f); }, s_ge);
+                __syncthreads();
+            }
+        } else {
         for (int it = iters - 1; it >= 0; --it) {
             stage(it);
             __syncthreads();
@@ -806,6 +870,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             GNND_PMARK(pf, 9);
             if (GNND_BWD_EXP != 2) __syncthreads();
             GNND_PMARK(pf, 10);
+        }
         }
     }
 
@@ -890,7 +955,7 @@ size_t train_lds(const gnnd_graph* g, int esz, int nl = -1, int waves = 0, bool 
     const GraphView& v = g->view;
     const size_t tab = (esz == 8 ? bwd_tab_bytes<double>() : 0) +
                        (((size_t)graph_table_ints(v.V, v.C, v.E) * 4 + 15) & ~(size_t)15);
-    size_t n = tab + (size_t)esz * 8 * (((size_t)v.E + 3) & ~(size_t)3);
+    size_t n = tab + (size_t)esz * 9 * (((size_t)v.E + 3) & ~(size_t)3);
     if (nl >= 0)
         n += (size_t)esz * (3 * (size_t)v.V + 2 * ((size_t)v.C + nl)) +
              4 * ((size_t)v.V + nl + (size_t)nl * v.V);
@@ -919,11 +984,15 @@ int launch_bwd(const gnnd_graph* g, const void* w, const void* x, const void* ou
     // fp32: 16 waves (128 VGPRs) by default, GNND_TRAIN_THREADS=512 for 8 waves (A/B)
     const int shape = sizeof(T) == 4 ? train_threads_f32(blocks) : 0;
     // (5122: two 8-wave workgroups per CU = 4 waves per SIMD, 128 VGPRs; 2564: four 4-wave ones)
-    auto kern = shape == 512 ? v24_bwd_kernel<T, 512> : shape == 5122 ? v24_bwd_kernel<T, 512, 4>
-              : shape == 2564 ? v24_bwd_kernel<T, 256, 4> : v24_bwd_kernel<T>;
     const int nthreads = shape == 512 || shape == 5122 ? 512 : shape == 2564 ? 256 : train_threads<T>();
     const int nlf = lossp.y ? lossp.nl : -1;
     const bool sibs = train_sibs(gk, sizeof(T), nlf, nthreads / 64);
+    auto kern = sibs ? (shape == 512 ? v24_bwd_kernel<T, 512> : shape == 5122 ? v24_bwd_kernel<T, 512, 4>
+                        : shape == 2564 ? v24_bwd_kernel<T, 256, 4> : v24_bwd_kernel<T>)
+                     : (shape == 512 ? v24_bwd_kernel<T, 512, 1, false>
+                        : shape == 5122 ? v24_bwd_kernel<T, 512, 4, false>
+                        : shape == 2564 ? v24_bwd_kernel<T, 256, 4, false>
+                        : v24_bwd_kernel<T, train_threads<T>(), 1, false>);
     const size_t lds = train_lds(gk, sizeof(T), nlf, nthreads / 64, sibs);
     if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
     if (lds > 64 * 1024)
