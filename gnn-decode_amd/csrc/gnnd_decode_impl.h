@@ -452,6 +452,11 @@ __device__ __forceinline__ f32x2 pk_fma_hi(f32x2 u, f32x2 w, f32x2 c) {
 // first unit's pair is {w2'_0, b2} (bias as its addend).  Units accumulate in order
 // 0..9 from b2 (no accumulator halves to combine): 20 packed ops per edge PAIR.  Same
 // power-of-two scaling as Mlp10F32 (bit-identical unit contributions).
+// GNND_MLP_ONEASM 1 (default): Mlp10Pair as one asm block per call (same-box A/B r05b: 0.4718 ->
+// 0.4640 ms, profiles/r05/experiments/ab_r05b.txt); 0: one asm statement per packed FMA
+#ifndef GNND_MLP_ONEASM
+#define GNND_MLP_ONEASM 1
+#endif
 struct Mlp10Pair {
     f32x2 w1b[10];     // {W1_k 2^-s_k, b1_k 2^-s_k}
     f32x2 w20b;        // {W2_0 2^s_0, b2}
@@ -459,21 +464,54 @@ struct Mlp10Pair {
     // MLP of the affine input u = in_scale v + in_bias with the output scaled by out_scale,
     // folded into the weights:  W1' = W1 in_scale, b1' = W1 in_bias + b1 (one fp32 fma),
     // W2' = W2 out_scale, b2' = b2 out_scale; vmax bounds |v| for the clamp scaling
+    // units evaluated per call: the live ones, in their original order (a unit whose
+    // pre-activation is <= 0 over the whole input range [0, vmax] adds exactly +0 to every
+    // output: dropping it changes no bit; BCH(63,45)'s trained message MLP has one)
+    int nlive;
     __device__ __forceinline__ void load(const float* w, float vmax, float in_scale = 1.f,
                                          float in_bias = 0.f, float out_scale = 1.f) {
+        f32x2 u1b[10];
+        float u2[10];
+        bool live[10];
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
             const float w1 = w[k] * in_scale, b1 = __builtin_fmaf(w[k], in_bias, w[10 + k]);
             int e;
             frexpf(fabsf(w1) * vmax + fabsf(b1), &e);
-            w1b[k] = f32x2{uniform(ldexpf(w1, -e)), uniform(ldexpf(b1, -e))};
-            const float v = uniform(ldexpf(w[20 + k] * out_scale, e));
-            if (k & 1) w2[k >> 1].y = v; else w2[k >> 1].x = v;
-            if (k == 0) w20b = f32x2{v, uniform(w[30] * out_scale)};
+            u1b[k] = f32x2{uniform(ldexpf(w1, -e)), uniform(ldexpf(b1, -e))};
+            u2[k] = uniform(ldexpf(w[20 + k] * out_scale, e));
+#ifdef GNND_MLP_NOPRUNE
+            live[k] = true;
+#else
+            live[k] = !(b1 <= 0.f && __builtin_fmaf(vmax, w1, b1) <= 0.f);
+#endif
+        }
+        // compact the live units to the front (uniform selects, once per kernel); the slots
+        // past them get zero weights (clamp(0) * 0: exact +0 if ever evaluated)
+        f32x2 c1b[10];
+        float c2[10];
+#pragma unroll
+        for (int j = 0; j < 10; ++j) { c1b[j] = f32x2{0.f, 0.f}; c2[j] = 0.f; }
+        int rank = 0;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+#pragma unroll
+            for (int j = 0; j < 10; ++j)
+                if (live[k] && rank == j) { c1b[j] = u1b[k]; c2[j] = u2[k]; }
+            rank += live[k] ? 1 : 0;
+        }
+        nlive = __builtin_amdgcn_readfirstlane(rank);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            w1b[k] = f32x2{uniform(c1b[k].x), uniform(c1b[k].y)};
+            if (k & 1) w2[k >> 1].y = uniform(c2[k]); else w2[k >> 1].x = uniform(c2[k]);
+            if (k == 0) w20b = f32x2{uniform(c2[0]), uniform(w[30] * out_scale)};
         }
     }
-    __device__ __forceinline__ f32x2 operator()(f32x2 u) const {
-#ifdef GNND_MLP_ONEASM
+    // the live units (nlive, wave-uniform: the dead tail is skipped by a scalar branch; slots
+    // past nlive hold zero weights, so evaluating them would be exact too)
+    __device__ __forceinline__ f32x2 eval(f32x2 u) const {
+#if GNND_MLP_ONEASM
         // the whole MLP as ONE asm block: hipcc's hazard recognizer assumes an op_sel dst
         // forwarding hazard between consecutive inline-asm VALU blocks and puts an s_nop 0
         // before every one that reads the previous block's result (one per unit); inside a block
@@ -481,6 +519,31 @@ struct Mlp10Pair {
         // dst op_sel).  Layer 1 of unit k+1 is issued before unit k's layer-2 FMA (same
         // accumulation order: b2, then units 0..9 — identical bits).
         f32x2 acc, h0, h1;
+        if (nlive == 9) {
+            asm("v_pk_fma_f32 %1, %3, %4, %4 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %2, %3, %5, %5 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %1, %14, %14 op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+                "v_pk_fma_f32 %1, %3, %6, %6 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %2, %15, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+                "v_pk_fma_f32 %2, %3, %7, %7 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %1, %16, %0 op_sel_hi:[1,0,1]\n\t"
+                "v_pk_fma_f32 %1, %3, %8, %8 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %2, %16, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+                "v_pk_fma_f32 %2, %3, %9, %9 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %1, %17, %0 op_sel_hi:[1,0,1]\n\t"
+                "v_pk_fma_f32 %1, %3, %10, %10 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %2, %17, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+                "v_pk_fma_f32 %2, %3, %11, %11 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %1, %18, %0 op_sel_hi:[1,0,1]\n\t"
+                "v_pk_fma_f32 %1, %3, %12, %12 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
+                "v_pk_fma_f32 %0, %2, %18, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+                "v_pk_fma_f32 %0, %1, %19, %0 op_sel_hi:[1,0,1]"
+                : "=&v"(acc), "=&v"(h0), "=&v"(h1)
+                : "v"(u), "s"(w1b[0]), "s"(w1b[1]), "s"(w1b[2]), "s"(w1b[3]), "s"(w1b[4]),
+                  "s"(w1b[5]), "s"(w1b[6]), "s"(w1b[7]), "s"(w1b[8]), "s"(w1b[9]), "s"(w20b),
+                  "s"(w2[0]), "s"(w2[1]), "s"(w2[2]), "s"(w2[3]), "s"(w2[4]));
+            return acc;
+        }
         asm("v_pk_fma_f32 %1, %3, %4, %4 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
             "v_pk_fma_f32 %2, %3, %5, %5 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
             "v_pk_fma_f32 %0, %1, %14, %14 op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
@@ -513,6 +576,7 @@ struct Mlp10Pair {
         acc = pk_fma_sb(h, w20b);
 #pragma unroll
         for (int k = 1; k < 10; ++k) {
+            if (k >= 8 && k >= nlive) break;          // (uniform) pruned dead units
             asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
                 : "=v"(h) : "v"(u), "s"(w1b[k]));
             acc = (k & 1) ? pk_fma_hi(h, w2[k >> 1], acc) : pk_fma_lo(h, w2[k >> 1], acc);
@@ -520,6 +584,7 @@ struct Mlp10Pair {
         return acc;
 #endif
     }
+    __device__ __forceinline__ f32x2 operator()(f32x2 u) const { return eval(u); }
     // N edge pairs at once, unit-major: the N accumulation chains interleave, so no packed
     // FMA waits on the one just issued (same per-pair operation order: identical bits)
     template <int N>
