@@ -1898,6 +1898,30 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     // pads each such group to one degree (weighted BP keeps the identity layout: its
     // per-edge weight tables are indexed by edge id)
     const bool vuni = !WBP && vfixed && g.vgroup * CW >= 64;
+#ifndef GNND_VAR_CACHE
+#define GNND_VAR_CACHE 0          // 1: cache the first var_ord entries (A/B builds)
+#endif
+#ifndef GNND_VAR_CACHE_N
+#define GNND_VAR_CACHE_N 2         // cached entries per lane (4 spilled the 128-VGPR kernel)
+#endif
+    // the uniform variable step's first kVC var_ord entries of this lane (loop-invariant over the
+    // iterations): message-run base, T row position and the wave-uniform padded degree, so an
+    // iteration's variable sums start with the message reads instead of an LDS round trip for the
+    // entry and its decode
+    constexpr int kVC = GNND_VAR_CACHE ? GNND_VAR_CACHE_N : 0;
+    // one VGPR per entry: message-run position (vmbase included, < 2^16: the tile's LDS message
+    // block) | T row position << 16; the padded degree in an SGPR
+    uint32_t vc_mt[kVC > 0 ? kVC : 1];
+    int vc_dp[kVC > 0 ? kVC : 1];
+    if constexpr (kVC > 0) {
+#pragma unroll
+        for (int k = 0; k < kVC; ++k) {
+            const int i = vi0 + k * vstep;
+            const uint2 o = s_vord[i < V ? i : V - 1];
+            vc_mt[k] = (uint32_t)(vmbase + (int)(o.y & 0xffffu)) | (o.y & 0xffff0000u);
+            vc_dp[k] = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));
+        }
+    }
 
     for (int it = 0; it < iters; ++it) {
         if constexpr (kPair) {
@@ -2305,8 +2329,19 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             // degree, so the sum is straight-line code selected by a wave-uniform switch —
             // no masks, no per-edge address or loop arithmetic.  Reference (index_add) order;
             // the padding zeros come last (s + 0 == s).
-            if (vact)
-                for (int i = vi0; i < V; i += vstep) {
+            if (vact) {
+#pragma unroll
+                for (int k = 0; k < kVC; ++k) {
+                    const int i = vi0 + k * vstep;
+                    if (i < V) {
+                        // (v: the readout's output row, needed in the last iteration only)
+                        const int v = last ? (int)(s_vord[i].x & 0xffffu) : 0;
+                        const int pm = (int)(vc_mt[k] & 0xffffu), pt = (int)(vc_mt[k] >> 16);
+                        GNND_DCHECK(pm - vmbase + vc_dp[k] <= E1, GNND_DBG_LDS_POS);
+                        var_out(vb, vsbase, vtbase, v, pt, var_sum_uniform(s_m + pm, vc_dp[k]));
+                    }
+                }
+                for (int i = vi0 + kVC * vstep; i < V; i += vstep) {
                     const uint2 o = s_vord[i];
                     const int dp = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));
                     const int v = (int)(o.x & 0xffffu);
@@ -2314,6 +2349,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     var_out(vb, vsbase, vtbase, v, (int)(o.y >> 16),
                             var_sum_uniform(s_m + vmbase + (int)(o.y & 0xffffu), dp));
                 }
+            }
         } else if (vfixed) {
             // CW divides 256: f = tid + k 256 keeps f mod CW, so the lane's codeword and its
             // LDS bases are loop-invariant (no per-item division or 32-bit multiplies: those
