@@ -466,7 +466,9 @@ struct Mlp10Pair {
     // W2' = W2 out_scale, b2' = b2 out_scale; vmax bounds |v| for the clamp scaling
     // units evaluated per call: the live ones, in their original order (a unit whose
     // pre-activation is <= 0 over the whole input range [0, vmax] adds exactly +0 to every
-    // output: dropping it changes no bit; BCH(63,45)'s trained message MLP has one)
+    // output: dropping it changes no bit; BCH(63,45)'s trained message MLP has one).
+    // GNND_MLP_PRUNE only (A/B builds): the per-call scalar branch cost more than the unit
+    // (BCH -0.3 %, LDPC -5 %, profiles/r05/experiments/ab_r05d.txt); by default all 10 run
     int nlive;
     __device__ __forceinline__ void load(const float* w, float vmax, float in_scale = 1.f,
                                          float in_bias = 0.f, float out_scale = 1.f) {
@@ -480,7 +482,7 @@ struct Mlp10Pair {
             frexpf(fabsf(w1) * vmax + fabsf(b1), &e);
             u1b[k] = f32x2{uniform(ldexpf(w1, -e)), uniform(ldexpf(b1, -e))};
             u2[k] = uniform(ldexpf(w[20 + k] * out_scale, e));
-#ifdef GNND_MLP_NOPRUNE
+#ifndef GNND_MLP_PRUNE
             live[k] = true;
 #else
             live[k] = !(b1 <= 0.f && __builtin_fmaf(vmax, w1, b1) <= 0.f);
@@ -519,6 +521,7 @@ struct Mlp10Pair {
         // dst op_sel).  Layer 1 of unit k+1 is issued before unit k's layer-2 FMA (same
         // accumulation order: b2, then units 0..9 — identical bits).
         f32x2 acc, h0, h1;
+#ifdef GNND_MLP_PRUNE
         if (nlive == 9) {
             asm("v_pk_fma_f32 %1, %3, %4, %4 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
                 "v_pk_fma_f32 %2, %3, %5, %5 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
@@ -544,6 +547,7 @@ struct Mlp10Pair {
                   "s"(w2[0]), "s"(w2[1]), "s"(w2[2]), "s"(w2[3]), "s"(w2[4]));
             return acc;
         }
+#endif
         asm("v_pk_fma_f32 %1, %3, %4, %4 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
             "v_pk_fma_f32 %2, %3, %5, %5 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp\n\t"
             "v_pk_fma_f32 %0, %1, %14, %14 op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
@@ -576,7 +580,9 @@ struct Mlp10Pair {
         acc = pk_fma_sb(h, w20b);
 #pragma unroll
         for (int k = 1; k < 10; ++k) {
+#ifdef GNND_MLP_PRUNE
             if (k >= 8 && k >= nlive) break;          // (uniform) pruned dead units
+#endif
             asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] clamp"
                 : "=v"(h) : "v"(u), "s"(w1b[k]));
             acc = (k & 1) ? pk_fma_hi(h, w2[k >> 1], acc) : pk_fma_lo(h, w2[k >> 1], acc);
@@ -1899,7 +1905,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     // per-edge weight tables are indexed by edge id)
     const bool vuni = !WBP && vfixed && g.vgroup * CW >= 64;
 #ifndef GNND_VAR_CACHE
-#define GNND_VAR_CACHE 0          // 1: cache the first var_ord entries (A/B builds)
+#define GNND_VAR_CACHE 1          // cache the first var_ord entries (r05d A/B: 0.4637 -> 0.4595 ms)
 #endif
 #ifndef GNND_VAR_CACHE_N
 #define GNND_VAR_CACHE_N 2         // cached entries per lane (4 spilled the 128-VGPR kernel)
