@@ -2340,8 +2340,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                 for (int k = 0; k < kVC; ++k) {
                     const int i = vi0 + k * vstep;
                     if (i < V) {
-                        // (v: the readout's output row, needed in the last iteration only)
-                        const int v = last ? (int)(s_vord[i].x & 0xffffu) : 0;
+                        // (v: the readout's output row in the last iteration; every iteration
+                        // of the {S_v, x_v} layouts, whose S_v row it indexes)
+                        const int v = (last || !kTX) ? (int)(s_vord[i].x & 0xffffu) : 0;
                         const int pm = (int)(vc_mt[k] & 0xffffu), pt = (int)(vc_mt[k] >> 16);
                         GNND_DCHECK(pm - vmbase + vc_dp[k] <= E1, GNND_DBG_LDS_POS);
                         var_out(vb, vsbase, vtbase, v, pt, var_sum_uniform(s_m + pm, vc_dp[k]));
