@@ -1582,6 +1582,1052 @@ __constant__ static const double kSpTab[4100] = {
     0x1.d6c224053da70p-47, 0x1.d6c224053da3ap-47, 0x1.cf75bdfc6a74fp-47, 0x1.cf75bdfc6a71bp-47,
     0x1.c8464f7616435p-47, 0x1.c8464f7616402p-47, 0x0.0p+0, 0x0.0p+0,
 };
+// Signed Softplus table (tools/gen_fp64_tables.py): {g(c_j), 1/2 - sigmoid(c_j)} with
+// g(h) = softplus(h) - h/2, c_j = j * kSgStep, j = -1280..799, and two linear end entries (h >= 20:
+// g = h/2, torch's threshold; h < -32.03: g = -h/2) (softplus_sg, the fp64 decoder_v2_4 forward)
+__constant__ static const double kSgTab[4164] = {
+    0x1.005c37b6fe8f3p+4, 0x1.0000000000000p-1, 0x1.0028fc5154b1ap+4, 0x1.fffffffffff20p-2,
+    0x1.ffeb81d755a7dp+3, 0x1.fffffffffff1bp-2, 0x1.ff850b0c01ec6p+3, 0x1.fffffffffff15p-2,
+    0x1.ff1e9440ae30ep+3, 0x1.fffffffffff0fp-2, 0x1.feb81d755a757p+3, 0x1.fffffffffff09p-2,
+    0x1.fe51a6aa06b9fp+3, 0x1.fffffffffff03p-2, 0x1.fdeb2fdeb2fe8p+3, 0x1.ffffffffffefcp-2,
+    0x1.fd84b9135f431p+3, 0x1.ffffffffffef6p-2, 0x1.fd1e42480b879p+3, 0x1.ffffffffffeefp-2,
+    0x1.fcb7cb7cb7cc2p+3, 0x1.ffffffffffee8p-2, 0x1.fc5154b16410ap+3, 0x1.ffffffffffee1p-2,
+    0x1.fbeadde610553p+3, 0x1.ffffffffffedap-2, 0x1.fb84671abc99cp+3, 0x1.ffffffffffed2p-2,
+    0x1.fb1df04f68de4p+3, 0x1.ffffffffffecap-2, 0x1.fab779841522dp+3, 0x1.ffffffffffec3p-2,
+    0x1.fa5102b8c1675p+3, 0x1.ffffffffffebbp-2, 0x1.f9ea8bed6dabep+3, 0x1.ffffffffffeb2p-2,
+    0x1.f984152219f07p+3, 0x1.ffffffffffeaap-2, 0x1.f91d9e56c634fp+3, 0x1.ffffffffffea1p-2,
+    0x1.f8b7278b72798p+3, 0x1.ffffffffffe98p-2, 0x1.f850b0c01ebe1p+3, 0x1.ffffffffffe8fp-2,
+    0x1.f7ea39f4cb029p+3, 0x1.ffffffffffe86p-2, 0x1.f783c32977472p+3, 0x1.ffffffffffe7cp-2,
+    0x1.f71d4c5e238bbp+3, 0x1.ffffffffffe72p-2, 0x1.f6b6d592cfd03p+3, 0x1.ffffffffffe68p-2,
+    0x1.f6505ec77c14cp+3, 0x1.ffffffffffe5ep-2, 0x1.f5e9e7fc28595p+3, 0x1.ffffffffffe53p-2,
+    0x1.f5837130d49ddp+3, 0x1.ffffffffffe49p-2, 0x1.f51cfa6580e26p+3, 0x1.ffffffffffe3dp-2,
+    0x1.f4b6839a2d26fp+3, 0x1.ffffffffffe32p-2, 0x1.f4500cced96b7p+3, 0x1.ffffffffffe26p-2,
+    0x1.f3e9960385b00p+3, 0x1.ffffffffffe1ap-2, 0x1.f3831f3831f49p+3, 0x1.ffffffffffe0ep-2,
+    0x1.f31ca86cde392p+3, 0x1.ffffffffffe01p-2, 0x1.f2b631a18a7dap+3, 0x1.ffffffffffdf5p-2,
+    0x1.f24fbad636c23p+3, 0x1.ffffffffffde7p-2, 0x1.f1e9440ae306cp+3, 0x1.ffffffffffddap-2,
+    0x1.f182cd3f8f4b5p+3, 0x1.ffffffffffdccp-2, 0x1.f11c56743b8fep+3, 0x1.ffffffffffdbdp-2,
+    0x1.f0b5dfa8e7d46p+3, 0x1.ffffffffffdafp-2, 0x1.f04f68dd9418fp+3, 0x1.ffffffffffda0p-2,
+    0x1.efe8f212405d8p+3, 0x1.ffffffffffd90p-2, 0x1.ef827b46eca21p+3, 0x1.ffffffffffd81p-2,
+    0x1.ef1c047b98e6ap+3, 0x1.ffffffffffd70p-2, 0x1.eeb58db0452b3p+3, 0x1.ffffffffffd60p-2,
+    0x1.ee4f16e4f16fcp+3, 0x1.ffffffffffd4fp-2, 0x1.ede8a0199db45p+3, 0x1.ffffffffffd3dp-2,
+    0x1.ed82294e49f8ep+3, 0x1.ffffffffffd2bp-2, 0x1.ed1bb282f63d6p+3, 0x1.ffffffffffd19p-2,
+    0x1.ecb53bb7a281fp+3, 0x1.ffffffffffd06p-2, 0x1.ec4ec4ec4ec68p+3, 0x1.ffffffffffcf3p-2,
+    0x1.ebe84e20fb0b1p+3, 0x1.ffffffffffcdfp-2, 0x1.eb81d755a74fap+3, 0x1.ffffffffffccbp-2,
+    0x1.eb1b608a53943p+3, 0x1.ffffffffffcb6p-2, 0x1.eab4e9beffd8cp+3, 0x1.ffffffffffca1p-2,
+    0x1.ea4e72f3ac1d5p+3, 0x1.ffffffffffc8bp-2, 0x1.e9e7fc285861fp+3, 0x1.ffffffffffc74p-2,
+    0x1.e981855d04a68p+3, 0x1.ffffffffffc5dp-2, 0x1.e91b0e91b0eb1p+3, 0x1.ffffffffffc46p-2,
+    0x1.e8b497c65d2fap+3, 0x1.ffffffffffc2ep-2, 0x1.e84e20fb09743p+3, 0x1.ffffffffffc15p-2,
+    0x1.e7e7aa2fb5b8cp+3, 0x1.ffffffffffbfbp-2, 0x1.e781336461fd5p+3, 0x1.ffffffffffbe1p-2,
+    0x1.e71abc990e41ep+3, 0x1.ffffffffffbc7p-2, 0x1.e6b445cdba868p+3, 0x1.ffffffffffbabp-2,
+    0x1.e64dcf0266cb1p+3, 0x1.ffffffffffb8fp-2, 0x1.e5e75837130fap+3, 0x1.ffffffffffb72p-2,
+    0x1.e580e16bbf544p+3, 0x1.ffffffffffb55p-2, 0x1.e51a6aa06b98dp+3, 0x1.ffffffffffb37p-2,
+    0x1.e4b3f3d517dd6p+3, 0x1.ffffffffffb18p-2, 0x1.e44d7d09c4220p+3, 0x1.ffffffffffaf8p-2,
+    0x1.e3e7063e70669p+3, 0x1.ffffffffffad7p-2, 0x1.e3808f731cab2p+3, 0x1.ffffffffffab6p-2,
+    0x1.e31a18a7c8efcp+3, 0x1.ffffffffffa93p-2, 0x1.e2b3a1dc75345p+3, 0x1.ffffffffffa70p-2,
+    0x1.e24d2b112178fp+3, 0x1.ffffffffffa4cp-2, 0x1.e1e6b445cdbd8p+3, 0x1.ffffffffffa27p-2,
+    0x1.e1803d7a7a022p+3, 0x1.ffffffffffa01p-2, 0x1.e119c6af2646bp+3, 0x1.ffffffffff9dap-2,
+    0x1.e0b34fe3d28b5p+3, 0x1.ffffffffff9b2p-2, 0x1.e04cd9187ecffp+3, 0x1.ffffffffff98ap-2,
+    0x1.dfe6624d2b148p+3, 0x1.ffffffffff960p-2, 0x1.df7feb81d7592p+3, 0x1.ffffffffff935p-2,
+    0x1.df1974b6839dcp+3, 0x1.ffffffffff909p-2, 0x1.deb2fdeb2fe25p+3, 0x1.ffffffffff8dcp-2,
+    0x1.de4c871fdc26fp+3, 0x1.ffffffffff8adp-2, 0x1.dde61054886b9p+3, 0x1.ffffffffff87ep-2,
+    0x1.dd7f998934b03p+3, 0x1.ffffffffff84dp-2, 0x1.dd1922bde0f4dp+3, 0x1.ffffffffff81bp-2,
+    0x1.dcb2abf28d397p+3, 0x1.ffffffffff7e8p-2, 0x1.dc4c3527397e1p+3, 0x1.ffffffffff7b3p-2,
+    0x1.dbe5be5be5c2bp+3, 0x1.ffffffffff77ep-2, 0x1.db7f479092075p+3, 0x1.ffffffffff746p-2,
+    0x1.db18d0c53e4bfp+3, 0x1.ffffffffff70ep-2, 0x1.dab259f9ea909p+3, 0x1.ffffffffff6d4p-2,
+    0x1.da4be32e96d54p+3, 0x1.ffffffffff698p-2, 0x1.d9e56c634319ep+3, 0x1.ffffffffff65bp-2,
+    0x1.d97ef597ef5e8p+3, 0x1.ffffffffff61dp-2, 0x1.d9187ecc9ba33p+3, 0x1.ffffffffff5ddp-2,
+    0x1.d8b2080147e7dp+3, 0x1.ffffffffff59bp-2, 0x1.d84b9135f42c7p+3, 0x1.ffffffffff558p-2,
+    0x1.d7e51a6aa0712p+3, 0x1.ffffffffff512p-2, 0x1.d77ea39f4cb5dp+3, 0x1.ffffffffff4ccp-2,
+    0x1.d7182cd3f8fa7p+3, 0x1.ffffffffff483p-2, 0x1.d6b1b608a53f2p+3, 0x1.ffffffffff438p-2,
+    0x1.d64b3f3d5183dp+3, 0x1.ffffffffff3ecp-2, 0x1.d5e4c871fdc87p+3, 0x1.ffffffffff39ep-2,
+    0x1.d57e51a6aa0d2p+3, 0x1.ffffffffff34dp-2, 0x1.d517dadb5651dp+3, 0x1.ffffffffff2fbp-2,
+    0x1.d4b1641002968p+3, 0x1.ffffffffff2a7p-2, 0x1.d44aed44aedb3p+3, 0x1.ffffffffff250p-2,
+    0x1.d3e476795b1fep+3, 0x1.ffffffffff1f7p-2, 0x1.d37dffae0764ap+3, 0x1.ffffffffff19cp-2,
+    0x1.d31788e2b3a95p+3, 0x1.ffffffffff13fp-2, 0x1.d2b112175fee0p+3, 0x1.ffffffffff0dfp-2,
+    0x1.d24a9b4c0c32cp+3, 0x1.ffffffffff07dp-2, 0x1.d1e42480b8777p+3, 0x1.ffffffffff019p-2,
+    0x1.d17dadb564bc3p+3, 0x1.fffffffffefb1p-2, 0x1.d11736ea1100ep+3, 0x1.fffffffffef48p-2,
+    0x1.d0b0c01ebd45ap+3, 0x1.fffffffffeedbp-2, 0x1.d04a4953698a6p+3, 0x1.fffffffffee6cp-2,
+    0x1.cfe3d28815cf2p+3, 0x1.fffffffffedfap-2, 0x1.cf7d5bbcc213ep+3, 0x1.fffffffffed85p-2,
+    0x1.cf16e4f16e58ap+3, 0x1.fffffffffed0dp-2, 0x1.ceb06e261a9d6p+3, 0x1.fffffffffec93p-2,
+    0x1.ce49f75ac6e23p+3, 0x1.fffffffffec15p-2, 0x1.cde3808f7326fp+3, 0x1.fffffffffeb93p-2,
+    0x1.cd7d09c41f6bcp+3, 0x1.fffffffffeb0fp-2, 0x1.cd1692f8cbb08p+3, 0x1.fffffffffea87p-2,
+    0x1.ccb01c2d77f55p+3, 0x1.fffffffffe9fcp-2, 0x1.cc49a562243a2p+3, 0x1.fffffffffe96dp-2,
+    0x1.cbe32e96d07efp+3, 0x1.fffffffffe8dbp-2, 0x1.cb7cb7cb7cc3cp+3, 0x1.fffffffffe845p-2,
+    0x1.cb16410029089p+3, 0x1.fffffffffe7abp-2, 0x1.caafca34d54d6p+3, 0x1.fffffffffe70dp-2,
+    0x1.ca49536981924p+3, 0x1.fffffffffe66bp-2, 0x1.c9e2dc9e2dd71p+3, 0x1.fffffffffe5c5p-2,
+    0x1.c97c65d2da1bfp+3, 0x1.fffffffffe51bp-2, 0x1.c915ef078660dp+3, 0x1.fffffffffe46dp-2,
+    0x1.c8af783c32a5bp+3, 0x1.fffffffffe3bap-2, 0x1.c8490170deea9p+3, 0x1.fffffffffe303p-2,
+    0x1.c7e28aa58b2f7p+3, 0x1.fffffffffe247p-2, 0x1.c77c13da37745p+3, 0x1.fffffffffe186p-2,
+    0x1.c7159d0ee3b94p+3, 0x1.fffffffffe0c0p-2, 0x1.c6af26438ffe3p+3, 0x1.fffffffffdff6p-2,
+    0x1.c648af783c431p+3, 0x1.fffffffffdf26p-2, 0x1.c5e238ace8880p+3, 0x1.fffffffffde51p-2,
+    0x1.c57bc1e194cd0p+3, 0x1.fffffffffdd76p-2, 0x1.c5154b164111fp+3, 0x1.fffffffffdc96p-2,
+    0x1.c4aed44aed56fp+3, 0x1.fffffffffdbb1p-2, 0x1.c4485d7f999bep+3, 0x1.fffffffffdac5p-2,
+    0x1.c3e1e6b445e0ep+3, 0x1.fffffffffd9d4p-2, 0x1.c37b6fe8f225ep+3, 0x1.fffffffffd8dcp-2,
+    0x1.c314f91d9e6afp+3, 0x1.fffffffffd7dep-2, 0x1.c2ae82524aaffp+3, 0x1.fffffffffd6dap-2,
+    0x1.c2480b86f6f50p+3, 0x1.fffffffffd5cfp-2, 0x1.c1e194bba33a1p+3, 0x1.fffffffffd4bep-2,
+    0x1.c17b1df04f7f2p+3, 0x1.fffffffffd3a5p-2, 0x1.c114a724fbc43p+3, 0x1.fffffffffd286p-2,
+    0x1.c0ae3059a8095p+3, 0x1.fffffffffd15fp-2, 0x1.c047b98e544e7p+3, 0x1.fffffffffd030p-2,
+    0x1.bfe142c300939p+3, 0x1.fffffffffcefap-2, 0x1.bf7acbf7acd8bp+3, 0x1.fffffffffcdbcp-2,
+    0x1.bf14552c591ddp+3, 0x1.fffffffffcc76p-2, 0x1.beadde6105630p+3, 0x1.fffffffffcb28p-2,
+    0x1.be476795b1a83p+3, 0x1.fffffffffc9d2p-2, 0x1.bde0f0ca5ded7p+3, 0x1.fffffffffc872p-2,
+    0x1.bd7a79ff0a32ap+3, 0x1.fffffffffc70ap-2, 0x1.bd140333b677ep+3, 0x1.fffffffffc599p-2,
+    0x1.bcad8c6862bd2p+3, 0x1.fffffffffc41ep-2, 0x1.bc47159d0f027p+3, 0x1.fffffffffc29ap-2,
+    0x1.bbe09ed1bb47cp+3, 0x1.fffffffffc10bp-2, 0x1.bb7a2806678d1p+3, 0x1.fffffffffbf73p-2,
+    0x1.bb13b13b13d26p+3, 0x1.fffffffffbdd0p-2, 0x1.baad3a6fc017cp+3, 0x1.fffffffffbc23p-2,
+    0x1.ba46c3a46c5d2p+3, 0x1.fffffffffba6bp-2, 0x1.b9e04cd918a29p+3, 0x1.fffffffffb8a8p-2,
+    0x1.b979d60dc4e7fp+3, 0x1.fffffffffb6d9p-2, 0x1.b9135f42712d7p+3, 0x1.fffffffffb4ffp-2,
+    0x1.b8ace8771d72ep+3, 0x1.fffffffffb319p-2, 0x1.b84671abc9b86p+3, 0x1.fffffffffb126p-2,
+    0x1.b7dffae075fdep+3, 0x1.fffffffffaf27p-2, 0x1.b779841522437p+3, 0x1.fffffffffad1ap-2,
+    0x1.b7130d49ce890p+3, 0x1.fffffffffab01p-2, 0x1.b6ac967e7aceap+3, 0x1.fffffffffa8dap-2,
+    0x1.b6461fb327144p+3, 0x1.fffffffffa6a4p-2, 0x1.b5dfa8e7d359ep+3, 0x1.fffffffffa461p-2,
+    0x1.b579321c7f9f9p+3, 0x1.fffffffffa20fp-2, 0x1.b512bb512be55p+3, 0x1.fffffffff9faep-2,
+    0x1.b4ac4485d82b1p+3, 0x1.fffffffff9d3dp-2, 0x1.b445cdba8470dp+3, 0x1.fffffffff9abcp-2,
+    0x1.b3df56ef30b6ap+3, 0x1.fffffffff982cp-2, 0x1.b378e023dcfc7p+3, 0x1.fffffffff958bp-2,
+    0x1.b312695889425p+3, 0x1.fffffffff92d8p-2, 0x1.b2abf28d35884p+3, 0x1.fffffffff9014p-2,
+    0x1.b2457bc1e1ce3p+3, 0x1.fffffffff8d3fp-2, 0x1.b1df04f68e142p+3, 0x1.fffffffff8a56p-2,
+    0x1.b1788e2b3a5a3p+3, 0x1.fffffffff875bp-2, 0x1.b112175fe6a03p+3, 0x1.fffffffff844dp-2,
+    0x1.b0aba09492e65p+3, 0x1.fffffffff812bp-2, 0x1.b04529c93f2c7p+3, 0x1.fffffffff7df4p-2,
+    0x1.afdeb2fdeb72ap+3, 0x1.fffffffff7aa9p-2, 0x1.af783c3297b8dp+3, 0x1.fffffffff7748p-2,
+    0x1.af11c56743ff1p+3, 0x1.fffffffff73d2p-2, 0x1.aeab4e9bf0456p+3, 0x1.fffffffff7045p-2,
+    0x1.ae44d7d09c8bbp+3, 0x1.fffffffff6ca1p-2, 0x1.adde610548d22p+3, 0x1.fffffffff68e5p-2,
+    0x1.ad77ea39f5189p+3, 0x1.fffffffff6511p-2, 0x1.ad11736ea15f0p+3, 0x1.fffffffff6124p-2,
+    0x1.acaafca34da59p+3, 0x1.fffffffff5d1ep-2, 0x1.ac4485d7f9ec2p+3, 0x1.fffffffff58fep-2,
+    0x1.abde0f0ca632dp+3, 0x1.fffffffff54c3p-2, 0x1.ab77984152798p+3, 0x1.fffffffff506dp-2,
+    0x1.ab112175fec04p+3, 0x1.fffffffff4bfap-2, 0x1.aaaaaaaaab070p+3, 0x1.fffffffff476bp-2,
+    0x1.aa4433df574dep+3, 0x1.fffffffff42bep-2, 0x1.a9ddbd140394dp+3, 0x1.fffffffff3df2p-2,
+    0x1.a9774648afdbdp+3, 0x1.fffffffff3908p-2, 0x1.a910cf7d5c22dp+3, 0x1.fffffffff33fep-2,
+    0x1.a8aa58b20869fp+3, 0x1.fffffffff2ed3p-2, 0x1.a843e1e6b4b12p+3, 0x1.fffffffff2986p-2,
+    0x1.a7dd6b1b60f86p+3, 0x1.fffffffff2417p-2, 0x1.a776f4500d3fap+3, 0x1.fffffffff1e85p-2,
+    0x1.a7107d84b9871p+3, 0x1.fffffffff18cfp-2, 0x1.a6aa06b965ce8p+3, 0x1.fffffffff12f4p-2,
+    0x1.a6438fee12160p+3, 0x1.fffffffff0cf3p-2, 0x1.a5dd1922be5dap+3, 0x1.fffffffff06cbp-2,
+    0x1.a576a2576aa55p+3, 0x1.fffffffff007ap-2, 0x1.a5102b8c16ed1p+3, 0x1.ffffffffefa01p-2,
+    0x1.a4a9b4c0c334ep+3, 0x1.ffffffffef35fp-2, 0x1.a4433df56f7cdp+3, 0x1.ffffffffeec90p-2,
+    0x1.a3dcc72a1bc4dp+3, 0x1.ffffffffee596p-2, 0x1.a376505ec80cfp+3, 0x1.ffffffffede6fp-2,
+    0x1.a30fd99374552p+3, 0x1.ffffffffed719p-2, 0x1.a2a962c8209d6p+3, 0x1.ffffffffecf94p-2,
+    0x1.a242ebfccce5cp+3, 0x1.ffffffffec7dep-2, 0x1.a1dc7531792e4p+3, 0x1.ffffffffebff6p-2,
+    0x1.a175fe662576dp+3, 0x1.ffffffffeb7dap-2, 0x1.a10f879ad1bf8p+3, 0x1.ffffffffeaf8ap-2,
+    0x1.a0a910cf7e085p+3, 0x1.ffffffffea704p-2, 0x1.a0429a042a513p+3, 0x1.ffffffffe9e47p-2,
+    0x1.9fdc2338d69a3p+3, 0x1.ffffffffe9551p-2, 0x1.9f75ac6d82e35p+3, 0x1.ffffffffe8c22p-2,
+    0x1.9f0f35a22f2c9p+3, 0x1.ffffffffe82b6p-2, 0x1.9ea8bed6db75ep+3, 0x1.ffffffffe790dp-2,
+    0x1.9e42480b87bf6p+3, 0x1.ffffffffe6f26p-2, 0x1.9ddbd1403408fp+3, 0x1.ffffffffe64ffp-2,
+    0x1.9d755a74e052bp+3, 0x1.ffffffffe5a96p-2, 0x1.9d0ee3a98c9c9p+3, 0x1.ffffffffe4fe9p-2,
+    0x1.9ca86cde38e69p+3, 0x1.ffffffffe44f7p-2, 0x1.9c41f612e530bp+3, 0x1.ffffffffe39bep-2,
+    0x1.9bdb7f47917afp+3, 0x1.ffffffffe2e3cp-2, 0x1.9b75087c3dc56p+3, 0x1.ffffffffe2270p-2,
+    0x1.9b0e91b0ea0ffp+3, 0x1.ffffffffe1657p-2, 0x1.9aa81ae5965abp+3, 0x1.ffffffffe09efp-2,
+    0x1.9a41a41a42a59p+3, 0x1.ffffffffdfd38p-2, 0x1.99db2d4eeef0ap+3, 0x1.ffffffffdf02dp-2,
+    0x1.9974b6839b3bdp+3, 0x1.ffffffffde2cfp-2, 0x1.990e3fb847873p+3, 0x1.ffffffffdd519p-2,
+    0x1.98a7c8ecf3d2cp+3, 0x1.ffffffffdc70bp-2, 0x1.98415221a01e7p+3, 0x1.ffffffffdb8a1p-2,
+    0x1.97dadb564c6a6p+3, 0x1.ffffffffda9dap-2, 0x1.9774648af8b68p+3, 0x1.ffffffffd9ab3p-2,
+    0x1.970dedbfa502cp+3, 0x1.ffffffffd8b2ap-2, 0x1.96a776f4514f4p+3, 0x1.ffffffffd7b3cp-2,
+    0x1.96410028fd9bfp+3, 0x1.ffffffffd6ae7p-2, 0x1.95da895da9e8dp+3, 0x1.ffffffffd5a28p-2,
+    0x1.957412925635fp+3, 0x1.ffffffffd48fcp-2, 0x1.950d9bc702834p+3, 0x1.ffffffffd3761p-2,
+    0x1.94a724fbaed0dp+3, 0x1.ffffffffd2554p-2, 0x1.9440ae305b1eap+3, 0x1.ffffffffd12d2p-2,
+    0x1.93da3765076cap+3, 0x1.ffffffffcffd8p-2, 0x1.9373c099b3baep+3, 0x1.ffffffffcec62p-2,
+    0x1.930d49ce60096p+3, 0x1.ffffffffcd86fp-2, 0x1.92a6d3030c582p+3, 0x1.ffffffffcc3fap-2,
+    0x1.92405c37b8a72p+3, 0x1.ffffffffcaf00p-2, 0x1.91d9e56c64f66p+3, 0x1.ffffffffc997fp-2,
+    0x1.91736ea11145fp+3, 0x1.ffffffffc8372p-2, 0x1.910cf7d5bd95cp+3, 0x1.ffffffffc6cd6p-2,
+    0x1.90a6810a69e5ep+3, 0x1.ffffffffc55a7p-2, 0x1.90400a3f16365p+3, 0x1.ffffffffc3de2p-2,
+    0x1.8fd99373c2870p+3, 0x1.ffffffffc2583p-2, 0x1.8f731ca86ed80p+3, 0x1.ffffffffc0c86p-2,
+    0x1.8f0ca5dd1b296p+3, 0x1.ffffffffbf2e7p-2, 0x1.8ea62f11c77b0p+3, 0x1.ffffffffbd8a1p-2,
+    0x1.8e3fb84673cd0p+3, 0x1.ffffffffbbdb2p-2, 0x1.8dd9417b201f5p+3, 0x1.ffffffffba213p-2,
+    0x1.8d72caafcc720p+3, 0x1.ffffffffb85c2p-2, 0x1.8d0c53e478c51p+3, 0x1.ffffffffb68b9p-2,
+    0x1.8ca5dd1925187p+3, 0x1.ffffffffb4af3p-2, 0x1.8c3f664dd16c4p+3, 0x1.ffffffffb2c6dp-2,
+    0x1.8bd8ef827dc07p+3, 0x1.ffffffffb0d20p-2, 0x1.8b7278b72a150p+3, 0x1.ffffffffaed09p-2,
+    0x1.8b0c01ebd669fp+3, 0x1.ffffffffacc21p-2, 0x1.8aa58b2082bf6p+3, 0x1.ffffffffaaa65p-2,
+    0x1.8a3f14552f153p+3, 0x1.ffffffffa87cdp-2, 0x1.89d89d89db6b7p+3, 0x1.ffffffffa6455p-2,
+    0x1.897226be87c22p+3, 0x1.ffffffffa3ff7p-2, 0x1.890baff334195p+3, 0x1.ffffffffa1aadp-2,
+    0x1.88a53927e070fp+3, 0x1.ffffffff9f472p-2, 0x1.883ec25c8cc91p+3, 0x1.ffffffff9cd3ep-2,
+    0x1.87d84b913921bp+3, 0x1.ffffffff9a50cp-2, 0x1.8771d4c5e57adp+3, 0x1.ffffffff97bd6p-2,
+    0x1.870b5dfa91d47p+3, 0x1.ffffffff95194p-2, 0x1.86a4e72f3e2eap+3, 0x1.ffffffff92640p-2,
+    0x1.863e7063ea896p+3, 0x1.ffffffff8f9d4p-2, 0x1.85d7f99896e4bp+3, 0x1.ffffffff8cc47p-2,
+    0x1.857182cd43409p+3, 0x1.ffffffff89d93p-2, 0x1.850b0c01ef9d0p+3, 0x1.ffffffff86db0p-2,
+    0x1.84a495369bfa2p+3, 0x1.ffffffff83c96p-2, 0x1.843e1e6b4857dp+3, 0x1.ffffffff80a3ep-2,
+    0x1.83d7a79ff4b62p+3, 0x1.ffffffff7d6a0p-2, 0x1.837130d4a1152p+3, 0x1.ffffffff7a1b3p-2,
+    0x1.830aba094d74cp+3, 0x1.ffffffff76b6fp-2, 0x1.82a4433df9d52p+3, 0x1.ffffffff733cap-2,
+    0x1.823dcc72a6363p+3, 0x1.ffffffff6fabdp-2, 0x1.81d755a75297fp+3, 0x1.ffffffff6c03ep-2,
+    0x1.8170dedbfefa7p+3, 0x1.ffffffff68444p-2, 0x1.810a6810ab5dbp+3, 0x1.ffffffff646c5p-2,
+    0x1.80a3f14557c1cp+3, 0x1.ffffffff607b6p-2, 0x1.803d7a7a0426ap+3, 0x1.ffffffff5c70fp-2,
+    0x1.7fd703aeb08c5p+3, 0x1.ffffffff584c5p-2, 0x1.7f708ce35cf2dp+3, 0x1.ffffffff540cdp-2,
+    0x1.7f0a1618095a3p+3, 0x1.ffffffff4fb1cp-2, 0x1.7ea39f4cb5c27p+3, 0x1.ffffffff4b3a7p-2,
+    0x1.7e3d2881622b9p+3, 0x1.ffffffff46a63p-2, 0x1.7dd6b1b60e95ap+3, 0x1.ffffffff41f44p-2,
+    0x1.7d703aeabb00bp+3, 0x1.ffffffff3d23dp-2, 0x1.7d09c41f676cbp+3, 0x1.ffffffff38343p-2,
+    0x1.7ca34d5413d9bp+3, 0x1.ffffffff33249p-2, 0x1.7c3cd688c047cp+3, 0x1.ffffffff2df42p-2,
+    0x1.7bd65fbd6cb6dp+3, 0x1.ffffffff28a20p-2, 0x1.7b6fe8f219270p+3, 0x1.ffffffff232d6p-2,
+    0x1.7b097226c5984p+3, 0x1.ffffffff1d957p-2, 0x1.7aa2fb5b720abp+3, 0x1.ffffffff17d93p-2,
+    0x1.7a3c84901e7e4p+3, 0x1.ffffffff11f7bp-2, 0x1.79d60dc4caf30p+3, 0x1.ffffffff0bf02p-2,
+    0x1.796f96f977690p+3, 0x1.ffffffff05c17p-2, 0x1.7909202e23e04p+3, 0x1.fffffffeff6abp-2,
+    0x1.78a2a962d058cp+3, 0x1.fffffffef8eacp-2, 0x1.783c32977cd29p+3, 0x1.fffffffef240cp-2,
+    0x1.77d5bbcc294dcp+3, 0x1.fffffffeeb6b8p-2, 0x1.776f4500d5ca5p+3, 0x1.fffffffee469fp-2,
+    0x1.7708ce3582485p+3, 0x1.fffffffedd3afp-2, 0x1.76a2576a2ec7cp+3, 0x1.fffffffed5dd6p-2,
+    0x1.763be09edb48bp+3, 0x1.fffffffece500p-2, 0x1.75d569d387cb3p+3, 0x1.fffffffec691bp-2,
+    0x1.756ef308344f4p+3, 0x1.fffffffebea13p-2, 0x1.75087c3ce0d4ep+3, 0x1.fffffffeb67d3p-2,
+    0x1.74a205718d5c3p+3, 0x1.fffffffeae246p-2, 0x1.743b8ea639e53p+3, 0x1.fffffffea5957p-2,
+    0x1.73d517dae66fep+3, 0x1.fffffffe9ccf0p-2, 0x1.736ea10f92fc6p+3, 0x1.fffffffe93cfbp-2,
+    0x1.73082a443f8abp+3, 0x1.fffffffe8a960p-2, 0x1.72a1b378ec1aep+3, 0x1.fffffffe81207p-2,
+    0x1.723b3cad98ad0p+3, 0x1.fffffffe776dap-2, 0x1.71d4c5e245411p+3, 0x1.fffffffe6d7bep-2,
+    0x1.716e4f16f1d73p+3, 0x1.fffffffe6349bp-2, 0x1.7107d84b9e6f5p+3, 0x1.fffffffe58d55p-2,
+    0x1.70a161804b09ap+3, 0x1.fffffffe4e1d3p-2, 0x1.703aeab4f7a61p+3, 0x1.fffffffe431f8p-2,
+    0x1.6fd473e9a444cp+3, 0x1.fffffffe37da9p-2, 0x1.6f6dfd1e50e5bp+3, 0x1.fffffffe2c4c9p-2,
+    0x1.6f078652fd890p+3, 0x1.fffffffe2073ap-2, 0x1.6ea10f87aa2ebp+3, 0x1.fffffffe144dep-2,
+    0x1.6e3a98bc56d6ep+3, 0x1.fffffffe07d96p-2, 0x1.6dd421f103819p+3, 0x1.fffffffdfb141p-2,
+    0x1.6d6dab25b02edp+3, 0x1.fffffffdedfbfp-2, 0x1.6d07345a5cdecp+3, 0x1.fffffffde08eep-2,
+    0x1.6ca0bd8f09917p+3, 0x1.fffffffdd2cadp-2, 0x1.6c3a46c3b646ep+3, 0x1.fffffffdc4ad7p-2,
+    0x1.6bd3cff862ff3p+3, 0x1.fffffffdb6348p-2, 0x1.6b6d592d0fba6p+3, 0x1.fffffffda75dcp-2,
+    0x1.6b06e261bc78ap+3, 0x1.fffffffd9826dp-2, 0x1.6aa06b966939fp+3, 0x1.fffffffd888d3p-2,
+    0x1.6a39f4cb15fe7p+3, 0x1.fffffffd788e6p-2, 0x1.69d37dffc2c63p+3, 0x1.fffffffd6827dp-2,
+    0x1.696d07346f914p+3, 0x1.fffffffd5756fp-2, 0x1.690690691c5fbp+3, 0x1.fffffffd46190p-2,
+    0x1.68a0199dc931ap+3, 0x1.fffffffd346b5p-2, 0x1.6839a2d276073p+3, 0x1.fffffffd224afp-2,
+    0x1.67d32c0722e06p+3, 0x1.fffffffd0fb50p-2, 0x1.676cb53bcfbd6p+3, 0x1.fffffffcfca69p-2,
+    0x1.67063e707c9e3p+3, 0x1.fffffffce91c8p-2, 0x1.669fc7a529830p+3, 0x1.fffffffcd513cp-2,
+    0x1.663950d9d66bdp+3, 0x1.fffffffcc0892p-2, 0x1.65d2da0e8358ep+3, 0x1.fffffffcab794p-2,
+    0x1.656c6343304a2p+3, 0x1.fffffffc95e0dp-2, 0x1.6505ec77dd3fdp+3, 0x1.fffffffc7fbc5p-2,
+    0x1.649f75ac8a39fp+3, 0x1.fffffffc69084p-2, 0x1.6438fee13738bp+3, 0x1.fffffffc51c0fp-2,
+    0x1.63d28815e43c3p+3, 0x1.fffffffc39e2bp-2, 0x1.636c114a91448p+3, 0x1.fffffffc2169bp-2,
+    0x1.63059a7f3e51cp+3, 0x1.fffffffc0851fp-2, 0x1.629f23b3eb642p+3, 0x1.fffffffbee978p-2,
+    0x1.6238ace8987bbp+3, 0x1.fffffffbd4363p-2, 0x1.61d2361d45989p+3, 0x1.fffffffbb929dp-2,
+    0x1.616bbf51f2bafp+3, 0x1.fffffffb9d6e1p-2, 0x1.610548869fe30p+3, 0x1.fffffffb80fe7p-2,
+    0x1.609ed1bb4d10cp+3, 0x1.fffffffb63d67p-2, 0x1.60385aeffa447p+3, 0x1.fffffffb45f15p-2,
+    0x1.5fd1e424a77e3p+3, 0x1.fffffffb274a6p-2, 0x1.5f6b6d5954be2p+3, 0x1.fffffffb07dcbp-2,
+    0x1.5f04f68e02047p+3, 0x1.fffffffae7a32p-2, 0x1.5e9e7fc2af515p+3, 0x1.fffffffac698ap-2,
+    0x1.5e3808f75ca4dp+3, 0x1.fffffffaa4b7ep-2, 0x1.5dd1922c09ff4p+3, 0x1.fffffffa81fb7p-2,
+    0x1.5d6b1b60b760bp+3, 0x1.fffffffa5e5dbp-2, 0x1.5d04a49564c96p+3, 0x1.fffffffa39d91p-2,
+    0x1.5c9e2dca12397p+3, 0x1.fffffffa14679p-2, 0x1.5c37b6febfb11p+3, 0x1.fffffff9ee034p-2,
+    0x1.5bd140336d308p+3, 0x1.fffffff9c6a60p-2, 0x1.5b6ac9681ab7fp+3, 0x1.fffffff99e498p-2,
+    0x1.5b04529cc8479p+3, 0x1.fffffff974e73p-2, 0x1.5a9ddbd175df8p+3, 0x1.fffffff94a789p-2,
+    0x1.5a37650623802p+3, 0x1.fffffff91ef6dp-2, 0x1.59d0ee3ad1298p+3, 0x1.fffffff8f25aep-2,
+    0x1.596a776f7edbfp+3, 0x1.fffffff8c49dbp-2, 0x1.590400a42c97ap+3, 0x1.fffffff895b7ep-2,
+    0x1.589d89d8da5cdp+3, 0x1.fffffff865a1fp-2, 0x1.5837130d882bdp+3, 0x1.fffffff834543p-2,
+    0x1.57d09c423604cp+3, 0x1.fffffff801c6bp-2, 0x1.576a2576e3e7fp+3, 0x1.fffffff7cdf17p-2,
+    0x1.5703aeab91d5ap+3, 0x1.fffffff798cc0p-2, 0x1.569d37e03fce1p+3, 0x1.fffffff7624dfp-2,
+    0x1.5636c114edd19p+3, 0x1.fffffff72a6e8p-2, 0x1.55d04a499be07p+3, 0x1.fffffff6f124bp-2,
+    0x1.5569d37e49faep+3, 0x1.fffffff6b6677p-2, 0x1.55035cb2f8213p+3, 0x1.fffffff67a2d4p-2,
+    0x1.549ce5e7a653cp+3, 0x1.fffffff63c6c9p-2, 0x1.54366f1c5492dp+3, 0x1.fffffff5fd1b6p-2,
+    0x1.53cff85102debp+3, 0x1.fffffff5bc2f9p-2, 0x1.53698185b137cp+3, 0x1.fffffff5799edp-2,
+    0x1.53030aba5f9e4p+3, 0x1.fffffff5355e6p-2, 0x1.529c93ef0e12ap+3, 0x1.fffffff4ef635p-2,
+    0x1.52361d23bc953p+3, 0x1.fffffff4a7a27p-2, 0x1.51cfa6586b264p+3, 0x1.fffffff45e105p-2,
+    0x1.51692f8d19c64p+3, 0x1.fffffff412a11p-2, 0x1.5102b8c1c8759p+3, 0x1.fffffff3c548ap-2,
+    0x1.509c41f677348p+3, 0x1.fffffff375faap-2, 0x1.5035cb2b26039p+3, 0x1.fffffff324aa6p-2,
+    0x1.4fcf545fd4e31p+3, 0x1.fffffff2d14adp-2, 0x1.4f68dd9483d37p+3, 0x1.fffffff27bceap-2,
+    0x1.4f0266c932d53p+3, 0x1.fffffff224280p-2, 0x1.4e9beffde1e8bp+3, 0x1.fffffff1ca491p-2,
+    0x1.4e357932910e6p+3, 0x1.fffffff16e235p-2, 0x1.4dcf02674046cp+3, 0x1.fffffff10fa80p-2,
+    0x1.4d688b9bef925p+3, 0x1.fffffff0aec80p-2, 0x1.4d0214d09ef17p+3, 0x1.fffffff04b73cp-2,
+    0x1.4c9b9e054e64cp+3, 0x1.ffffffefe59b6p-2, 0x1.4c352739fdecap+3, 0x1.ffffffef7d2eap-2,
+    0x1.4bceb06ead89cp+3, 0x1.ffffffef121cap-2, 0x1.4b6839a35d3c8p+3, 0x1.ffffffeea4546p-2,
+    0x1.4b01c2d80d059p+3, 0x1.ffffffee33c43p-2, 0x1.4a9b4c0cbce56p+3, 0x1.ffffffedc05a0p-2,
+    0x1.4a34d5416cdcap+3, 0x1.ffffffed4a037p-2, 0x1.49ce5e761cebdp+3, 0x1.ffffffecd0ad7p-2,
+    0x1.4967e7aacd13ap+3, 0x1.ffffffec5444ap-2, 0x1.490170df7d54ap+3, 0x1.ffffffebd4b51p-2,
+    0x1.489afa142daf8p+3, 0x1.ffffffeb51ea4p-2, 0x1.48348348de24ep+3, 0x1.ffffffeacbcf5p-2,
+    0x1.47ce0c7d8eb56p+3, 0x1.ffffffea424ebp-2, 0x1.476795b23f61dp+3, 0x1.ffffffe9b5527p-2,
+    0x1.47011ee6f02acp+3, 0x1.ffffffe924c3fp-2, 0x1.469aa81ba1111p+3, 0x1.ffffffe8908c0p-2,
+    0x1.4634315052156p+3, 0x1.ffffffe7f892ep-2, 0x1.45cdba8503387p+3, 0x1.ffffffe75cc04p-2,
+    0x1.456743b9b47b2p+3, 0x1.ffffffe6bcfb3p-2, 0x1.4500ccee65de3p+3, 0x1.ffffffe6192a0p-2,
+    0x1.449a562317627p+3, 0x1.ffffffe571329p-2, 0x1.4433df57c908cp+3, 0x1.ffffffe4c4f9dp-2,
+    0x1.43cd688c7ad1fp+3, 0x1.ffffffe414645p-2, 0x1.4366f1c12cbefp+3, 0x1.ffffffe35f55bp-2,
+    0x1.43007af5ded0ap+3, 0x1.ffffffe2a5b0fp-2, 0x1.429a042a9107ep+3, 0x1.ffffffe1e7586p-2,
+    0x1.42338d5f4365cp+3, 0x1.ffffffe1242d6p-2, 0x1.41cd1693f5eb3p+3, 0x1.ffffffe05c10dp-2,
+    0x1.41669fc8a8992p+3, 0x1.ffffffdf8ee29p-2, 0x1.410028fd5b70bp+3, 0x1.ffffffdebc81cp-2,
+    0x1.4099b2320e72ep+3, 0x1.ffffffdde4cccp-2, 0x1.40333b66c1a0cp+3, 0x1.ffffffdd07a0ep-2,
+    0x1.3fccc49b74fb8p+3, 0x1.ffffffdc24dacp-2, 0x1.3f664dd028842p+3, 0x1.ffffffdb3c561p-2,
+    0x1.3effd704dc3bfp+3, 0x1.ffffffda4ded9p-2, 0x1.3e99603990241p+3, 0x1.ffffffd9597b0p-2,
+    0x1.3e32e96e443dbp+3, 0x1.ffffffd85ed74p-2, 0x1.3dcc72a2f88a2p+3, 0x1.ffffffd75dda3p-2,
+    0x1.3d65fbd7ad0aap+3, 0x1.ffffffd6565aap-2, 0x1.3cff850c61c08p+3, 0x1.ffffffd5482e5p-2,
+    0x1.3c990e4116ad3p+3, 0x1.ffffffd4332a0p-2, 0x1.3c329775cbd20p+3, 0x1.ffffffd317214p-2,
+    0x1.3bcc20aa81305p+3, 0x1.ffffffd1f3e6ap-2, 0x1.3b65a9df36c9bp+3, 0x1.ffffffd0c94b8p-2,
+    0x1.3aff3313ec9f9p+3, 0x1.ffffffcf971ffp-2, 0x1.3a98bc48a2b38p+3, 0x1.ffffffce5d32fp-2,
+    0x1.3a32457d59071p+3, 0x1.ffffffcd1b523p-2, 0x1.39cbceb20f9bdp+3, 0x1.ffffffcbd14a2p-2,
+    0x1.396557e6c6738p+3, 0x1.ffffffca7ee5ep-2, 0x1.38fee11b7d8fcp+3, 0x1.ffffffc923ef4p-2,
+    0x1.38986a5034f24p+3, 0x1.ffffffc7c02ebp-2, 0x1.3831f384ec9cep+3, 0x1.ffffffc6536b2p-2,
+    0x1.37cb7cb9a4917p+3, 0x1.ffffffc4dd6a2p-2, 0x1.376505ee5cd1dp+3, 0x1.ffffffc35defdp-2,
+    0x1.36fe8f23155fep+3, 0x1.ffffffc1d4becp-2, 0x1.36981857ce3d9p+3, 0x1.ffffffc04197ep-2,
+    0x1.3631a18c876d0p+3, 0x1.ffffffbea43abp-2, 0x1.35cb2ac140f04p+3, 0x1.ffffffbcfc64fp-2,
+    0x1.3564b3f5fac95p+3, 0x1.ffffffbb49d2bp-2, 0x1.34fe3d2ab4fa8p+3, 0x1.ffffffb98c3e6p-2,
+    0x1.3497c65f6f85fp+3, 0x1.ffffffb7c3609p-2, 0x1.34314f942a6e0p+3, 0x1.ffffffb5eef01p-2,
+    0x1.33cad8c8e5b4fp+3, 0x1.ffffffb40ea1dp-2, 0x1.336461fda15d4p+3, 0x1.ffffffb22228fp-2,
+    0x1.32fdeb325d695p+3, 0x1.ffffffb029368p-2, 0x1.3297746719dbcp+3, 0x1.ffffffae23799p-2,
+    0x1.3230fd9bd6b72p+3, 0x1.ffffffac109f3p-2, 0x1.31ca86d093fe1p+3, 0x1.ffffffa9f0526p-2,
+    0x1.3164100551b34p+3, 0x1.ffffffa7c23bfp-2, 0x1.30fd993a0fd99p+3, 0x1.ffffffa586026p-2,
+    0x1.3097226ece73ep+3, 0x1.ffffffa33b4a1p-2, 0x1.3030aba38d851p+3, 0x1.ffffffa0e1b51p-2,
+    0x1.2fca34d84d102p+3, 0x1.ffffff9e78e2ep-2, 0x1.2f63be0d0d184p+3, 0x1.ffffff9c0070dp-2,
+    0x1.2efd4741cda08p+3, 0x1.ffffff9977f97p-2, 0x1.2e96d0768eac2p+3, 0x1.ffffff96df14ep-2,
+    0x1.2e3059ab503e9p+3, 0x1.ffffff943558bp-2, 0x1.2dc9e2e0125b2p+3, 0x1.ffffff917a579p-2,
+    0x1.2d636c14d5055p+3, 0x1.ffffff8eada19p-2, 0x1.2cfcf5499840cp+3, 0x1.ffffff8bcec3ep-2,
+    0x1.2c967e7e5c112p+3, 0x1.ffffff88dd48bp-2, 0x1.2c3007b3207a3p+3, 0x1.ffffff85d8b76p-2,
+    0x1.2bc990e7e57fdp+3, 0x1.ffffff82c0943p-2, 0x1.2b631a1cab25fp+3, 0x1.ffffff7f94602p-2,
+    0x1.2afca3517170bp+3, 0x1.ffffff7c53992p-2, 0x1.2a962c8638643p+3, 0x1.ffffff78fdb9bp-2,
+    0x1.2a2fb5bb0004cp+3, 0x1.ffffff7592392p-2, 0x1.29c93eefc856bp+3, 0x1.ffffff72108b2p-2,
+    0x1.2962c824915e9p+3, 0x1.ffffff6e781fep-2, 0x1.28fc51595b210p+3, 0x1.ffffff6ac863fp-2,
+    0x1.2895da8e25a2ap+3, 0x1.ffffff6700c01p-2, 0x1.282f63c2f0e86p+3, 0x1.ffffff6320995p-2,
+    0x1.27c8ecf7bcf73p+3, 0x1.ffffff5f2750ap-2, 0x1.2762762c89d42p+3, 0x1.ffffff5b14432p-2,
+    0x1.26fbff6157847p+3, 0x1.ffffff56e6c9ap-2, 0x1.26958896260d8p+3, 0x1.ffffff529e38dp-2,
+    0x1.262f11caf574cp+3, 0x1.ffffff4e39e11p-2, 0x1.25c89affc5bfep+3, 0x1.ffffff49b90e3p-2,
+    0x1.2562243496f49p+3, 0x1.ffffff451b078p-2, 0x1.24fbad696918ep+3, 0x1.ffffff405f0fbp-2,
+    0x1.2495369e3c32cp+3, 0x1.ffffff3b84647p-2, 0x1.242ebfd310487p+3, 0x1.ffffff368a3eep-2,
+    0x1.23c84907e5605p+3, 0x1.ffffff316fd2bp-2, 0x1.2361d23cbb810p+3, 0x1.ffffff2c344eap-2,
+    0x1.22fb5b7192b11p+3, 0x1.ffffff26d6dc2p-2, 0x1.2294e4a66af78p+3, 0x1.ffffff21569f3p-2,
+    0x1.222e6ddb445b5p+3, 0x1.ffffff1bb2b61p-2, 0x1.21c7f7101ee3cp+3, 0x1.ffffff15ea399p-2,
+    0x1.21618044fa982p+3, 0x1.ffffff0ffc3c7p-2, 0x1.20fb0979d7803p+3, 0x1.ffffff09e7cb7p-2,
+    0x1.209492aeb5a3bp+3, 0x1.ffffff03abed5p-2, 0x1.202e1be3950a9p+3, 0x1.fffffefd47a25p-2,
+    0x1.1fc7a51875bd0p+3, 0x1.fffffef6b9e46p-2, 0x1.1f612e4d57c37p+3, 0x1.fffffef001a6ap-2,
+    0x1.1efab7823b268p+3, 0x1.fffffee91dd58p-2, 0x1.1e9440b71fef0p+3, 0x1.fffffee20d567p-2,
+    0x1.1e2dc9ec06260p+3, 0x1.fffffedacf07bp-2, 0x1.1dc75320edd4cp+3, 0x1.fffffed361c02p-2,
+    0x1.1d60dc55d704dp+3, 0x1.fffffecbc44f4p-2, 0x1.1cfa658ac1bfep+3, 0x1.fffffec3f57cap-2,
+    0x1.1c93eebfae101p+3, 0x1.fffffebbf4082p-2, 0x1.1c2d77f49bff9p+3, 0x1.fffffeb3bea96p-2,
+    0x1.1bc701298b98ep+3, 0x1.fffffeab540fcp-2, 0x1.1b608a5e7ce6dp+3, 0x1.fffffea2b2e1fp-2,
+    0x1.1afa13936ff48p+3, 0x1.fffffe99d9be3p-2, 0x1.1a939cc864cd2p+3, 0x1.fffffe90c7398p-2,
+    0x1.1a2d25fd5b7c7p+3, 0x1.fffffe8779dfcp-2, 0x1.19c6af32540e6p+3, 0x1.fffffe7df0338p-2,
+    0x1.196038674e8f1p+3, 0x1.fffffe7428ad9p-2, 0x1.18f9c19c4b0b2p+3, 0x1.fffffe6a21bcep-2,
+    0x1.18934ad1498f6p+3, 0x1.fffffe5fd9c62p-2, 0x1.182cd4064a28fp+3, 0x1.fffffe554f23bp-2,
+    0x1.17c65d3b4ce57p+3, 0x1.fffffe4a80253p-2, 0x1.175fe67051d2ap+3, 0x1.fffffe3f6b0f6p-2,
+    0x1.16f96fa558fecp+3, 0x1.fffffe340e1bcp-2, 0x1.1692f8da62787p+3, 0x1.fffffe2867783p-2,
+    0x1.162c820f6e4e8p+3, 0x1.fffffe1c7546ep-2, 0x1.15c60b447c904p+3, 0x1.fffffe10359dep-2,
+    0x1.155f94798d4d8p+3, 0x1.fffffe03a686ep-2, 0x1.14f91daea0965p+3, 0x1.fffffdf6c5febp-2,
+    0x1.1492a6e3b67b2p+3, 0x1.fffffde991f54p-2, 0x1.142c3018cf0cep+3, 0x1.fffffddc084d1p-2,
+    0x1.13c5b94dea5d0p+3, 0x1.fffffdce26dadp-2, 0x1.135f4283087d3p+3, 0x1.fffffdbfeb655p-2,
+    0x1.12f8cbb8297fcp+3, 0x1.fffffdb153a4dp-2, 0x1.129254ed4d775p+3, 0x1.fffffda25d42cp-2,
+    0x1.122bde2274772p+3, 0x1.fffffd9305d99p-2, 0x1.11c567579e92dp+3, 0x1.fffffd834af40p-2,
+    0x1.115ef08ccbde9p+3, 0x1.fffffd732a0cep-2, 0x1.10f879c1fc6f1p+3, 0x1.fffffd62a08edp-2,
+    0x1.109202f730597p+3, 0x1.fffffd51abd38p-2, 0x1.102b8c2c67b37p+3, 0x1.fffffd4049238p-2,
+    0x1.0fc51561a2936p+3, 0x1.fffffd2e75b5cp-2, 0x1.0f5e9e96e1102p+3, 0x1.fffffd1c2eaf4p-2,
+    0x1.0ef827cc23411p+3, 0x1.fffffd0971226p-2, 0x1.0e91b101693e3p+3, 0x1.fffffcf63a0e6p-2,
+    0x1.0e2b3a36b3203p+3, 0x1.fffffce2865f5p-2, 0x1.0dc4c36c01005p+3, 0x1.fffffcce52ed2p-2,
+    0x1.0d5e4ca152f86p+3, 0x1.fffffcb99c7b4p-2, 0x1.0cf7d5d6a9230p+3, 0x1.fffffca45fb83p-2,
+    0x1.0c915f0c039b6p+3, 0x1.fffffc8e993d0p-2, 0x1.0c2ae841627d6p+3, 0x1.fffffc78458c8p-2,
+    0x1.0bc47176c5e5cp+3, 0x1.fffffc6161132p-2, 0x1.0b5dfaac2df1bp+3, 0x1.fffffc49e825dp-2,
+    0x1.0af783e19abf5p+3, 0x1.fffffc31d7021p-2, 0x1.0a910d170c6d8p+3, 0x1.fffffc1929ccap-2,
+    0x1.0a2a964c831bep+3, 0x1.fffffbffdc919p-2, 0x1.09c41f81feeaep+3, 0x1.fffffbe5eb432p-2,
+    0x1.095da8b77ffbbp+3, 0x1.fffffbcb51b95p-2, 0x1.08f731ed06707p+3, 0x1.fffffbb00bb13p-2,
+    0x1.0890bb22926c2p+3, 0x1.fffffb9414cc3p-2, 0x1.082a445824129p+3, 0x1.fffffb77688f5p-2,
+    0x1.07c3cd8dbb888p+3, 0x1.fffffb5a0262bp-2, 0x1.075d56c358f39p+3, 0x1.fffffb3bdd909p-2,
+    0x1.06f6dff8fc7a8p+3, 0x1.fffffb1cf5449p-2, 0x1.0690692ea644dp+3, 0x1.fffffafd448b2p-2,
+    0x1.0629f264567b3p+3, 0x1.fffffadcc6508p-2, 0x1.05c37b9a0d474p+3, 0x1.fffffabb75600p-2,
+    0x1.055d04cfcad3ap+3, 0x1.fffffa994c635p-2, 0x1.04f68e058f4c4p+3, 0x1.fffffa7645e15p-2,
+    0x1.0490173b5addep+3, 0x1.fffffa525c3d9p-2, 0x1.0429a0712db6ap+3, 0x1.fffffa2d89b73p-2,
+    0x1.03c329a70805ap+3, 0x1.fffffa07c867ep-2, 0x1.035cb2dce9fb5p+3, 0x1.fffff9e112434p-2,
+    0x1.02f63c12d3c94p+3, 0x1.fffff9b961159p-2, 0x1.028fc548c5a26p+3, 0x1.fffff990ae82fp-2,
+    0x1.02294e7ebfbadp+3, 0x1.fffff966f4064p-2, 0x1.01c2d7b4c2480p+3, 0x1.fffff93c2af01p-2,
+    0x1.015c60eacd80ep+3, 0x1.fffff9104c659p-2, 0x1.00f5ea20e19dap+3, 0x1.fffff8e3515f9p-2,
+    0x1.008f7356fed7dp+3, 0x1.fffff8b532a94p-2, 0x1.0028fc8d256abp+3, 0x1.fffff885e8df1p-2,
+    0x1.ff850b86ab258p+2, 0x1.fffff8556c6dap-2, 0x1.feb81df31f1c7p+2, 0x1.fffff823b5904p-2,
+    0x1.fdeb305fa7398p+2, 0x1.fffff7f0bc501p-2, 0x1.fd1e42cc43ff7p+2, 0x1.fffff7bc78827p-2,
+    0x1.fc515538f5f43p+2, 0x1.fffff786e1c7ep-2, 0x1.fb8467a5bda11p+2, 0x1.fffff74fef8a6p-2,
+    0x1.fab77a129b930p+2, 0x1.fffff71798fc9p-2, 0x1.f9ea8c7f905a6p+2, 0x1.fffff6ddd517cp-2,
+    0x1.f91d9eec9c8b4p+2, 0x1.fffff6a29a9adp-2, 0x1.f850b159c0bd8p+2, 0x1.fffff665e008ap-2,
+    0x1.f783c3c6fd8cbp+2, 0x1.fffff6279ba66p-2, 0x1.f6b6d63453989p+2, 0x1.fffff5e7c37a7p-2,
+    0x1.f5e9e8a1c384ap+2, 0x1.fffff5a64d4a3p-2, 0x1.f51cfb0f4df8dp+2, 0x1.fffff5632e98fp-2,
+    0x1.f4500d7cf3a12p+2, 0x1.fffff51e5ca5dp-2, 0x1.f3831feab52dfp+2, 0x1.fffff4d7cc6a5p-2,
+    0x1.f2b6325893542p+2, 0x1.fffff48f72986p-2, 0x1.f1e944c68ecd3p+2, 0x1.fffff4454398ap-2,
+    0x1.f11c5734a8575p+2, 0x1.fffff3f933889p-2, 0x1.f04f69a2e0b57p+2, 0x1.fffff3ab3638ap-2,
+    0x1.ef827c1138af7p+2, 0x1.fffff35b3f2a3p-2, 0x1.eeb58e7fb1125p+2, 0x1.fffff309418dap-2,
+    0x1.ede8a0ee4ab04p+2, 0x1.fffff2b530403p-2, 0x1.ed1bb35d0660cp+2, 0x1.fffff25efdca0p-2,
+    0x1.ec4ec5cbe500dp+2, 0x1.fffff2069c5bep-2, 0x1.eb81d83ae772dp+2, 0x1.fffff1abfdccfp-2,
+    0x1.eab4eaaa0e9f4p+2, 0x1.fffff14f1398bp-2, 0x1.e9e7fd195b742p+2, 0x1.fffff0efcedc5p-2,
+    0x1.e91b0f88cee5cp+2, 0x1.fffff08e20549p-2, 0x1.e84e21f869ee8p+2, 0x1.fffff029f85b3p-2,
+    0x1.e78134682d8f1p+2, 0x1.ffffefc346e46p-2, 0x1.e6b446d81acebp+2, 0x1.ffffef59fb7c7p-2,
+    0x1.e5e7594832bb5p+2, 0x1.ffffeeee0544ep-2, 0x1.e51a6bb87669bp+2, 0x1.ffffee7f52f1cp-2,
+    0x1.e44d7e28e6f58p+2, 0x1.ffffee0dd2c72p-2, 0x1.e38090998581cp+2, 0x1.ffffed997295ep-2,
+    0x1.e2b3a30a5338cp+2, 0x1.ffffed221fb91p-2, 0x1.e1e6b57b514c5p+2, 0x1.ffffeca7c712dp-2,
+    0x1.e119c7ec80f62p+2, 0x1.ffffec2a55096p-2, 0x1.e04cda5de377bp+2, 0x1.ffffeba9b583dp-2,
+    0x1.df7feccf7a1abp+2, 0x1.ffffeb25d3e6cp-2, 0x1.deb2ff4146314p+2, 0x1.ffffea9e9b116p-2,
+    0x1.dde611b34915fp+2, 0x1.ffffea13f559dp-2, 0x1.dd192425842c3p+2, 0x1.ffffe985cc89ap-2,
+    0x1.dc4c3697f8e07p+2, 0x1.ffffe8f409da6p-2, 0x1.db7f490aa8a83p+2, 0x1.ffffe85e95f20p-2,
+    0x1.dab25b7d9502ap+2, 0x1.ffffe7c558deep-2, 0x1.d9e56df0bf78ap+2, 0x1.ffffe7283a145p-2,
+    0x1.d9188064299ccp+2, 0x1.ffffe68720662p-2, 0x1.d84b92d7d50c2p+2, 0x1.ffffe5e1f2053p-2,
+    0x1.d77ea54bc36e2p+2, 0x1.ffffe538947adp-2, 0x1.d6b1b7bff674dp+2, 0x1.ffffe48aeca4cp-2,
+    0x1.d5e4ca346fdd7p+2, 0x1.ffffe3d8deb0ep-2, 0x1.d517dca931705p+2, 0x1.ffffe3224e189p-2,
+    0x1.d44aef1e3d017p+2, 0x1.ffffe2671d9c4p-2, 0x1.d37e01939470bp+2, 0x1.ffffe1a72f3eap-2,
+    0x1.d2b1140939aa0p+2, 0x1.ffffe0e264400p-2, 0x1.d1e4267f2ea5ep+2, 0x1.ffffe0189d194p-2,
+    0x1.d11738f575698p+2, 0x1.ffffdf49b976dp-2, 0x1.d04a4b6c10073p+2, 0x1.ffffde7598337p-2,
+    0x1.cf7d5de3009ebp+2, 0x1.ffffdd9c17531p-2, 0x1.ceb0705a495d9p+2, 0x1.ffffdcbd13fd2p-2,
+    0x1.cde382d1ec7f8p+2, 0x1.ffffdbd86a772p-2, 0x1.cd169549ec4e9p+2, 0x1.ffffdaedf61eep-2,
+    0x1.cc49a7c24b23dp+2, 0x1.ffffd9fd9164bp-2, 0x1.cb7cba3b0b677p+2, 0x1.ffffd90715c52p-2,
+    0x1.caafccb42f913p+2, 0x1.ffffd80a5bc34p-2, 0x1.c9e2df2dba28fp+2, 0x1.ffffd7073ae1ep-2,
+    0x1.c915f1a7adc6fp+2, 0x1.ffffd5fd899d5p-2, 0x1.c84904220d144p+2, 0x1.ffffd4ed1d64bp-2,
+    0x1.c77c169cdacb2p+2, 0x1.ffffd3d5ca930p-2, 0x1.c6af291819b7ap+2, 0x1.ffffd2b764685p-2,
+    0x1.c5e23b93ccb7ep+2, 0x1.ffffd191bd027p-2, 0x1.c5154e0ff6bc9p+2, 0x1.ffffd064a555dp-2,
+    0x1.c448608c9ac99p+2, 0x1.ffffcf2fed258p-2, 0x1.c37b7309bbf62p+2, 0x1.ffffcdf362fc1p-2,
+    0x1.c2ae85875d6dcp+2, 0x1.ffffccaed4232p-2, 0x1.c1e1980582705p+2, 0x1.ffffcb620c9b8p-2,
+    0x1.c114aa842e52ep+2, 0x1.ffffca0cd714fp-2, 0x1.c047bd0364801p+2, 0x1.ffffc8aefce54p-2,
+    0x1.bf7acf832878bp+2, 0x1.ffffc74845fffp-2, 0x1.beade2037dd43p+2, 0x1.ffffc5d878ed0p-2,
+    0x1.bde0f48468417p+2, 0x1.ffffc45f5abfbp-2, 0x1.bd140705eb871p+2, 0x1.ffffc2dcaf0d4p-2,
+    0x1.bc4719880b844p+2, 0x1.ffffc15037e31p-2, 0x1.bb7a2c0acc314p+2, 0x1.ffffbfb9b5bcep-2,
+    0x1.baad3e8e31a02p+2, 0x1.ffffbe18e77a7p-2, 0x1.b9e051123ffd3p+2, 0x1.ffffbc6d8a555p-2,
+    0x1.b9136396fb901p+2, 0x1.ffffbab759d5ep-2, 0x1.b846761c68bbdp+2, 0x1.ffffb8f60fc8ap-2,
+    0x1.b77988a28c004p+2, 0x1.ffffb7296432ep-2, 0x1.b6ac9b2969fa3p+2, 0x1.ffffb5510d470p-2,
+    0x1.b5dfadb107646p+2, 0x1.ffffb36cbf58fp-2, 0x1.b512c03969183p+2, 0x1.ffffb17c2cd1ep-2,
+    0x1.b445d2c2940e9p+2, 0x1.ffffaf7f0623cp-2, 0x1.b378e54c8d60bp+2, 0x1.ffffad74f9bcdp-2,
+    0x1.b2abf7d75a48ap+2, 0x1.ffffab5db3fa3p-2, 0x1.b1df0a6300228p+2, 0x1.ffffa938df1acp-2,
+    0x1.b1121cef846d2p+2, 0x1.ffffa70623312p-2, 0x1.b0452f7ceccb1p+2, 0x1.ffffa4c52615fp-2,
+    0x1.af78420b3f034p+2, 0x1.ffffa2758b592p-2, 0x1.aeab549a81023p+2, 0x1.ffffa016f4333p-2,
+    0x1.adde672ab8dacp+2, 0x1.ffff9da8ff760p-2, 0x1.ad1179bbecc73p+2, 0x1.ffff9b2b497d4p-2,
+    0x1.ac448c4e232a4p+2, 0x1.ffff989d6c1e7p-2, 0x1.ab779ee1628ffp+2, 0x1.ffff95fefe98bp-2,
+    0x1.aaaab175b1aedp+2, 0x1.ffff934f9583cp-2, 0x1.a9ddc40b1768ep+2, 0x1.ffff908ec2bedp-2,
+    0x1.a910d6a19accep+2, 0x1.ffff8dbc155efp-2, 0x1.a843e93943175p+2, 0x1.ffff8ad7199d1p-2,
+    0x1.a776fbd217b37p+2, 0x1.ffff87df58c34p-2, 0x1.a6aa0e6c203cep+2, 0x1.ffff84d45919bp-2,
+    0x1.a5dd210764806p+2, 0x1.ffff81b59dd37p-2, 0x1.a51033a3ec7d7p+2, 0x1.ffff7e82a6fa3p-2,
+    0x1.a4434641c0673p+2, 0x1.ffff7b3af159cp-2, 0x1.a37658e0e8a64p+2, 0x1.ffff77ddf66b4p-2,
+    0x1.a2a96b816dd97p+2, 0x1.ffff746b2c3f6p-2, 0x1.a1dc7e2358d7cp+2, 0x1.ffff70e205686p-2,
+    0x1.a10f90c6b2b15p+2, 0x1.ffff6d41f0e37p-2, 0x1.a042a36b84b12p+2, 0x1.ffff698a5a014p-2,
+    0x1.9f75b611d85e6p+2, 0x1.ffff65baa84e8p-2, 0x1.9ea8c8b9b77e3p+2, 0x1.ffff61d23f7b4p-2,
+    0x1.9ddbdb632c14ep+2, 0x1.ffff5dd07f41cp-2, 0x1.9d0eee0e4067cp+2, 0x1.ffff59b4c34d3p-2,
+    0x1.9c4200bafefecp+2, 0x1.ffff557e631f0p-2, 0x1.9b75136972a62p+2, 0x1.ffff512cb1f40p-2,
+    0x1.9aa82619a6702p+2, 0x1.ffff4cbefea8cp-2, 0x1.99db38cba5b6dp+2, 0x1.ffff4834939d1p-2,
+    0x1.990e4b7f7c1dcp+2, 0x1.ffff438cb6970p-2, 0x1.98415e3535942p+2, 0x1.ffff3ec6a8a50p-2,
+    0x1.977470ecde568p+2, 0x1.ffff39e1a5ff6p-2, 0x1.96a783a682f0bp+2, 0x1.ffff34dce5e8dp-2,
+    0x1.95da9662303ffp+2, 0x1.ffff2fb79a8e5p-2, 0x1.950da91ff374ep+2, 0x1.ffff2a70f0e62p-2,
+    0x1.9440bbdfda15bp+2, 0x1.ffff2508108e1p-2, 0x1.9373cea1f2005p+2, 0x1.ffff1f7c1ba8cp-2,
+    0x1.92a6e166496c8p+2, 0x1.ffff19cc2eba2p-2, 0x1.91d9f42ceeee3p+2, 0x1.ffff13f76082fp-2,
+    0x1.910d06f5f1781p+2, 0x1.ffff0dfcc1db8p-2, 0x1.904019c1605d7p+2, 0x1.ffff07db5d8d3p-2,
+    0x1.8f732c8f4b555p+2, 0x1.ffff0192382b6p-2, 0x1.8ea63f5fc27c5p+2, 0x1.fffefb204feb1p-2,
+    0x1.8dd95232d657cp+2, 0x1.fffef4849c797p-2, 0x1.8d0c650897d7fp+2, 0x1.fffeedbe0ed1dp-2,
+    0x1.8c3f77e1185b2p+2, 0x1.fffee6cb91120p-2, 0x1.8b728abc69b02p+2, 0x1.fffedfac064dep-2,
+    0x1.8aa59d9a9e194p+2, 0x1.fffed85e4a61ap-2, 0x1.89d8b07bc84f4p+2, 0x1.fffed0e131c34p-2,
+    0x1.890bc35ffb843p+2, 0x1.fffec93389522p-2, 0x1.883ed6474b66bp+2, 0x1.fffec15416264p-2,
+    0x1.8771e931cc24fp+2, 0x1.fffeb941955d8p-2, 0x1.86a4fc1f92702p+2, 0x1.fffeb0fabbe81p-2,
+    0x1.85d80f10b37f8p+2, 0x1.fffea87e36534p-2, 0x1.850b22054513dp+2, 0x1.fffe9fcaa8936p-2,
+    0x1.843e34fd5d7b1p+2, 0x1.fffe96deadcbbp-2, 0x1.837147f91393cp+2, 0x1.fffe8db8d8158p-2,
+    0x1.82a45af87ed0cp+2, 0x1.fffe8457b0454p-2, 0x1.81d76dfbb73d0p+2, 0x1.fffe7ab9b5aeep-2,
+    0x1.810a8102d57f4p+2, 0x1.fffe70dd5de7bp-2, 0x1.803d940df2de2p+2, 0x1.fffe66c114878p-2,
+    0x1.7f70a71d29445p+2, 0x1.fffe5c633ae7bp-2, 0x1.7ea3ba3093445p+2, 0x1.fffe51c227e10p-2,
+    0x1.7dd6cd484c1d3p+2, 0x1.fffe46dc27872p-2, 0x1.7d09e0646fbe8p+2, 0x1.fffe3baf7ae33p-2,
+    0x1.7c3cf3851acd0p+2, 0x1.fffe303a57abdp-2, 0x1.7b7006aa6aa74p+2, 0x1.fffe247ae7fc3p-2,
+    0x1.7aa319d47d6a2p+2, 0x1.fffe186f4a083p-2, 0x1.79d62d0371f60p+2, 0x1.fffe0c158fcfdp-2,
+    0x1.7909403767f34p+2, 0x1.fffdff6bbecf9p-2, 0x1.783c53707fd79p+2, 0x1.fffdf26fcfaf9p-2,
+    0x1.776f66aedaeb5p+2, 0x1.fffde51fadf07p-2, 0x1.76a279f29b4e6p+2, 0x1.fffdd7793795bp-2,
+    0x1.75d58d3be3fe4p+2, 0x1.fffdc97a3ccebp-2, 0x1.7508a08ad8db1p+2, 0x1.fffdbb207f9cap-2,
+    0x1.743bb3df9eadbp+2, 0x1.fffdac69b376cp-2, 0x1.736ec73a5b2dap+2, 0x1.fffd9d537cec1p-2,
+    0x1.72a1da9b3506bp+2, 0x1.fffd8ddb7142ap-2, 0x1.71d4ee0253dfcp+2, 0x1.fffd7dff1614ap-2,
+    0x1.7108016fe060ap+2, 0x1.fffd6dbbe0ea8p-2, 0x1.703b14e40438dp+2, 0x1.fffd5d0f36d2fp-2,
+    0x1.6f6e285eea263p+2, 0x1.fffd4bf66bf7fp-2, 0x1.6ea13be0bdfb9p+2, 0x1.fffd3a6ec3318p-2,
+    0x1.6dd44f69aca83p+2, 0x1.fffd28756d94fp-2, 0x1.6d0762f9e43e9p+2, 0x1.fffd16078a023p-2,
+    0x1.6c3a769193fbfp+2, 0x1.fffd032224ad4p-2, 0x1.6b6d8a30ec4ffp+2, 0x1.fffcefc236a5bp-2,
+    0x1.6aa09dd81ee44p+2, 0x1.fffcdbe4a55a0p-2, 0x1.69d3b1875ea49p+2, 0x1.fffcc7864218ap-2,
+    0x1.6906c53edfc6cp+2, 0x1.fffcb2a3c98d8p-2, 0x1.6839d8fed7d35p+2, 0x1.fffc9d39e33c1p-2,
+    0x1.676cecc77dadep+2, 0x1.fffc874520f64p-2, 0x1.66a00099099dep+2, 0x1.fffc70c1fe4fep-2,
+    0x1.65d31473b557ep+2, 0x1.fffc59ace00e3p-2, 0x1.65062857bc066p+2, 0x1.fffc420213944p-2,
+    0x1.64393c455a53ep+2, 0x1.fffc29bdce4b4p-2, 0x1.636c503cce73ep+2, 0x1.fffc10dc2d071p-2,
+    0x1.629f643e582d8p+2, 0x1.fffbf7593366cp-2, 0x1.61d2784a38e55p+2, 0x1.fffbdd30cb316p-2,
+    0x1.61058c60b3a7ep+2, 0x1.fffbc25ec3ae4p-2, 0x1.6038a0820d34ap+2, 0x1.fffba6ded0f96p-2,
+    0x1.5f6bb4ae8c08bp+2, 0x1.fffb8aac8b52ep-2, 0x1.5e9ec8e6786a6p+2, 0x1.fffb6dc36e6aep-2,
+    0x1.5dd1dd2a1c748p+2, 0x1.fffb501ed8a81p-2, 0x1.5d04f179c4227p+2, 0x1.fffb31ba0a69ep-2,
+    0x1.5c3805d5bd5c7p+2, 0x1.fffb12902545bp-2, 0x1.5b6b1a3e5803ap+2, 0x1.fffaf29c2b3f8p-2,
+    0x1.5a9e2eb3e5ff5p+2, 0x1.fffad1d8fdfd2p-2, 0x1.59d14336bb49dp+2, 0x1.fffab0415df45p-2,
+    0x1.590457c72dfe0p+2, 0x1.fffa8dcfe993bp-2, 0x1.58376c659664fp+2, 0x1.fffa6a7f1c661p-2,
+    0x1.576a81124f047p+2, 0x1.fffa46494e306p-2, 0x1.569d95cdb4acfp+2, 0x1.fffa2128b209bp-2,
+    0x1.55d0aa9826890p+2, 0x1.fff9fb17556d9p-2, 0x1.5503bf72062c1p+2, 0x1.fff9d40f1f482p-2,
+    0x1.5436d45bb7a26p+2, 0x1.fff9ac09cefc0p-2, 0x1.5369e955a180ep+2, 0x1.fff98300fb626p-2,
+    0x1.529cfe602cf5ap+2, 0x1.fff958ee11c40p-2, 0x1.51d0137bc5d8cp+2, 0x1.fff92dca54cb9p-2,
+    0x1.510328a8dabd9p+2, 0x1.fff9018edb71fp-2, 0x1.50363de7dd047p+2, 0x1.fff8d4348fe28p-2,
+    0x1.4f69533940ecep+2, 0x1.fff8a5b42e58fp-2, 0x1.4e9c689d7da82p+2, 0x1.fff8760643f77p-2,
+    0x1.4dcf7e150d6c4p+2, 0x1.fff845232d956p-2, 0x1.4d0293a06d87cp+2, 0x1.fff8130316866p-2,
+    0x1.4c35a9401e75bp+2, 0x1.fff7df9df7594p-2, 0x1.4b68bef4a3f21p+2, 0x1.fff7aaeb948efp-2,
+    0x1.4a9bd4be850f3p+2, 0x1.fff774e37d497p-2, 0x1.49ceea9e4c4b0p+2, 0x1.fff73d7d09f14p-2,
+    0x1.4902009487a58p+2, 0x1.fff704af5ad36p-2, 0x1.483516a1c8b78p+2, 0x1.fff6ca7156b53p-2,
+    0x1.47682cc6a4c9ap+2, 0x1.fff68eb9a95fbp-2, 0x1.469b4303b4ecap+2, 0x1.fff6517ec2217p-2,
+    0x1.45ce595996118p+2, 0x1.fff612b6d2463p-2, 0x1.45016fc8e9232p+2, 0x1.fff5d257cb856p-2,
+    0x1.44348652531f7p+2, 0x1.fff590575e65dp-2, 0x1.43679cf67d324p+2, 0x1.fff54caaf8975p-2,
+    0x1.429ab3b614d06p+2, 0x1.fff50747c341bp-2, 0x1.41cdca91cbd2fp+2, 0x1.fff4c022a1483p-2,
+    0x1.4100e18a58948p+2, 0x1.fff477302d82ap-2, 0x1.4033f8a0760ddp+2, 0x1.fff42c64b8ea2p-2,
+    0x1.3f670fd4e3f3dp+2, 0x1.fff3dfb448bacp-2, 0x1.3e9a272866d68p+2, 0x1.fff3911294887p-2,
+    0x1.3dcd3e9bc8403p+2, 0x1.fff340730447fp-2, 0x1.3d00562fd6d60p+2, 0x1.fff2edc8ae4adp-2,
+    0x1.3c336de56678dp+2, 0x1.fff29906552e9p-2, 0x1.3b6685bd50671p+2, 0x1.fff2421e65be0p-2,
+    0x1.3a999db8735fep+2, 0x1.fff1e902f4c59p-2, 0x1.39ccb5d7b3c67p+2, 0x1.fff18da5bcd8bp-2,
+    0x1.38ffce1bfbc6ap+2, 0x1.fff12ff81c09cp-2, 0x1.3832e6863b7aap+2, 0x1.fff0cfeb11924p-2,
+    0x1.3765ff1769113p+2, 0x1.fff06d6f3b6ccp-2, 0x1.369917d080f51p+2, 0x1.fff00874d3de6p-2,
+    0x1.35cc30b285f5bp+2, 0x1.ffefa0ebaef15p-2, 0x1.34ff49be81704p+2, 0x1.ffef36c337de3p-2,
+    0x1.343262f5837a6p+2, 0x1.ffeec9ea6e651p-2, 0x1.33657c58a30d9p+2, 0x1.ffee5a4fe4157p-2,
+    0x1.329895e8fe341p+2, 0x1.ffede7e1b9843p-2, 0x1.31cbafa7ba367p+2, 0x1.ffed728d9b6fcp-2,
+    0x1.30fec99603ca8p+2, 0x1.ffecfa40bfd21p-2, 0x1.3031e3b50f43dp+2, 0x1.ffec7ee7e2dedp-2,
+    0x1.2f64fe0618c47p+2, 0x1.ffec006f43ef0p-2, 0x1.2e98188a64703p+2, 0x1.ffeb7ec2a2582p-2,
+    0x1.2dcb33433e9ffp+2, 0x1.ffeaf9cd3a2f2p-2, 0x1.2cfe4e31fc175p+2, 0x1.ffea7179c0f62p-2,
+    0x1.2c316957fa3acp+2, 0x1.ffe9e5b262353p-2, 0x1.2b6484b69f47ep+2, 0x1.ffe95660bbfc7p-2,
+    0x1.2a97a04f5a8e8p+2, 0x1.ffe8c36ddb502p-2, 0x1.29cabc23a4abbp+2, 0x1.ffe82cc2387d2p-2,
+    0x1.28fdd834ffc5ap+2, 0x1.ffe79245b3563p-2, 0x1.2830f484f7c9fp+2, 0x1.ffe6f3df8f586p-2,
+    0x1.2764111522ac9p+2, 0x1.ffe651766fb6dp-2, 0x1.26972de720a92p+2, 0x1.ffe5aaf0534d0p-2,
+    0x1.25ca4afc9c853p+2, 0x1.ffe5003290768p-2, 0x1.24fd68574bd4dp+2, 0x1.ffe45121d0cc3p-2,
+    0x1.243085f8ef408p+2, 0x1.ffe39da20cc5fp-2, 0x1.2363a3e352ccdp+2, 0x1.ffe2e596873f7p-2,
+    0x1.2296c2184e244p+2, 0x1.ffe228e1c8e10p-2, 0x1.21c9e099c4e28p+2, 0x1.ffe167659b6a3p-2,
+    0x1.20fcff69a6e1fp+2, 0x1.ffe0a10304ddcp-2, 0x1.20301e89f08afp+2, 0x1.ffdfd59a428f0p-2,
+    0x1.1f633dfcab252p+2, 0x1.ffdf050ac40ebp-2, 0x1.1e965dc3ed2adp+2, 0x1.ffde2f3325f79p-2,
+    0x1.1dc97de1da9eap+2, 0x1.ffdd53f12c98ep-2, 0x1.1cfc9e58a562fp+2, 0x1.ffdc7321be7ecp-2,
+    0x1.1c2fbf2a8d93fp+2, 0x1.ffdb8ca0ded73p-2, 0x1.1b62e059e1e3bp+2, 0x1.ffdaa049a7b2bp-2,
+    0x1.1a9601e8fff89p+2, 0x1.ffd9adf644202p-2, 0x1.19c923da54ce4p+2, 0x1.ffd8b57fea222p-2,
+    0x1.18fc46305d18fp+2, 0x1.ffd7b6bed47e2p-2, 0x1.182f68eda5ab4p+2, 0x1.ffd6b18a3c629p-2,
+    0x1.17628c14cbde7p+2, 0x1.ffd5a5b852e4ep-2, 0x1.1695afa87dfddp+2, 0x1.ffd4931e3a552p-2,
+    0x1.15c8d3ab7bb3fp+2, 0x1.ffd3798fff66cp-2, 0x1.14fbf820967bap+2, 0x1.ffd258e0922d0p-2,
+    0x1.142f1d0ab2132p+2, 0x1.ffd130e1beea1p-2, 0x1.1362426cc4f23p+2, 0x1.ffd0016426b08p-2,
+    0x1.12956849d8c3ap+2, 0x1.ffceca3737d3fp-2, 0x1.11c88ea50ae19p+2, 0x1.ffcd8b29262a6p-2,
+    0x1.10fbb5818cd4bp+2, 0x1.ffcc4406e31a7p-2, 0x1.102edce2a4d73p+2, 0x1.ffcaf49c15773p-2,
+    0x1.0f6204cbae5a9p+2, 0x1.ffc99cb311272p-2, 0x1.0e952d401a912p+2, 0x1.ffc83c14ce957p-2,
+    0x1.0dc8564370fa9p+2, 0x1.ffc6d288e1ec1p-2, 0x1.0cfb7fd94ff4cp+2, 0x1.ffc55fd57215ap-2,
+    0x1.0c2eaa056d4f5p+2, 0x1.ffc3e3bf2f84dp-2, 0x1.0b61d4cb96e3bp+2, 0x1.ffc25e094ac10p-2,
+    0x1.0a95002fb330cp+2, 0x1.ffc0ce756ab59p-2, 0x1.09c82c35c1fa0p+2, 0x1.ffbf34c3a2c35p-2,
+    0x1.08fb58e1dceb8p+2, 0x1.ffbd90b268916p-2, 0x1.082e863838416p+2, 0x1.ffbbe1fe899d3p-2,
+    0x1.0761b43d23739p+2, 0x1.ffba286320871p-2, 0x1.0694e2f509e68p+2, 0x1.ffb863998a19cp-2,
+    0x1.05c81264739f3p+2, 0x1.ffb693595a0bbp-2, 0x1.04fb429005fd2p+2, 0x1.ffb4b7584f782p-2,
+    0x1.042e737c84778p+2, 0x1.ffb2cf4a490dfp-2, 0x1.0361a52ed1609p+2, 0x1.ffb0dae138f23p-2,
+    0x1.0294d7abeeaccp+2, 0x1.ffaed9cd18559p-2, 0x1.01c80af8febfap+2, 0x1.ffaccbbbdab9cp-2,
+    0x1.00fb3f1b453dap+2, 0x1.ffaab05960e4cp-2, 0x1.002e741827e2ep+2, 0x1.ffa8874f6b80ep-2,
+    0x1.fec353ea5ec05p+1, 0x1.ffa650458d66cp-2, 0x1.fd29c17010795p+1, 0x1.ffa40ae11d8f7p-2,
+    0x1.fb9030cd077bap+1, 0x1.ffa1b6c528ac0p-2, 0x1.f9f6a20d31a9fp+1, 0x1.ff9f539262616p-2,
+    0x1.f85d153cca25cp+1, 0x1.ff9ce0e716250p-2, 0x1.f6c38a685b42ep+1, 0x1.ff9a5e5f17b8bp-2,
+    0x1.f52a019cc087ap+1, 0x1.ff97cb93b342fp-2, 0x1.f3907ae728b96p+1, 0x1.ff95281b9d01ap-2,
+    0x1.f1f6f65517f72p+1, 0x1.ff92738ae0942p-2, 0x1.f05d73f469e0ap+1, 0x1.ff8fad72cfda6p-2,
+    0x1.eec3f3d353cc9p+1, 0x1.ff8cd561f166dp-2, 0x1.ed2a7600670bbp+1, 0x1.ff89eae3ee7f4p-2,
+    0x1.eb90fa8a933b9p+1, 0x1.ff86ed8180ab9p-2, 0x1.e9f7818128a7ep+1, 0x1.ff83dcc05ecdcp-2,
+    0x1.e85e0af3dabaep+1, 0x1.ff80b82329c1ap-2, 0x1.e6c496f2c27ddp+1, 0x1.ff7d7f295880dp-2,
+    0x1.e52b258e61296p+1, 0x1.ff7a314f23c76p-2, 0x1.e391b6d7a2c69p+1, 0x1.ff76ce0d71374p-2,
+    0x1.e1f84adfe0e08p+1, 0x1.ff7354d9bdf65p-2, 0x1.e05ee1b8e547bp+1, 0x1.ff6fc52608c3dp-2,
+    0x1.dec57b74ece6fp+1, 0x1.ff6c1e60bb829p-2, 0x1.dd2c1826aaaa5p+1, 0x1.ff685ff49433dp-2,
+    0x1.db92b7e14a791p+1, 0x1.ff6489488d5fap-2, 0x1.d9f95ab874428p+1, 0x1.ff6099bfc5e6dp-2,
+    0x1.d86000c04f1e8p+1, 0x1.ff5c90b9683b8p-2, 0x1.d6c6aa0d84821p+1, 0x1.ff586d9090fbdp-2,
+    0x1.d52d56b543887p+1, 0x1.ff542f9c34eb3p-2, 0x1.d39406cd44516p+1, 0x1.ff4fd62f06467p-2,
+    0x1.d1faba6bcb750p+1, 0x1.ff4b6097596e6p-2, 0x1.d06171a7ad8dfp+1, 0x1.ff46ce1f08e52p-2,
+    0x1.cec82c9852d9dp+1, 0x1.ff421e0b5899dp-2, 0x1.cd2eeb55baf15p+1, 0x1.ff3d4f9cd87e1p-2,
+    0x1.cb95adf880983p+1, 0x1.ff38620f46616p-2, 0x1.c9fc7499dda51p+1, 0x1.ff3354996f0dfp-2,
+    0x1.c8633f53af034p+1, 0x1.ff2e266d0ea15p-2, 0x1.c6ca0e4078cd1p+1, 0x1.ff28d6b6b01dap-2,
+    0x1.c530e17b6a81ap+1, 0x1.ff23649d8c2dbp-2, 0x1.c397b92063547p+1, 0x1.ff1dcf4367172p-2,
+    0x1.c1fe954bf6998p+1, 0x1.ff1815c46dd5ap-2, 0x1.c065761b704d3p+1, 0x1.ff123737125a8p-2,
+    0x1.becc5bacd9b92p+1, 0x1.ff0c32abe6ea9p-2, 0x1.bd33461efe371p+1, 0x1.ff06072d7895ap-2,
+    0x1.bb9a35917011ap+1, 0x1.feffb3c028c1cp-2, 0x1.ba012a248d84ep+1, 0x1.fef9376205c4fp-2,
+    0x1.b86823f985de2p+1, 0x1.fef2910aa2874p-2, 0x1.b6cf23325ebd3p+1, 0x1.feebbfaaed276p-2,
+    0x1.b53627f1f9766p+1, 0x1.fee4c22d049c4p-2, 0x1.b39d325c18977p+1, 0x1.fedd97740d4d2p-2,
+    0x1.b2044295658f5p+1, 0x1.fed63e5c0499ep-2, 0x1.b06b58c3767a1p+1, 0x1.feceb5b9934d3p-2,
+    0x1.aed2750cd411dp+1, 0x1.fec6fc59def26p-2, 0x1.ad399798ffc51p+1, 0x1.febf11025a07ap-2,
+    0x1.aba0c09079f44p+1, 0x1.feb6f2709306dp-2, 0x1.aa07f01cc856ep+1, 0x1.feae9f5a023c6p-2,
+    0x1.a86f26687c88dp+1, 0x1.fea6166bd6672p-2, 0x1.a6d6639f3ac20p+1, 0x1.fe9d564ac0180p-2,
+    0x1.a53da7edc0b7fp+1, 0x1.fe945d92bbcb8p-2, 0x1.a3a4f381ecabbp+1, 0x1.fe8b2ad6dab4bp-2,
+    0x1.a20c468ac4a3ep+1, 0x1.fe81bca10a32ap-2, 0x1.a073a1387dd50p+1, 0x1.fe781171d9e79p-2,
+    0x1.9edb03bc84386p+1, 0x1.fe6e27c0406a8p-2, 0x1.9d426e4982532p+1, 0x1.fe63fdf95e8b5p-2,
+    0x1.9ba9e113692ecp+1, 0x1.fe599280411fep-2, 0x1.9a115c4f78837p+1, 0x1.fe4ee3ada152cp-2,
+    0x1.9878e03447169p+1, 0x1.fe43efcfa36b0p-2, 0x1.96e06cf9cb4dap+1, 0x1.fe38b5299402bp-2,
+    0x1.954802d963f7bp+1, 0x1.fe2d31f3a3a54p-2, 0x1.93afa20de14dap+1, 0x1.fe21645aa0cb0p-2,
+    0x1.92174ad38e2bap+1, 0x1.fe154a7fb028fp-2, 0x1.907efd6839849p+1, 0x1.fe08e278034bap-2,
+    0x1.8ee6ba0b4010cp+1, 0x1.fdfc2a4c8d72ep-2, 0x1.8d4e80fd9639ap+1, 0x1.fdef1ff9b6a52p-2,
+    0x1.8bb65281d243cp+1, 0x1.fde1c16f0ceffp-2, 0x1.8a1e2edc36b88p+1, 0x1.fdd40c8ef3cb4p-2,
+    0x1.88861652bd115p+1, 0x1.fdc5ff2e51961p-2, 0x1.86ee092d20a55p+1, 0x1.fdb797143b205p-2,
+    0x1.855607b4e9dbcp+1, 0x1.fda8d1f99d395p-2, 0x1.83be123579a44p+1, 0x1.fd99ad88e4356p-2,
+    0x1.822628fc1536dp+1, 0x1.fd8a275da1624p-2, 0x1.808e4c57f21d0p+1, 0x1.fd7a3d042e5c8p-2,
+    0x1.7ef67c9a42864p+1, 0x1.fd69ebf94e3c5p-2, 0x1.7d5eba1641e91p+1, 0x1.fd5931a9cc8d2p-2,
+    0x1.7bc7052141f29p+1, 0x1.fd480b721a04ep-2, 0x1.7a2f5e12b7c6bp+1, 0x1.fd36769de6edep-2,
+    0x1.7897c54449926p+1, 0x1.fd247067bb38dp-2, 0x1.77003b11dc722p+1, 0x1.fd11f5f88c28ep-2,
+    0x1.7568bfd9a2ae8p+1, 0x1.fcff04674f8eap-2, 0x1.73d153fc2a50fp+1, 0x1.fceb98b88c84dp-2,
+    0x1.7239f7dc6c122p+1, 0x1.fcd7afdde9a1bp-2, 0x1.70a2abdfdaa52p+1, 0x1.fcc346b5b890dp-2,
+    0x1.6f0b706e72606p+1, 0x1.fcae5a0a7f078p-2, 0x1.6d7445f2c9472p+1, 0x1.fc98e6927d070p-2,
+    0x1.6bdd2cda1f757p+1, 0x1.fc82e8ef305f1p-2, 0x1.6a4625946ff0fp+1, 0x1.fc6c5dacd562dp-2,
+    0x1.68af309481e0bp+1, 0x1.fc554141e4c30p-2, 0x1.67184e4ffa2e5p+1, 0x1.fc3d900e8e7fbp-2,
+    0x1.65817f3f6d92cp+1, 0x1.fc25465c31e29p-2, 0x1.63eac3de73118p+1, 0x1.fc0c605cd2755p-2,
+    0x1.62541cabb6e3ap+1, 0x1.fbf2da2a89e4bp-2, 0x1.60bd8a290dd69p+1, 0x1.fbd8afc6f6c2cp-2,
+    0x1.5f270cdb89202p+1, 0x1.fbbddd1aa819bp-2, 0x1.5d90a54b8aaa8p+1, 0x1.fba25df485c13p-2,
+    0x1.5bfa5404d9db1p+1, 0x1.fb862e0935674p-2, 0x1.5a641996b8d6dp+1, 0x1.fb6948f27c3eep-2,
+    0x1.58cdf693fa467p+1, 0x1.fb4baa2e9d458p-2, 0x1.5737eb93179ddp+1, 0x1.fb2d4d1fb410ep-2,
+    0x1.55a1f92e47e89p+1, 0x1.fb0e2d0b0c16dp-2, 0x1.540c2003971f5p+1, 0x1.faee45187460dp-2,
+    0x1.527660b4fe08bp+1, 0x1.facd90518f9bdp-2, 0x1.50e0bbe87aa83p+1, 0x1.faac09a12077dp-2,
+    0x1.4f4b3248293e4p+1, 0x1.fa89abd252469p-2, 0x1.4db5c4825ddd3p+1, 0x1.fa66718ffdcd4p-2,
+    0x1.4c207349be94fp+1, 0x1.fa425563ea39ep-2, 0x1.4a8b3f555e39cp+1, 0x1.fa1d51b60a2ebp-2,
+    0x1.48f62960d7c81p+1, 0x1.f9f760cbb4d69p-2, 0x1.4761322c6a69ap+1, 0x1.f9d07cc6daf34p-2,
+    0x1.45cc5a7d161e8p+1, 0x1.f9a89fa537da3p-2, 0x1.4437a31cb90d8p+1, 0x1.f97fc33f7e512p-2,
+    0x1.42a30cda2d7f4p+1, 0x1.f955e148813f4p-2, 0x1.410e988968874p+1, 0x1.f92af34c58250p-2,
+    0x1.3f7a4703995ebp+1, 0x1.f8fef2af7f4ffp-2, 0x1.3de6192749739p+1, 0x1.f8d1d8adf3be8p-2,
+    0x1.3c520fd87d30bp+1, 0x1.f8a39e5a4aa85p-2, 0x1.3abe2c00d5813p+1, 0x1.f8743c9cc4a0ep-2,
+    0x1.392a6e8fb213bp+1, 0x1.f843ac325c4adp-2, 0x1.3796d87a54601p+1, 0x1.f811e5abd0914p-2,
+    0x1.36036abc03745p+1, 0x1.f7dee16caa604p-2, 0x1.34702656308abp+1, 0x1.f7aa97aa3dd26p-2,
+    0x1.32dd0c509c6eap+1, 0x1.f775006aa6cdfp-2, 0x1.314a1db97db2bp+1, 0x1.f73e1383c10a4p-2,
+    0x1.2fb75ba5a7bb4p+1, 0x1.f705c89a1b784p-2, 0x1.2e24c730b2a33p+1, 0x1.f6cc171fe7096p-2,
+    0x1.2c92617d23fbbp+1, 0x1.f690f653e0d20p-2, 0x1.2b002bb4986dcp+1, 0x1.f6545d4037842p-2,
+    0x1.296e2707ee3e8p+1, 0x1.f61642b96c42ap-2, 0x1.27dc54af70bc4p+1, 0x1.f5d69d5d2ecbep-2,
+    0x1.264ab5eb04965p+1, 0x1.f595639134fe3p-2, 0x1.24b94c0255247p+1, 0x1.f5528b820db93p-2,
+    0x1.2328184502a0ep+1, 0x1.f50e0b21ef202p-2, 0x1.21971c0ad1594p+1, 0x1.f4c7d82780447p-2,
+    0x1.200658b3d9d99p+1, 0x1.f47fe80c9e3f9p-2, 0x1.1e75cfa8ba14fp+1, 0x1.f436300d1cc73p-2,
+    0x1.1ce5825ac7905p+1, 0x1.f3eaa52582473p-2, 0x1.1b5572444291bp+1, 0x1.f39d3c11bf8f8p-2,
+    0x1.19c5a0e88a583p+1, 0x1.f34de94be326bp-2, 0x1.18360fd452601p+1, 0x1.f2fca10ac853ep-2,
+    0x1.16a6c09dd8b65p+1, 0x1.f2a95740c1f57p-2, 0x1.1517b4e51d5eep+1, 0x1.f253ff9a413c0p-2,
+    0x1.1388ee541ad0cp+1, 0x1.f1fc8d7c78657p-2, 0x1.11fa6e9eff8b6p+1, 0x1.f1a2f403f9951p-2,
+    0x1.106c378468c87p+1, 0x1.f147260351ea1p-2, 0x1.0ede4acd9e4c6p+1, 0x1.f0e91601a0f8bp-2,
+    0x1.0d50aa4ecf594p+1, 0x1.f088b6392ccdap-2, 0x1.0bc357e750c62p+1, 0x1.f025f895f2a71p-2,
+    0x1.0a365581dc3e1p+1, 0x1.efc0ceb43492dp-2, 0x1.08a9a514d0a81p+1, 0x1.ef5929df04244p-2,
+    0x1.071d48a273bbap+1, 0x1.eeeefb0eca7acp-2, 0x1.0591423934c32p+1, 0x1.ee8232e7cdd2ap-2,
+    0x1.040593f3f08d9p+1, 0x1.ee12c1b8b4e38p-2, 0x1.027a3ffa36928p+1, 0x1.eda09779084f8p-2,
+    0x1.00ef48808f484p+1, 0x1.ed2ba3c7b26f4p-2, 0x1.fec95f91875d9p+0, 0x1.ecb3d5e97dc9ep-2,
+    0x1.fbb4f0444c1e5p+0, 0x1.ec391cc7928eep-2, 0x1.f8a147d3b7e1ep+0, 0x1.ebbb66edf36cfp-2,
+    0x1.f58e6b16528b5p+0, 0x1.eb3aa289fa275p-2, 0x1.f27c5eff79945p+0, 0x1.eab6bd68d4513p-2,
+    0x1.ef6b289ffb3c1p+0, 0x1.ea2fa4f6009e1p-2, 0x1.ec5acd26b41fdp+0, 0x1.e9a54639cd3b7p-2,
+    0x1.e94b51e12f3c7p+0, 0x1.e9178dd7d7b10p-2, 0x1.e63cbc3c4854ep+0, 0x1.e886680d8ecb0p-2,
+    0x1.e32f11c4d0ba3p+0, 0x1.e7f1c0b0b719fp-2, 0x1.e022582836717p+0, 0x1.e759832df29c1p-2,
+    0x1.dd1695352db08p+0, 0x1.e6bd9a874c2bep-2, 0x1.da0bcedc5cac2p+0, 0x1.e61df152c7586p-2,
+    0x1.d7020b3109af8p+0, 0x1.e57a71b8f5556p-2, 0x1.d3f95069cb745p+0, 0x1.e4d305738fb9bp-2,
+    0x1.d0f1a4e13bb20p+0, 0x1.e42795cc19cc8p-2, 0x1.cdeb0f16abd87p+0, 0x1.e3780b9a892b3p-2,
+    0x1.cae595aedbe9ep+0, 0x1.e2c44f43f69dcp-2, 0x1.c7e13f74b3664p+0, 0x1.e20c48b957f74p-2,
+    0x1.c4de1359fc396p+0, 0x1.e14fdf7643ecfp-2, 0x1.c1dc18781f99ep+0, 0x1.e08efa7fc0d9dp-2,
+    0x1.bedb5610e4c7fp+0, 0x1.dfc980631f6dbp-2, 0x1.bbdbd38f31974p+0, 0x1.deff5734e2557p-2,
+    0x1.b8dd9887ccaebp+0, 0x1.de30648fb3f47p-2, 0x1.b5e0acba21663p+0, 0x1.dd5c8d936b536p-2,
+    0x1.b2e518110529ep+0, 0x1.dc83b6e421775p-2, 0x1.afeae2a37e467p+0, 0x1.dba5c4a9585e3p-2,
+    0x1.acf214b58c02ap+0, 0x1.dac29a8d34ec8p-2, 0x1.a9fab6b8efe52p+0, 0x1.d9da1bbbcd263p-2,
+    0x1.a704d14df8065p+0, 0x1.d8ec2ae28c186p-2, 0x1.a4106d444a49ap+0, 0x1.d7f8aa2face92p-2,
+    0x1.a11d939bb057ap+0, 0x1.d6ff7b51ce8f9p-2, 0x1.9e2c4d84e4318p+0, 0x1.d6007f77a1c5fp-2,
+    0x1.9b3ca4625d315p+0, 0x1.d4fb974fb2d45p-2, 0x1.984ea1c91d498p+0, 0x1.d3f0a30850e14p-2,
+    0x1.95624f817e53cp+0, 0x1.d2df824f94867p-2, 0x1.9277b787ff3a6p+0, 0x1.d1c8145387720p-2,
+    0x1.8f8ee40e10c75p+0, 0x1.d0aa37c26ef00p-2, 0x1.8ca7df7ae1ddbp+0, 0x1.cf85cacb3b423p-2,
+    0x1.89c2b46c2ae34p+0, 0x1.ce5aab1e1dbe7p-2, 0x1.86df6db6f8186p+0, 0x1.cd28b5ed47b70p-2,
+    0x1.83fe1668729cdp+0, 0x1.cbefc7edd43fdp-2, 0x1.811eb9c6a7da8p+0, 0x1.caafbd58def23p-2,
+    0x1.7e4163514f0c0p+0, 0x1.c96871ecc9dc2p-2, 0x1.7b661ec28c92cp+0, 0x1.c819c0eeb4d6cp-2,
+    0x1.788cf80fb2ca7p+0, 0x1.c6c3852c288bap-2, 0x1.75b5fb6a0006ap+0, 0x1.c56598fcf77d9p-2,
+    0x1.72e1353f5960dp+0, 0x1.c3ffd64557728p-2, 0x1.700eb23b01fb7p+0, 0x1.c292167835aabp-2,
+    0x1.6d3e7f464e5a3p+0, 0x1.c11c3299c8574p-2, 0x1.6a70a989536a3p+0, 0x1.bf9e03425fce4p-2,
+    0x1.67a53e6b90d37p+0, 0x1.be1760a179fffp-2, 0x1.64dc4b949626bp+0, 0x1.bc8822811aba4p-2,
+    0x1.6215deeca2775p+0, 0x1.baf020496b4a0p-2, 0x1.5f52069d3dedbp+0, 0x1.b94f3104a4110p-2,
+    0x1.5c90d111ccd8fp+0, 0x1.b7a52b6342a76p-2, 0x1.59d24cf81bc32p+0, 0x1.b5f1e5c08f224p-2,
+    0x1.57168940e4086p+0, 0x1.b435362773184p-2, 0x1.545d9520486a8p+0, 0x1.b26ef257a4f87p-2,
+    0x1.51a7800e49190p+0, 0x1.b09eefcb2a461p-2, 0x1.4ef459c72ea02p+0, 0x1.aec503bc33429p-2,
+    0x1.4c44324beb2d6p+0, 0x1.ace1032b52868p-2, 0x1.499719e271951p+0, 0x1.aaf2c2e612ff3p-2,
+    0x1.46ed2116017f3p+0, 0x1.a8fa178deeb73p-2, 0x1.444658b7681ecp+0, 0x1.a6f6d59fa8bf5p-2,
+    0x1.41a2d1dd34d41p+0, 0x1.a4e8d17b0c78dp-2, 0x1.3f029de3e1144p+0, 0x1.a2cfdf6b146afp-2,
+    0x1.3c65ce6deaf02p+0, 0x1.a0abd3ae7ab21p-2, 0x1.39cc7563e18f2p+0, 0x1.9e7c8280b4f94p-2,
+    0x1.3736a4f462effp+0, 0x1.9c41c0235dcc4p-2, 0x1.34a46f940a407p+0, 0x1.99fb60e80cebbp-2,
+    0x1.3215e7fd4e175p+0, 0x1.97a9393aa020dp-2, 0x1.2f8b21304ddcdp+0, 0x1.954b1dabf5e36p-2,
+    0x1.2d042e728da94p+0, 0x1.92e0e2fd1aef2p-2, 0x1.2a81234e9fe22p+0, 0x1.906a5e2aebb2ap-2,
+    0x1.28021393bbdafp+0, 0x1.8de7647a2a42fp-2, 0x1.2587135540befp+0, 0x1.8b57cb840942dp-2,
+    0x1.231036ea2408cp+0, 0x1.88bb69432be5cp-2, 0x1.209d92ec4acbap+0, 0x1.861214211aee3p-2,
+    0x1.1e2f3c37cd14bp+0, 0x1.835ba3042e38cp-2, 0x1.1bc547ea22a87p+0, 0x1.8097ed5dea11fp-2,
+    0x1.195fcb613865bp+0, 0x1.7dc6cb39cf3c9p-2, 0x1.16fedc3a6d95cp+0, 0x1.7ae8154c9c312p-2,
+    0x1.14a290517877fp+0, 0x1.77fba503fdbddp-2, 0x1.124afdbf3155bp+0, 0x1.75015496acc4ap-2,
+    0x1.0ff83ad843749p+0, 0x1.71f8ff14f66d7p-2, 0x1.0daa5e2bc33cep+0, 0x1.6ee28079abad1p-2,
+    0x1.0b617e81a8f31p+0, 0x1.6bbdb5bb74903p-2, 0x1.091db2d92f66dp+0, 0x1.688a7cde833d1p-2,
+    0x1.06df126716026p+0, 0x1.6548b506a2232p-2, 0x1.04a5b493c5ac1p+0, 0x1.61f83e89984bep-2,
+    0x1.0271b0f957f4ep+0, 0x1.5e98fb01de3c3p-2, 0x1.00431f6180172p+0, 0x1.5b2acd619d4b9p-2,
+    0x1.fc342f86aaa7ap-1, 0x1.57ad9a05f2cc3p-2, 0x1.f7ed6481fc8fep-1, 0x1.542146ca6fce7p-2,
+    0x1.f3b20e4a79bcbp-1, 0x1.5085bb1ccdbcep-2, 0x1.ef825dc1b520fp-1, 0x1.4cdae010cf793p-2,
+    0x1.eb5e840fe96b5p-1, 0x1.4920a0744611dp-2, 0x1.e746b29e515f7p-1, 0x1.4556e8e32f943p-2,
+    0x1.e33b1b113fa55p-1, 0x1.417da7dbe5ec7p-2, 0x1.df3bef41f5ecfp-1, 0x1.3d94cdd35332ap-2,
+    0x1.db4961383b665p-1, 0x1.399c4d4920352p-2, 0x1.d763a323b2b35p-1, 0x1.35941adbd182bp-2,
+    0x1.d38ae754ef9e0p-1, 0x1.317c2d5cc6acfp-2, 0x1.cfbf60364d088p-1, 0x1.2d547de40ef74p-2,
+    0x1.cc01404483b29p-1, 0x1.291d07e40624cp-2, 0x1.c850ba07029edp-1, 0x1.24d5c93cab9f3p-2,
+    0x1.c4ae00080a0c4p-1, 0x1.207ec24ea5bd8p-2, 0x1.c11944cc8a291p-1, 0x1.1c17f60de2866p-2,
+    0x1.bd92bacbc6d10p-1, 0x1.17a16a13c6e91p-2, 0x1.ba1a9466c1dcdp-1, 0x1.131b26b0dd111p-2,
+    0x1.b6b103df6db67p-1, 0x1.0e8536fdf22c9p-2, 0x1.b3563b4faa1c6p-1, 0x1.09dfa8ec93bd4p-2,
+    0x1.b00a6ca00d2e4p-1, 0x1.052a8d56dc5b1p-2, 0x1.accdc97e7b128p-1, 0x1.0065f80e7fa9bp-2,
+    0x1.a9a083548eb86p-1, 0x1.f723ffd60a5e7p-3, 0x1.a682cb3dd66e6p-1, 0x1.ed5d7dae4369bp-3,
+    0x1.a374d1fde7390p-1, 0x1.e378a3ba3dccdp-3, 0x1.a076c7f64a098p-1, 0x1.d975b264820a4p-3,
+    0x1.9d88dd1c4628bp-1, 0x1.cf54f0823563fp-3, 0x1.9aab40ee8c5bdp-1, 0x1.c516ab657e31cp-3,
+    0x1.97de226ac67b9p-1, 0x1.babb36ed863afp-3, 0x1.9521b0030f65fp-1, 0x1.b042ed93fd2edp-3,
+    0x1.927617935762dp-1, 0x1.a5ae3077fe597p-3, 0x1.8fdb8656b93fdp-1, 0x1.9afd67663ddf2p-3,
+    0x1.8d5228dcc4947p-1, 0x1.903100de631f7p-3, 0x1.8ada2afec1c74p-1, 0x1.854972157761ap-3,
+    0x1.8873b7d4f494bp-1, 0x1.7a4736f551990p-3, 0x1.861ef9abe1fa1p-1, 0x1.6f2ad218e9e29p-3,
+    0x1.83dc19f99e8a5p-1, 0x1.63f4ccc5815c4p-3, 0x1.81ab41532a4cdp-1, 0x1.58a5b6e08d1b6p-3,
+    0x1.7f8c9761df626p-1, 0x1.4d3e26e25552ap-3, 0x1.7d8042d8f8c13p-1, 0x1.41beb9c53c26fp-3,
+    0x1.7b86696b366b6p-1, 0x1.362812f1a246fp-3, 0x1.799f2fc0a490ep-1, 0x1.2a7adc2662074p-3,
+    0x1.77cab96c8b170p-1, 0x1.1eb7c55ddc97bp-3, 0x1.760928e38b05ap-1, 0x1.12df84af97cbcp-3,
+    0x1.745a9f71ef576p-1, 0x1.06f2d62e6df39p-3, 0x1.72bf3d3236a95p-1, 0x1.f5e4f786a8a56p-4,
+    0x1.71372103db391p-1, 0x1.ddbe7a097fcd7p-4, 0x1.6fc268825e93cp-1, 0x1.c573ce1566b96p-4,
+    0x1.6e612ffc9e438p-1, 0x1.ad06987f08932p-4, 0x1.6d13926c76afep-1, 0x1.9478885ad1e35p-4,
+    0x1.6bd9a96eb947ap-1, 0x1.7bcb5691c6421p-4, 0x1.6ab38d3b7ae6fp-1, 0x1.6300c5703f8d5p-4,
+    0x1.69a1549ebf444p-1, 0x1.4a1aa02ecc4e7p-4, 0x1.68a314f186016p-1, 0x1.311aba7569234p-4,
+    0x1.67b8e2133dcaap-1, 0x1.1802efd956fc0p-4, 0x1.66e2ce63a1b92p-1, 0x1.fdaa46abab965p-5,
+    0x1.6620eabd04ef0p-1, 0x1.cb267d8021a62p-5, 0x1.6573466f1026cp-1, 0x1.987e646d1e0bdp-5,
+    0x1.64d9ef39f4a9bp-1, 0x1.65b5e718fdd09p-5, 0x1.6454f14a17d9ap-1, 0x1.32d0fb6274144p-5,
+    0x1.63e457343a2f3p-1, 0x1.ffa7405181bd4p-6, 0x1.638829f21c3e6p-1, 0x1.9983b81bc0859p-6,
+    0x1.634070dfa4028p-1, 0x1.333f7867025b5p-6, 0x1.630d31b8845dbp-1, 0x1.99c54bce64e3dp-7,
+    0x1.62ee709668617p-1, 0x1.99d5b4ab7f73cp-8, 0x1.62e42fefa39efp-1, 0x0.0p+0,
+    0x1.62ee709668617p-1, -0x1.99d5b4ab7f73cp-8, 0x1.630d31b8845dbp-1, -0x1.99c54bce64e3dp-7,
+    0x1.634070dfa4028p-1, -0x1.333f7867025b5p-6, 0x1.638829f21c3e6p-1, -0x1.9983b81bc0859p-6,
+    0x1.63e457343a2f3p-1, -0x1.ffa7405181bd4p-6, 0x1.6454f14a17d9ap-1, -0x1.32d0fb6274144p-5,
+    0x1.64d9ef39f4a9bp-1, -0x1.65b5e718fdd09p-5, 0x1.6573466f1026cp-1, -0x1.987e646d1e0bdp-5,
+    0x1.6620eabd04ef0p-1, -0x1.cb267d8021a62p-5, 0x1.66e2ce63a1b92p-1, -0x1.fdaa46abab965p-5,
+    0x1.67b8e2133dcaap-1, -0x1.1802efd956fc0p-4, 0x1.68a314f186016p-1, -0x1.311aba7569234p-4,
+    0x1.69a1549ebf444p-1, -0x1.4a1aa02ecc4e7p-4, 0x1.6ab38d3b7ae6fp-1, -0x1.6300c5703f8d5p-4,
+    0x1.6bd9a96eb947ap-1, -0x1.7bcb5691c6421p-4, 0x1.6d13926c76afep-1, -0x1.9478885ad1e35p-4,
+    0x1.6e612ffc9e438p-1, -0x1.ad06987f08932p-4, 0x1.6fc268825e93cp-1, -0x1.c573ce1566b96p-4,
+    0x1.71372103db391p-1, -0x1.ddbe7a097fcd7p-4, 0x1.72bf3d3236a95p-1, -0x1.f5e4f786a8a56p-4,
+    0x1.745a9f71ef576p-1, -0x1.06f2d62e6df39p-3, 0x1.760928e38b05ap-1, -0x1.12df84af97cbcp-3,
+    0x1.77cab96c8b170p-1, -0x1.1eb7c55ddc97bp-3, 0x1.799f2fc0a490ep-1, -0x1.2a7adc2662074p-3,
+    0x1.7b86696b366b6p-1, -0x1.362812f1a246fp-3, 0x1.7d8042d8f8c13p-1, -0x1.41beb9c53c26fp-3,
+    0x1.7f8c9761df626p-1, -0x1.4d3e26e25552ap-3, 0x1.81ab41532a4cdp-1, -0x1.58a5b6e08d1b6p-3,
+    0x1.83dc19f99e8a5p-1, -0x1.63f4ccc5815c4p-3, 0x1.861ef9abe1fa1p-1, -0x1.6f2ad218e9e29p-3,
+    0x1.8873b7d4f494bp-1, -0x1.7a4736f551990p-3, 0x1.8ada2afec1c74p-1, -0x1.854972157761ap-3,
+    0x1.8d5228dcc4947p-1, -0x1.903100de631f7p-3, 0x1.8fdb8656b93fdp-1, -0x1.9afd67663ddf2p-3,
+    0x1.927617935762dp-1, -0x1.a5ae3077fe597p-3, 0x1.9521b0030f65fp-1, -0x1.b042ed93fd2edp-3,
+    0x1.97de226ac67b9p-1, -0x1.babb36ed863afp-3, 0x1.9aab40ee8c5bdp-1, -0x1.c516ab657e31cp-3,
+    0x1.9d88dd1c4628bp-1, -0x1.cf54f0823563fp-3, 0x1.a076c7f64a098p-1, -0x1.d975b264820a4p-3,
+    0x1.a374d1fde7390p-1, -0x1.e378a3ba3dccdp-3, 0x1.a682cb3dd66e6p-1, -0x1.ed5d7dae4369bp-3,
+    0x1.a9a083548eb86p-1, -0x1.f723ffd60a5e7p-3, 0x1.accdc97e7b128p-1, -0x1.0065f80e7fa9bp-2,
+    0x1.b00a6ca00d2e4p-1, -0x1.052a8d56dc5b1p-2, 0x1.b3563b4faa1c6p-1, -0x1.09dfa8ec93bd4p-2,
+    0x1.b6b103df6db67p-1, -0x1.0e8536fdf22c9p-2, 0x1.ba1a9466c1dcdp-1, -0x1.131b26b0dd111p-2,
+    0x1.bd92bacbc6d10p-1, -0x1.17a16a13c6e91p-2, 0x1.c11944cc8a291p-1, -0x1.1c17f60de2866p-2,
+    0x1.c4ae00080a0c4p-1, -0x1.207ec24ea5bd8p-2, 0x1.c850ba07029edp-1, -0x1.24d5c93cab9f3p-2,
+    0x1.cc01404483b29p-1, -0x1.291d07e40624cp-2, 0x1.cfbf60364d088p-1, -0x1.2d547de40ef74p-2,
+    0x1.d38ae754ef9e0p-1, -0x1.317c2d5cc6acfp-2, 0x1.d763a323b2b35p-1, -0x1.35941adbd182bp-2,
+    0x1.db4961383b665p-1, -0x1.399c4d4920352p-2, 0x1.df3bef41f5ecfp-1, -0x1.3d94cdd35332ap-2,
+    0x1.e33b1b113fa55p-1, -0x1.417da7dbe5ec7p-2, 0x1.e746b29e515f7p-1, -0x1.4556e8e32f943p-2,
+    0x1.eb5e840fe96b5p-1, -0x1.4920a0744611dp-2, 0x1.ef825dc1b520fp-1, -0x1.4cdae010cf793p-2,
+    0x1.f3b20e4a79bcbp-1, -0x1.5085bb1ccdbcep-2, 0x1.f7ed6481fc8fep-1, -0x1.542146ca6fce7p-2,
+    0x1.fc342f86aaa7ap-1, -0x1.57ad9a05f2cc3p-2, 0x1.00431f6180172p+0, -0x1.5b2acd619d4b9p-2,
+    0x1.0271b0f957f4ep+0, -0x1.5e98fb01de3c3p-2, 0x1.04a5b493c5ac1p+0, -0x1.61f83e89984bep-2,
+    0x1.06df126716026p+0, -0x1.6548b506a2232p-2, 0x1.091db2d92f66dp+0, -0x1.688a7cde833d1p-2,
+    0x1.0b617e81a8f31p+0, -0x1.6bbdb5bb74903p-2, 0x1.0daa5e2bc33cep+0, -0x1.6ee28079abad1p-2,
+    0x1.0ff83ad843749p+0, -0x1.71f8ff14f66d7p-2, 0x1.124afdbf3155bp+0, -0x1.75015496acc4ap-2,
+    0x1.14a290517877fp+0, -0x1.77fba503fdbddp-2, 0x1.16fedc3a6d95cp+0, -0x1.7ae8154c9c312p-2,
+    0x1.195fcb613865bp+0, -0x1.7dc6cb39cf3c9p-2, 0x1.1bc547ea22a87p+0, -0x1.8097ed5dea11fp-2,
+    0x1.1e2f3c37cd14bp+0, -0x1.835ba3042e38cp-2, 0x1.209d92ec4acbap+0, -0x1.861214211aee3p-2,
+    0x1.231036ea2408cp+0, -0x1.88bb69432be5cp-2, 0x1.2587135540befp+0, -0x1.8b57cb840942dp-2,
+    0x1.28021393bbdafp+0, -0x1.8de7647a2a42fp-2, 0x1.2a81234e9fe22p+0, -0x1.906a5e2aebb2ap-2,
+    0x1.2d042e728da94p+0, -0x1.92e0e2fd1aef2p-2, 0x1.2f8b21304ddcdp+0, -0x1.954b1dabf5e36p-2,
+    0x1.3215e7fd4e175p+0, -0x1.97a9393aa020dp-2, 0x1.34a46f940a407p+0, -0x1.99fb60e80cebbp-2,
+    0x1.3736a4f462effp+0, -0x1.9c41c0235dcc4p-2, 0x1.39cc7563e18f2p+0, -0x1.9e7c8280b4f94p-2,
+    0x1.3c65ce6deaf02p+0, -0x1.a0abd3ae7ab21p-2, 0x1.3f029de3e1144p+0, -0x1.a2cfdf6b146afp-2,
+    0x1.41a2d1dd34d41p+0, -0x1.a4e8d17b0c78dp-2, 0x1.444658b7681ecp+0, -0x1.a6f6d59fa8bf5p-2,
+    0x1.46ed2116017f3p+0, -0x1.a8fa178deeb73p-2, 0x1.499719e271951p+0, -0x1.aaf2c2e612ff3p-2,
+    0x1.4c44324beb2d6p+0, -0x1.ace1032b52868p-2, 0x1.4ef459c72ea02p+0, -0x1.aec503bc33429p-2,
+    0x1.51a7800e49190p+0, -0x1.b09eefcb2a461p-2, 0x1.545d9520486a8p+0, -0x1.b26ef257a4f87p-2,
+    0x1.57168940e4086p+0, -0x1.b435362773184p-2, 0x1.59d24cf81bc32p+0, -0x1.b5f1e5c08f224p-2,
+    0x1.5c90d111ccd8fp+0, -0x1.b7a52b6342a76p-2, 0x1.5f52069d3dedbp+0, -0x1.b94f3104a4110p-2,
+    0x1.6215deeca2775p+0, -0x1.baf020496b4a0p-2, 0x1.64dc4b949626bp+0, -0x1.bc8822811aba4p-2,
+    0x1.67a53e6b90d37p+0, -0x1.be1760a179fffp-2, 0x1.6a70a989536a3p+0, -0x1.bf9e03425fce4p-2,
+    0x1.6d3e7f464e5a3p+0, -0x1.c11c3299c8574p-2, 0x1.700eb23b01fb7p+0, -0x1.c292167835aabp-2,
+    0x1.72e1353f5960dp+0, -0x1.c3ffd64557728p-2, 0x1.75b5fb6a0006ap+0, -0x1.c56598fcf77d9p-2,
+    0x1.788cf80fb2ca7p+0, -0x1.c6c3852c288bap-2, 0x1.7b661ec28c92cp+0, -0x1.c819c0eeb4d6cp-2,
+    0x1.7e4163514f0c0p+0, -0x1.c96871ecc9dc2p-2, 0x1.811eb9c6a7da8p+0, -0x1.caafbd58def23p-2,
+    0x1.83fe1668729cdp+0, -0x1.cbefc7edd43fdp-2, 0x1.86df6db6f8186p+0, -0x1.cd28b5ed47b70p-2,
+    0x1.89c2b46c2ae34p+0, -0x1.ce5aab1e1dbe7p-2, 0x1.8ca7df7ae1ddbp+0, -0x1.cf85cacb3b423p-2,
+    0x1.8f8ee40e10c75p+0, -0x1.d0aa37c26ef00p-2, 0x1.9277b787ff3a6p+0, -0x1.d1c8145387720p-2,
+    0x1.95624f817e53cp+0, -0x1.d2df824f94867p-2, 0x1.984ea1c91d498p+0, -0x1.d3f0a30850e14p-2,
+    0x1.9b3ca4625d315p+0, -0x1.d4fb974fb2d45p-2, 0x1.9e2c4d84e4318p+0, -0x1.d6007f77a1c5fp-2,
+    0x1.a11d939bb057ap+0, -0x1.d6ff7b51ce8f9p-2, 0x1.a4106d444a49ap+0, -0x1.d7f8aa2face92p-2,
+    0x1.a704d14df8065p+0, -0x1.d8ec2ae28c186p-2, 0x1.a9fab6b8efe52p+0, -0x1.d9da1bbbcd263p-2,
+    0x1.acf214b58c02ap+0, -0x1.dac29a8d34ec8p-2, 0x1.afeae2a37e467p+0, -0x1.dba5c4a9585e3p-2,
+    0x1.b2e518110529ep+0, -0x1.dc83b6e421775p-2, 0x1.b5e0acba21663p+0, -0x1.dd5c8d936b536p-2,
+    0x1.b8dd9887ccaebp+0, -0x1.de30648fb3f47p-2, 0x1.bbdbd38f31974p+0, -0x1.deff5734e2557p-2,
+    0x1.bedb5610e4c7fp+0, -0x1.dfc980631f6dbp-2, 0x1.c1dc18781f99ep+0, -0x1.e08efa7fc0d9dp-2,
+    0x1.c4de1359fc396p+0, -0x1.e14fdf7643ecfp-2, 0x1.c7e13f74b3664p+0, -0x1.e20c48b957f74p-2,
+    0x1.cae595aedbe9ep+0, -0x1.e2c44f43f69dcp-2, 0x1.cdeb0f16abd87p+0, -0x1.e3780b9a892b3p-2,
+    0x1.d0f1a4e13bb20p+0, -0x1.e42795cc19cc8p-2, 0x1.d3f95069cb745p+0, -0x1.e4d305738fb9bp-2,
+    0x1.d7020b3109af8p+0, -0x1.e57a71b8f5556p-2, 0x1.da0bcedc5cac2p+0, -0x1.e61df152c7586p-2,
+    0x1.dd1695352db08p+0, -0x1.e6bd9a874c2bep-2, 0x1.e022582836717p+0, -0x1.e759832df29c1p-2,
+    0x1.e32f11c4d0ba3p+0, -0x1.e7f1c0b0b719fp-2, 0x1.e63cbc3c4854ep+0, -0x1.e886680d8ecb0p-2,
+    0x1.e94b51e12f3c7p+0, -0x1.e9178dd7d7b10p-2, 0x1.ec5acd26b41fdp+0, -0x1.e9a54639cd3b7p-2,
+    0x1.ef6b289ffb3c1p+0, -0x1.ea2fa4f6009e1p-2, 0x1.f27c5eff79945p+0, -0x1.eab6bd68d4513p-2,
+    0x1.f58e6b16528b5p+0, -0x1.eb3aa289fa275p-2, 0x1.f8a147d3b7e1ep+0, -0x1.ebbb66edf36cfp-2,
+    0x1.fbb4f0444c1e5p+0, -0x1.ec391cc7928eep-2, 0x1.fec95f91875d9p+0, -0x1.ecb3d5e97dc9ep-2,
+    0x1.00ef48808f484p+1, -0x1.ed2ba3c7b26f4p-2, 0x1.027a3ffa36928p+1, -0x1.eda09779084f8p-2,
+    0x1.040593f3f08d9p+1, -0x1.ee12c1b8b4e38p-2, 0x1.0591423934c32p+1, -0x1.ee8232e7cdd2ap-2,
+    0x1.071d48a273bbap+1, -0x1.eeeefb0eca7acp-2, 0x1.08a9a514d0a81p+1, -0x1.ef5929df04244p-2,
+    0x1.0a365581dc3e1p+1, -0x1.efc0ceb43492dp-2, 0x1.0bc357e750c62p+1, -0x1.f025f895f2a71p-2,
+    0x1.0d50aa4ecf594p+1, -0x1.f088b6392ccdap-2, 0x1.0ede4acd9e4c6p+1, -0x1.f0e91601a0f8bp-2,
+    0x1.106c378468c87p+1, -0x1.f147260351ea1p-2, 0x1.11fa6e9eff8b6p+1, -0x1.f1a2f403f9951p-2,
+    0x1.1388ee541ad0cp+1, -0x1.f1fc8d7c78657p-2, 0x1.1517b4e51d5eep+1, -0x1.f253ff9a413c0p-2,
+    0x1.16a6c09dd8b65p+1, -0x1.f2a95740c1f57p-2, 0x1.18360fd452601p+1, -0x1.f2fca10ac853ep-2,
+    0x1.19c5a0e88a583p+1, -0x1.f34de94be326bp-2, 0x1.1b5572444291bp+1, -0x1.f39d3c11bf8f8p-2,
+    0x1.1ce5825ac7905p+1, -0x1.f3eaa52582473p-2, 0x1.1e75cfa8ba14fp+1, -0x1.f436300d1cc73p-2,
+    0x1.200658b3d9d99p+1, -0x1.f47fe80c9e3f9p-2, 0x1.21971c0ad1594p+1, -0x1.f4c7d82780447p-2,
+    0x1.2328184502a0ep+1, -0x1.f50e0b21ef202p-2, 0x1.24b94c0255247p+1, -0x1.f5528b820db93p-2,
+    0x1.264ab5eb04965p+1, -0x1.f595639134fe3p-2, 0x1.27dc54af70bc4p+1, -0x1.f5d69d5d2ecbep-2,
+    0x1.296e2707ee3e8p+1, -0x1.f61642b96c42ap-2, 0x1.2b002bb4986dcp+1, -0x1.f6545d4037842p-2,
+    0x1.2c92617d23fbbp+1, -0x1.f690f653e0d20p-2, 0x1.2e24c730b2a33p+1, -0x1.f6cc171fe7096p-2,
+    0x1.2fb75ba5a7bb4p+1, -0x1.f705c89a1b784p-2, 0x1.314a1db97db2bp+1, -0x1.f73e1383c10a4p-2,
+    0x1.32dd0c509c6eap+1, -0x1.f775006aa6cdfp-2, 0x1.34702656308abp+1, -0x1.f7aa97aa3dd26p-2,
+    0x1.36036abc03745p+1, -0x1.f7dee16caa604p-2, 0x1.3796d87a54601p+1, -0x1.f811e5abd0914p-2,
+    0x1.392a6e8fb213bp+1, -0x1.f843ac325c4adp-2, 0x1.3abe2c00d5813p+1, -0x1.f8743c9cc4a0ep-2,
+    0x1.3c520fd87d30bp+1, -0x1.f8a39e5a4aa85p-2, 0x1.3de6192749739p+1, -0x1.f8d1d8adf3be8p-2,
+    0x1.3f7a4703995ebp+1, -0x1.f8fef2af7f4ffp-2, 0x1.410e988968874p+1, -0x1.f92af34c58250p-2,
+    0x1.42a30cda2d7f4p+1, -0x1.f955e148813f4p-2, 0x1.4437a31cb90d8p+1, -0x1.f97fc33f7e512p-2,
+    0x1.45cc5a7d161e8p+1, -0x1.f9a89fa537da3p-2, 0x1.4761322c6a69ap+1, -0x1.f9d07cc6daf34p-2,
+    0x1.48f62960d7c81p+1, -0x1.f9f760cbb4d69p-2, 0x1.4a8b3f555e39cp+1, -0x1.fa1d51b60a2ebp-2,
+    0x1.4c207349be94fp+1, -0x1.fa425563ea39ep-2, 0x1.4db5c4825ddd3p+1, -0x1.fa66718ffdcd4p-2,
+    0x1.4f4b3248293e4p+1, -0x1.fa89abd252469p-2, 0x1.50e0bbe87aa83p+1, -0x1.faac09a12077dp-2,
+    0x1.527660b4fe08bp+1, -0x1.facd90518f9bdp-2, 0x1.540c2003971f5p+1, -0x1.faee45187460dp-2,
+    0x1.55a1f92e47e89p+1, -0x1.fb0e2d0b0c16dp-2, 0x1.5737eb93179ddp+1, -0x1.fb2d4d1fb410ep-2,
+    0x1.58cdf693fa467p+1, -0x1.fb4baa2e9d458p-2, 0x1.5a641996b8d6dp+1, -0x1.fb6948f27c3eep-2,
+    0x1.5bfa5404d9db1p+1, -0x1.fb862e0935674p-2, 0x1.5d90a54b8aaa8p+1, -0x1.fba25df485c13p-2,
+    0x1.5f270cdb89202p+1, -0x1.fbbddd1aa819bp-2, 0x1.60bd8a290dd69p+1, -0x1.fbd8afc6f6c2cp-2,
+    0x1.62541cabb6e3ap+1, -0x1.fbf2da2a89e4bp-2, 0x1.63eac3de73118p+1, -0x1.fc0c605cd2755p-2,
+    0x1.65817f3f6d92cp+1, -0x1.fc25465c31e29p-2, 0x1.67184e4ffa2e5p+1, -0x1.fc3d900e8e7fbp-2,
+    0x1.68af309481e0bp+1, -0x1.fc554141e4c30p-2, 0x1.6a4625946ff0fp+1, -0x1.fc6c5dacd562dp-2,
+    0x1.6bdd2cda1f757p+1, -0x1.fc82e8ef305f1p-2, 0x1.6d7445f2c9472p+1, -0x1.fc98e6927d070p-2,
+    0x1.6f0b706e72606p+1, -0x1.fcae5a0a7f078p-2, 0x1.70a2abdfdaa52p+1, -0x1.fcc346b5b890dp-2,
+    0x1.7239f7dc6c122p+1, -0x1.fcd7afdde9a1bp-2, 0x1.73d153fc2a50fp+1, -0x1.fceb98b88c84dp-2,
+    0x1.7568bfd9a2ae8p+1, -0x1.fcff04674f8eap-2, 0x1.77003b11dc722p+1, -0x1.fd11f5f88c28ep-2,
+    0x1.7897c54449926p+1, -0x1.fd247067bb38dp-2, 0x1.7a2f5e12b7c6bp+1, -0x1.fd36769de6edep-2,
+    0x1.7bc7052141f29p+1, -0x1.fd480b721a04ep-2, 0x1.7d5eba1641e91p+1, -0x1.fd5931a9cc8d2p-2,
+    0x1.7ef67c9a42864p+1, -0x1.fd69ebf94e3c5p-2, 0x1.808e4c57f21d0p+1, -0x1.fd7a3d042e5c8p-2,
+    0x1.822628fc1536dp+1, -0x1.fd8a275da1624p-2, 0x1.83be123579a44p+1, -0x1.fd99ad88e4356p-2,
+    0x1.855607b4e9dbcp+1, -0x1.fda8d1f99d395p-2, 0x1.86ee092d20a55p+1, -0x1.fdb797143b205p-2,
+    0x1.88861652bd115p+1, -0x1.fdc5ff2e51961p-2, 0x1.8a1e2edc36b88p+1, -0x1.fdd40c8ef3cb4p-2,
+    0x1.8bb65281d243cp+1, -0x1.fde1c16f0ceffp-2, 0x1.8d4e80fd9639ap+1, -0x1.fdef1ff9b6a52p-2,
+    0x1.8ee6ba0b4010cp+1, -0x1.fdfc2a4c8d72ep-2, 0x1.907efd6839849p+1, -0x1.fe08e278034bap-2,
+    0x1.92174ad38e2bap+1, -0x1.fe154a7fb028fp-2, 0x1.93afa20de14dap+1, -0x1.fe21645aa0cb0p-2,
+    0x1.954802d963f7bp+1, -0x1.fe2d31f3a3a54p-2, 0x1.96e06cf9cb4dap+1, -0x1.fe38b5299402bp-2,
+    0x1.9878e03447169p+1, -0x1.fe43efcfa36b0p-2, 0x1.9a115c4f78837p+1, -0x1.fe4ee3ada152cp-2,
+    0x1.9ba9e113692ecp+1, -0x1.fe599280411fep-2, 0x1.9d426e4982532p+1, -0x1.fe63fdf95e8b5p-2,
+    0x1.9edb03bc84386p+1, -0x1.fe6e27c0406a8p-2, 0x1.a073a1387dd50p+1, -0x1.fe781171d9e79p-2,
+    0x1.a20c468ac4a3ep+1, -0x1.fe81bca10a32ap-2, 0x1.a3a4f381ecabbp+1, -0x1.fe8b2ad6dab4bp-2,
+    0x1.a53da7edc0b7fp+1, -0x1.fe945d92bbcb8p-2, 0x1.a6d6639f3ac20p+1, -0x1.fe9d564ac0180p-2,
+    0x1.a86f26687c88dp+1, -0x1.fea6166bd6672p-2, 0x1.aa07f01cc856ep+1, -0x1.feae9f5a023c6p-2,
+    0x1.aba0c09079f44p+1, -0x1.feb6f2709306dp-2, 0x1.ad399798ffc51p+1, -0x1.febf11025a07ap-2,
+    0x1.aed2750cd411dp+1, -0x1.fec6fc59def26p-2, 0x1.b06b58c3767a1p+1, -0x1.feceb5b9934d3p-2,
+    0x1.b2044295658f5p+1, -0x1.fed63e5c0499ep-2, 0x1.b39d325c18977p+1, -0x1.fedd97740d4d2p-2,
+    0x1.b53627f1f9766p+1, -0x1.fee4c22d049c4p-2, 0x1.b6cf23325ebd3p+1, -0x1.feebbfaaed276p-2,
+    0x1.b86823f985de2p+1, -0x1.fef2910aa2874p-2, 0x1.ba012a248d84ep+1, -0x1.fef9376205c4fp-2,
+    0x1.bb9a35917011ap+1, -0x1.feffb3c028c1cp-2, 0x1.bd33461efe371p+1, -0x1.ff06072d7895ap-2,
+    0x1.becc5bacd9b92p+1, -0x1.ff0c32abe6ea9p-2, 0x1.c065761b704d3p+1, -0x1.ff123737125a8p-2,
+    0x1.c1fe954bf6998p+1, -0x1.ff1815c46dd5ap-2, 0x1.c397b92063547p+1, -0x1.ff1dcf4367172p-2,
+    0x1.c530e17b6a81ap+1, -0x1.ff23649d8c2dbp-2, 0x1.c6ca0e4078cd1p+1, -0x1.ff28d6b6b01dap-2,
+    0x1.c8633f53af034p+1, -0x1.ff2e266d0ea15p-2, 0x1.c9fc7499dda51p+1, -0x1.ff3354996f0dfp-2,
+    0x1.cb95adf880983p+1, -0x1.ff38620f46616p-2, 0x1.cd2eeb55baf15p+1, -0x1.ff3d4f9cd87e1p-2,
+    0x1.cec82c9852d9dp+1, -0x1.ff421e0b5899dp-2, 0x1.d06171a7ad8dfp+1, -0x1.ff46ce1f08e52p-2,
+    0x1.d1faba6bcb750p+1, -0x1.ff4b6097596e6p-2, 0x1.d39406cd44516p+1, -0x1.ff4fd62f06467p-2,
+    0x1.d52d56b543887p+1, -0x1.ff542f9c34eb3p-2, 0x1.d6c6aa0d84821p+1, -0x1.ff586d9090fbdp-2,
+    0x1.d86000c04f1e8p+1, -0x1.ff5c90b9683b8p-2, 0x1.d9f95ab874428p+1, -0x1.ff6099bfc5e6dp-2,
+    0x1.db92b7e14a791p+1, -0x1.ff6489488d5fap-2, 0x1.dd2c1826aaaa5p+1, -0x1.ff685ff49433dp-2,
+    0x1.dec57b74ece6fp+1, -0x1.ff6c1e60bb829p-2, 0x1.e05ee1b8e547bp+1, -0x1.ff6fc52608c3dp-2,
+    0x1.e1f84adfe0e08p+1, -0x1.ff7354d9bdf65p-2, 0x1.e391b6d7a2c69p+1, -0x1.ff76ce0d71374p-2,
+    0x1.e52b258e61296p+1, -0x1.ff7a314f23c76p-2, 0x1.e6c496f2c27ddp+1, -0x1.ff7d7f295880dp-2,
+    0x1.e85e0af3dabaep+1, -0x1.ff80b82329c1ap-2, 0x1.e9f7818128a7ep+1, -0x1.ff83dcc05ecdcp-2,
+    0x1.eb90fa8a933b9p+1, -0x1.ff86ed8180ab9p-2, 0x1.ed2a7600670bbp+1, -0x1.ff89eae3ee7f4p-2,
+    0x1.eec3f3d353cc9p+1, -0x1.ff8cd561f166dp-2, 0x1.f05d73f469e0ap+1, -0x1.ff8fad72cfda6p-2,
+    0x1.f1f6f65517f72p+1, -0x1.ff92738ae0942p-2, 0x1.f3907ae728b96p+1, -0x1.ff95281b9d01ap-2,
+    0x1.f52a019cc087ap+1, -0x1.ff97cb93b342fp-2, 0x1.f6c38a685b42ep+1, -0x1.ff9a5e5f17b8bp-2,
+    0x1.f85d153cca25cp+1, -0x1.ff9ce0e716250p-2, 0x1.f9f6a20d31a9fp+1, -0x1.ff9f539262616p-2,
+    0x1.fb9030cd077bap+1, -0x1.ffa1b6c528ac0p-2, 0x1.fd29c17010795p+1, -0x1.ffa40ae11d8f7p-2,
+    0x1.fec353ea5ec05p+1, -0x1.ffa650458d66cp-2, 0x1.002e741827e2ep+2, -0x1.ffa8874f6b80ep-2,
+    0x1.00fb3f1b453dap+2, -0x1.ffaab05960e4cp-2, 0x1.01c80af8febfap+2, -0x1.ffaccbbbdab9cp-2,
+    0x1.0294d7abeeaccp+2, -0x1.ffaed9cd18559p-2, 0x1.0361a52ed1609p+2, -0x1.ffb0dae138f23p-2,
+    0x1.042e737c84778p+2, -0x1.ffb2cf4a490dfp-2, 0x1.04fb429005fd2p+2, -0x1.ffb4b7584f782p-2,
+    0x1.05c81264739f3p+2, -0x1.ffb693595a0bbp-2, 0x1.0694e2f509e68p+2, -0x1.ffb863998a19cp-2,
+    0x1.0761b43d23739p+2, -0x1.ffba286320871p-2, 0x1.082e863838416p+2, -0x1.ffbbe1fe899d3p-2,
+    0x1.08fb58e1dceb8p+2, -0x1.ffbd90b268916p-2, 0x1.09c82c35c1fa0p+2, -0x1.ffbf34c3a2c35p-2,
+    0x1.0a95002fb330cp+2, -0x1.ffc0ce756ab59p-2, 0x1.0b61d4cb96e3bp+2, -0x1.ffc25e094ac10p-2,
+    0x1.0c2eaa056d4f5p+2, -0x1.ffc3e3bf2f84dp-2, 0x1.0cfb7fd94ff4cp+2, -0x1.ffc55fd57215ap-2,
+    0x1.0dc8564370fa9p+2, -0x1.ffc6d288e1ec1p-2, 0x1.0e952d401a912p+2, -0x1.ffc83c14ce957p-2,
+    0x1.0f6204cbae5a9p+2, -0x1.ffc99cb311272p-2, 0x1.102edce2a4d73p+2, -0x1.ffcaf49c15773p-2,
+    0x1.10fbb5818cd4bp+2, -0x1.ffcc4406e31a7p-2, 0x1.11c88ea50ae19p+2, -0x1.ffcd8b29262a6p-2,
+    0x1.12956849d8c3ap+2, -0x1.ffceca3737d3fp-2, 0x1.1362426cc4f23p+2, -0x1.ffd0016426b08p-2,
+    0x1.142f1d0ab2132p+2, -0x1.ffd130e1beea1p-2, 0x1.14fbf820967bap+2, -0x1.ffd258e0922d0p-2,
+    0x1.15c8d3ab7bb3fp+2, -0x1.ffd3798fff66cp-2, 0x1.1695afa87dfddp+2, -0x1.ffd4931e3a552p-2,
+    0x1.17628c14cbde7p+2, -0x1.ffd5a5b852e4ep-2, 0x1.182f68eda5ab4p+2, -0x1.ffd6b18a3c629p-2,
+    0x1.18fc46305d18fp+2, -0x1.ffd7b6bed47e2p-2, 0x1.19c923da54ce4p+2, -0x1.ffd8b57fea222p-2,
+    0x1.1a9601e8fff89p+2, -0x1.ffd9adf644202p-2, 0x1.1b62e059e1e3bp+2, -0x1.ffdaa049a7b2bp-2,
+    0x1.1c2fbf2a8d93fp+2, -0x1.ffdb8ca0ded73p-2, 0x1.1cfc9e58a562fp+2, -0x1.ffdc7321be7ecp-2,
+    0x1.1dc97de1da9eap+2, -0x1.ffdd53f12c98ep-2, 0x1.1e965dc3ed2adp+2, -0x1.ffde2f3325f79p-2,
+    0x1.1f633dfcab252p+2, -0x1.ffdf050ac40ebp-2, 0x1.20301e89f08afp+2, -0x1.ffdfd59a428f0p-2,
+    0x1.20fcff69a6e1fp+2, -0x1.ffe0a10304ddcp-2, 0x1.21c9e099c4e28p+2, -0x1.ffe167659b6a3p-2,
+    0x1.2296c2184e244p+2, -0x1.ffe228e1c8e10p-2, 0x1.2363a3e352ccdp+2, -0x1.ffe2e596873f7p-2,
+    0x1.243085f8ef408p+2, -0x1.ffe39da20cc5fp-2, 0x1.24fd68574bd4dp+2, -0x1.ffe45121d0cc3p-2,
+    0x1.25ca4afc9c853p+2, -0x1.ffe5003290768p-2, 0x1.26972de720a92p+2, -0x1.ffe5aaf0534d0p-2,
+    0x1.2764111522ac9p+2, -0x1.ffe651766fb6dp-2, 0x1.2830f484f7c9fp+2, -0x1.ffe6f3df8f586p-2,
+    0x1.28fdd834ffc5ap+2, -0x1.ffe79245b3563p-2, 0x1.29cabc23a4abbp+2, -0x1.ffe82cc2387d2p-2,
+    0x1.2a97a04f5a8e8p+2, -0x1.ffe8c36ddb502p-2, 0x1.2b6484b69f47ep+2, -0x1.ffe95660bbfc7p-2,
+    0x1.2c316957fa3acp+2, -0x1.ffe9e5b262353p-2, 0x1.2cfe4e31fc175p+2, -0x1.ffea7179c0f62p-2,
+    0x1.2dcb33433e9ffp+2, -0x1.ffeaf9cd3a2f2p-2, 0x1.2e98188a64703p+2, -0x1.ffeb7ec2a2582p-2,
+    0x1.2f64fe0618c47p+2, -0x1.ffec006f43ef0p-2, 0x1.3031e3b50f43dp+2, -0x1.ffec7ee7e2dedp-2,
+    0x1.30fec99603ca8p+2, -0x1.ffecfa40bfd21p-2, 0x1.31cbafa7ba367p+2, -0x1.ffed728d9b6fcp-2,
+    0x1.329895e8fe341p+2, -0x1.ffede7e1b9843p-2, 0x1.33657c58a30d9p+2, -0x1.ffee5a4fe4157p-2,
+    0x1.343262f5837a6p+2, -0x1.ffeec9ea6e651p-2, 0x1.34ff49be81704p+2, -0x1.ffef36c337de3p-2,
+    0x1.35cc30b285f5bp+2, -0x1.ffefa0ebaef15p-2, 0x1.369917d080f51p+2, -0x1.fff00874d3de6p-2,
+    0x1.3765ff1769113p+2, -0x1.fff06d6f3b6ccp-2, 0x1.3832e6863b7aap+2, -0x1.fff0cfeb11924p-2,
+    0x1.38ffce1bfbc6ap+2, -0x1.fff12ff81c09cp-2, 0x1.39ccb5d7b3c67p+2, -0x1.fff18da5bcd8bp-2,
+    0x1.3a999db8735fep+2, -0x1.fff1e902f4c59p-2, 0x1.3b6685bd50671p+2, -0x1.fff2421e65be0p-2,
+    0x1.3c336de56678dp+2, -0x1.fff29906552e9p-2, 0x1.3d00562fd6d60p+2, -0x1.fff2edc8ae4adp-2,
+    0x1.3dcd3e9bc8403p+2, -0x1.fff340730447fp-2, 0x1.3e9a272866d68p+2, -0x1.fff3911294887p-2,
+    0x1.3f670fd4e3f3dp+2, -0x1.fff3dfb448bacp-2, 0x1.4033f8a0760ddp+2, -0x1.fff42c64b8ea2p-2,
+    0x1.4100e18a58948p+2, -0x1.fff477302d82ap-2, 0x1.41cdca91cbd2fp+2, -0x1.fff4c022a1483p-2,
+    0x1.429ab3b614d06p+2, -0x1.fff50747c341bp-2, 0x1.43679cf67d324p+2, -0x1.fff54caaf8975p-2,
+    0x1.44348652531f7p+2, -0x1.fff590575e65dp-2, 0x1.45016fc8e9232p+2, -0x1.fff5d257cb856p-2,
+    0x1.45ce595996118p+2, -0x1.fff612b6d2463p-2, 0x1.469b4303b4ecap+2, -0x1.fff6517ec2217p-2,
+    0x1.47682cc6a4c9ap+2, -0x1.fff68eb9a95fbp-2, 0x1.483516a1c8b78p+2, -0x1.fff6ca7156b53p-2,
+    0x1.4902009487a58p+2, -0x1.fff704af5ad36p-2, 0x1.49ceea9e4c4b0p+2, -0x1.fff73d7d09f14p-2,
+    0x1.4a9bd4be850f3p+2, -0x1.fff774e37d497p-2, 0x1.4b68bef4a3f21p+2, -0x1.fff7aaeb948efp-2,
+    0x1.4c35a9401e75bp+2, -0x1.fff7df9df7594p-2, 0x1.4d0293a06d87cp+2, -0x1.fff8130316866p-2,
+    0x1.4dcf7e150d6c4p+2, -0x1.fff845232d956p-2, 0x1.4e9c689d7da82p+2, -0x1.fff8760643f77p-2,
+    0x1.4f69533940ecep+2, -0x1.fff8a5b42e58fp-2, 0x1.50363de7dd047p+2, -0x1.fff8d4348fe28p-2,
+    0x1.510328a8dabd9p+2, -0x1.fff9018edb71fp-2, 0x1.51d0137bc5d8cp+2, -0x1.fff92dca54cb9p-2,
+    0x1.529cfe602cf5ap+2, -0x1.fff958ee11c40p-2, 0x1.5369e955a180ep+2, -0x1.fff98300fb626p-2,
+    0x1.5436d45bb7a26p+2, -0x1.fff9ac09cefc0p-2, 0x1.5503bf72062c1p+2, -0x1.fff9d40f1f482p-2,
+    0x1.55d0aa9826890p+2, -0x1.fff9fb17556d9p-2, 0x1.569d95cdb4acfp+2, -0x1.fffa2128b209bp-2,
+    0x1.576a81124f047p+2, -0x1.fffa46494e306p-2, 0x1.58376c659664fp+2, -0x1.fffa6a7f1c661p-2,
+    0x1.590457c72dfe0p+2, -0x1.fffa8dcfe993bp-2, 0x1.59d14336bb49dp+2, -0x1.fffab0415df45p-2,
+    0x1.5a9e2eb3e5ff5p+2, -0x1.fffad1d8fdfd2p-2, 0x1.5b6b1a3e5803ap+2, -0x1.fffaf29c2b3f8p-2,
+    0x1.5c3805d5bd5c7p+2, -0x1.fffb12902545bp-2, 0x1.5d04f179c4227p+2, -0x1.fffb31ba0a69ep-2,
+    0x1.5dd1dd2a1c748p+2, -0x1.fffb501ed8a81p-2, 0x1.5e9ec8e6786a6p+2, -0x1.fffb6dc36e6aep-2,
+    0x1.5f6bb4ae8c08bp+2, -0x1.fffb8aac8b52ep-2, 0x1.6038a0820d34ap+2, -0x1.fffba6ded0f96p-2,
+    0x1.61058c60b3a7ep+2, -0x1.fffbc25ec3ae4p-2, 0x1.61d2784a38e55p+2, -0x1.fffbdd30cb316p-2,
+    0x1.629f643e582d8p+2, -0x1.fffbf7593366cp-2, 0x1.636c503cce73ep+2, -0x1.fffc10dc2d071p-2,
+    0x1.64393c455a53ep+2, -0x1.fffc29bdce4b4p-2, 0x1.65062857bc066p+2, -0x1.fffc420213944p-2,
+    0x1.65d31473b557ep+2, -0x1.fffc59ace00e3p-2, 0x1.66a00099099dep+2, -0x1.fffc70c1fe4fep-2,
+    0x1.676cecc77dadep+2, -0x1.fffc874520f64p-2, 0x1.6839d8fed7d35p+2, -0x1.fffc9d39e33c1p-2,
+    0x1.6906c53edfc6cp+2, -0x1.fffcb2a3c98d8p-2, 0x1.69d3b1875ea49p+2, -0x1.fffcc7864218ap-2,
+    0x1.6aa09dd81ee44p+2, -0x1.fffcdbe4a55a0p-2, 0x1.6b6d8a30ec4ffp+2, -0x1.fffcefc236a5bp-2,
+    0x1.6c3a769193fbfp+2, -0x1.fffd032224ad4p-2, 0x1.6d0762f9e43e9p+2, -0x1.fffd16078a023p-2,
+    0x1.6dd44f69aca83p+2, -0x1.fffd28756d94fp-2, 0x1.6ea13be0bdfb9p+2, -0x1.fffd3a6ec3318p-2,
+    0x1.6f6e285eea263p+2, -0x1.fffd4bf66bf7fp-2, 0x1.703b14e40438dp+2, -0x1.fffd5d0f36d2fp-2,
+    0x1.7108016fe060ap+2, -0x1.fffd6dbbe0ea8p-2, 0x1.71d4ee0253dfcp+2, -0x1.fffd7dff1614ap-2,
+    0x1.72a1da9b3506bp+2, -0x1.fffd8ddb7142ap-2, 0x1.736ec73a5b2dap+2, -0x1.fffd9d537cec1p-2,
+    0x1.743bb3df9eadbp+2, -0x1.fffdac69b376cp-2, 0x1.7508a08ad8db1p+2, -0x1.fffdbb207f9cap-2,
+    0x1.75d58d3be3fe4p+2, -0x1.fffdc97a3ccebp-2, 0x1.76a279f29b4e6p+2, -0x1.fffdd7793795bp-2,
+    0x1.776f66aedaeb5p+2, -0x1.fffde51fadf07p-2, 0x1.783c53707fd79p+2, -0x1.fffdf26fcfaf9p-2,
+    0x1.7909403767f34p+2, -0x1.fffdff6bbecf9p-2, 0x1.79d62d0371f60p+2, -0x1.fffe0c158fcfdp-2,
+    0x1.7aa319d47d6a2p+2, -0x1.fffe186f4a083p-2, 0x1.7b7006aa6aa74p+2, -0x1.fffe247ae7fc3p-2,
+    0x1.7c3cf3851acd0p+2, -0x1.fffe303a57abdp-2, 0x1.7d09e0646fbe8p+2, -0x1.fffe3baf7ae33p-2,
+    0x1.7dd6cd484c1d3p+2, -0x1.fffe46dc27872p-2, 0x1.7ea3ba3093445p+2, -0x1.fffe51c227e10p-2,
+    0x1.7f70a71d29445p+2, -0x1.fffe5c633ae7bp-2, 0x1.803d940df2de2p+2, -0x1.fffe66c114878p-2,
+    0x1.810a8102d57f4p+2, -0x1.fffe70dd5de7bp-2, 0x1.81d76dfbb73d0p+2, -0x1.fffe7ab9b5aeep-2,
+    0x1.82a45af87ed0cp+2, -0x1.fffe8457b0454p-2, 0x1.837147f91393cp+2, -0x1.fffe8db8d8158p-2,
+    0x1.843e34fd5d7b1p+2, -0x1.fffe96deadcbbp-2, 0x1.850b22054513dp+2, -0x1.fffe9fcaa8936p-2,
+    0x1.85d80f10b37f8p+2, -0x1.fffea87e36534p-2, 0x1.86a4fc1f92702p+2, -0x1.fffeb0fabbe81p-2,
+    0x1.8771e931cc24fp+2, -0x1.fffeb941955d8p-2, 0x1.883ed6474b66bp+2, -0x1.fffec15416264p-2,
+    0x1.890bc35ffb843p+2, -0x1.fffec93389522p-2, 0x1.89d8b07bc84f4p+2, -0x1.fffed0e131c34p-2,
+    0x1.8aa59d9a9e194p+2, -0x1.fffed85e4a61ap-2, 0x1.8b728abc69b02p+2, -0x1.fffedfac064dep-2,
+    0x1.8c3f77e1185b2p+2, -0x1.fffee6cb91120p-2, 0x1.8d0c650897d7fp+2, -0x1.fffeedbe0ed1dp-2,
+    0x1.8dd95232d657cp+2, -0x1.fffef4849c797p-2, 0x1.8ea63f5fc27c5p+2, -0x1.fffefb204feb1p-2,
+    0x1.8f732c8f4b555p+2, -0x1.ffff0192382b6p-2, 0x1.904019c1605d7p+2, -0x1.ffff07db5d8d3p-2,
+    0x1.910d06f5f1781p+2, -0x1.ffff0dfcc1db8p-2, 0x1.91d9f42ceeee3p+2, -0x1.ffff13f76082fp-2,
+    0x1.92a6e166496c8p+2, -0x1.ffff19cc2eba2p-2, 0x1.9373cea1f2005p+2, -0x1.ffff1f7c1ba8cp-2,
+    0x1.9440bbdfda15bp+2, -0x1.ffff2508108e1p-2, 0x1.950da91ff374ep+2, -0x1.ffff2a70f0e62p-2,
+    0x1.95da9662303ffp+2, -0x1.ffff2fb79a8e5p-2, 0x1.96a783a682f0bp+2, -0x1.ffff34dce5e8dp-2,
+    0x1.977470ecde568p+2, -0x1.ffff39e1a5ff6p-2, 0x1.98415e3535942p+2, -0x1.ffff3ec6a8a50p-2,
+    0x1.990e4b7f7c1dcp+2, -0x1.ffff438cb6970p-2, 0x1.99db38cba5b6dp+2, -0x1.ffff4834939d1p-2,
+    0x1.9aa82619a6702p+2, -0x1.ffff4cbefea8cp-2, 0x1.9b75136972a62p+2, -0x1.ffff512cb1f40p-2,
+    0x1.9c4200bafefecp+2, -0x1.ffff557e631f0p-2, 0x1.9d0eee0e4067cp+2, -0x1.ffff59b4c34d3p-2,
+    0x1.9ddbdb632c14ep+2, -0x1.ffff5dd07f41cp-2, 0x1.9ea8c8b9b77e3p+2, -0x1.ffff61d23f7b4p-2,
+    0x1.9f75b611d85e6p+2, -0x1.ffff65baa84e8p-2, 0x1.a042a36b84b12p+2, -0x1.ffff698a5a014p-2,
+    0x1.a10f90c6b2b15p+2, -0x1.ffff6d41f0e37p-2, 0x1.a1dc7e2358d7cp+2, -0x1.ffff70e205686p-2,
+    0x1.a2a96b816dd97p+2, -0x1.ffff746b2c3f6p-2, 0x1.a37658e0e8a64p+2, -0x1.ffff77ddf66b4p-2,
+    0x1.a4434641c0673p+2, -0x1.ffff7b3af159cp-2, 0x1.a51033a3ec7d7p+2, -0x1.ffff7e82a6fa3p-2,
+    0x1.a5dd210764806p+2, -0x1.ffff81b59dd37p-2, 0x1.a6aa0e6c203cep+2, -0x1.ffff84d45919bp-2,
+    0x1.a776fbd217b37p+2, -0x1.ffff87df58c34p-2, 0x1.a843e93943175p+2, -0x1.ffff8ad7199d1p-2,
+    0x1.a910d6a19accep+2, -0x1.ffff8dbc155efp-2, 0x1.a9ddc40b1768ep+2, -0x1.ffff908ec2bedp-2,
+    0x1.aaaab175b1aedp+2, -0x1.ffff934f9583cp-2, 0x1.ab779ee1628ffp+2, -0x1.ffff95fefe98bp-2,
+    0x1.ac448c4e232a4p+2, -0x1.ffff989d6c1e7p-2, 0x1.ad1179bbecc73p+2, -0x1.ffff9b2b497d4p-2,
+    0x1.adde672ab8dacp+2, -0x1.ffff9da8ff760p-2, 0x1.aeab549a81023p+2, -0x1.ffffa016f4333p-2,
+    0x1.af78420b3f034p+2, -0x1.ffffa2758b592p-2, 0x1.b0452f7ceccb1p+2, -0x1.ffffa4c52615fp-2,
+    0x1.b1121cef846d2p+2, -0x1.ffffa70623312p-2, 0x1.b1df0a6300228p+2, -0x1.ffffa938df1acp-2,
+    0x1.b2abf7d75a48ap+2, -0x1.ffffab5db3fa3p-2, 0x1.b378e54c8d60bp+2, -0x1.ffffad74f9bcdp-2,
+    0x1.b445d2c2940e9p+2, -0x1.ffffaf7f0623cp-2, 0x1.b512c03969183p+2, -0x1.ffffb17c2cd1ep-2,
+    0x1.b5dfadb107646p+2, -0x1.ffffb36cbf58fp-2, 0x1.b6ac9b2969fa3p+2, -0x1.ffffb5510d470p-2,
+    0x1.b77988a28c004p+2, -0x1.ffffb7296432ep-2, 0x1.b846761c68bbdp+2, -0x1.ffffb8f60fc8ap-2,
+    0x1.b9136396fb901p+2, -0x1.ffffbab759d5ep-2, 0x1.b9e051123ffd3p+2, -0x1.ffffbc6d8a555p-2,
+    0x1.baad3e8e31a02p+2, -0x1.ffffbe18e77a7p-2, 0x1.bb7a2c0acc314p+2, -0x1.ffffbfb9b5bcep-2,
+    0x1.bc4719880b844p+2, -0x1.ffffc15037e31p-2, 0x1.bd140705eb871p+2, -0x1.ffffc2dcaf0d4p-2,
+    0x1.bde0f48468417p+2, -0x1.ffffc45f5abfbp-2, 0x1.beade2037dd43p+2, -0x1.ffffc5d878ed0p-2,
+    0x1.bf7acf832878bp+2, -0x1.ffffc74845fffp-2, 0x1.c047bd0364801p+2, -0x1.ffffc8aefce54p-2,
+    0x1.c114aa842e52ep+2, -0x1.ffffca0cd714fp-2, 0x1.c1e1980582705p+2, -0x1.ffffcb620c9b8p-2,
+    0x1.c2ae85875d6dcp+2, -0x1.ffffccaed4232p-2, 0x1.c37b7309bbf62p+2, -0x1.ffffcdf362fc1p-2,
+    0x1.c448608c9ac99p+2, -0x1.ffffcf2fed258p-2, 0x1.c5154e0ff6bc9p+2, -0x1.ffffd064a555dp-2,
+    0x1.c5e23b93ccb7ep+2, -0x1.ffffd191bd027p-2, 0x1.c6af291819b7ap+2, -0x1.ffffd2b764685p-2,
+    0x1.c77c169cdacb2p+2, -0x1.ffffd3d5ca930p-2, 0x1.c84904220d144p+2, -0x1.ffffd4ed1d64bp-2,
+    0x1.c915f1a7adc6fp+2, -0x1.ffffd5fd899d5p-2, 0x1.c9e2df2dba28fp+2, -0x1.ffffd7073ae1ep-2,
+    0x1.caafccb42f913p+2, -0x1.ffffd80a5bc34p-2, 0x1.cb7cba3b0b677p+2, -0x1.ffffd90715c52p-2,
+    0x1.cc49a7c24b23dp+2, -0x1.ffffd9fd9164bp-2, 0x1.cd169549ec4e9p+2, -0x1.ffffdaedf61eep-2,
+    0x1.cde382d1ec7f8p+2, -0x1.ffffdbd86a772p-2, 0x1.ceb0705a495d9p+2, -0x1.ffffdcbd13fd2p-2,
+    0x1.cf7d5de3009ebp+2, -0x1.ffffdd9c17531p-2, 0x1.d04a4b6c10073p+2, -0x1.ffffde7598337p-2,
+    0x1.d11738f575698p+2, -0x1.ffffdf49b976dp-2, 0x1.d1e4267f2ea5ep+2, -0x1.ffffe0189d194p-2,
+    0x1.d2b1140939aa0p+2, -0x1.ffffe0e264400p-2, 0x1.d37e01939470bp+2, -0x1.ffffe1a72f3eap-2,
+    0x1.d44aef1e3d017p+2, -0x1.ffffe2671d9c4p-2, 0x1.d517dca931705p+2, -0x1.ffffe3224e189p-2,
+    0x1.d5e4ca346fdd7p+2, -0x1.ffffe3d8deb0ep-2, 0x1.d6b1b7bff674dp+2, -0x1.ffffe48aeca4cp-2,
+    0x1.d77ea54bc36e2p+2, -0x1.ffffe538947adp-2, 0x1.d84b92d7d50c2p+2, -0x1.ffffe5e1f2053p-2,
+    0x1.d9188064299ccp+2, -0x1.ffffe68720662p-2, 0x1.d9e56df0bf78ap+2, -0x1.ffffe7283a145p-2,
+    0x1.dab25b7d9502ap+2, -0x1.ffffe7c558deep-2, 0x1.db7f490aa8a83p+2, -0x1.ffffe85e95f20p-2,
+    0x1.dc4c3697f8e07p+2, -0x1.ffffe8f409da6p-2, 0x1.dd192425842c3p+2, -0x1.ffffe985cc89ap-2,
+    0x1.dde611b34915fp+2, -0x1.ffffea13f559dp-2, 0x1.deb2ff4146314p+2, -0x1.ffffea9e9b116p-2,
+    0x1.df7feccf7a1abp+2, -0x1.ffffeb25d3e6cp-2, 0x1.e04cda5de377bp+2, -0x1.ffffeba9b583dp-2,
+    0x1.e119c7ec80f62p+2, -0x1.ffffec2a55096p-2, 0x1.e1e6b57b514c5p+2, -0x1.ffffeca7c712dp-2,
+    0x1.e2b3a30a5338cp+2, -0x1.ffffed221fb91p-2, 0x1.e38090998581cp+2, -0x1.ffffed997295ep-2,
+    0x1.e44d7e28e6f58p+2, -0x1.ffffee0dd2c72p-2, 0x1.e51a6bb87669bp+2, -0x1.ffffee7f52f1cp-2,
+    0x1.e5e7594832bb5p+2, -0x1.ffffeeee0544ep-2, 0x1.e6b446d81acebp+2, -0x1.ffffef59fb7c7p-2,
+    0x1.e78134682d8f1p+2, -0x1.ffffefc346e46p-2, 0x1.e84e21f869ee8p+2, -0x1.fffff029f85b3p-2,
+    0x1.e91b0f88cee5cp+2, -0x1.fffff08e20549p-2, 0x1.e9e7fd195b742p+2, -0x1.fffff0efcedc5p-2,
+    0x1.eab4eaaa0e9f4p+2, -0x1.fffff14f1398bp-2, 0x1.eb81d83ae772dp+2, -0x1.fffff1abfdccfp-2,
+    0x1.ec4ec5cbe500dp+2, -0x1.fffff2069c5bep-2, 0x1.ed1bb35d0660cp+2, -0x1.fffff25efdca0p-2,
+    0x1.ede8a0ee4ab04p+2, -0x1.fffff2b530403p-2, 0x1.eeb58e7fb1125p+2, -0x1.fffff309418dap-2,
+    0x1.ef827c1138af7p+2, -0x1.fffff35b3f2a3p-2, 0x1.f04f69a2e0b57p+2, -0x1.fffff3ab3638ap-2,
+    0x1.f11c5734a8575p+2, -0x1.fffff3f933889p-2, 0x1.f1e944c68ecd3p+2, -0x1.fffff4454398ap-2,
+    0x1.f2b6325893542p+2, -0x1.fffff48f72986p-2, 0x1.f3831feab52dfp+2, -0x1.fffff4d7cc6a5p-2,
+    0x1.f4500d7cf3a12p+2, -0x1.fffff51e5ca5dp-2, 0x1.f51cfb0f4df8dp+2, -0x1.fffff5632e98fp-2,
+    0x1.f5e9e8a1c384ap+2, -0x1.fffff5a64d4a3p-2, 0x1.f6b6d63453989p+2, -0x1.fffff5e7c37a7p-2,
+    0x1.f783c3c6fd8cbp+2, -0x1.fffff6279ba66p-2, 0x1.f850b159c0bd8p+2, -0x1.fffff665e008ap-2,
+    0x1.f91d9eec9c8b4p+2, -0x1.fffff6a29a9adp-2, 0x1.f9ea8c7f905a6p+2, -0x1.fffff6ddd517cp-2,
+    0x1.fab77a129b930p+2, -0x1.fffff71798fc9p-2, 0x1.fb8467a5bda11p+2, -0x1.fffff74fef8a6p-2,
+    0x1.fc515538f5f43p+2, -0x1.fffff786e1c7ep-2, 0x1.fd1e42cc43ff7p+2, -0x1.fffff7bc78827p-2,
+    0x1.fdeb305fa7398p+2, -0x1.fffff7f0bc501p-2, 0x1.feb81df31f1c7p+2, -0x1.fffff823b5904p-2,
+    0x1.ff850b86ab258p+2, -0x1.fffff8556c6dap-2, 0x1.0028fc8d256abp+3, -0x1.fffff885e8df1p-2,
+    0x1.008f7356fed7dp+3, -0x1.fffff8b532a94p-2, 0x1.00f5ea20e19dap+3, -0x1.fffff8e3515f9p-2,
+    0x1.015c60eacd80ep+3, -0x1.fffff9104c659p-2, 0x1.01c2d7b4c2480p+3, -0x1.fffff93c2af01p-2,
+    0x1.02294e7ebfbadp+3, -0x1.fffff966f4064p-2, 0x1.028fc548c5a26p+3, -0x1.fffff990ae82fp-2,
+    0x1.02f63c12d3c94p+3, -0x1.fffff9b961159p-2, 0x1.035cb2dce9fb5p+3, -0x1.fffff9e112434p-2,
+    0x1.03c329a70805ap+3, -0x1.fffffa07c867ep-2, 0x1.0429a0712db6ap+3, -0x1.fffffa2d89b73p-2,
+    0x1.0490173b5addep+3, -0x1.fffffa525c3d9p-2, 0x1.04f68e058f4c4p+3, -0x1.fffffa7645e15p-2,
+    0x1.055d04cfcad3ap+3, -0x1.fffffa994c635p-2, 0x1.05c37b9a0d474p+3, -0x1.fffffabb75600p-2,
+    0x1.0629f264567b3p+3, -0x1.fffffadcc6508p-2, 0x1.0690692ea644dp+3, -0x1.fffffafd448b2p-2,
+    0x1.06f6dff8fc7a8p+3, -0x1.fffffb1cf5449p-2, 0x1.075d56c358f39p+3, -0x1.fffffb3bdd909p-2,
+    0x1.07c3cd8dbb888p+3, -0x1.fffffb5a0262bp-2, 0x1.082a445824129p+3, -0x1.fffffb77688f5p-2,
+    0x1.0890bb22926c2p+3, -0x1.fffffb9414cc3p-2, 0x1.08f731ed06707p+3, -0x1.fffffbb00bb13p-2,
+    0x1.095da8b77ffbbp+3, -0x1.fffffbcb51b95p-2, 0x1.09c41f81feeaep+3, -0x1.fffffbe5eb432p-2,
+    0x1.0a2a964c831bep+3, -0x1.fffffbffdc919p-2, 0x1.0a910d170c6d8p+3, -0x1.fffffc1929ccap-2,
+    0x1.0af783e19abf5p+3, -0x1.fffffc31d7021p-2, 0x1.0b5dfaac2df1bp+3, -0x1.fffffc49e825dp-2,
+    0x1.0bc47176c5e5cp+3, -0x1.fffffc6161132p-2, 0x1.0c2ae841627d6p+3, -0x1.fffffc78458c8p-2,
+    0x1.0c915f0c039b6p+3, -0x1.fffffc8e993d0p-2, 0x1.0cf7d5d6a9230p+3, -0x1.fffffca45fb83p-2,
+    0x1.0d5e4ca152f86p+3, -0x1.fffffcb99c7b4p-2, 0x1.0dc4c36c01005p+3, -0x1.fffffcce52ed2p-2,
+    0x1.0e2b3a36b3203p+3, -0x1.fffffce2865f5p-2, 0x1.0e91b101693e3p+3, -0x1.fffffcf63a0e6p-2,
+    0x1.0ef827cc23411p+3, -0x1.fffffd0971226p-2, 0x1.0f5e9e96e1102p+3, -0x1.fffffd1c2eaf4p-2,
+    0x1.0fc51561a2936p+3, -0x1.fffffd2e75b5cp-2, 0x1.102b8c2c67b37p+3, -0x1.fffffd4049238p-2,
+    0x1.109202f730597p+3, -0x1.fffffd51abd38p-2, 0x1.10f879c1fc6f1p+3, -0x1.fffffd62a08edp-2,
+    0x1.115ef08ccbde9p+3, -0x1.fffffd732a0cep-2, 0x1.11c567579e92dp+3, -0x1.fffffd834af40p-2,
+    0x1.122bde2274772p+3, -0x1.fffffd9305d99p-2, 0x1.129254ed4d775p+3, -0x1.fffffda25d42cp-2,
+    0x1.12f8cbb8297fcp+3, -0x1.fffffdb153a4dp-2, 0x1.135f4283087d3p+3, -0x1.fffffdbfeb655p-2,
+    0x1.13c5b94dea5d0p+3, -0x1.fffffdce26dadp-2, 0x1.142c3018cf0cep+3, -0x1.fffffddc084d1p-2,
+    0x1.1492a6e3b67b2p+3, -0x1.fffffde991f54p-2, 0x1.14f91daea0965p+3, -0x1.fffffdf6c5febp-2,
+    0x1.155f94798d4d8p+3, -0x1.fffffe03a686ep-2, 0x1.15c60b447c904p+3, -0x1.fffffe10359dep-2,
+    0x1.162c820f6e4e8p+3, -0x1.fffffe1c7546ep-2, 0x1.1692f8da62787p+3, -0x1.fffffe2867783p-2,
+    0x1.16f96fa558fecp+3, -0x1.fffffe340e1bcp-2, 0x1.175fe67051d2ap+3, -0x1.fffffe3f6b0f6p-2,
+    0x1.17c65d3b4ce57p+3, -0x1.fffffe4a80253p-2, 0x1.182cd4064a28fp+3, -0x1.fffffe554f23bp-2,
+    0x1.18934ad1498f6p+3, -0x1.fffffe5fd9c62p-2, 0x1.18f9c19c4b0b2p+3, -0x1.fffffe6a21bcep-2,
+    0x1.196038674e8f1p+3, -0x1.fffffe7428ad9p-2, 0x1.19c6af32540e6p+3, -0x1.fffffe7df0338p-2,
+    0x1.1a2d25fd5b7c7p+3, -0x1.fffffe8779dfcp-2, 0x1.1a939cc864cd2p+3, -0x1.fffffe90c7398p-2,
+    0x1.1afa13936ff48p+3, -0x1.fffffe99d9be3p-2, 0x1.1b608a5e7ce6dp+3, -0x1.fffffea2b2e1fp-2,
+    0x1.1bc701298b98ep+3, -0x1.fffffeab540fcp-2, 0x1.1c2d77f49bff9p+3, -0x1.fffffeb3bea96p-2,
+    0x1.1c93eebfae101p+3, -0x1.fffffebbf4082p-2, 0x1.1cfa658ac1bfep+3, -0x1.fffffec3f57cap-2,
+    0x1.1d60dc55d704dp+3, -0x1.fffffecbc44f4p-2, 0x1.1dc75320edd4cp+3, -0x1.fffffed361c02p-2,
+    0x1.1e2dc9ec06260p+3, -0x1.fffffedacf07bp-2, 0x1.1e9440b71fef0p+3, -0x1.fffffee20d567p-2,
+    0x1.1efab7823b268p+3, -0x1.fffffee91dd58p-2, 0x1.1f612e4d57c37p+3, -0x1.fffffef001a6ap-2,
+    0x1.1fc7a51875bd0p+3, -0x1.fffffef6b9e46p-2, 0x1.202e1be3950a9p+3, -0x1.fffffefd47a25p-2,
+    0x1.209492aeb5a3bp+3, -0x1.ffffff03abed5p-2, 0x1.20fb0979d7803p+3, -0x1.ffffff09e7cb7p-2,
+    0x1.21618044fa982p+3, -0x1.ffffff0ffc3c7p-2, 0x1.21c7f7101ee3cp+3, -0x1.ffffff15ea399p-2,
+    0x1.222e6ddb445b5p+3, -0x1.ffffff1bb2b61p-2, 0x1.2294e4a66af78p+3, -0x1.ffffff21569f3p-2,
+    0x1.22fb5b7192b11p+3, -0x1.ffffff26d6dc2p-2, 0x1.2361d23cbb810p+3, -0x1.ffffff2c344eap-2,
+    0x1.23c84907e5605p+3, -0x1.ffffff316fd2bp-2, 0x1.242ebfd310487p+3, -0x1.ffffff368a3eep-2,
+    0x1.2495369e3c32cp+3, -0x1.ffffff3b84647p-2, 0x1.24fbad696918ep+3, -0x1.ffffff405f0fbp-2,
+    0x1.2562243496f49p+3, -0x1.ffffff451b078p-2, 0x1.25c89affc5bfep+3, -0x1.ffffff49b90e3p-2,
+    0x1.262f11caf574cp+3, -0x1.ffffff4e39e11p-2, 0x1.26958896260d8p+3, -0x1.ffffff529e38dp-2,
+    0x1.26fbff6157847p+3, -0x1.ffffff56e6c9ap-2, 0x1.2762762c89d42p+3, -0x1.ffffff5b14432p-2,
+    0x1.27c8ecf7bcf73p+3, -0x1.ffffff5f2750ap-2, 0x1.282f63c2f0e86p+3, -0x1.ffffff6320995p-2,
+    0x1.2895da8e25a2ap+3, -0x1.ffffff6700c01p-2, 0x1.28fc51595b210p+3, -0x1.ffffff6ac863fp-2,
+    0x1.2962c824915e9p+3, -0x1.ffffff6e781fep-2, 0x1.29c93eefc856bp+3, -0x1.ffffff72108b2p-2,
+    0x1.2a2fb5bb0004cp+3, -0x1.ffffff7592392p-2, 0x1.2a962c8638643p+3, -0x1.ffffff78fdb9bp-2,
+    0x1.2afca3517170bp+3, -0x1.ffffff7c53992p-2, 0x1.2b631a1cab25fp+3, -0x1.ffffff7f94602p-2,
+    0x1.2bc990e7e57fdp+3, -0x1.ffffff82c0943p-2, 0x1.2c3007b3207a3p+3, -0x1.ffffff85d8b76p-2,
+    0x1.2c967e7e5c112p+3, -0x1.ffffff88dd48bp-2, 0x1.2cfcf5499840cp+3, -0x1.ffffff8bcec3ep-2,
+    0x1.2d636c14d5055p+3, -0x1.ffffff8eada19p-2, 0x1.2dc9e2e0125b2p+3, -0x1.ffffff917a579p-2,
+    0x1.2e3059ab503e9p+3, -0x1.ffffff943558bp-2, 0x1.2e96d0768eac2p+3, -0x1.ffffff96df14ep-2,
+    0x1.2efd4741cda08p+3, -0x1.ffffff9977f97p-2, 0x1.2f63be0d0d184p+3, -0x1.ffffff9c0070dp-2,
+    0x1.2fca34d84d102p+3, -0x1.ffffff9e78e2ep-2, 0x1.3030aba38d851p+3, -0x1.ffffffa0e1b51p-2,
+    0x1.3097226ece73ep+3, -0x1.ffffffa33b4a1p-2, 0x1.30fd993a0fd99p+3, -0x1.ffffffa586026p-2,
+    0x1.3164100551b34p+3, -0x1.ffffffa7c23bfp-2, 0x1.31ca86d093fe1p+3, -0x1.ffffffa9f0526p-2,
+    0x1.3230fd9bd6b72p+3, -0x1.ffffffac109f3p-2, 0x1.3297746719dbcp+3, -0x1.ffffffae23799p-2,
+    0x1.32fdeb325d695p+3, -0x1.ffffffb029368p-2, 0x1.336461fda15d4p+3, -0x1.ffffffb22228fp-2,
+    0x1.33cad8c8e5b4fp+3, -0x1.ffffffb40ea1dp-2, 0x1.34314f942a6e0p+3, -0x1.ffffffb5eef01p-2,
+    0x1.3497c65f6f85fp+3, -0x1.ffffffb7c3609p-2, 0x1.34fe3d2ab4fa8p+3, -0x1.ffffffb98c3e6p-2,
+    0x1.3564b3f5fac95p+3, -0x1.ffffffbb49d2bp-2, 0x1.35cb2ac140f04p+3, -0x1.ffffffbcfc64fp-2,
+    0x1.3631a18c876d0p+3, -0x1.ffffffbea43abp-2, 0x1.36981857ce3d9p+3, -0x1.ffffffc04197ep-2,
+    0x1.36fe8f23155fep+3, -0x1.ffffffc1d4becp-2, 0x1.376505ee5cd1dp+3, -0x1.ffffffc35defdp-2,
+    0x1.37cb7cb9a4917p+3, -0x1.ffffffc4dd6a2p-2, 0x1.3831f384ec9cep+3, -0x1.ffffffc6536b2p-2,
+    0x1.38986a5034f24p+3, -0x1.ffffffc7c02ebp-2, 0x1.38fee11b7d8fcp+3, -0x1.ffffffc923ef4p-2,
+    0x1.396557e6c6738p+3, -0x1.ffffffca7ee5ep-2, 0x1.39cbceb20f9bdp+3, -0x1.ffffffcbd14a2p-2,
+    0x1.3a32457d59071p+3, -0x1.ffffffcd1b523p-2, 0x1.3a98bc48a2b38p+3, -0x1.ffffffce5d32fp-2,
+    0x1.3aff3313ec9f9p+3, -0x1.ffffffcf971ffp-2, 0x1.3b65a9df36c9bp+3, -0x1.ffffffd0c94b8p-2,
+    0x1.3bcc20aa81305p+3, -0x1.ffffffd1f3e6ap-2, 0x1.3c329775cbd20p+3, -0x1.ffffffd317214p-2,
+    0x1.3c990e4116ad3p+3, -0x1.ffffffd4332a0p-2, 0x1.3cff850c61c08p+3, -0x1.ffffffd5482e5p-2,
+    0x1.3d65fbd7ad0aap+3, -0x1.ffffffd6565aap-2, 0x1.3dcc72a2f88a2p+3, -0x1.ffffffd75dda3p-2,
+    0x1.3e32e96e443dbp+3, -0x1.ffffffd85ed74p-2, 0x1.3e99603990241p+3, -0x1.ffffffd9597b0p-2,
+    0x1.3effd704dc3bfp+3, -0x1.ffffffda4ded9p-2, 0x1.3f664dd028842p+3, -0x1.ffffffdb3c561p-2,
+    0x1.3fccc49b74fb8p+3, -0x1.ffffffdc24dacp-2, 0x1.40333b65a9dddp+3, -0x1.0000000000000p-1,
+};
 constexpr int kExpTabN = 256;                 // 2^(j/256)
 constexpr int kFp64TabDoubles = kExpTabN + 514;
 
@@ -1804,32 +2850,90 @@ __device__ __forceinline__ double sig_half_poly(double r, double s) {
     return __builtin_fma(t * r, p, -b2);
 }
 
-// The fp64 decoder_v2_4 MLPs' Softplus table in LDS: GNND_F64_SPTAB 1 (default) the one-read
-// kSpTab form (softplus_sp), 0 the exp + log1p tables (softplus_fast; A/B builds)
+// g(h) = softplus(h) - h/2 from ONE read of the signed table kSgTab: h = c_j + r, c_j = j kSgStep
+// (j = round(h kSgScale) clamped to [kSgLo, kSgHi] by one v_med3_i32, r = h - c_j by one FMA
+// after the int -> double conversion), and the degree-4 Taylor polynomial of g about c_j:
+// g' = -sig, g'' = t = 1/4 - sig^2, g^(3) = 2 sig t, g^(4) = t (1 - 6t): sp_poly's Horner form
+// with s - 1/2 -> sig.  No |h|, no threshold compare and select, and no separate |h|/2 term: the
+// clamp entries are exactly linear (t = 0): j = kSgHi covers h > 20 (torch's threshold, Softplus =
+// h: g = h/2; kSgScale puts 20 on the entry boundary, h = 20 itself takes entry 799), j = kSgLo
+// h < -32.03 (g = -h/2, Softplus < 1.3e-14).  Step 1/39.975: remainder (step/2)^5/120 max|g^(5)|
+// = 3.3e-13 ABSOLUTE (kSpTab's 1/64 step: 3.1e-14, but at 53 KB instead of 33 KB: one workgroup
+// per CU fewer); tests/test_fastmath_cpu.py.  Valid for |h| < 2^31 / 40.  16 VALU per MLP unit
+// in decode_kernel (layer 1, index, polynomial, layer 2) instead of 19 with kSpTab.
+constexpr double kSgScale = 0x1.3fcccccccccccp+5;   // 39.974999999999994 (gen_fp64_tables.py)
+constexpr double kSgStep = 1.0 / kSgScale;
+constexpr int kSgLo = -1281, kSgHi = 800;
+constexpr int kSgN = kSgHi - kSgLo + 1;
+constexpr int kSgTabDoubles = 2 * kSgN;
+__device__ __forceinline__ SpIdx sg_index(double x) {
+    const double tk = __builtin_fma(x, kSgScale, kRoundMagic);
+    int k = round_magic_lo(tk);
+    k = k < kSgLo ? kSgLo : k;
+    k = k > kSgHi ? kSgHi : k;
+    SpIdx q;
+    q.r = __builtin_fma((double)k, -kSgStep, x);
+    q.j = k - kSgLo;
+    return q;
+}
+// g(c + r) from the entry {f0 = g(c), sig = 1/2 - sigmoid(c)}: 8 VALU
+__device__ __forceinline__ double sg_poly(double r, double f0, double sig) {
+    const double t = __builtin_fma(-sig, sig, 0.25);
+    const double u = t * r;
+    const double b = sig * (1.0 / 3);
+    double p = __builtin_fma(r, 1.0 / 24, b);
+    p = __builtin_fma(u, -0.25, p);
+    p = __builtin_fma(p, r, 0.5);
+    return __builtin_fma(__builtin_fma(u, p, -sig), r, f0);
+}
+__device__ __forceinline__ double softplus_sg(double x, const double* __restrict__ tab) {
+    const SpIdx q = sg_index(x);
+    const SpEntry e = sp_entry(tab, q.j);
+    return sg_poly(q.r, e.f0, e.s) + 0.5 * x;
+}
+
+// The fp64 decoder_v2_4 MLPs' Softplus table in LDS: GNND_F64_SPTAB 1 (default) a one-read
+// table (GNND_F64_SGTAB 1, default: kSgTab, softplus_sg; 0: kSpTab, softplus_sp), 0 the exp +
+// log1p tables (softplus_fast; A/B builds)
 #ifndef GNND_F64_SPTAB
 #define GNND_F64_SPTAB 1
 #endif
-constexpr int kV24F64TabDoubles = GNND_F64_SPTAB ? kSpTabDoubles : kFp64TabDoubles;
+#ifndef GNND_F64_SGTAB
+#define GNND_F64_SGTAB GNND_F64_SPTAB
+#endif
+constexpr int kV24F64TabDoubles =
+    GNND_F64_SGTAB ? kSgTabDoubles : GNND_F64_SPTAB ? kSpTabDoubles : kFp64TabDoubles;
 __device__ __forceinline__ double v24_f64_tab_entry(int i) {
+    if (GNND_F64_SGTAB) return kSgTab[i];
     if (GNND_F64_SPTAB) return kSpTab[i];
     return i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
 }
 __device__ __forceinline__ double softplus_v24(double x, const double* __restrict__ tab) {
+    if (GNND_F64_SGTAB) return softplus_sg(x, tab);
     if (GNND_F64_SPTAB) return softplus_sp(x, tab);
     return softplus_fast(x, tab);
 }
-// softplus(x) - x/2 = |x|/2 + ln(1 + e^-|x|) with the one-read table (one FMA instead of relu's
-// max + add; the linear x/2 is summed per MLP: decode_kernel mlp_lin); the exp + log1p form
-// (GNND_F64_SPTAB 0) keeps the whole value
+// softplus(x) - x/2 (the linear x/2 is summed per MLP: decode_kernel mlp_lin): kSgTab's g(x)
+// directly, or |x|/2 + ln(1 + e^-|x|) from kSpTab (one FMA instead of relu's max + add); the
+// exp + log1p form (GNND_F64_SPTAB 0) keeps the whole value
 #ifndef GNND_F64_LINFOLD
 #define GNND_F64_LINFOLD GNND_F64_SPTAB   // 0: whole Softplus per unit, no per-MLP linear part (A/B)
 #endif
+// the one-read forms in two steps (index, then the value from the read entry), so a caller can
+// issue several units' table reads together (decode_kernel mlp128d_chains_cm)
+__device__ __forceinline__ SpIdx v24_sp_index(double x) {
+    if (GNND_F64_SGTAB) return sg_index(x);
+    return sp_index(x);
+}
+__device__ __forceinline__ double v24_sp_half(const SpIdx& q, const SpEntry& e, double x) {
+    if (GNND_F64_SGTAB) return sg_poly(q.r, e.f0, e.s);
+    return __builtin_fma(__builtin_fabs(x), 0.5, sp_poly(q.r, e.f0, e.s));
+}
 __device__ __forceinline__ double softplus_v24_half(double x, const double* __restrict__ tab) {
     if (!GNND_F64_LINFOLD) return softplus_v24(x, tab);
     if (GNND_F64_SPTAB) {
-        const SpIdx q = sp_index(x);
-        const SpEntry e = sp_entry(tab, q.j);
-        return __builtin_fma(__builtin_fabs(x), 0.5, sp_poly(q.r, e.f0, e.s));
+        const SpIdx q = v24_sp_index(x);
+        return v24_sp_half(q, sp_entry(tab, q.j), x);
     }
     return softplus_fast(x, tab);
 }

@@ -318,15 +318,15 @@ __device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u
 #pragma unroll
         for (int s = 0; s < UT; ++s) {
             h[s] = TWO ? fma(u0, e[s].w1a, fma(u1, e[s].w1b, e[s].b1)) : fma(u0, e[s].w1a, e[s].b1);
-            q[s] = sp_index(h[s]);
+            q[s] = v24_sp_index(h[s]);
         }
 #pragma unroll
         for (int s = 0; s < UT; ++s) t[s] = sp_entry(tab, q[s].j);
 #pragma unroll
         for (int s = 0; s < UT; ++s) {
-            const double g = sp_poly(q[s].r, t[s].f0, t[s].s);
-            c[s % NC] = fma(GNND_F64_LINFOLD ? __builtin_fma(__builtin_fabs(h[s]), 0.5, g) : relu_f64(h[s]) + g,
-                            e[s].w2, c[s % NC]);
+            const double g = GNND_F64_LINFOLD ? v24_sp_half(q[s], t[s], h[s])
+                                              : relu_f64(h[s]) + sp_poly(q[s].r, t[s].f0, t[s].s);
+            c[s % NC] = fma(g, e[s].w2, c[s % NC]);
         }
     }
     if constexpr (NC == 2) return c[0] + c[1];

@@ -32,7 +32,7 @@ int main() {
     std::mt19937_64 g(1);
     double me = 0, ml = 0, mt = 0, mm = 0, ms = 0, mst = 0, met = 0, mlt = 0, msl = 0;
     long nfast = 0;
-    double msp = 0, msg = 0;
+    double msp = 0, msg = 0, msgt = 0, mthr = 0;
     static double TAB[kFp64TabDoubles];
     for (int i = 0; i < kFp64TabDoubles; ++i) TAB[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
     std::uniform_real_distribution<double> U(-700, 700), L(-300, 300), T(-12, 12), S(-60, 30);
@@ -63,8 +63,22 @@ int main() {
         const double sa = sig_poly(q.r, kSpTab[2 * q.j + 1]);
         const double sg = hs > 20 ? 1.0 : (hs >= 0 ? 1.0 - sa : sa);
         msg = fmax(msg, fabs(sg - 1.0 / (1.0 + exp(-hs))) * (hs > 20 ? 0.0 : 1.0));
+        // the signed one-read Softplus (softplus_sg, the fp64 forward's kSgTab), far tails too
+        const double hg = (i % 13 == 0) ? U(g) : hs;
+        msgt = fmax(msgt, fabs(softplus_sg(hg, kSgTab) - (hg > 20 ? hg : log1p(exp(hg)))));
     }
-    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %ld %.3e %.3e\n", me, ml, mt, mm, ms, mst, met, mlt, msl, nfast, msp, msg);
+    // torch's threshold and the clamp entries: Softplus = h exactly above 20 (g = h/2 from the
+    // linear entry), log1p(exp(h)) at 20 itself, -h/2 + 0 far below
+    const double th[] = {20.0, nextafter(20.0, 30.0), 20.5, 1e3, 1e6, -40.0, -1e3};
+    for (double h : th) {
+        const SpIdx q = sg_index(h);
+        const double gv = sg_poly(q.r, kSgTab[2 * q.j], kSgTab[2 * q.j + 1]);
+        const double ref = h > 20 ? h : log1p(exp(h));
+        mthr = fmax(mthr, fabs((gv + 0.5 * h) - ref) / fmax(1.0, fabs(ref)));
+        if (h > 20 && (q.j != kSgN - 1 || gv != 0.5 * h)) mthr = 1;
+        if (h == 20.0 && q.j != kSgN - 2) mthr = 1;
+    }
+    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %ld %.3e %.3e %.3e %.3e\n", me, ml, mt, mm, ms, mst, met, mlt, msl, nfast, msp, msg, msgt, mthr);
 }
 '''
 
@@ -97,3 +111,9 @@ def test_fp64_fast_math_ulp(tmp_path):
     # (sig_poly, the reverse pass's derivative, degree 4 since r05) <= 1e-13 absolute
     assert float(out[10]) <= 5e-14, out[10]
     assert float(out[11]) <= 1e-13, out[11]
+    # softplus_sg (the fp64 forward since r05: signed table kSgTab, step 1/39.975, no threshold
+    # compare): <= 4e-13 absolute over the decoders' range and [-700, 700] (bound 3.3e-13,
+    # measured 3.2e-13; tools/gen_fp64_tables.py); torch's threshold exact (h = 20 on the Taylor
+    # side, h/2 exactly from the linear entry above it), the far tails within an ulp
+    assert float(out[12]) <= 4e-13, out[12]
+    assert float(out[13]) <= 2.3e-16, out[13]
