@@ -52,9 +52,10 @@ __device__ __forceinline__ int gnnd_dcheck_idx(int i, int n, int bit) {
 #endif
 
 // ---------------------------------------------------------------------------------------
-// phase timing (timing experiments only, -DGNND_PHASE_PROF): one wave of workgroup 0 sums the
-// shader-clock cycles (s_memtime) spent between consecutive marks and prints the per-phase
-// totals at the end of the launch.  Release builds compile the marks away.
+// phase timing (timing experiments only, -DGNND_PHASE_PROF): one wave of workgroup 0 (every wave
+// with -DGNND_PPROF_ALLWAVES=1) sums the shader-clock cycles (s_memtime) spent between
+// consecutive marks and prints the per-phase totals at the end of the launch.  Release builds
+// compile the marks away.
 // ---------------------------------------------------------------------------------------
 struct PhaseProf {
 #ifdef GNND_PHASE_PROF
@@ -76,8 +77,8 @@ struct PhaseProf {
     }
     __device__ void report(const char* tag, int n, int iters) {
         if (on && (threadIdx.x & 63) == 0)
-            printf("PHASE %s iters %d | %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n",
-                   tag, iters, (unsigned long long)acc[0], (unsigned long long)acc[1],
+            printf("PHASE %s w%d iters %d | %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu %llu\n",
+                   tag, (int)(threadIdx.x >> 6), iters, (unsigned long long)acc[0], (unsigned long long)acc[1],
                    (unsigned long long)acc[2], (unsigned long long)acc[3], (unsigned long long)acc[4],
                    (unsigned long long)acc[5], (unsigned long long)acc[6], (unsigned long long)acc[7],
                    (unsigned long long)acc[8], (unsigned long long)acc[9], (unsigned long long)acc[10],
@@ -88,6 +89,9 @@ struct PhaseProf {
     }
 #endif
 };
+#ifndef GNND_PPROF_ALLWAVES
+#define GNND_PPROF_ALLWAVES 0      // 1: every wave of workgroup 0 reports (the reverse pass)
+#endif
 #ifdef GNND_PHASE_PROF
 #define GNND_PPROF(pf) PhaseProf pf
 #define GNND_PSTART(pf, on) pf.start(on)
@@ -2885,6 +2889,16 @@ __device__ __forceinline__ double sg_poly(double r, double f0, double sig) {
     p = __builtin_fma(u, -0.25, p);
     p = __builtin_fma(p, r, 0.5);
     return __builtin_fma(__builtin_fma(u, p, -sig), r, f0);
+}
+// g'(c + r) = sigmoid(c + r) - 1/2 about the same entry, degree 4 (the fp64 reverse pass's
+// Softplus derivative): g^(5) = 2 sig t (1 - 12 t), so g' = -sig + t r (1 + r (sig + r ((1/6 - t)
+// + r sig (1/12 - t)))) -- sig_half_poly with s - 1/2 -> sig; u = t r shared with sg_poly.  The
+// clamp entries (t = 0) give exactly 1/2 (h > 20: torch's gradient 1) and -1/2 (h < -32.03)
+__device__ __forceinline__ double sg_grad_poly(double r, double sig) {
+    const double t = __builtin_fma(-sig, sig, 0.25);
+    const double c2 = sig * (1.0 / 12 - t);
+    const double p = __builtin_fma(__builtin_fma(__builtin_fma(c2, r, 1.0 / 6 - t), r, sig), r, 1.0);
+    return __builtin_fma(t * r, p, -sig);
 }
 __device__ __forceinline__ double softplus_sg(double x, const double* __restrict__ tab) {
     const SpIdx q = sg_index(x);

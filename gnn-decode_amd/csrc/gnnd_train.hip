@@ -34,32 +34,46 @@ namespace {
 
 // threads per workgroup: 16 waves (4 per SIMD) in fp32 (128 VGPRs), 8 in fp64 (169 VGPRs)
 template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
+// fp64 Softplus table of the reverse pass: GNND_BWD_SGTAB 1 (default) the signed one-read table
+// (kSgTab, sg_index / sg_poly / sg_grad_poly), 0 the |h|-indexed kSpTab (A/B builds)
+#ifndef GNND_BWD_SGTAB
+#define GNND_BWD_SGTAB 1
+#endif
+constexpr int kBwdTabDoubles = GNND_BWD_SGTAB ? kSgTabDoubles : kSpTabDoubles;
+__device__ __forceinline__ double bwd_tab_entry(int i) { return GNND_BWD_SGTAB ? kSgTab[i] : kSpTab[i]; }
 // LDS bytes of the Softplus tables the fp64 reverse pass stages ahead of its graph tables
-template <typename T> constexpr size_t bwd_tab_bytes() { return sizeof(T) == 8 ? (size_t)kSpTabDoubles * 8 : 0; }
+template <typename T> constexpr size_t bwd_tab_bytes() { return sizeof(T) == 8 ? (size_t)kBwdTabDoubles * 8 : 0; }
 constexpr int kV24W = 1283;                 // packed plain weights (gnnd.h)
 
-// fp64 Softplus and its derivative at N arguments h from the kSpTab entries (gnnd_common.h
-// sp_index / sp_poly / sig_poly; the reverse pass stages the table whichever form its forward
-// used), all N 16-byte reads issued before the first use (hipcc otherwise schedules the chains
-// one after another, lgkmcnt(0) after each read):
-//   sph = |h|/2 + ln(1 + e^-|h|) = softplus(h) - h/2  (the linear h/2 part is summed once per
-//         wave, Units::sx*, instead of a max + add per unit),
-//   sg  = sigmoid(h) = 1 - s(|h|) (h >= 0) or s(|h|), as 1/2 + copysign(1/2 - s(|h|), h).
-// Above torch's threshold (h > 20) the zero entry gives sph = h/2 (softplus = h) and sg = 1.
+// fp64 Softplus and its derivative at N arguments h from one table entry each, all N 16-byte
+// reads issued before the first use (hipcc otherwise schedules the chains one after another,
+// lgkmcnt(0) after each read):
+//   sph = softplus(h) - h/2  (the linear h/2 part is summed once per wave, Units::sx*, instead
+//         of a max + add per unit),
+//   sg  = sigmoid(h).
+// kSgTab: sph = g(h) and sg = 1/2 + g'(h) from the signed entry (no |h|, no threshold select, no
+// sign copy); the linear clamp entries give sph = h/2, sg = 1 above torch's threshold (h > 20).
+// kSpTab: sph = |h|/2 + ln(1 + e^-|h|), sg = 1/2 + copysign(1/2 - s(|h|), h), the zero entry
+// above the threshold.
 template <int N>
 __device__ __forceinline__ void sph_and_grad_n(const double (&h)[N], double (&sph)[N],
                                                double (&sg)[N], const double* tab) {
     SpIdx q[N];
     SpEntry e[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) q[i] = sp_index(h[i]);
+    for (int i = 0; i < N; ++i) q[i] = GNND_BWD_SGTAB ? sg_index(h[i]) : sp_index(h[i]);
 #pragma unroll
     for (int i = 0; i < N; ++i) e[i] = sp_entry(tab, q[i].j);
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        sph[i] = __builtin_fma(__builtin_fabs(h[i]), 0.5, sp_poly(q[i].r, e[i].f0, e[i].s));
-        // sigmoid(h) = 1/2 + copysign(1/2 - s(|h|), h)
-        sg[i] = 0.5 + __builtin_copysign(sig_half_poly(q[i].r, e[i].s), h[i]);
+        if (GNND_BWD_SGTAB) {
+            sph[i] = sg_poly(q[i].r, e[i].f0, e[i].s);
+            sg[i] = 0.5 + sg_grad_poly(q[i].r, e[i].s);
+        } else {
+            sph[i] = __builtin_fma(__builtin_fabs(h[i]), 0.5, sp_poly(q[i].r, e[i].f0, e[i].s));
+            // sigmoid(h) = 1/2 + copysign(1/2 - s(|h|), h)
+            sg[i] = 0.5 + __builtin_copysign(sig_half_poly(q[i].r, e[i].s), h[i]);
+        }
     }
 }
 __device__ __forceinline__ void sp_and_grad(float h, float& sp, float& sg, const float*) {
@@ -424,7 +438,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     constexpr bool sibs = kSibs;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     GNND_PPROF(pf);
-    GNND_PSTART(pf, blockIdx.x == 0 && threadIdx.x < 64);
+    GNND_PSTART(pf, blockIdx.x == 0 && (GNND_PPROF_ALLWAVES || threadIdx.x < 64));
     GraphView g = g0;
     int blk = blockIdx.x, nblk = gridDim.x, comp = 0;
     if (views) {                       // uniform: component k
@@ -441,7 +455,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
 #define GNND_BWD_PARK 1
 #endif
     constexpr bool kParkF32 = sizeof(T) == 4 && GNND_BWD_PARK;
-    // fp64: the forward's Softplus table (kSpTab) at LDS byte 0 (sp_and_grad_n)
+    // fp64: the Softplus table (kSgTab; kSpTab in GNND_BWD_SGTAB=0 builds) at LDS byte 0 (sph_and_grad_n)
     constexpr size_t kTabB = bwd_tab_bytes<T>();
     T* s_ftab = (T*)smem;
     int* s_tab = (int*)(smem + kTabB);
@@ -502,7 +516,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     }
     for (int i = tid; i < nints; i += kTrainThreads) s_tab[i] = gtab[i];
     if constexpr (kTabB > 0)
-        for (int i = tid; i < kSpTabDoubles; i += kTrainThreads) s_ftab[i] = kSpTab[i];
+        for (int i = tid; i < kBwdTabDoubles; i += kTrainThreads) s_ftab[i] = bwd_tab_entry(i);
     for (int i = tid; i < 9 * (Ep - E); i += kTrainThreads) s_dm[(i / (Ep - E)) * Ep + E + i % (Ep - E)] = T(0);
     if (floss) {
         for (int v = tid; v < V; v += kTrainThreads) s_lmask[v] = nl > 0 ? lossp.lmask[g.o0 + v] : 0u;
@@ -542,6 +556,27 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
     // The uniform results of step k go to lane k of two VGPRs (compare + select), stored by the
     // lanes after every 64 steps (no per-step exec-masked lane-0 stores).
+    // issue fairness between the waves of a SIMD in the unit passes (A/B, GNND_BWD_FAIR 1): the
+    // arbiter issues oldest-first, so a SIMD's older wave finishes its share of a pass well before
+    // the younger ones, which then run alone with their latencies exposed (per-wave phase
+    // profile r05h: fp64 pass A 145k vs 233k cycles, fp32 38k / 57k / 80k / 99k by age).  Each
+    // wave lowers its priority as it completes its steps (3 -> 1 over the pass), so a lagging
+    // wave takes the issue slots until it has caught up.
+#ifndef GNND_BWD_FAIR
+#define GNND_BWD_FAIR 0
+#endif
+    const int nsteps4 = ((E + 3) / 4 + kTrainWaves - 1) / kTrainWaves;   // wave steps per pass
+    auto fair_prio = [&](int k) {
+        if constexpr (GNND_BWD_FAIR) {
+            const int q = 3 * k / nsteps4;               // wave-uniform
+            if (q == 0) __builtin_amdgcn_s_setprio(3);
+            else if (q == 1) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(1);
+        }
+    };
+    auto fair_end = [&]() {
+        if constexpr (GNND_BWD_FAIR) __builtin_amdgcn_s_setprio(0);
+    };
     auto unit_pass = [&](auto& U, auto two_tag, const T* in0, const T* in1, auto dy_of, auto dy4_of,
                          T* outp) {
         constexpr bool TWO = decltype(two_tag)::value;
@@ -592,7 +627,8 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                     // pass): only the active MLP's 16 partial VGPRs live, not all three MLPs' 48
                     const int eo = row_edge(lane >> 4);
                     U.zero_pg();
-                    for (int f = 4 * f0; f < E; f += 4 * kTrainWaves) {
+                    for (int f = 4 * f0, ks = 0; f < E; f += 4 * kTrainWaves, ++ks) {
+                        fair_prio(ks);
                         const f32x4 v0 = *(const f32x4*)(in0 + f);
                         const f32x4 v1 = TWO ? *(const f32x4*)(in1 + f) : f32x4{0.f, 0.f, 0.f, 0.f};
                         const float r = U.template bwd4_rows<TWO>(v0, v1, dy4_of(f));
@@ -607,6 +643,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
 #endif
                     }
                     U.fold();
+                    fair_end();
                     break;                       // (one pass covers every edge)
                 }
                 const int fl = f0 + kStride4 * lane;
@@ -623,7 +660,8 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             // fp64: four consecutive edges f..f+3 per wave step (f = 4 (wave + W k)); padding
             // entries E..Ep-1 are zero inputs with dy = 0, and every lane stores its row's total
             const int eo = row_edge(lane >> 4);
-            for (int f = 4 * wave; f < E; f += 4 * kTrainWaves) {
+            for (int f = 4 * wave, ks = 0; f < E; f += 4 * kTrainWaves, ++ks) {
+                fair_prio(ks);
                 double a0[4], a1[4], dy[4];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
@@ -633,6 +671,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                 }
                 outp[f + eo] = U.template bwd4_rows_f64<TWO>(a0, a1, dy, s_ftab);
             }
+            fair_end();
         }
     };
 
@@ -760,6 +799,7 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
             for (int it = iters - 1; it >= 0; --it) {
                 stage(it);
                 __syncthreads();
+                GNND_PMARK(pf, 2);
                 if (it > 0) prefetch(it - 1);
                 if (it < iters - 1) {          // D of the previous step, for this wave's edges
                     for (int j = lane;; j += 64) {
@@ -776,11 +816,14 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                         s_dm[f] += sv - s_ge[f];
                     }
                 }
+                GNND_PMARK(pf, 9);
                 // A: m^{t+1} = MLP_c(u) s_c + m^t
                 if constexpr (kParkF32) uc.unpark(s_wp + 640, lane);
                 unit_pass(uc, std::false_type{}, s_u, nullptr, [&](int f) { return s_dm[f] * s_sc[f]; },
                           [&](int f) { return ld4(s_dm, f) * ld4(s_sc, f); }, s_g);
+                GNND_PMARK(pf, 3);
                 __syncthreads();
+                GNND_PMARK(pf, 4);
                 for (int j = lane;; j += 64) {   // B, for this wave's edges
                     const int f = my_edge(j);
                     if (f >= E) break;
@@ -795,11 +838,14 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
                     const T t = s_t[f];
                     s_da[f] = ((sc - s_g[f]) * (T(1) - t * t)) / T(2);
                 }
+                GNND_PMARK(pf, 5);
                 // C: a = MLP_v(ext, x_v)
                 if constexpr (kParkF32) uv.unpark(s_wp, lane);
                 unit_pass(uv, std::true_type{}, s_ext, s_xv, [&](int f) { return s_da[f]; },
                           [&](int f) { return ld4(s_da, f); }, s_ge);
+                GNND_PMARK(pf, 7);
                 __syncthreads();
+                GNND_PMARK(pf, 8);
             }
         } else {
         for (int it = iters - 1; it >= 0; --it) {

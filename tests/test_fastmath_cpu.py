@@ -32,7 +32,7 @@ int main() {
     std::mt19937_64 g(1);
     double me = 0, ml = 0, mt = 0, mm = 0, ms = 0, mst = 0, met = 0, mlt = 0, msl = 0;
     long nfast = 0;
-    double msp = 0, msg = 0, msgt = 0, mthr = 0;
+    double msp = 0, msg = 0, msgt = 0, mthr = 0, msgd = 0;
     static double TAB[kFp64TabDoubles];
     for (int i = 0; i < kFp64TabDoubles; ++i) TAB[i] = i < kExpTabN ? kExpTab[i] : kLogTab[i - kExpTabN];
     std::uniform_real_distribution<double> U(-700, 700), L(-300, 300), T(-12, 12), S(-60, 30);
@@ -66,6 +66,10 @@ int main() {
         // the signed one-read Softplus (softplus_sg, the fp64 forward's kSgTab), far tails too
         const double hg = (i % 13 == 0) ? U(g) : hs;
         msgt = fmax(msgt, fabs(softplus_sg(hg, kSgTab) - (hg > 20 ? hg : log1p(exp(hg)))));
+        // its derivative (sg_grad_poly, the fp64 reverse pass): sigmoid, exactly 1 above 20
+        const SpIdx qg = sg_index(hg);
+        const double sgd = 0.5 + sg_grad_poly(qg.r, kSgTab[2 * qg.j + 1]);
+        msgd = fmax(msgd, hg > 20 ? (sgd == 1.0 ? 0.0 : 1.0) : fabs(sgd - 1.0 / (1.0 + exp(-hg))));
     }
     // torch's threshold and the clamp entries: Softplus = h exactly above 20 (g = h/2 from the
     // linear entry), log1p(exp(h)) at 20 itself, -h/2 + 0 far below
@@ -78,7 +82,7 @@ int main() {
         if (h > 20 && (q.j != kSgN - 1 || gv != 0.5 * h)) mthr = 1;
         if (h == 20.0 && q.j != kSgN - 2) mthr = 1;
     }
-    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %ld %.3e %.3e %.3e %.3e\n", me, ml, mt, mm, ms, mst, met, mlt, msl, nfast, msp, msg, msgt, mthr);
+    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %ld %.3e %.3e %.3e %.3e %.3e\n", me, ml, mt, mm, ms, mst, met, mlt, msl, nfast, msp, msg, msgt, mthr, msgd);
 }
 '''
 
@@ -117,3 +121,6 @@ def test_fp64_fast_math_ulp(tmp_path):
     # side, h/2 exactly from the linear entry above it), the far tails within an ulp
     assert float(out[12]) <= 4e-13, out[12]
     assert float(out[13]) <= 2.3e-16, out[13]
+    # sg_grad_poly (its sigmoid, the fp64 reverse pass since r05): <= 1e-12 absolute, exactly 1
+    # above the threshold
+    assert float(out[14]) <= 1e-12, out[14]
