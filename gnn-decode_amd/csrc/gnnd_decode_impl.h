@@ -299,7 +299,14 @@ __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, c
 struct WcmEntry {
     double w1a, w1b, b1, w2;
 };
-template <int NC, int J0, bool TWO>
+// FAIR (the unit split, GNND_FWD_FAIR, default 1): the wave lowers its issue priority as it walks
+// its units (3 -> 1, then 0 before the partials meet), so the SIMD's younger waves are not left
+// to finish their units alone (the arbiter issues oldest-first; v24_bwd_kernel's GNND_BWD_FAIR).
+// Same-box A/B (r05k, config-5 step at B = 128): fp32 0.1766 -> 0.1743 ms, fp64 0.3908 -> 0.3845
+#ifndef GNND_FWD_FAIR
+#define GNND_FWD_FAIR 1
+#endif
+template <int NC, int J0, bool TWO, bool FAIR = false>
 __device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u0, double u1,
                                                     const double* tab) {
     constexpr int UT = 4, NU = 32 * NC;       // units per stage (NC divides UT), per call
@@ -309,6 +316,11 @@ __device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u
     for (int jj = 0; jj < NC; ++jj) c[jj] = 0.0;
 #pragma unroll 2
     for (int t0 = 0; t0 < NU; t0 += UT) {
+        if constexpr (FAIR) {            // (mlp128_upair's FAIR, in thirds of the units)
+            if (t0 == 0) __builtin_amdgcn_s_setprio(3);
+            if (t0 == (NU / UT / 3) * UT) __builtin_amdgcn_s_setprio(2);
+            if (t0 == (2 * NU / UT / 3) * UT) __builtin_amdgcn_s_setprio(1);
+        }
         WcmEntry e[UT];
         double h[UT];
         SpIdx q[UT];
@@ -329,6 +341,7 @@ __device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u
             c[s % NC] = fma(g, e[s].w2, c[s % NC]);
         }
     }
+    if constexpr (FAIR) __builtin_amdgcn_s_setprio(0);
     if constexpr (NC == 2) return c[0] + c[1];
     else return c[0];
 }
@@ -363,11 +376,12 @@ __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, co
         double p = 0.0;
         if (!idle) {
 #if GNND_F64_SPTAB
+            constexpr bool F = GNND_FWD_FAIR;
             switch (sub) {
-                case 0: p = mlp128d_chains_cm<NC, 0, TWO>(wl, u0, u1, tab); break;
-                case 1: p = mlp128d_chains_cm<NC, NC, TWO>(wl, u0, u1, tab); break;
-                case 2: if constexpr (US == 4) p = mlp128d_chains_cm<1, 2, TWO>(wl, u0, u1, tab); break;
-                default: if constexpr (US == 4) p = mlp128d_chains_cm<1, 3, TWO>(wl, u0, u1, tab); break;
+                case 0: p = mlp128d_chains_cm<NC, 0, TWO, F>(wl, u0, u1, tab); break;
+                case 1: p = mlp128d_chains_cm<NC, NC, TWO, F>(wl, u0, u1, tab); break;
+                case 2: if constexpr (US == 4) p = mlp128d_chains_cm<1, 2, TWO, F>(wl, u0, u1, tab); break;
+                default: if constexpr (US == 4) p = mlp128d_chains_cm<1, 3, TWO, F>(wl, u0, u1, tab); break;
             }
 #else
             switch (sub) {
@@ -737,7 +751,7 @@ struct UpairLds {
     static constexpr int kL1 = 0, kW2 = 256, kWA = 384;          // float offsets in an MLP block
     static constexpr int kMlp0 = 0, kMlp1 = 512, kMlp2 = 896, kFloats = 1280;   // ggc1, ggc2, mlp
 };
-template <int NP, int P0, bool TWO>
+template <int NP, int P0, bool TWO, bool FAIR = false>
 __device__ __forceinline__ float mlp128_upair(const float* wl, V24Lin lin, float u0, float u1) {
     const f32x4* l1 = (const f32x4*)(wl + UpairLds::kL1);
     const f32x2* w2 = (const f32x2*)(wl + UpairLds::kW2);
@@ -751,6 +765,11 @@ __device__ __forceinline__ float mlp128_upair(const float* wl, V24Lin lin, float
                      : __builtin_fmaf(u0, lin.a0, lin.b);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
+        if constexpr (FAIR) {
+            if (i == 0) __builtin_amdgcn_s_setprio(3);
+            if (i == 6) __builtin_amdgcn_s_setprio(2);
+            if (i == 11) __builtin_amdgcn_s_setprio(1);
+        }
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
             const int e = (P0 + q) * 16 + i;
@@ -762,6 +781,7 @@ __device__ __forceinline__ float mlp128_upair(const float* wl, V24Lin lin, float
             c[q] = __builtin_elementwise_fma(softplus_tail2(h), w2[e], c[q]);
         }
     }
+    if constexpr (FAIR) __builtin_amdgcn_s_setprio(0);
     if constexpr (NP == 4)
         return ((c[0].x + c[0].y) + (c[1].x + c[1].y)) + ((c[2].x + c[2].y) + (c[3].x + c[3].y));
     else if constexpr (NP == 2) return (c[0].x + c[0].y) + (c[1].x + c[1].y);
@@ -781,11 +801,12 @@ __device__ __forceinline__ float mlp128_upair_split(const float* wl, V24Lin lin,
         constexpr int NP = 4 / US;
         float p = 0.f;
         if (!idle) {
+            constexpr bool F = GNND_FWD_FAIR;
             switch (sub) {
-                case 0: p = mlp128_upair<NP, 0, TWO>(wl, lin, u0, u1); break;
-                case 1: p = mlp128_upair<NP, NP, TWO>(wl, lin, u0, u1); break;
-                case 2: if constexpr (US == 4) p = mlp128_upair<1, 2, TWO>(wl, lin, u0, u1); break;
-                default: if constexpr (US == 4) p = mlp128_upair<1, 3, TWO>(wl, lin, u0, u1); break;
+                case 0: p = mlp128_upair<NP, 0, TWO, F>(wl, lin, u0, u1); break;
+                case 1: p = mlp128_upair<NP, NP, TWO, F>(wl, lin, u0, u1); break;
+                case 2: if constexpr (US == 4) p = mlp128_upair<1, 2, TWO, F>(wl, lin, u0, u1); break;
+                default: if constexpr (US == 4) p = mlp128_upair<1, 3, TWO, F>(wl, lin, u0, u1); break;
             }
         }
         buf[sub * IL + itid] = p;
@@ -1726,6 +1747,37 @@ template <typename T> __device__ __forceinline__ T var_sum_uniform(const T* mp, 
     return s;
 }
 
+// two variables' sums at once (wave-uniform degrees da, db): their common part in one loop of
+// independent reads and adds (twice the LDS reads in flight of var_sum_uniform's chain), then
+// each one's tail.  Every sum is still accumulated strictly in position order: the same bits.
+template <typename T>
+__device__ __forceinline__ void var_sum_uniform2(const T* ma, int da, const T* mb, int db, T& sa, T& sb) {
+    T a = ma[0], b = mb[0];
+    const int dm = da < db ? da : db;
+    int k = 1;
+    for (; k + 4 <= dm; k += 4) {
+        const T a0 = ma[k], a1 = ma[k + 1], a2 = ma[k + 2], a3 = ma[k + 3];
+        const T b0 = mb[k], b1 = mb[k + 1], b2 = mb[k + 2], b3 = mb[k + 3];
+        a += a0; b += b0; a += a1; b += b1; a += a2; b += b2; a += a3; b += b3;
+    }
+    auto tail = [&](const T* mp, int dp, T s) {
+        int j = k;
+        for (; j + 4 <= dp; j += 4) {
+            const T c0 = mp[j], c1 = mp[j + 1], c2 = mp[j + 2], c3 = mp[j + 3];
+            s += c0; s += c1; s += c2; s += c3;
+        }
+        if (j + 2 <= dp) {
+            const T c0 = mp[j], c1 = mp[j + 1];
+            s += c0; s += c1;
+            j += 2;
+        }
+        if (j < dp) s += mp[j];
+        return s;
+    };
+    sa = tail(ma, da, a);
+    sb = tail(mb, db, b);
+}
+
 // ---------------------------------------------------------------------------------------
 // resident kernel (light models: CGNNI, QGNNI, CBP, QBP)
 // ---------------------------------------------------------------------------------------
@@ -2335,7 +2387,21 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             // degree, so the sum is straight-line code selected by a wave-uniform switch —
             // no masks, no per-edge address or loop arithmetic.  Reference (index_add) order;
             // the padding zeros come last (s + 0 == s).
-            if (vact) {
+#ifndef GNND_VAR_PAIR
+#define GNND_VAR_PAIR 0            // 1: the two cached entries' sums interleaved (A/B)
+#endif
+            if (vact && GNND_VAR_PAIR && kVC == 2 && vi0 + vstep < V) {
+                // both cached entries (every lane has them: vi0 + vstep < V)
+                const int va = (last || !kTX) ? (int)(s_vord[vi0].x & 0xffffu) : 0;
+                const int vbb = (last || !kTX) ? (int)(s_vord[vi0 + vstep].x & 0xffffu) : 0;
+                const int pa = (int)(vc_mt[0] & 0xffffu), ta = (int)(vc_mt[0] >> 16);
+                constexpr int k1 = kVC > 1 ? 1 : 0;
+                const int pb = (int)(vc_mt[k1] & 0xffffu), tb = (int)(vc_mt[k1] >> 16);
+                T sa, sb;
+                var_sum_uniform2(s_m + pa, vc_dp[0], s_m + pb, vc_dp[k1], sa, sb);
+                var_out(vb, vsbase, vtbase, va, ta, sa);
+                var_out(vb, vsbase, vtbase, vbb, tb, sb);
+            } else if (vact) {
 #pragma unroll
                 for (int k = 0; k < kVC; ++k) {
                     const int i = vi0 + k * vstep;
@@ -2348,6 +2414,8 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                         var_out(vb, vsbase, vtbase, v, pt, var_sum_uniform(s_m + pm, vc_dp[k]));
                     }
                 }
+            }
+            if (vact) {
                 for (int i = vi0 + kVC * vstep; i < V; i += vstep) {
                     const uint2 o = s_vord[i];
                     const int dp = __builtin_amdgcn_readfirstlane((int)(o.x >> 16));

@@ -556,14 +556,15 @@ v24_bwd_kernel(GraphView g0, const T* __restrict__ w, const T* __restrict__ x,
     // out[f] = d/d in of MLP at (in0[f], in1[f]) for upstream dy(f)
     // The uniform results of step k go to lane k of two VGPRs (compare + select), stored by the
     // lanes after every 64 steps (no per-step exec-masked lane-0 stores).
-    // issue fairness between the waves of a SIMD in the unit passes (A/B, GNND_BWD_FAIR 1): the
+    // issue fairness between the waves of a SIMD in the unit passes (GNND_BWD_FAIR, default 1): the
     // arbiter issues oldest-first, so a SIMD's older wave finishes its share of a pass well before
     // the younger ones, which then run alone with their latencies exposed (per-wave phase
     // profile r05h: fp64 pass A 145k vs 233k cycles, fp32 38k / 57k / 80k / 99k by age).  Each
     // wave lowers its priority as it completes its steps (3 -> 1 over the pass), so a lagging
-    // wave takes the issue slots until it has caught up.
+    // wave takes the issue slots until it has caught up.  Same-box A/B (r05j): config-5 step at
+    // B = 128 fp32 0.1801 -> 0.1773 ms, fp64 0.3926 -> 0.3888 ms.
 #ifndef GNND_BWD_FAIR
-#define GNND_BWD_FAIR 0
+#define GNND_BWD_FAIR 1
 #endif
     const int nsteps4 = ((E + 3) / 4 + kTrainWaves - 1) / kTrainWaves;   // wave steps per pass
     auto fair_prio = [&](int k) {
