@@ -1966,7 +1966,11 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     // iterations): message-run base, T row position and the wave-uniform padded degree, so an
     // iteration's variable sums start with the message reads instead of an LDS round trip for the
     // entry and its decode
-    constexpr int kVC = GNND_VAR_CACHE ? GNND_VAR_CACHE_N : 0;
+#ifndef GNND_VAR_CACHE_NL
+#define GNND_VAR_CACHE_NL 5        // ... for fp32 plans with <= 64 item-state VGPRs (Q (2R + 2)):
+#endif                             // r05n A/B LDPC CGNNI +1.1 %, toric QGNNI +1.4 %, QBP +2.3 %
+    constexpr bool kLightRegs = sizeof(T) == 4 && QMAX * (2 * R + 2) <= 64;
+    constexpr int kVC = GNND_VAR_CACHE ? (kLightRegs ? GNND_VAR_CACHE_NL : GNND_VAR_CACHE_N) : 0;
     // one VGPR per entry: message-run position (vmbase included, < 2^16: the tile's LDS message
     // block) | T row position << 16; the padded degree in an SGPR
     uint32_t vc_mt[kVC > 0 ? kVC : 1];
