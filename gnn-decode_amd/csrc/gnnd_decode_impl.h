@@ -1142,8 +1142,10 @@ __device__ __forceinline__ double fwd_wave_sum(double v) {
 // Split graphs (gnnd_graph::comp, `views` non-null): blocks [k*cblk, (k+1)*cblk) decode
 // component k of every codeword, each block a tile of CW codewords of that component's graph
 // views[k]; the component's rows are addressed through its GraphView addressing fields.
-template <int MODEL, typename T, int R, bool TAPE = false, int US = 1>
-__global__ void __launch_bounds__(unit_split_lanes<US>() * US)
+// WIDE (US = 1 only): WIDE x 256 work-item lanes per workgroup, so several waves' worth of items
+// share one copy of the workgroup's LDS tables (fp64 decoder_v2_4: the 33 KB Softplus table)
+template <int MODEL, typename T, int R, bool TAPE = false, int US = 1, int WIDE = 1>
+__global__ void __launch_bounds__(unit_split_lanes<US>() * US * WIDE)
 decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict__ x,
               T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
               FastDiv dN, TapeView<T> tape, const GraphView* __restrict__ views, int cblk) {
@@ -1162,7 +1164,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     }
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
-    constexpr int IL = unit_split_lanes<US>();        // work-item lanes
+    static_assert(WIDE == 1 || US == 1, "wide workgroups: no unit split");
+    constexpr int IL = unit_split_lanes<US>() * WIDE;  // work-item lanes
     constexpr int NT = IL * US;
     static_assert(US == 1 || (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2) ||
                       (MODEL == GNND_V24 && sizeof(T) == 8 && US <= 4),
@@ -2531,6 +2534,7 @@ struct Plan {
     int q;        // work items per lane (resident)
     size_t lds;   // bytes of dynamic LDS
     int us = 1;   // unit split of the streaming kernel (fp32 decoder_v2_4, small batches)
+    int wide = 1; // work-item lanes / 256 of the streaming kernel (fp64 decoder_v2_4, GNND_V24F64_WIDE)
     int ncomp = 1;                       // split graph: components per codeword (streaming)
     const GraphView* dviews = nullptr;   // device [ncomp] views of the plan's kind
 };
@@ -2579,6 +2583,17 @@ int v24f64_us_big() {
     }();
     return v;
 }
+// fp64 decoder_v2_4 large batches in workgroups of 512 work-item lanes, two per CU (make_plan;
+// GNND_V24F64_WIDE = 1 / 4: 256 lanes three per CU / 1 024 lanes one per CU).  Same-box A/B
+// (profiles/r05/experiments/ab_r05r_f64_wide.txt, config 3): 23.29 / 23.11 / 24.90 ms
+int v24f64_wide() {
+    static int v = [] {
+        const char* e = getenv("GNND_V24F64_WIDE");
+        const int n = e ? atoi(e) : 2;
+        return n == 1 || n == 4 ? n : 2;
+    }();
+    return v;
+}
 // GNND_V24_UPAIR=0: fp32 decoder_v2_4 small batches on the R = 2 edge-pair plan (A/B of the
 // unit-pair MLPs)
 bool v24_upair_disabled() {
@@ -2600,7 +2615,8 @@ int v24_split_forced() {
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
 // B = batch of the launch (plan queries without one assume a large batch)
-int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = INT64_MAX) {
+int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = INT64_MAX,
+              bool allow_wide = true) {
     const size_t esz = dtype == GNND_F64 ? 8 : 4;
     const size_t wb = align16((size_t)lds_weights(model) * esz);
     const size_t target = lds_target();
@@ -2705,6 +2721,16 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         tgt = (kLdsMax / 2) & ~(size_t)15;
     const int us_big = model == GNND_V24 && dtype == GNND_F64 && g.R <= 2 ? v24f64_us_big() : 1;
     const size_t bufb = us_big > 1 ? (size_t)2 * us_big * GNND_BLOCK * 8 + 8 : 0;
+    // fp64 decoder_v2_4 at large batches (v24f64_wide: 2 by default): workgroups of 512 / 1 024
+    // work-item lanes at a half / all of the CU's LDS, so one copy of the Softplus table serves
+    // 8 / 16 waves (4 per SIMD instead of 3)
+    int wide = 1;
+    if (allow_wide && model == GNND_V24 && dtype == GNND_F64 && us_big == 1 &&
+        tgt == (size_t)GNND_V24F64_LDS && tgt != target) {
+        wide = v24f64_wide();
+        if (wide > 1) tgt = (kLdsMax / (4 / wide)) & ~(size_t)15;
+    }
+    const size_t lanes = (size_t)GNND_BLOCK * wide;
     size_t n = fixed + bufb + per >= tgt ? 1 : (tgt - fixed - bufb) / per;
     if (n > 64) n = 64;
     // step-1 lane utilisation: the tile's C*G work items run in rounds of 256 lanes; among
@@ -2716,20 +2742,24 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         size_t best = n;
         double bu = 0;
         for (size_t c = n; c >= 1 && 2 * c >= n; --c) {
-            const size_t items = c * IC, rounds = (items + GNND_BLOCK - 1) / GNND_BLOCK;
-            const double u = (double)items / (double)(rounds * GNND_BLOCK);
+            const size_t items = c * IC, rounds = (items + lanes - 1) / lanes;
+            const double u = (double)items / (double)(rounds * lanes);
             if (u > bu + 1e-9) { bu = u; best = c; }
         }
         n = best;
     }
     // small batches (training steps, latency-bound decodes): at least ~2 workgroups per CU
     // before grouping codewords (B = 128 -> one codeword per workgroup, 128 workgroups)
-    if ((int64_t)n * 512 > B) n = (size_t)(B / 512 > 1 ? B / 512 : 1);
+    if ((int64_t)n * 512 > B) {
+        if (wide > 1) return make_plan(model, dtype, gr, p, B, false);
+        n = (size_t)(B / 512 > 1 ? B / 512 : 1);
+    }
     p->view = &g;
     p->resident = false;
     p->cw = (int)n;
     p->q = 0;
     p->lds = fixed + n * per;
+    p->wide = wide;
     // fp32 decoder_v2_4 at one codeword per workgroup (training steps, small decodes) is
     // latency-bound: one wave per SIMD walks 128 hidden units per edge pair.  Split the units
     // over US waves (B <= 256: 4, one 16-wave workgroup per CU; B <= 512: 2; US = 8 runs 128
@@ -2807,13 +2837,13 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         return GNND_OK;
     };
     // the streaming kernel: every component of a split graph in the same launch
-    auto go_s = [&](auto kern, int us = 1) -> int {
+    auto go_s = [&](auto kern, int us = 1, int wide = 1) -> int {
         if (p.lds > 64 * 1024)
             GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
         const int64_t grid = blocks * p.ncomp;
         if (grid > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
-        const int il = us == 8 ? 128 : GNND_BLOCK;          // unit_split_lanes<US>()
+        const int il = (us == 8 ? 128 : GNND_BLOCK) * wide;  // unit_split_lanes<US>() * WIDE
         kern<<<(unsigned)grid, il * us, p.lds, st>>>(g, (const T*)w, nw, (const TI*)x, (TI*)out,
                                                              B, iters, p.cw, dI, dV, dN, tape,
                                                              p.ncomp > 1 ? p.dviews : nullptr,
@@ -2872,6 +2902,11 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         if (p.us != 1) return GNND_ERR_UNSUPPORTED;
         if constexpr (MODEL == GNND_V24)
             if (tape.ext) return go_s(decode_kernel<MODEL, T, R, true>);
+        if constexpr (MODEL == GNND_V24 && sizeof(T) == 8 && R <= 2) {
+            // (the plan's tile fits any lane count: WIDE only changes the rounds' width)
+            if (p.wide == 2) return go_s(decode_kernel<MODEL, T, R, false, 1, 2>, 1, 2);
+            if (p.wide == 4) return go_s(decode_kernel<MODEL, T, R, false, 1, 4>, 1, 4);
+        }
         return go_s(decode_kernel<MODEL, T, R>);
     }
 }
