@@ -32,7 +32,7 @@ GNND_DEBUG_TU(train)
 
 namespace {
 
-// threads per workgroup: 16 waves (4 per SIMD) in fp32 (128 VGPRs), 8 in fp64 (169 VGPRs)
+// threads per workgroup: 16 waves (4 per SIMD) in fp32 (128 VGPRs), 8 in fp64 (<= 256 VGPRs)
 template <typename T> constexpr int train_threads() { return sizeof(T) == 4 ? 1024 : 512; }
 // fp64 Softplus table of the reverse pass: GNND_BWD_SGTAB 1 (default) the signed one-read table
 // (kSgTab, sg_index / sg_poly / sg_grad_poly), 0 the |h|-indexed kSpTab (A/B builds)
