@@ -2706,8 +2706,9 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
                          (upair ? (size_t)UpairLds::kFloats * 4 + 16 : 0);
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
-    // fp64 decoder_v2_4 stages its 32.8 KB Softplus table per workgroup: a third of the CU's LDS
-    // per workgroup (3 per CU; toric-5: 4 codewords, 3 full item rounds).  Same-box A/B
+    // fp64 decoder_v2_4 stages its 33 KB Softplus table per workgroup: a third of the CU's LDS
+    // per 256-lane workgroup (3 per CU; toric-5: 4 codewords, 3 full item rounds; the default
+    // 512-lane form below: half, 2 per CU, 8 codewords).  Same-box A/B
     // (profiles/r04/experiments/v24_f64_shapes_ab_r04g.txt): 2.24 M cw/s vs 1.96 M at 80 KB
     // (2 per CU), 2.17 M with the units split over 2 waves, 1.74 M over 4
 #ifndef GNND_V24F64_LDS
