@@ -58,6 +58,11 @@ def flops_per_codeword(model, g, T):
     raise ValueError(model)
 
 
+# Hardware transcendental ops (v_exp / v_log / v_rcp_f32) the fp32 BP check step issues per edge
+# and iteration (decode_resident_kernel, product form: tanh = exp + rcp, the leave-one-out rcp,
+# CBP log((1 + p) / (1 - p)) = rcp + log, QBP log(1 + p) - log(1 - p) = 2 log)
+HW_TRANS_PER_EDGE = {'cbp': 5, 'qbp': 5}
+
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
 PEAK_FP64_TFLOPS = 78.6
 PEAK_HBM_GBS = 8000.0
@@ -808,19 +813,25 @@ def decode_run(a, world, rank, dev, cpu='full'):
     ch_ber = float(ch_errs.item()) / (a.batch * g.V * world)
 
     if rank == 0:
+        # SURVEY §8(d)'s algorithmic count: `frac` is always this fraction
         fl, trans = flops_per_codeword(a.model, g, T)
-        sp_flops = None
-        if a.model == 'v24' and dtype == torch.float64:
-            # fp64 has no hardware exp/log: price each Softplus at the fp64 FLOPs of its
-            # minimal table form (softplus_tab_lite, gnnd_common.h: 11 FMAs + 6 adds/muls = 28)
-            sp_flops = 28
-            fl = fl + sp_flops * trans
         achieved = fl * a.batch / kernel_s / 1e12
         peak = PEAK_FP32_TFLOPS if dtype == torch.float32 else PEAK_FP64_TFLOPS
-        # SURVEY §8(d)'s algorithmic count (each Softplus one transcendental, no FLOPs): the
-        # fraction without the fp64 Softplus pricing, reported beside it
-        frac_alg = (fl - (sp_flops or 0) * trans) * a.batch / kernel_s / 1e12 / peak
+        frac_alg = achieved / peak
+        frac_sp = None
+        if a.model == 'v24' and dtype == torch.float64:
+            # fp64 has no hardware exp/log: the fraction with each Softplus priced at the fp64
+            # FLOPs of a minimal table form (11 FMAs + 6 adds/muls = 28), reported beside it only
+            frac_sp = (fl + 28 * trans) * a.batch / kernel_s / 1e12 / peak
         trans_frac = 2 * trans * a.batch / kernel_s / TRANS_OPS_PER_S
+        # fp32 BP: the hardware transcendental ops (v_exp/v_log/v_rcp_f32) the kernel issues per
+        # edge and iteration, at their 8-cycle issue rate: the binding roofline
+        hw_ops = HW_TRANS_PER_EDGE.get(a.model) if dtype == torch.float32 else None
+        trans_hw = None
+        if hw_ops:
+            ops_s = hw_ops * g.E * T * a.batch / kernel_s
+            trans_hw = {'achieved': ops_s / 1e12, 'peak': TRANS_OPS_PER_S / 1e12, 'unit': 'Tops/s',
+                        'frac': ops_s / TRANS_OPS_PER_S, 'ops_per_edge_iteration': hw_ops}
         esz = {torch.float32: 4, torch.float64: 8, torch.bfloat16: 2}[io_dtype]
         io_bytes = (g.N + gd.ops.decode_out_rows(g, a.model, 1, T)) * esz * a.batch
         plan = gd.ops.decode_plan(g, a.model, dtype)
@@ -852,20 +863,26 @@ def decode_run(a, world, rank, dev, cpu='full'):
                                   ': compute cost is weight-independent; BER parity vs the '
                                   'oracle is in cpu_baseline'},
             'roofline': {'bound': 'valu', 'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s',
-                         'frac': achieved / peak, 'traffic': traffic,
+                         'frac': frac_alg, 'traffic': traffic,
                          'kernel': f"{plan['kernel']}<{a.model}, {a.dtype}>",
                          # per-class VALU counts x measured per-class issue costs (ISSUE_NS)
                          'issue_model': issue_model(cls, a.batch, kernel_s) if cls else None,
                          'kernel_ms': kernel_s * 1e3,
                          'flops_per_codeword': fl, 'transcendentals_per_codeword': trans,
-                         'softplus_flops_included': sp_flops,
                          'frac_algorithmic_count': frac_alg,
+                         'frac_softplus_priced_28flop': frac_sp,
                          # >= 2 hardware transcendental ops per function vs the 8-cycle issue
                          # rate (fp32; fp64 has no hardware transcendentals)
                          'transcendental_op_frac': trans_frac if dtype == torch.float32 else None,
                          'hbm_io_bytes_per_launch': io_bytes,
                          'hbm_io_frac': io_bytes / kernel_s / 1e9 / PEAK_HBM_GBS},
         }
+        if trans_hw is not None:
+            # transcendental-bound (fp32 BP): the binding roofline; the FLOP fraction beside it
+            rf = res['roofline']
+            rf.update(bound='transcendental', achieved=trans_hw['achieved'], peak=trans_hw['peak'],
+                      unit=trans_hw['unit'], frac=trans_hw['frac'], frac_flop=frac_alg,
+                      trans_ops_per_edge_iteration=hw_ops)
         if a.cpu_seconds > 0 and world == 1 and cpu != 'off':
             # the oracle decodes the same (for bf16: widened) inputs in fp32
             res['cpu_baseline'] = cpu_baseline(a.model, H, state, x.to(dtype), pred, labels, g, T,
@@ -885,6 +902,18 @@ def decode_run(a, world, rank, dev, cpu='full'):
 SUB_CONFIGS = [
     ('config3_toric5_v24_f64', 'decode', dict(model='v24', code='toric_5', batch=65536, dtype='f64',
                                               steps=10, warmup=2, prewarm_s=0.3)),
+    # config 2 as BASELINE writes it: bf16 x / out in HBM, fp32 weights and arithmetic
+    ('config2_bch_cgnni_bf16', 'decode', dict(model='cgnni', code='bch_63_45', batch=65536,
+                                              dtype='bf16', steps=20, warmup=2, prewarm_s=0.3)),
+    # the decoders SURVEY §8(d) names as the matched-BER references: classical BP
+    # (classical/BP.py:231-259) on configs 1/2's BCH and config 4's LDPC, quantum BP
+    # (quantum/BP.py:191-219) on config 3's toric-5 in the reference dtype
+    ('bp_bch_cbp_f32', 'decode', dict(model='cbp', code='bch_63_45', batch=65536, dtype='f32',
+                                      steps=20, warmup=2, prewarm_s=0.3)),
+    ('bp_ldpc648_cbp_f32', 'decode', dict(model='cbp', code='ldpc_648_324', batch=131072, dtype='f32',
+                                          steps=10, warmup=2, prewarm_s=0.3)),
+    ('bp_toric5_qbp_f64', 'decode', dict(model='qbp', code='toric_5', batch=65536, dtype='f64',
+                                         steps=20, warmup=2, prewarm_s=0.3)),
     ('config4_ldpc648_cgnni_shard', 'decode', dict(model='cgnni', code='ldpc_648_324', batch=131072,
                                                    dtype='f32', steps=20, warmup=2, prewarm_s=0.3)),
     # (200 / 100 timed steps: ~40 / ~120 ms, so the synchronize/barrier around the timed region
@@ -993,7 +1022,7 @@ def compact_entry(r, top=False):
     rf = r.get('roofline') or {}
     roof = _pick(rf, (['bound', 'achieved', 'peak', 'unit', 'frac', 'traffic', 'kernel_ms',
                        'frac_algorithmic_count', 'hbm_io_frac', 'kernel'] if top else
-                      ['frac', 'achieved', 'peak', 'traffic', 'kernel_ms', 'frac_algorithmic_count']), 4)
+                      ['bound', 'frac', 'achieved', 'peak', 'traffic', 'kernel_ms', 'frac_flop']), 4)
     if roof is not None:
         roof.setdefault('traffic', None)
         im = rf.get('issue_model')
@@ -1043,17 +1072,38 @@ def driver_line(res, full_path=None, limit=LINE_LIMIT):
     if full_path:
         line['full_record'] = full_path
     s = json.dumps(line, separators=(',', ':'))
-    # shed optional detail until the line fits (never the contract fields)
-    for drop in (('cpu_baseline', 'sample'), ('cpu_baseline', 'cpu_model'), ('roofline', 'kernel'),
-                 ('data',)):
+    # shed optional detail until the line fits (never the contract fields): the headline's
+    # free text first, then per-config detail in order of decreasing expendability
+    cfg = line.get('configs') or {}
+    b16 = [e for n, e in cfg.items() if '_b16' in n]      # the per-GPU-16 strong-scaling points
+
+    def each(fn, es=None):
+        return lambda: [fn(e) for e in (cfg.values() if es is None else es)]
+    sheds = [lambda: (line.get('cpu_baseline') or {}).pop('sample', None),
+             lambda: (line.get('cpu_baseline') or {}).pop('cpu_model', None),
+             lambda: (line.get('roofline') or {}).pop('kernel', None),
+             lambda: line.pop('data', None),
+             each(lambda e: (e.pop('unit', None), e.pop('steps', None))),
+             each(lambda e: e.pop('cpu_baseline', None), b16),
+             each(lambda e: (e.get('roofline') or {}).pop('peak', None)),
+             each(lambda e: (e.get('roofline') or {}).pop('achieved', None)),
+             each(lambda e: e.pop('workload', None)),
+             each(lambda e: e.pop('cpu_baseline', None)),
+             each(lambda e: e.pop('parity', None))]
+    s = json.dumps(line, separators=(',', ':'))
+    for shed in sheds:
         if len(s) <= limit:
             break
-        d = line
-        for k in drop[:-1]:
-            d = d.get(k) or {}
-        d.pop(drop[-1], None)
+        shed()
         s = json.dumps(line, separators=(',', ':'))
-    assert len(s) <= limit, f'bench line {len(s)} bytes > {limit}'
+    if len(s) > limit:
+        # last resort: the contract fields alone, the full record named; never an
+        # exception after the whole run
+        keep = ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step',
+                'higher_is_better', 'scaling', 'vs_baseline', 'dtype', 'config', 'roofline',
+                'cpu_baseline', 'full_record')
+        s = json.dumps({k: line[k] for k in keep if k in line}, separators=(',', ':'))
+        print(f'bench: driver line over {limit} bytes; configs left to {full_path}', file=sys.stderr)
     return s
 
 

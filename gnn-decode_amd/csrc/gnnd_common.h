@@ -9,6 +9,17 @@
 #define GNND_BLOCK 256            // threads per decode workgroup (tuning variants: -DGNND_BLOCK=128)
 #endif
 
+// Planner A/B switches (GNND_NO_RESIDENT, GNND_LDS_TARGET, ...) are read from the environment
+// only in tuning builds (tools/build_variant*.sh pass -DGNND_TUNING): the release library's
+// kernel choice, and so its output bits, never depend on the caller's environment
+// (tests/test_abi.py::test_release_library_reads_no_tuning_env checks the built .so).
+#ifdef GNND_TUNING
+#include <stdlib.h>
+#define gnnd_tune_env(name) getenv(name)
+#else
+#define gnnd_tune_env(name) ((const char*)nullptr)
+#endif
+
 // ---------------------------------------------------------------------------------------
 // debug build (make debug -> gnndecode/libgnnd_debug.so, -DGNND_DEBUG): the kernels check
 // the table-derived indices they otherwise trust (LDS positions, variable ids, slots) and

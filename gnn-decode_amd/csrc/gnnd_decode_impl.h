@@ -2491,12 +2491,12 @@ constexpr int kResidentRegBudget = 88;          // Q * (2R + 2) state VGPRs (<= 
 // LDS budget per workgroup: 40 KiB -> 4 workgroups (16 waves) per CU.  GNND_LDS_TARGET
 // (bytes) overrides it for tuning sweeps; GNND_NO_RESIDENT=1 forces the streaming kernel.
 bool lds_target_set() {                // GNND_LDS_TARGET given (A/B): it overrides every budget
-    static const bool v = getenv("GNND_LDS_TARGET") != nullptr;
+    static const bool v = gnnd_tune_env("GNND_LDS_TARGET") != nullptr;
     return v;
 }
 size_t lds_target() {
     static size_t v = [] {
-        const char* e = getenv("GNND_LDS_TARGET");
+        const char* e = gnnd_tune_env("GNND_LDS_TARGET");
         long n = e ? atol(e) : 0;
         return n >= 4096 && n <= (long)kLdsMax ? (size_t)n : (size_t)(40 * 1024);
     }();
@@ -2505,14 +2505,14 @@ size_t lds_target() {
 // GNND_NO_F64_RESIDENT=1: fp64 light models on the streaming kernel (A/B)
 bool f64_resident_disabled() {
     static bool v = [] {
-        const char* e = getenv("GNND_NO_F64_RESIDENT");
+        const char* e = gnnd_tune_env("GNND_NO_F64_RESIDENT");
         return e && e[0] == '1';
     }();
     return v;
 }
 bool resident_disabled() {
     static bool v = [] {
-        const char* e = getenv("GNND_NO_RESIDENT");
+        const char* e = gnnd_tune_env("GNND_NO_RESIDENT");
         return e && e[0] == '1';
     }();
     return v;
@@ -2521,7 +2521,7 @@ bool resident_disabled() {
 // GNND_NO_VLAYOUT=1: resident kernel on the identity message layout (A/B measurements)
 bool vlayout_disabled() {
     static bool v = [] {
-        const char* e = getenv("GNND_NO_VLAYOUT");
+        const char* e = gnnd_tune_env("GNND_NO_VLAYOUT");
         return e && e[0] == '1';
     }();
     return v;
@@ -2558,7 +2558,7 @@ int device_cus() {
 }
 bool split_pays(int64_t B) {
     static bool always = [] {
-        const char* e = getenv("GNND_SPLIT_ALWAYS");
+        const char* e = gnnd_tune_env("GNND_SPLIT_ALWAYS");
         return e && e[0] == '1';
     }();
     return always || B < device_cus();
@@ -2566,7 +2566,7 @@ bool split_pays(int64_t B) {
 // GNND_NO_SPLIT=1: decode split graphs whole (A/B of the component split)
 bool split_disabled() {
     static bool v = [] {
-        const char* e = getenv("GNND_NO_SPLIT");
+        const char* e = gnnd_tune_env("GNND_NO_SPLIT");
         return e && e[0] == '1';
     }();
     return v;
@@ -2577,7 +2577,7 @@ bool split_disabled() {
 // the MLP units split over US waves as well (A/B; default 1)
 int v24f64_us_big() {
     static int v = [] {
-        const char* e = getenv("GNND_V24F64_US");
+        const char* e = gnnd_tune_env("GNND_V24F64_US");
         const int n = e ? atoi(e) : 0;
         return n == 2 || n == 4 ? n : 1;
     }();
@@ -2588,7 +2588,7 @@ int v24f64_us_big() {
 // (profiles/r05/experiments/ab_r05r_f64_wide.txt, config 3): 23.29 / 23.11 / 24.90 ms
 int v24f64_wide() {
     static int v = [] {
-        const char* e = getenv("GNND_V24F64_WIDE");
+        const char* e = gnnd_tune_env("GNND_V24F64_WIDE");
         const int n = e ? atoi(e) : 2;
         return n == 1 || n == 4 ? n : 2;
     }();
@@ -2598,14 +2598,14 @@ int v24f64_wide() {
 // unit-pair MLPs)
 bool v24_upair_disabled() {
     static bool v = [] {
-        const char* e = getenv("GNND_V24_UPAIR");
+        const char* e = gnnd_tune_env("GNND_V24_UPAIR");
         return e && e[0] == '0';
     }();
     return v;
 }
 int v24_split_forced() {
     static int v = [] {
-        const char* e = getenv("GNND_V24_SPLIT");
+        const char* e = gnnd_tune_env("GNND_V24_SPLIT");
         const int n = e ? atoi(e) : 0;
         return n == 1 || n == 2 || n == 4 || n == 8 ? n : 0;
     }();
@@ -2665,7 +2665,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         int best = 0, bestq = 0;
         double bestu = 0;
         static const int force_q = [] {
-            const char* e = getenv("GNND_RESIDENT_Q");
+            const char* e = gnnd_tune_env("GNND_RESIDENT_Q");
             return e ? atoi(e) : 0;
         }();
         for (int q : kResidentQ) {
@@ -2702,8 +2702,11 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
     const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kV24F64TabDoubles + 3 * 128 + 12) * 8 : 0;
+    // (decode_kernel stages the unit-pair weights whenever fp32 V24 runs a one-slot plan, kUP:
+    // reserve them for every such plan, not only for the upair choice above — ADVICE r05)
+    const bool up_lds = v24f32 && g.R == 1;
     const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab +
-                         (upair ? (size_t)UpairLds::kFloats * 4 + 16 : 0);
+                         (up_lds ? (size_t)UpairLds::kFloats * 4 + 16 : 0);
     const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     // fp64 decoder_v2_4 stages its 33 KB Softplus table per workgroup: a third of the CU's LDS
@@ -2800,13 +2803,17 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
 // streaming kernel on a split graph (gnnd_graph::comp) decodes each component of a codeword in
 // its own workgroup(s); the plan is made for component 0 (all components share its shape and
 // slot plans) at the launch's B * ncomp component-codewords.
-int plan_for(int model, int dtype, const gnnd_graph* g, Plan* p, int64_t B = INT64_MAX) {
+// allow_wide = false: the training forward (TAPE), whose decode_kernel instantiation runs 256
+// work-item lanes, is planned for 256-lane workgroups (a WIDE plan's tile and LDS
+// target would leave it at two workgroups per CU)
+int plan_for(int model, int dtype, const gnnd_graph* g, Plan* p, int64_t B = INT64_MAX,
+             bool allow_wide = true) {
     if (model == GNND_V24 && g->ncomp > 1 && g->dcomp && !g->nosplit && !split_disabled() &&
         split_pays(B)) {
         const int K = g->ncomp;
         const gnnd_graph* c0 = g->comp[0];
         const int64_t BK = B > INT64_MAX / K ? INT64_MAX : B * K;
-        const int rc = make_plan(model, dtype, c0, p, BK);
+        const int rc = make_plan(model, dtype, c0, p, BK, allow_wide);
         if (rc != GNND_OK) return rc;
         if (!p->resident) {
             const int kind = p->view == &c0->view ? 0 : p->view == &c0->rview ? 1 : 2;
@@ -2816,7 +2823,7 @@ int plan_for(int model, int dtype, const gnnd_graph* g, Plan* p, int64_t B = INT
             return GNND_OK;
         }
     }
-    return make_plan(model, dtype, g, p, B);
+    return make_plan(model, dtype, g, p, B, allow_wide);
 }
 
 template <int MODEL, typename T, int R, typename TI = T>
@@ -2929,8 +2936,9 @@ int launch_decode_r(const gnnd_graph* g, const void* w, const void* x, void* out
                     int iters, hipStream_t st, void* tape_base = nullptr,
                     const FwdLoss* floss = nullptr) {
     Plan p;
-    int rc = plan_for(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p, B);
+    int rc = plan_for(MODEL, sizeof(T) == 8 ? GNND_F64 : GNND_F32, g, &p, B, tape_base == nullptr);
     if (rc != GNND_OK) return rc;
+    if (tape_base && p.wide != 1) return GNND_ERR_UNSUPPORTED;   // (planned without WIDE above)
     TapeView<T> tape{};
     if (tape_base) {                        // [ext | u | t] x [iters][B][E], then mT [B][E]
         if (p.resident) return GNND_ERR_UNSUPPORTED;

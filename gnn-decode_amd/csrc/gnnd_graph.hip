@@ -66,7 +66,7 @@ struct HostTables {
 // GNND_NO_SLOT_SPREAD=1: the x-augmented layouts keep the slot plan's edge order (A/B)
 bool slot_spread_disabled() {
     static bool v = [] {
-        const char* e = getenv("GNND_NO_SLOT_SPREAD");
+        const char* e = gnnd_tune_env("GNND_NO_SLOT_SPREAD");
         return e && e[0] == '1';
     }();
     return v;
@@ -158,7 +158,7 @@ void spread_check_slots(int C, int G, int R, int cw, int P, const std::vector<in
     }
     slot = best;
     static const bool log = [] {
-        const char* e = getenv("GNND_SLOT_SPREAD_LOG");
+        const char* e = gnnd_tune_env("GNND_SLOT_SPREAD_LOG");
         return e && e[0] == '1';
     }();
     if (log) {
@@ -170,7 +170,7 @@ void spread_check_slots(int C, int G, int R, int cw, int P, const std::vector<in
 // GNND_NO_TPERM=1: the x layouts keep T rows in variable order (ts = V, tpos(v) = v) (A/B)
 bool tperm_disabled() {
     static bool v = [] {
-        const char* e = getenv("GNND_NO_TPERM");
+        const char* e = gnnd_tune_env("GNND_NO_TPERM");
         return e && e[0] == '1';
     }();
     return v;
@@ -298,7 +298,7 @@ void place_t_rows(int C, int G, int R, int cw, int V, const std::vector<int>& vo
         }
     }
     static const bool log = [] {
-        const char* e = getenv("GNND_SLOT_SPREAD_LOG");
+        const char* e = gnnd_tune_env("GNND_SLOT_SPREAD_LOG");
         return e && e[0] == '1';
     }();
     if (log) {
@@ -344,7 +344,7 @@ int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, 
     // butterfly steps per edge: toric QGNNI 147 -> 159 M cw/s, LDPC CGNNI 12.7 -> 13.9 M).
     // GNND_GROUP_R forces R in both (tuning sweeps) when it yields G <= 64.
     static const int force_r = [] {
-        const char* e = getenv("GNND_GROUP_R");
+        const char* e = gnnd_tune_env("GNND_GROUP_R");
         return e ? atoi(e) : 0;
     }();
     // tie preference: 0 = smaller R, 1 = larger R, 2 = R = 2 (the paired-edge fp32 V24

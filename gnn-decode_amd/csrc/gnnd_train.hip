@@ -972,7 +972,7 @@ __global__ void grad_reduce_kernel(const T* __restrict__ gpart, int rows, T* __r
 // GNND_TRAIN_THREADS forces one (A/B).
 int train_threads_f32(int64_t blocks) {
     static int forced = [] {
-        const char* e = getenv("GNND_TRAIN_THREADS");
+        const char* e = gnnd_tune_env("GNND_TRAIN_THREADS");
         const int n = e ? atoi(e) : 0;
         return n == 512 || n == 5122 || n == 2564 || n == 1024 ? n : 0;
     }();

@@ -585,7 +585,12 @@ class FusedGnnTrainer(_GraphedStep):
             # mean gradient and loss weighted by its codeword count, summed, divided by the
             # global count -- the full-batch mean for any shard sizes (shard_bounds of an odd
             # global batch gives unequal shards)
-            self._gl.mul_(float(self._nb))
+            # (an empty shard -- global batch < world -- has a NaN mean; it contributes nothing,
+            # and NaN * 0 would still be NaN: zero it)
+            if self._nb == 0:
+                self._gl.zero_()
+            else:
+                self._gl.mul_(float(self._nb))
             self._count.fill_(float(self._nb))
             dist.all_reduce(self._gbuf, op=dist.ReduceOp.SUM, group=self.group)
             self._gl.div_(self._count)

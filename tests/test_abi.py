@@ -24,6 +24,25 @@ def test_library_present_and_loads():
     assert lib.gnnd_version() == 1
 
 
+def test_release_library_reads_no_tuning_env():
+    """the planner's A/B switches (gnnd_tune_env in gnnd_common.h) are
+    compiled into tuning builds only, so the release library's kernel choice -- and its output
+    bits -- cannot depend on the caller's environment.  Every knob the sources name is absent
+    from the built release .so, and no source calls getenv directly."""
+    csrc = os.path.join(ROOT, 'gnn-decode_amd', 'csrc')
+    knobs = set()
+    for f in os.listdir(csrc):
+        src = open(os.path.join(csrc, f)).read()
+        knobs |= set(re.findall(r'gnnd_tune_env\("(GNND_[A-Z0-9_]+)"\)', src))
+        code = re.sub(r'//[^\n]*', '', src)
+        calls = re.findall(r'\bgetenv\s*\(', code)
+        assert f == 'gnnd_common.h' or not calls, f'{f} calls getenv outside gnnd_tune_env'
+    assert len(knobs) >= 15, knobs
+    lib = open(os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'libgnnd.so'), 'rb').read()
+    found = sorted(k for k in knobs if k.encode() in lib)
+    assert not found, f'tuning knobs compiled into the release library: {found}'
+
+
 def test_every_header_symbol_is_exported_and_bound():
     lib = _lib.get()
     names = header_functions()

@@ -87,6 +87,14 @@ def _full_size_record():
     c = r['configs']
     c['config5_toric7_v24_train_b16'] = dict(c['config5_toric7_v24_train_global128'])
     c['config5_toric7_v24_train_b16_f64'] = dict(c['config5_toric7_v24_train_global128_f64'])
+    # round 6: config 2 in bf16 and the BP decoders (transcendental-bound rooflines)
+    c['config2_bch_cgnni_bf16'] = json.loads(json.dumps(r))
+    c['config2_bch_cgnni_bf16'].pop('configs')
+    for n in ('bp_bch_cbp_f32', 'bp_ldpc648_cbp_f32', 'bp_toric5_qbp_f64'):
+        e = json.loads(json.dumps(c['config4_ldpc648_cgnni_shard']))
+        e['roofline'].update(bound='transcendental', unit='Tops/s', frac_flop=0.1)
+        c[n] = e
+    assert set(c) == {n for n, _, _ in bench.SUB_CONFIGS}
     r['scaling_efficiency_global128'] = bench.strong_scaling(c)
     r['dist'] = {'backend': 'nccl', 'world_size': 8,
                  'ranks': [{'rank': i, 'device': i, 'host': 'h' * 24, 'pci_bus': 10 + i}
@@ -115,13 +123,22 @@ def test_driver_line_fits_and_keeps_every_config():
     for name, e in line['configs'].items():
         assert e['value'] > 0 and e['ms_per_step'] > 0, name
         assert e['roofline']['frac'] > 0 and 'traffic' in e['roofline'], name
-        assert e['cpu_baseline']['value'] > 0, name
+        assert e['roofline']['bound'], name
+        if '_b16' not in name:          # (the per-GPU-16 points may shed their CPU legs)
+            assert e['cpu_baseline']['value'] > 0, name
         assert e['parity'], name
+    for n in ('bp_bch_cbp_f32', 'bp_ldpc648_cbp_f32', 'bp_toric5_qbp_f64'):
+        assert line['configs'][n]['roofline']['bound'] == 'transcendental'
+        assert line['configs'][n]['roofline']['frac_flop'] > 0
     assert line['dist']['world_size'] == 8 and len(line['dist']['ranks']) == 8
     assert line['scaling_efficiency_global128']['f32']['eff_8gpu'] > 0
     # a line over the limit sheds optional detail, never a contract field, and asserts
     tight = bench.driver_line(r, None, limit=len(s) - 50)
     assert len(tight) <= len(s) - 50 and 'cpu_baseline' in json.loads(tight)
+    # far over: the contract fields alone, no exception after the whole run
+    tiny = json.loads(bench.driver_line(r, 'f.json', limit=1500))
+    assert tiny['value'] == line['value'] and tiny['full_record'] == 'f.json'
+    assert 'roofline' in tiny and 'configs' not in tiny
 
 
 def _rank_map_worker(rank, world, port, q):

@@ -125,3 +125,45 @@ def test_local_trainer_in_a_multi_rank_job_issues_no_collective():
     x, y = _data(B)
     assert losses == [float(tr.step(x, y)) for _ in range(steps)]
     assert not train._collective(train.LOCAL, True)
+
+
+def _reduce_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    # FusedGnnTrainer's CGNNI reduce on its own (no device kernels): [gradient | loss | count]
+    tr = train.FusedGnnTrainer.__new__(train.FusedGnnTrainer)
+    tr.model = type('M', (), {'kind': 'cgnni'})()
+    tr.group = None
+    n = 4
+    tr._gbuf = torch.zeros(n + 2, dtype=torch.float64)
+    tr._gl, tr._count = tr._gbuf[:n + 1], tr._gbuf[n + 1]
+    sizes = [1, 1, 0]                   # global batch 2 over 3 ranks: rank 2's shard is empty
+    assert [e - s for s, e in (train.shard_bounds(2, r, world) for r in range(world))] == sizes
+    tr._nb = sizes[rank]
+    if tr._nb:
+        tr._gl.copy_(torch.arange(n + 1, dtype=torch.float64) * (rank + 1))
+    else:
+        tr._gl.fill_(float('nan'))      # the mean over zero codewords
+    tr._reduce(None, None)
+    q.put((rank, tr._gl.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_cgnni_reduce_with_an_empty_shard_gloo3():
+    """global batch < world leaves a rank with no codewords; its NaN mean must not
+    reach the summed gradient (3 gloo ranks, global batch 2)."""
+    world = 3
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reduce_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [(1.0 * i + 2.0 * i) / 2 for i in range(5)]     # the full-batch mean of ranks 0, 1
+    for _, gl in res:
+        assert gl == want

@@ -4,6 +4,8 @@
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
+# the knobs are read by the tuning build only (make -C gnn-decode_amd tuning)
+export GNND_LIB="$ROOT/gnn-decode_amd/gnndecode/libgnnd_tuning.so"
 OUT="$1"; KNOB="$2"; mkdir -p "$OUT"
 : > "$OUT/ab.jsonl"
 run() {  # tag args...

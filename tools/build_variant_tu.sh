@@ -11,7 +11,7 @@ pids=()
 for t in $tus; do
   x=""
   case $t in gnnd_decode_cgnni|gnnd_decode_qgnni|gnnd_decode_cbp|gnnd_decode_qbp|gnnd_decode_nbp|gnnd_decode_v10|gnnd_decode_v22) x=-fno-slp-vectorize;; esac
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $x $flags -c csrc/$t.hip -o build_$name/$t.o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DGNND_TUNING $x $flags -c csrc/$t.hip -o build_$name/$t.o &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p; done
