@@ -185,6 +185,7 @@ struct gnnd_graph {
     gnnd_graph* comp[8];
     GraphView* dcomp;
     int nosplit;              // gnnd_graph_set_split(g, 0): decode / train the graph whole
+    int min_dc;               // smallest check degree (the fp32 BP ratio-form check step needs 2)
 };
 constexpr int kMaxComp = 8;
 

@@ -401,6 +401,119 @@ __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, co
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// decoder_v2_4's check-side MLP as a per-launch table (fp64).  ggc2.mlp
+// (Linear(1, 128) -> Softplus -> Linear(128, 1), quantum/decoder_v2_4.py:241-243, :253-257) is
+// applied to ONE scalar u = S_c(tanh(m/2)) - tanh(m_e/2) (:135-136), a sum of at most dc - 1
+// values in [-1, 1]: |u| <= R = max_dc - 1.  f(u) = W2 . softplus(W1 u + b1) + b2 is analytic
+// there, so each launch tabulates it once as degree-7 Taylor polynomials about c_j = j / 32,
+// j = -32 R .. 32 R (|u - c_j| <= 1/64), and the decode evaluates it as one index (4 VALU), one
+// 64-byte entry (4 ds_read_b128) and 7 FMAs instead of 128 hidden units (~16 VALU each).
+// Coefficients a_n = sum_k W2_k W1_k^n softplus^(n)(h_k) / n!, h_k = W1_k c_j + b1_k, from the
+// exact derivatives: softplus' = sigma, sigma^(n) = tau U_n(q) with tau = sigma (1 - sigma),
+// q = 1 - 2 sigma, U_1 = 1, U_{n+1} = q U_n - (1 - q^2) U_n' / 2 (no cancellation near
+// |h| large: tau = e / (1 + e)^2 with e = exp(-|h|)).  Remainder <= (1/64)^8 / 8! * max|sigma^(7)|
+// (= 1.0625) * sum_k |W2_k| |W1_k|^8: 8.5e-16 for the reference's epoch-67 weights.  The table
+// is used only when that bound is <= 1e-13 and no unit's h range crosses torch's Softplus
+// threshold 20 inside [-R, R] (the jump there is not polynomial); otherwise the per-unit path.
+// ---------------------------------------------------------------------------------------
+#ifndef GNND_V24_CTAB
+#define GNND_V24_CTAB 1          // 0: the per-unit check MLP everywhere (A/B builds)
+#endif
+constexpr int kCtabInv = 32;                 // centres c_j = j / kCtabInv
+struct alignas(16) CtabEntry {
+    double a[8];                             // Taylor coefficients a_0 .. a_7 about c_j
+};
+__host__ __device__ constexpr int ctab_entries(int max_dc) {
+    return 2 * kCtabInv * (max_dc > 1 ? max_dc - 1 : 0) + 1;
+}
+// U_n(q) / (n + 1)!  for n = 1..6 (the coefficients of softplus^(n+1) = sigma^(n) = tau U_n(q)
+// divided by the Taylor factorial), ascending powers of q
+__device__ __forceinline__ double ctab_un(int n, double q) {
+    const double q2 = q * q;
+    switch (n) {
+        case 1: return 1.0 / 2;
+        case 2: return q / 6;
+        case 3: return fma(q2, 1.5, -0.5) / 24;
+        case 4: return q * fma(q2, 3.0, -2.0) / 120;
+        case 5: return fma(q2, fma(q2, 7.5, -7.5), 1.0) / 720;
+        default: return q * fma(q2, fma(q2, 22.5, -30.0), 8.5) / 5040;
+    }
+}
+// Every thread of the workgroup calls it (one __syncthreads_or).  wm = ggc2.mlp's packed weights
+// {W1[128], b1[128], W2[128], b2}; returns true when the table is valid (see above).  Each
+// entry's 128-unit sums run as 4 chunks of 32 units in fixed order, combined by a fixed 4-lane
+// butterfly: the same bits in every workgroup and for every workgroup size.
+__device__ bool build_ctab(const double* __restrict__ wm, CtabEntry* tab, int R, int tid, int NT) {
+    constexpr int QC = 4, KU = 128 / QC;
+    const int NE = 2 * kCtabInv * R + 1;
+    int bad = 0;
+    for (int base = 0; base < NE * QC; base += NT) {        // (uniform trip count)
+        const int it = base + tid;
+        const bool live = it < NE * QC;
+        const int j = live ? it / QC : 0, q = it % QC;
+        const double c = (double)(j - kCtabInv * R) * (1.0 / kCtabInv);
+        double a[8];
+#pragma unroll
+        for (int n = 0; n < 8; ++n) a[n] = 0.0;
+        double w8 = 0.0;                                     // sum |W2| |W1|^8 (remainder bound)
+        for (int i = 0; i < KU; ++i) {
+            const int k = q * KU + i;
+            const double W1 = wm[k], b1 = wm[128 + k], W2 = wm[256 + k];
+            const double h = fma(W1, c, b1);
+            const double hlo = b1 - fabs(W1) * R, hhi = b1 + fabs(W1) * R;
+            double d[8];
+            if (hlo > 20.0) {                  // torch's threshold over the whole range: h
+                d[0] = h;
+                d[1] = 1.0;
+#pragma unroll
+                for (int n = 2; n < 8; ++n) d[n] = 0.0;
+            } else {
+                if (hhi > 20.0) bad = 1;       // the threshold's jump lies inside [-R, R]
+                const double e = exp(-fabs(h));
+                const double s = 1.0 / (1.0 + e);
+                const double tau = e * s * s;
+                const double qv = h >= 0.0 ? (e - 1.0) * s : (1.0 - e) * s;
+                d[0] = fmax(h, 0.0) + log1p(e);
+                d[1] = h >= 0.0 ? s : e * s;
+#pragma unroll
+                for (int n = 2; n < 8; ++n) d[n] = tau * ctab_un(n - 1, qv);
+            }
+            double p = W2;
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                a[n] = fma(p, d[n], a[n]);
+                p *= W1;
+            }
+            const double w2 = W1 * W1, w4 = w2 * w2;
+            w8 = fma(fabs(W2), w4 * w4, w8);
+        }
+#pragma unroll
+        for (int n = 0; n < 8; ++n) a[n] = group_sum_c<QC>(a[n]);
+        w8 = group_sum_c<QC>(w8);
+        if (live && q == 0) {
+            a[0] += wm[384];
+            CtabEntry& en = tab[j];
+#pragma unroll
+            for (int n = 0; n < 8; ++n) en.a[n] = a[n];
+            // (1/64)^8 / 8! * 1.0625 * sum |W2| |W1|^8 <= 1e-13
+            if (j == 0 && w8 * (1.0625 / 40320.0 / 281474976710656.0) > 1e-13) bad = 1;
+        }
+    }
+    return !__syncthreads_or(bad);
+}
+// MLP_c(u) from the table (R32 = kCtabInv * R): the nearest centre, then Horner in r = u - c_j
+__device__ __forceinline__ double ctab_eval(const CtabEntry* tab, double u, int R32) {
+    int k = round_magic_lo(__builtin_fma(u, (double)kCtabInv, kRoundMagic));
+    k = k < -R32 ? -R32 : (k > R32 ? R32 : k);                // (u is within [-R, R] + rounding)
+    const double r = __builtin_fma((double)k, -1.0 / kCtabInv, u);
+    const CtabEntry e = tab[k + R32];
+    double p = e.a[7];
+#pragma unroll
+    for (int n = 6; n >= 0; --n) p = fma(p, r, e.a[n]);
+    return p;
+}
+
 // fp32 forms: TWO EDGES per call, riding the two halves of packed FMAs (the lane's
 // slots are processed in pairs).  Prepared layout (gnnd_prepare_weights; base-2 rescaled:
 // W1', b1' = W1, b1 x log2(e); w2' = W2 x ln(2)):
@@ -1182,11 +1295,15 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     T* s_tab = nullptr;
     T* s_bias = nullptr;
     T* s_lin = nullptr;        // [3][4] {A, B, C, 0} per MLP (mlp_lin), after the biases
+    CtabEntry* s_ctab = nullptr;   // [ctab_entries(max_dc)] check-MLP table (build_ctab)
+    const int R32 = kCtabInv * (g.max_dc > 1 ? g.max_dc - 1 : 0);
     if constexpr (kTab) {
         s_tab = (T*)smem;
         s_bias = s_tab + kV24F64TabDoubles;
         s_lin = s_bias + 3 * 128;
-        off = (size_t)(kV24F64TabDoubles + 3 * 128 + 12) * 8;
+        s_ctab = (CtabEntry*)(s_lin + 16);
+        off = (size_t)(kV24F64TabDoubles + 3 * 128 + 16) * 8 +
+              (GNND_V24_CTAB ? (size_t)ctab_entries(g.max_dc) * sizeof(CtabEntry) : 0);
         if (tid < 64) {            // wave 0: fixed-order 128-term dot products (same in every block)
             for (int m = 0; m < 3; ++m) {
                 const T* wm = w + (m == 0 ? kV24Ggc1 : m == 1 ? kV24Ggc2 : kV24Mlp);
@@ -1209,6 +1326,9 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             s_bias[i] = w[m == 0 ? kV24Ggc1 + 256 + k : (m == 1 ? kV24Ggc2 : kV24Mlp) + 128 + k];
         }
     }
+    // the check-side MLP's table (uniform: every thread gets the same verdict)
+    bool ctab_ok = false;
+    if constexpr (kTab && GNND_V24_CTAB) ctab_ok = build_ctab((const double*)w + kV24Ggc2, s_ctab, R32 / kCtabInv, tid, NT);
     const int nslot = C * G * R;
     uint32_t* s_slot = (uint32_t*)(smem + off);
     int* s_vptr = (int*)(s_slot + nslot);
@@ -1222,8 +1342,6 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // not flat ones as through an integer cast of the pointer)
     f32x2* s_part = (f32x2*)(smem + ((((char*)(s_xc + (size_t)CW * C) - smem) + 7) & ~(ptrdiff_t)7));
 
-    const int64_t b0 = (int64_t)blk * CW;
-    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
     constexpr bool kV24F64 = MODEL == GNND_V24 && sizeof(T) == 8;
     // fp32 V24 on the R = 1 slot plan (B <= 4096): the unit-pair MLPs (mlp128_upair), their
@@ -1246,6 +1364,14 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             s_wcm[i] = e;
         }
     }
+    // Tiles: tile = blk, blk + grid, ... below cblk (the launch's tiles per component).  A
+    // persistent launch (launch_decode: fp64 decoder_v2_4 at large batches, one workgroup per
+    // resident slot) runs several, paying the per-workgroup prologue above -- the Softplus
+    // table, the check-MLP table -- once per slot instead of once per tile; every other launch
+    // has one tile per workgroup (split graphs: exactly one).
+    for (int tile = blk; tile < cblk; tile += views ? cblk : (int)gridDim.x) {
+    const int64_t b0 = (int64_t)tile * CW;
+    const int nb = (int)((B - b0) < CW ? (B - b0) : CW);
     // fp32 decoder_v2_4 reads its weights through the scalar cache only (no LDS copy); with
     // every table and the tile's rows within one element per thread (small batches: one
     // component-codeword per workgroup) all global loads are issued before any LDS store, so
@@ -1348,6 +1474,10 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
         }
     }
     GNND_PMARK(pf, 11);
+    // fp64 unit split: the partial-sum buffer of the next mlp128d_split call (the two buffers
+    // alternate call by call, so a buffer is rewritten only after a barrier that follows every
+    // read of its previous contents)
+    int pbuf = 0;
     for (int it = 0; it < iters; ++it) {
         for (int f0 = 0; f0 < nItem; f0 += IL) {
             const int f = f0 + itid;
@@ -1441,7 +1571,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const T a = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
-                                                        s_pd + (r & 1) * US * GNND_BLOCK, itid, widle,
+                                                        s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid, widle,
                                                         s_tab, s_lin, s_wcm);
                     tv[r] = val[r] ? tanh_half_fast(a) : T(0);
                     cf[r] = T(0);
@@ -1530,9 +1660,14 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             } else if constexpr (kV24F64) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const T y = mlp128d_split<US, false>(wv + kV24Ggc2, s_bias + 128, Sc - tv[r], Sc - tv[r], sub,
-                                                         s_pd + ((R + r) & 1) * US * GNND_BLOCK, itid,
-                                                         widle, s_tab, s_lin + 4, s_wcm + 128);
+                    const T u = Sc - tv[r];
+                    T y;
+                    if (ctab_ok)                 // (uniform) every unit-split wave evaluates it
+                        y = ctab_eval(s_ctab, u, R32);
+                    else
+                        y = mlp128d_split<US, false>(wv + kV24Ggc2, s_bias + 128, u, u, sub,
+                                                     s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid,
+                                                     widle, s_tab, s_lin + 4, s_wcm + 128);
                     mn[r] = y * sc + mv[r];
                 }
             } else if constexpr (WBP) {
@@ -1711,6 +1846,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
         }
     }
     GNND_PMARK(pf, 10);
+    __syncthreads();                 // (the next tile restages the rows this one read)
+    }
     GNND_PREPORT(pf, TAPE ? "fwd_tape" : "fwd", US, iters);
 }
 
@@ -2701,7 +2838,11 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
                          : upair ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
-    const size_t tab = model == GNND_V24 && dtype == GNND_F64 ? (size_t)(kV24F64TabDoubles + 3 * 128 + 12) * 8 : 0;
+    // (fp64 V24: Softplus table, biases, linear parts, then the check-MLP table, build_ctab)
+    const size_t tab = model == GNND_V24 && dtype == GNND_F64
+                           ? (size_t)(kV24F64TabDoubles + 3 * 128 + 16) * 8 +
+                                 (GNND_V24_CTAB ? (size_t)ctab_entries(g.max_dc) * sizeof(CtabEntry) : 0)
+                           : 0;
     // (decode_kernel stages the unit-pair weights whenever fp32 V24 runs a one-slot plan, kUP:
     // reserve them for every such plan, not only for the upair choice above — ADVICE r05)
     const bool up_lds = v24f32 && g.R == 1;
@@ -2845,13 +2986,21 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         return GNND_OK;
     };
     // the streaming kernel: every component of a split graph in the same launch
-    auto go_s = [&](auto kern, int us = 1, int wide = 1) -> int {
+    // persist: one workgroup per resident slot (occupancy x CUs), each looping over tiles
+    // (decode_kernel's tile loop); split graphs never
+    auto go_s = [&](auto kern, int us = 1, int wide = 1, bool persist = false) -> int {
         if (p.lds > 64 * 1024)
             GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
-        const int64_t grid = blocks * p.ncomp;
+        int64_t grid = blocks * p.ncomp;
         if (grid > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
         const int il = (us == 8 ? 128 : GNND_BLOCK) * wide;  // unit_split_lanes<US>() * WIDE
+        if (persist && p.ncomp == 1) {
+            int per_cu = 0;
+            GNND_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, il * us, p.lds));
+            const int64_t slots = (int64_t)(per_cu > 0 ? per_cu : 1) * device_cus();
+            if (grid > slots) grid = slots;
+        }
         kern<<<(unsigned)grid, il * us, p.lds, st>>>(g, (const T*)w, nw, (const TI*)x, (TI*)out,
                                                              B, iters, p.cw, dI, dV, dN, tape,
                                                              p.ncomp > 1 ? p.dviews : nullptr,
@@ -2910,12 +3059,14 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         if (p.us != 1) return GNND_ERR_UNSUPPORTED;
         if constexpr (MODEL == GNND_V24)
             if (tape.ext) return go_s(decode_kernel<MODEL, T, R, true>);
+        // fp64 decoder_v2_4 decodes run persistent (their prologue builds two LDS tables)
+        constexpr bool kPersist = MODEL == GNND_V24 && sizeof(T) == 8;
         if constexpr (MODEL == GNND_V24 && sizeof(T) == 8 && R <= 2) {
             // (the plan's tile fits any lane count: WIDE only changes the rounds' width)
-            if (p.wide == 2) return go_s(decode_kernel<MODEL, T, R, false, 1, 2>, 1, 2);
-            if (p.wide == 4) return go_s(decode_kernel<MODEL, T, R, false, 1, 4>, 1, 4);
+            if (p.wide == 2) return go_s(decode_kernel<MODEL, T, R, false, 1, 2>, 1, 2, kPersist);
+            if (p.wide == 4) return go_s(decode_kernel<MODEL, T, R, false, 1, 4>, 1, 4, kPersist);
         }
-        return go_s(decode_kernel<MODEL, T, R>);
+        return go_s(decode_kernel<MODEL, T, R>, 1, 1, kPersist);
     }
 }
 

@@ -55,7 +55,7 @@ struct Layout {
 // everything gnnd_graph_create uploads, built on the host (also checked by
 // gnnd_graph_validate_host without a device)
 struct HostTables {
-    int V = 0, C = 0, E = 0, max_dv = 0, max_dc = 0, nints = 0, ord_off = 0, nsr = 0;
+    int V = 0, C = 0, E = 0, max_dv = 0, max_dc = 0, min_dc = 0, nints = 0, ord_off = 0, nsr = 0;
     int plan_off[3] = {0, 0, 0};
     SlotPlan plans[3];
     Layout lays[7], laysx[7];
@@ -332,7 +332,12 @@ int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, 
     }
     int max_dv = 0, max_dc = 0;
     for (int v = 0; v < V; ++v) { max_dv = vptr[v + 1] > max_dv ? vptr[v + 1] : max_dv; vptr[v + 1] += vptr[v]; }
-    for (int c = 0; c < C; ++c) { max_dc = cptr[c + 1] > max_dc ? cptr[c + 1] : max_dc; cptr[c + 1] += cptr[c]; }
+    int min_dc = C > 0 ? cptr[1] : 0;
+    for (int c = 0; c < C; ++c) {
+        max_dc = cptr[c + 1] > max_dc ? cptr[c + 1] : max_dc;
+        min_dc = cptr[c + 1] < min_dc ? cptr[c + 1] : min_dc;
+        cptr[c + 1] += cptr[c];
+    }
     {
         std::vector<int> fill(cptr.begin(), cptr.end() - 1);
         for (int e = 0; e < E; ++e) cedge[fill[h_chk[e]]++] = e;   // increasing e per check
@@ -496,7 +501,7 @@ int build_tables(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges, 
             memcpy(table.data() + o + 2 * V, L.slot.data(), sizeof(int) * nsr);
         }
 
-    T.V = V; T.C = C; T.E = E; T.max_dv = max_dv; T.max_dc = max_dc;
+    T.V = V; T.C = C; T.E = E; T.max_dv = max_dv; T.max_dc = max_dc; T.min_dc = min_dc;
     T.nints = nints; T.ord_off = ord_off; T.nsr = nsr;
     return GNND_OK;
 }
@@ -655,6 +660,7 @@ int create_single(const int64_t* h_var, const int64_t* h_chk, int64_t num_edges,
     gv.xs = V + C; gv.xv0 = 0; gv.xc0 = V; gv.os = V; gv.o0 = 0; gv.es = E; gv.e0 = 0;
     gv.ts = V;
     g->ncomp = 1;
+    g->min_dc = T.min_dc;
     g->rview = gv;
     g->pview = gv;
     for (int i = 0; i < 3; ++i) {

@@ -69,6 +69,7 @@ SIGNATURES = {
                                  ctypes.c_double, ctypes.c_double, _vp, _vp]),
     'gnnd_syndrome_loss': (_int, [_vp, _vp, _i32, _i32, _int, _vp, _vp, _vp, _vp, _i64, _vp]),
     'gnnd_decision_errors': (_int, [_vp, _vp, _i32, _int, _vp, _vp, _vp, _i64, _vp]),
+    'gnnd_v24_check_mlp_table': (_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     'gnnd_adam_step': (_int, [_int, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_double, ctypes.c_double,
                               ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp]),
     'gnnd_sample_toric': (_int, [_vp, _int, ctypes.POINTER(ctypes.c_double), _i32, ctypes.c_uint64,

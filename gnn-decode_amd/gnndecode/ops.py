@@ -413,6 +413,21 @@ def syndrome_loss(graph, logical_rows, logical_only, pred, y):
     return loss_b, dpred
 
 
+def v24_check_mlp_table(graph, w, u):
+    """decoder_v2_4's check-side MLP evaluated through the fp64 decoder's per-launch table
+    (gnnd_v24_check_mlp_table): (y [n] fp64, valid) where valid says whether the decoder uses
+    the table for these weights.  w: packed fp64 V24 weights (1 283); u: fp64 inputs within
+    [-(max_dc - 1), max_dc - 1]."""
+    _require_gpu(w, u)
+    w = w.to(torch.float64).contiguous()
+    u = u.to(torch.float64).contiguous().reshape(-1)
+    y = torch.empty_like(u)
+    ok = torch.zeros(1, dtype=torch.int32, device=u.device)
+    _lib.call('gnnd_v24_check_mlp_table', graph.handle, _ptr(w), _ptr(u), _ptr(y), u.numel(),
+              _ptr(ok), current_stream(u.device))
+    return y, bool(ok.item())
+
+
 def decision_errors(graph, logical_rows, pred, y):
     """(bit errors, frame errors, residual-syndrome failures, logical failures) of hard
     decisions pred > 0.5 against y, one HIP launch (gnnd_decision_errors); int64 tensor [4]

@@ -197,6 +197,18 @@ int gnnd_prepare_weights(int model, int dtype, const void* d_w, void* d_prepared
 int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
                 void* d_out, int64_t batch, int32_t iters, void* stream);
 
+/* decoder_v2_4's check-side MLP (ggc2.mlp: Linear(1,128) -> Softplus -> Linear(128,1),
+ * quantum/decoder_v2_4.py:241-243, :253-257) as the fp64 decoder evaluates it: its input
+ * u = S_c(tanh(m/2)) - tanh(m_e/2) lies in [-R, R], R = max check degree - 1, so every fp64
+ * decode tabulates the MLP once per launch (degree-7 Taylor polynomials about j/32) and reads
+ * the table instead of the 128 hidden units.  This evaluates the same table at d_u [n]
+ * (fp64, inside [-R, R]) into d_y [n]; d_w = the packed fp64 V24 weights (1 283).  *d_ok
+ * (device int32) = 1 when the table is valid -- the decoder uses it -- or 0 when a unit's
+ * pre-activation range crosses torch's Softplus threshold 20 or the Taylor remainder bound
+ * exceeds 1e-13 (the decoder then evaluates the units).                                    */
+int gnnd_v24_check_mlp_table(const gnnd_graph* g, const void* d_w, const void* d_u, void* d_y,
+                             int64_t n, int32_t* d_ok, void* stream);
+
 /* Codewords per workgroup the decoder would use (for roofline bookkeeping). */
 int gnnd_decode_tile(const gnnd_graph* g, int model, int dtype, int32_t* h_cw_per_block,
                      int32_t* h_lds_bytes);

@@ -1,0 +1,94 @@
+"""decoder_v2_4's check-side MLP through the fp64 decoder's per-launch table (build_ctab /
+ctab_eval in gnnd_decode_impl.h, exposed as gnnd_v24_check_mlp_table).
+
+ggc2.mlp (Linear(1,128) -> Softplus -> Linear(128,1), quantum/decoder_v2_4.py:241-243,
+:253-257) is evaluated on ONE scalar u = S_c(tanh(m/2)) - tanh(m_e/2) in [-(dc-1), dc-1]
+(:135-136), so the decoder tabulates it per launch (degree-7 Taylor polynomials about j/32).
+Held here against torch's own fp64 MLP (the reference module, Softplus threshold 20 included)
+at 1e-13 absolute over the whole input range; weights whose unit range crosses the Softplus
+threshold make the table invalid and the decoder falls back to the per-unit MLP (decode
+still equal to the oracle, rtol 1e-10, bit-exact decisions).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import gnn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOL = 1e-13
+
+
+def _model(L=5, weights='shipped', seed=0):
+    import gnndecode as gd
+    H = gd.codes.toric_code(L)
+    torch.manual_seed(seed)
+    m = gd.MODELS['v24'](15, H)
+    if weights == 'shipped':
+        z = np.load(os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights', 'v24_toric_5.npz'))
+        m.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files})
+    return m.to(DEV).double().eval(), H
+
+
+def _torch_mlp(m, u):
+    with torch.no_grad():
+        return m.ggc2.mlp(u.view(-1, 1)).view(-1)
+
+
+def _inputs(R):
+    u = torch.linspace(-R, R, 24001, dtype=torch.float64, device=DEV)
+    g = torch.Generator(device='cpu').manual_seed(1)
+    extra = (torch.rand(4000, generator=g, dtype=torch.float64) * 2 - 1).to(DEV) * R
+    return torch.cat([u, extra, torch.tensor([-R, R, 0.0, 1 / 64, -1 / 64], dtype=torch.float64, device=DEV)])
+
+
+@pytest.mark.parametrize('weights', ['shipped', 'random'])
+def test_table_matches_reference_mlp(weights):
+    import gnndecode as gd
+    m, H = _model(weights=weights)
+    g = m.graph(torch.device(DEV))
+    R = g.max_chk_degree - 1
+    assert R == 3
+    u = _inputs(R)
+    y, ok = gd.ops.v24_check_mlp_table(g, m.packed_weights().double(), u)
+    assert ok
+    err = float((y - _torch_mlp(m, u)).abs().max())
+    assert err <= TOL, err
+
+
+def test_threshold_crossing_unit_disables_table_and_decode_stays_exact():
+    """A unit whose pre-activation range over [-R, R] crosses torch's Softplus threshold (20):
+    the table is reported invalid, and the decoder's per-unit path still matches the oracle."""
+    import gnndecode as gd
+    m, H = _model(weights='shipped')
+    with torch.no_grad():
+        m.ggc2.mlp[0].weight[5, 0] = 2.0      # h = 2 u + 17 spans [11, 23] over u in [-3, 3]
+        m.ggc2.mlp[0].bias[5] = 17.0
+    g = m.graph(torch.device(DEV))
+    u = _inputs(3)
+    _, ok = gd.ops.v24_check_mlp_table(g, m.packed_weights().double(), u)
+    assert not ok
+    x, _ = gd.data.toric_batch(H, 64, seed=3, device=torch.device(DEV), dtype=torch.float64)
+    out = gd.ops.decode(g, 'v24', x, m.Nc, m.prepared_weights(torch.float64, torch.device(DEV)))
+    w = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    ref = O.decode('v24', H, x.cpu().numpy(), m.Nc, w)
+    got = out.cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
+    assert ((got > 0.5) == (ref > 0.5)).all()
+
+
+def test_large_weights_fail_the_remainder_bound():
+    """sum |W2| |W1|^8 large enough that the Taylor remainder bound exceeds 1e-13: invalid."""
+    import gnndecode as gd
+    m, H = _model(weights='shipped')
+    with torch.no_grad():
+        m.ggc2.mlp[0].weight[7, 0] = 6.0       # |W1|^8 = 1.7e6, bias keeps h below 20
+        m.ggc2.mlp[0].bias[7] = -10.0
+    g = m.graph(torch.device(DEV))
+    _, ok = gd.ops.v24_check_mlp_table(g, m.packed_weights().double(), _inputs(3))
+    assert not ok
