@@ -80,6 +80,17 @@ extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void*
     }
     size_t bytes = (size_t)n * (dtype == GNND_F64 ? 8 : 4);
     GNND_HIP_CHECK(hipMemcpyAsync(d_prepared, d_w, bytes, hipMemcpyDeviceToDevice, st));
+    // fp64 decoder_v2_4: [plain | bound, R limit, pad | check-MLP table] (ctab_build_kernel)
+    if (model == GNND_V24 && dtype == GNND_F64)
+        return launch_ctab_build((const double*)d_w, (double*)d_prepared, st);
+    return GNND_OK;
+}
+
+extern "C" int gnnd_prepared_weights_count(int model, int dtype, int64_t* h_count) {
+    int n = weights_count(model);
+    if (n == -1 || !h_count || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
+    if (n < 0) return GNND_ERR_UNSUPPORTED;
+    *h_count = model == GNND_V24 && dtype == GNND_F64 ? kV24PreparedF64 : n;
     return GNND_OK;
 }
 

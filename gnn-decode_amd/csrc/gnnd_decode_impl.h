@@ -402,115 +402,152 @@ __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, co
 }
 
 // ---------------------------------------------------------------------------------------
-// decoder_v2_4's check-side MLP as a per-launch table (fp64).  ggc2.mlp
-// (Linear(1, 128) -> Softplus -> Linear(128, 1), quantum/decoder_v2_4.py:241-243, :253-257) is
-// applied to ONE scalar u = S_c(tanh(m/2)) - tanh(m_e/2) (:135-136), a sum of at most dc - 1
-// values in [-1, 1]: |u| <= R = max_dc - 1.  f(u) = W2 . softplus(W1 u + b1) + b2 is analytic
-// there, so each launch tabulates it once as degree-7 Taylor polynomials about c_j = j / 32,
-// j = -32 R .. 32 R (|u - c_j| <= 1/64), and the decode evaluates it as one index (4 VALU), one
-// 64-byte entry (4 ds_read_b128) and 7 FMAs instead of 128 hidden units (~16 VALU each).
+// decoder_v2_4's check-side MLP as a table (fp64).  ggc2.mlp (Linear(1, 128)
+// -> Softplus -> Linear(128, 1), quantum/decoder_v2_4.py:241-243, :253-257) is applied to ONE
+// scalar u = S_c(tanh(m/2)) - tanh(m_e/2) (:135-136), a sum of at most dc - 1 values in
+// [-1, 1]: |u| <= R = max_dc - 1.  f(u) = W2 . softplus(W1 u + b1) + b2 is analytic there, so
+// gnnd_prepare_weights (and gnnd_train_update after every optimizer step) tabulates it once per
+// weight set in the prepared layout, as degree-11 Taylor polynomials about c_j = j / 8 for
+// |c_j| <= kCtabRcap (ctab_build_kernel), and the decoder stages the entries its graph needs
+// (|c_j| <= R) in LDS and evaluates f as one index (4 VALU), one 96-byte entry (6
+// ds_read_b128) and 11 FMAs instead of 128 hidden units (~16 VALU each).
 // Coefficients a_n = sum_k W2_k W1_k^n softplus^(n)(h_k) / n!, h_k = W1_k c_j + b1_k, from the
-// exact derivatives: softplus' = sigma, sigma^(n) = tau U_n(q) with tau = sigma (1 - sigma),
-// q = 1 - 2 sigma, U_1 = 1, U_{n+1} = q U_n - (1 - q^2) U_n' / 2 (no cancellation near
-// |h| large: tau = e / (1 + e)^2 with e = exp(-|h|)).  Remainder <= (1/64)^8 / 8! * max|sigma^(7)|
-// (= 1.0625) * sum_k |W2_k| |W1_k|^8: 8.5e-16 for the reference's epoch-67 weights.  The table
-// is used only when that bound is <= 1e-13 and no unit's h range crosses torch's Softplus
-// threshold 20 inside [-R, R] (the jump there is not polynomial); otherwise the per-unit path.
+// exact derivatives: softplus' = sigma, sigma^(n) = tau U_n(q), tau = sigma (1 - sigma) =
+// e / (1 + e)^2 with e = exp(-|h|) (no cancellation at large |h|), q = 1 - 2 sigma, U_1 = 1,
+// U_{n+1} = q U_n - (1 - q^2) U_n' / 2.  Remainder <= (1/16)^12 / 12! * max|sigma^(11)| (= 86.375)
+// * sum_k |W2_k| |W1_k|^12: 7.4e-16 for the reference's epoch-67 weights.  The decoder uses the
+// table only when that bound is <= 1e-13 and no unit's pre-activation crosses torch's Softplus
+// threshold 20 for some u in [-R, R] (the jump there is not polynomial); otherwise it evaluates
+// the 128 units (ctab_valid).
 // ---------------------------------------------------------------------------------------
 #ifndef GNND_V24_CTAB
 #define GNND_V24_CTAB 1          // 0: the per-unit check MLP everywhere (A/B builds)
 #endif
-constexpr int kCtabInv = 32;                 // centres c_j = j / kCtabInv
-struct alignas(16) CtabEntry {
-    double a[8];                             // Taylor coefficients a_0 .. a_7 about c_j
-};
+constexpr int kCtabInv = 8;                  // centres c_j = j / kCtabInv
+constexpr int kCtabNC = 12;                  // Taylor coefficients a_0 .. a_11 per entry
+constexpr int kCtabRcap = 31;                // prepared table: |c_j| <= 31 (max_dc <= 32)
+constexpr int kCtabCap = 2 * kCtabInv * kCtabRcap + 1;               // 497 entries
+constexpr int kV24CtabOff = 1288;            // doubles: prepared fp64 V24 = [1283 plain | pad | table]
+constexpr int kV24PreparedF64 = kV24CtabOff + kCtabCap * kCtabNC;    // 7 252
+// (1/16)^12 / 12! * max|sigma^(11)|: the remainder bound per unit of sum |W2| |W1|^12
+constexpr double kCtabBoundCoef = 86.375 / 479001600.0 / 281474976710656.0;
 __host__ __device__ constexpr int ctab_entries(int max_dc) {
     return 2 * kCtabInv * (max_dc > 1 ? max_dc - 1 : 0) + 1;
 }
-// U_n(q) / (n + 1)!  for n = 1..6 (the coefficients of softplus^(n+1) = sigma^(n) = tau U_n(q)
-// divided by the Taylor factorial), ascending powers of q
-__device__ __forceinline__ double ctab_un(int n, double q) {
-    const double q2 = q * q;
+// U_n(q) / (n + 1)!  for n = 1..10 (softplus^(n+1) / (n+1)! = tau U_n(q) / (n+1)!); U_n has the
+// parity of n - 1, so each is a polynomial in q^2 (times q for even n)
+__device__ __forceinline__ double ctab_un(int n, double q, double q2) {
     switch (n) {
         case 1: return 1.0 / 2;
-        case 2: return q / 6;
-        case 3: return fma(q2, 1.5, -0.5) / 24;
-        case 4: return q * fma(q2, 3.0, -2.0) / 120;
-        case 5: return fma(q2, fma(q2, 7.5, -7.5), 1.0) / 720;
-        default: return q * fma(q2, fma(q2, 22.5, -30.0), 8.5) / 5040;
+        case 2: return q * (1.0 / 6);
+        case 3: return fma(q2, 1.5, -0.5) * (1.0 / 24);
+        case 4: return q * fma(q2, 3.0, -2.0) * (1.0 / 120);
+        case 5: return fma(q2, fma(q2, 7.5, -7.5), 1.0) * (1.0 / 720);
+        case 6: return q * fma(q2, fma(q2, 22.5, -30.0), 8.5) * (1.0 / 5040);
+        case 7: return fma(q2, fma(q2, fma(q2, 78.75, -131.25), 57.75), -4.25) * (1.0 / 40320);
+        case 8: return q * fma(q2, fma(q2, fma(q2, 315.0, -630.0), 378.0), -62.0) * (1.0 / 362880);
+        case 9: return fma(q2, fma(q2, fma(q2, fma(q2, 1417.5, -3307.5), 2520.0), -660.0), 31.0) *
+                       (1.0 / 3628800);
+        default: return q * fma(q2, fma(q2, fma(q2, fma(q2, 7087.5, -18900.0), 17482.5), -6360.0), 691.0) *
+                        (1.0 / 39916800);
     }
 }
-// Every thread of the workgroup calls it (one __syncthreads_or).  wm = ggc2.mlp's packed weights
-// {W1[128], b1[128], W2[128], b2}; returns true when the table is valid (see above).  Each
-// entry's 128-unit sums run as 4 chunks of 32 units in fixed order, combined by a fixed 4-lane
-// butterfly: the same bits in every workgroup and for every workgroup size.
-__device__ bool build_ctab(const double* __restrict__ wm, CtabEntry* tab, int R, int tid, int NT) {
-    constexpr int QC = 4, KU = 128 / QC;
-    const int NE = 2 * kCtabInv * R + 1;
-    int bad = 0;
-    for (int base = 0; base < NE * QC; base += NT) {        // (uniform trip count)
-        const int it = base + tid;
-        const bool live = it < NE * QC;
-        const int j = live ? it / QC : 0, q = it % QC;
-        const double c = (double)(j - kCtabInv * R) * (1.0 / kCtabInv);
-        double a[8];
+// One entry per block (blockIdx.x = j + kCtabInv kCtabRcap), one hidden unit per thread (128):
+// w = plain packed V24 weights (ggc2.mlp at kV24Ggc2; may alias prep), prep = the prepared
+// buffer: table [kCtabCap][kCtabNC] at kV24CtabOff, and block 0 also writes prep[1283] = the
+// remainder bound (kCtabBoundCoef sum |W2| |W1|^12) and prep[1284] = the smallest distance, over
+// the units, of their pre-activation's crossing of torch's threshold 20 from u = 0 ((20 - b1) /
+// |W1|): the table holds for R below it.  The 128-unit sums run as two fixed 64-lane
+// butterflies and one fixed add: the same bits on every launch.
+__device__ __forceinline__ double group_min64(double v) {
 #pragma unroll
-        for (int n = 0; n < 8; ++n) a[n] = 0.0;
-        double w8 = 0.0;                                     // sum |W2| |W1|^8 (remainder bound)
-        for (int i = 0; i < KU; ++i) {
-            const int k = q * KU + i;
-            const double W1 = wm[k], b1 = wm[128 + k], W2 = wm[256 + k];
-            const double h = fma(W1, c, b1);
-            const double hlo = b1 - fabs(W1) * R, hhi = b1 + fabs(W1) * R;
-            double d[8];
-            if (hlo > 20.0) {                  // torch's threshold over the whole range: h
-                d[0] = h;
-                d[1] = 1.0;
+    for (int o = 1; o < 64; o <<= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__global__ void __launch_bounds__(128) ctab_build_kernel(const double* w, double* prep) {
+    const double* wm = w + kV24Ggc2;
+    const int k = threadIdx.x, j = blockIdx.x;
+    const double c = (double)(j - kCtabInv * kCtabRcap) * (1.0 / kCtabInv);
+    const double W1 = wm[k], b1 = wm[128 + k], W2 = wm[256 + k], b2 = wm[384];
+    const double h = fma(W1, c, b1);
+    double d[kCtabNC];
+    if (h > 20.0) {                            // torch's threshold: softplus(h) = h
+        d[0] = h;
+        d[1] = 1.0;
 #pragma unroll
-                for (int n = 2; n < 8; ++n) d[n] = 0.0;
-            } else {
-                if (hhi > 20.0) bad = 1;       // the threshold's jump lies inside [-R, R]
-                const double e = exp(-fabs(h));
-                const double s = 1.0 / (1.0 + e);
-                const double tau = e * s * s;
-                const double qv = h >= 0.0 ? (e - 1.0) * s : (1.0 - e) * s;
-                d[0] = fmax(h, 0.0) + log1p(e);
-                d[1] = h >= 0.0 ? s : e * s;
+        for (int n = 2; n < kCtabNC; ++n) d[n] = 0.0;
+    } else {
+        const double e = exp(-fabs(h));
+        const double sv = 1.0 / (1.0 + e);
+        const double tau = e * sv * sv;
+        const double q = h >= 0.0 ? (e - 1.0) * sv : (1.0 - e) * sv;
+        const double q2 = q * q;
+        d[0] = fmax(h, 0.0) + log1p(e);
+        d[1] = h >= 0.0 ? sv : e * sv;
 #pragma unroll
-                for (int n = 2; n < 8; ++n) d[n] = tau * ctab_un(n - 1, qv);
-            }
-            double p = W2;
+        for (int n = 2; n < kCtabNC; ++n) d[n] = tau * ctab_un(n - 1, q, q2);
+    }
+    __shared__ double part[kCtabNC + 2];
+    double t[kCtabNC];
+    double p = W2;
 #pragma unroll
-            for (int n = 0; n < 8; ++n) {
-                a[n] = fma(p, d[n], a[n]);
-                p *= W1;
-            }
-            const double w2 = W1 * W1, w4 = w2 * w2;
-            w8 = fma(fabs(W2), w4 * w4, w8);
-        }
+    for (int n = 0; n < kCtabNC; ++n) {
+        t[n] = group_sum_c<64>(p * d[n]);
+        p *= W1;
+    }
+    double s12 = 0.0, rk = 0.0;
+    if (j == 0) {                              // (uniform)
+        const double w2 = W1 * W1, w4 = w2 * w2;
+        s12 = group_sum_c<64>(fabs(W2) * (w4 * w4 * w4));
+        const double a = fabs(W1);
+        rk = group_min64(a > 0.0 ? fabs(20.0 - b1) / a : (b1 == 20.0 ? 0.0 : 1e300));
+    }
+    if (k == 64) {
 #pragma unroll
-        for (int n = 0; n < 8; ++n) a[n] = group_sum_c<QC>(a[n]);
-        w8 = group_sum_c<QC>(w8);
-        if (live && q == 0) {
-            a[0] += wm[384];
-            CtabEntry& en = tab[j];
+        for (int n = 0; n < kCtabNC; ++n) part[n] = t[n];
+        part[kCtabNC] = s12;
+        part[kCtabNC + 1] = rk;
+    }
+    __syncthreads();
+    if (k == 0) {
+        double* en = prep + kV24CtabOff + (size_t)j * kCtabNC;
 #pragma unroll
-            for (int n = 0; n < 8; ++n) en.a[n] = a[n];
-            // (1/64)^8 / 8! * 1.0625 * sum |W2| |W1|^8 <= 1e-13
-            if (j == 0 && w8 * (1.0625 / 40320.0 / 281474976710656.0) > 1e-13) bad = 1;
+        for (int n = 0; n < kCtabNC; ++n) en[n] = (t[n] + part[n]) + (n == 0 ? b2 : 0.0);
+        if (j == 0) {
+            prep[1283] = (s12 + part[kCtabNC]) * kCtabBoundCoef;
+            prep[1284] = fmin(rk, part[kCtabNC + 1]);
         }
     }
-    return !__syncthreads_or(bad);
 }
-// MLP_c(u) from the table (R32 = kCtabInv * R): the nearest centre, then Horner in r = u - c_j
-__device__ __forceinline__ double ctab_eval(const CtabEntry* tab, double u, int R32) {
+// the table of the plain weights w into the prepared buffer prep (w may alias prep)
+int launch_ctab_build(const double* w, double* prep, hipStream_t st) {
+    ctab_build_kernel<<<kCtabCap, 128, 0, st>>>(w, prep);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+// Whether the prepared table holds for a graph with |u| <= R (w = the prepared weights): no
+// unit's pre-activation reaches 20 for |u| <= R unless it stays above 20 there (a crossing at
+// distance rk from u = 0 lies outside [-R, R] iff R < rk), and the remainder bound <= 1e-13
+__device__ __forceinline__ bool ctab_valid(const double* __restrict__ w, int R) {
+    return GNND_V24_CTAB && R <= kCtabRcap && w[1283] <= 1e-13 && (double)R < w[1284];
+}
+// MLP_c(u) from the staged entries (tab[0] at c = -R, R8 = kCtabInv R): the nearest centre,
+// then Horner in r = u - c_j
+__device__ __forceinline__ double ctab_eval(const double* tab, double u, int R8) {
     int k = round_magic_lo(__builtin_fma(u, (double)kCtabInv, kRoundMagic));
-    k = k < -R32 ? -R32 : (k > R32 ? R32 : k);                // (u is within [-R, R] + rounding)
+    k = k < -R8 ? -R8 : (k > R8 ? R8 : k);                    // (u is within [-R, R] + rounding)
     const double r = __builtin_fma((double)k, -1.0 / kCtabInv, u);
-    const CtabEntry e = tab[k + R32];
-    double p = e.a[7];
+    const double2* e = (const double2*)(tab + (size_t)(k + R8) * kCtabNC);
+    double a[kCtabNC];
 #pragma unroll
-    for (int n = 6; n >= 0; --n) p = fma(p, r, e.a[n]);
+    for (int i = 0; i < kCtabNC / 2; ++i) {
+        const double2 v = e[i];
+        a[2 * i] = v.x;
+        a[2 * i + 1] = v.y;
+    }
+    double p = a[kCtabNC - 1];
+#pragma unroll
+    for (int n = kCtabNC - 2; n >= 0; --n) p = fma(p, r, a[n]);
     return p;
 }
 
@@ -1295,15 +1332,15 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     T* s_tab = nullptr;
     T* s_bias = nullptr;
     T* s_lin = nullptr;        // [3][4] {A, B, C, 0} per MLP (mlp_lin), after the biases
-    CtabEntry* s_ctab = nullptr;   // [ctab_entries(max_dc)] check-MLP table (build_ctab)
-    const int R32 = kCtabInv * (g.max_dc > 1 ? g.max_dc - 1 : 0);
+    double* s_ctab = nullptr;      // [ctab_entries(max_dc)][kCtabNC] check-MLP table entries
+    const int Rc = g.max_dc > 1 ? g.max_dc - 1 : 0, R8 = kCtabInv * Rc;
     if constexpr (kTab) {
         s_tab = (T*)smem;
         s_bias = s_tab + kV24F64TabDoubles;
         s_lin = s_bias + 3 * 128;
-        s_ctab = (CtabEntry*)(s_lin + 16);
+        s_ctab = s_lin + 16;
         off = (size_t)(kV24F64TabDoubles + 3 * 128 + 16) * 8 +
-              (GNND_V24_CTAB ? (size_t)ctab_entries(g.max_dc) * sizeof(CtabEntry) : 0);
+              (GNND_V24_CTAB ? (size_t)ctab_entries(g.max_dc) * kCtabNC * 8 : 0);
         if (tid < 64) {            // wave 0: fixed-order 128-term dot products (same in every block)
             for (int m = 0; m < 3; ++m) {
                 const T* wm = w + (m == 0 ? kV24Ggc1 : m == 1 ? kV24Ggc2 : kV24Mlp);
@@ -1326,9 +1363,16 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             s_bias[i] = w[m == 0 ? kV24Ggc1 + 256 + k : (m == 1 ? kV24Ggc2 : kV24Mlp) + 128 + k];
         }
     }
-    // the check-side MLP's table (uniform: every thread gets the same verdict)
+    // the check-side MLP's table entries |c_j| <= R from the prepared weights (uniform verdict)
     bool ctab_ok = false;
-    if constexpr (kTab && GNND_V24_CTAB) ctab_ok = build_ctab((const double*)w + kV24Ggc2, s_ctab, R32 / kCtabInv, tid, NT);
+    if constexpr (kTab && GNND_V24_CTAB) {
+        ctab_ok = ctab_valid((const double*)w, Rc);
+        if (ctab_ok) {
+            const double2* src = (const double2*)((const double*)w + kV24CtabOff +
+                                                  (size_t)(kCtabInv * kCtabRcap - R8) * kCtabNC);
+            for (int i = tid; i < ctab_entries(g.max_dc) * kCtabNC / 2; i += NT) ((double2*)s_ctab)[i] = src[i];
+        }
+    }
     const int nslot = C * G * R;
     uint32_t* s_slot = (uint32_t*)(smem + off);
     int* s_vptr = (int*)(s_slot + nslot);
@@ -1663,7 +1707,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     const T u = Sc - tv[r];
                     T y;
                     if (ctab_ok)                 // (uniform) every unit-split wave evaluates it
-                        y = ctab_eval(s_ctab, u, R32);
+                        y = ctab_eval(s_ctab, u, R8);
                     else
                         y = mlp128d_split<US, false>(wv + kV24Ggc2, s_bias + 128, u, u, sub,
                                                      s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid,
@@ -2838,10 +2882,10 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
                          : upair ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
-    // (fp64 V24: Softplus table, biases, linear parts, then the check-MLP table, build_ctab)
+    // (fp64 V24: Softplus table, biases, linear parts, then the check-MLP table entries)
     const size_t tab = model == GNND_V24 && dtype == GNND_F64
                            ? (size_t)(kV24F64TabDoubles + 3 * 128 + 16) * 8 +
-                                 (GNND_V24_CTAB ? (size_t)ctab_entries(g.max_dc) * sizeof(CtabEntry) : 0)
+                                 (GNND_V24_CTAB ? (size_t)ctab_entries(g.max_dc) * kCtabNC * 8 : 0)
                            : 0;
     // (decode_kernel stages the unit-pair weights whenever fp32 V24 runs a one-slot plan, kUP:
     // reserve them for every such plan, not only for the upair choice above — ADVICE r05)

@@ -24,35 +24,39 @@ int gnnd_launch_v24_tape_loss(const gnnd_graph* g, int dtype, const void* w, con
 }
 
 // ---------------------------------------------------------------------------------------
-// decoder_v2_4's check-side MLP through the per-launch table the fp64 decoder builds
-// (build_ctab / ctab_eval, gnnd_decode_impl.h): the same table and evaluation, exposed so
-// tests can hold it against the reference MLP (quantum/decoder_v2_4.py:241-243, :253-257)
+// decoder_v2_4's check-side MLP through the table the fp64 decoder reads (ctab_build_kernel /
+// ctab_valid / ctab_eval, gnnd_decode_impl.h): the same staged entries and evaluation, exposed
+// so tests can hold it against the reference MLP (quantum/decoder_v2_4.py:241-243, :253-257)
 // ---------------------------------------------------------------------------------------
 namespace {
 __global__ void __launch_bounds__(256)
-ctab_eval_kernel(const double* __restrict__ wm, int R, const double* __restrict__ u,
+ctab_eval_kernel(const double* __restrict__ w, int max_dc, const double* __restrict__ u,
                  double* __restrict__ y, int64_t n, int32_t* __restrict__ ok) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    CtabEntry* tab = (CtabEntry*)smem;
-    const bool valid = build_ctab(wm, tab, R, threadIdx.x, blockDim.x);
+    double* tab = (double*)smem;
+    const int R = max_dc > 1 ? max_dc - 1 : 0, R8 = kCtabInv * R;
+    const bool valid = ctab_valid(w, R);
     if (blockIdx.x == 0 && threadIdx.x == 0) *ok = valid ? 1 : 0;
+    if (!valid) return;                                       // (uniform)
+    const double2* src = (const double2*)(w + kV24CtabOff + (size_t)(kCtabInv * kCtabRcap - R8) * kCtabNC);
+    for (int i = threadIdx.x; i < ctab_entries(max_dc) * kCtabNC / 2; i += blockDim.x) ((double2*)tab)[i] = src[i];
+    __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        y[i] = ctab_eval(tab, u[i], kCtabInv * R);
+        y[i] = ctab_eval(tab, u[i], R8);
 }
 }  // namespace
 
 extern "C" int gnnd_v24_check_mlp_table(const gnnd_graph* g, const void* d_w, const void* d_u,
                                         void* d_y, int64_t n, int32_t* d_ok, void* stream) {
     if (!g || !d_w || !d_ok || n < 0 || (n > 0 && (!d_u || !d_y))) return GNND_ERR_INVALID_ARG;
-    const int R = g->view.max_dc > 1 ? g->view.max_dc - 1 : 0;
-    const size_t lds = (size_t)ctab_entries(g->view.max_dc) * sizeof(CtabEntry);
-    if (lds > 160 * 1024) return GNND_ERR_UNSUPPORTED;
+    const int max_dc = g->view.max_dc;
+    const size_t lds = (size_t)ctab_entries(max_dc < kCtabRcap + 1 ? max_dc : kCtabRcap + 1) * kCtabNC * 8;
     auto kern = ctab_eval_kernel;
     if (lds > 64 * 1024)
         GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int64_t blocks = n > 0 ? std::min<int64_t>((n + 255) / 256, 64) : 1;
-    kern<<<(unsigned)blocks, 256, lds, (hipStream_t)stream>>>((const double*)d_w + kV24Ggc2, R,
-                                                               (const double*)d_u, (double*)d_y, n, d_ok);
+    kern<<<(unsigned)blocks, 256, lds, (hipStream_t)stream>>>((const double*)d_w, max_dc, (const double*)d_u,
+                                                               (double*)d_y, n, d_ok);
     GNND_LAUNCH_CHECK();
     return GNND_OK;
 }

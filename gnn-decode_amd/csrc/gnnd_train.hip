@@ -1657,6 +1657,9 @@ extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64
             (double*)d_exp_avg, (double*)d_exp_avg_sq, d_step, d_sync, nw, lr, beta1, beta2,
             eps, weight_decay, (double*)d_prepared, 0);
     GNND_LAUNCH_CHECK();
+    // fp64 decoder_v2_4: the check-MLP table of the updated weights (the prepared layout's tail)
+    if (model == GNND_V24 && dtype == GNND_F64 && d_prepared)
+        return launch_ctab_build((const double*)d_prepared, (double*)d_prepared, st);
     return GNND_OK;
 }
 

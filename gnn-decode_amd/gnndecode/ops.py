@@ -168,6 +168,17 @@ def weights_count(model, graph=None, iters=None):
     return n.value
 
 
+def prepared_count(model, dtype, graph=None, iters=None):
+    """Elements of the kernel-layout weights (gnnd_prepared_weights_count): the packed count,
+    except fp64 decoder_v2_4, whose prepared weights carry the check-MLP table."""
+    if model in WEIGHTED_BP:
+        return weights_count(model, graph, iters)
+    n = ctypes.c_int64()
+    _lib.call('gnnd_prepared_weights_count', _lib.VARIANT[model],
+              dtype_code(torch.float32 if dtype == torch.bfloat16 else dtype), ctypes.byref(n))
+    return n.value
+
+
 def prepare_weights(model, flat):
     """Kernel-layout copy of a packed weight vector (gnnd_prepare_weights).  The weighted-BP
     tables are used as packed."""
@@ -180,7 +191,7 @@ def prepare_weights(model, flat):
         return None
     if flat.numel() != n:
         raise ValueError(f'{model}: expected {n} packed weights, got {flat.numel()}')
-    out = torch.empty_like(flat)
+    out = torch.empty(prepared_count(model, flat.dtype), dtype=flat.dtype, device=flat.device)
     _lib.call('gnnd_prepare_weights', _lib.VARIANT[model], dtype_code(flat.dtype), _ptr(flat),
               _ptr(out), current_stream(flat.device))
     return out
@@ -209,10 +220,10 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     if x.numel() % graph.N:
         raise ValueError(f'x has {x.numel()} rows, not a multiple of N={graph.N}')
     B = x.numel() // graph.N
-    nw = weights_count(model, graph, iters)
-    if nw and (prepared_weights is None or prepared_weights.numel() != nw):
-        raise ValueError(f'{model}: needs {nw} prepared weights')
     wdt = torch.float32 if x.dtype == torch.bfloat16 else x.dtype   # bf16 storage, fp32 math
+    nw = prepared_count(model, wdt, graph, iters)
+    if nw and (prepared_weights is None or prepared_weights.numel() != nw):
+        raise ValueError(f'{model}: needs {nw} prepared weights (prepare_weights)')
     if prepared_weights is not None and prepared_weights.dtype != wdt:
         raise TypeError(f'{x.dtype} inputs need {wdt} prepared weights')
     rows = decode_out_rows(graph, model, B, int(iters))
@@ -257,6 +268,9 @@ def train_forward(graph, model, x, prepared_weights, iters):
     x = x.contiguous()
     B = x.numel() // graph.N
     dt = dtype_code(x.dtype)
+    nw = prepared_count(model, x.dtype, graph, iters)
+    if nw and (prepared_weights is None or prepared_weights.numel() != nw):
+        raise ValueError(f'{model}: needs {nw} prepared weights (prepare_weights)')
     nb = ctypes.c_int64()
     _lib.call('gnnd_train_tape_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
               ctypes.byref(nb))
@@ -414,12 +428,14 @@ def syndrome_loss(graph, logical_rows, logical_only, pred, y):
 
 
 def v24_check_mlp_table(graph, w, u):
-    """decoder_v2_4's check-side MLP evaluated through the fp64 decoder's per-launch table
+    """decoder_v2_4's check-side MLP evaluated through the fp64 decoder's table
     (gnnd_v24_check_mlp_table): (y [n] fp64, valid) where valid says whether the decoder uses
-    the table for these weights.  w: packed fp64 V24 weights (1 283); u: fp64 inputs within
-    [-(max_dc - 1), max_dc - 1]."""
+    the table for these weights (y undefined when not).  w: packed fp64 V24 weights (1283,
+    prepared here) or prepared ones; u: fp64 inputs within [-(max_dc - 1), max_dc - 1]."""
     _require_gpu(w, u)
     w = w.to(torch.float64).contiguous()
+    if w.numel() == weights_count('v24'):
+        w = prepare_weights('v24', w)
     u = u.to(torch.float64).contiguous().reshape(-1)
     y = torch.empty_like(u)
     ok = torch.zeros(1, dtype=torch.int32, device=u.device)

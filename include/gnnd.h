@@ -186,7 +186,8 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  *            mlp {W1[10], b1[10], W2[10], b2}                                            = 137
  * gnnd_prepare_weights converts that layout into the kernel layout (for the fp32 V24
  * kernel the softplus layers are rescaled to base 2: layer-1 rows * log2(e), layer-2
- * weights * ln(2); every other model/dtype is a plain copy).  Call it once per weights.
+ * weights * ln(2); fp64 V24 appends the check-MLP table, gnnd_prepared_weights_count
+ * elements; every other model/dtype is a plain copy).  Call it once per weights.
  * gnnd_weights_count is the graph-independent count (GNND_ERR_UNSUPPORTED for NBP/V10/V22,
  * whose packed layout is passed to gnnd_decode as is, without preparation);
  * gnnd_decode_weights_count covers every model for a graph and iteration count.         */
@@ -194,18 +195,24 @@ int gnnd_weights_count(int model, int64_t* h_count);
 int gnnd_decode_weights_count(const gnnd_graph* g, int model, int32_t iters, int64_t* h_count);
 int gnnd_prepare_weights(int model, int dtype, const void* d_w, void* d_prepared,
                          void* stream);
+/* Elements of gnnd_prepare_weights' output: gnnd_weights_count, except fp64 V24 (7 252): the
+ * plain 1 283 weights, then the check-MLP table (gnnd_v24_check_mlp_table) the fp64 decoder
+ * and training forward read -- decode / train_fwd of fp64 V24 need this prepared buffer, not
+ * the plain weights.                                                                        */
+int gnnd_prepared_weights_count(int model, int dtype, int64_t* h_count);
 int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
                 void* d_out, int64_t batch, int32_t iters, void* stream);
 
 /* decoder_v2_4's check-side MLP (ggc2.mlp: Linear(1,128) -> Softplus -> Linear(128,1),
  * quantum/decoder_v2_4.py:241-243, :253-257) as the fp64 decoder evaluates it: its input
- * u = S_c(tanh(m/2)) - tanh(m_e/2) lies in [-R, R], R = max check degree - 1, so every fp64
- * decode tabulates the MLP once per launch (degree-7 Taylor polynomials about j/32) and reads
- * the table instead of the 128 hidden units.  This evaluates the same table at d_u [n]
- * (fp64, inside [-R, R]) into d_y [n]; d_w = the packed fp64 V24 weights (1 283).  *d_ok
- * (device int32) = 1 when the table is valid -- the decoder uses it -- or 0 when a unit's
- * pre-activation range crosses torch's Softplus threshold 20 or the Taylor remainder bound
- * exceeds 1e-13 (the decoder then evaluates the units).                                    */
+ * u = S_c(tanh(m/2)) - tanh(m_e/2) lies in [-R, R], R = max check degree - 1, so the fp64
+ * prepared weights carry it tabulated (degree-11 Taylor polynomials about j/8, |j/8| <= 31;
+ * gnnd_prepare_weights and gnnd_train_update build the table) and the decoder reads the table
+ * instead of the 128 hidden units.  This evaluates the same table at d_u [n] (fp64, inside
+ * [-R, R]) into d_y [n]; d_w = PREPARED fp64 V24 weights.  *d_ok (device int32) = 1 when the
+ * table is valid for this graph -- the decoder uses it -- or 0 (d_y untouched) when a unit's
+ * pre-activation crosses torch's Softplus threshold 20 for some u in [-R, R], the Taylor
+ * remainder bound exceeds 1e-13, or R > 31 (the decoder then evaluates the units).          */
 int gnnd_v24_check_mlp_table(const gnnd_graph* g, const void* d_w, const void* d_u, void* d_y,
                              int64_t n, int32_t* d_ok, void* stream);
 

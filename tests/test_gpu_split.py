@@ -100,7 +100,8 @@ def test_fused_update_matches_separate_kernels(dtype):
         sync = torch.zeros(1, dtype=torch.int32, device=DEV)
         loss = torch.zeros((), dtype=dtype, device=DEV)
         grad = torch.zeros_like(p0)
-        prep = torch.zeros_like(p0)
+        # (the kernel layout: fp64 carries the check-MLP table after the weights)
+        prep = torch.zeros(gd.ops.prepared_count('v24', dtype), dtype=dtype, device=DEV)
         for it in range(3):
             gd.ops.train_update('v24', dtype, rows=R, n_rows=rows, grad=grad, loss_b=loss_b,
                                 loss=loss, param=pa, exp_avg=ma, exp_avg_sq=va, step=sa, sync=sync,

@@ -3,7 +3,8 @@ ctab_eval in gnnd_decode_impl.h, exposed as gnnd_v24_check_mlp_table).
 
 ggc2.mlp (Linear(1,128) -> Softplus -> Linear(128,1), quantum/decoder_v2_4.py:241-243,
 :253-257) is evaluated on ONE scalar u = S_c(tanh(m/2)) - tanh(m_e/2) in [-(dc-1), dc-1]
-(:135-136), so the decoder tabulates it per launch (degree-7 Taylor polynomials about j/32).
+(:135-136), so the fp64 prepared weights carry it tabulated (degree-11 Taylor polynomials
+about j/8, built by gnnd_prepare_weights and after every fused optimizer step).
 Held here against torch's own fp64 MLP (the reference module, Softplus threshold 20 included)
 at 1e-13 absolute over the whole input range; weights whose unit range crosses the Softplus
 threshold make the table invalid and the decoder falls back to the per-unit MLP (decode
@@ -73,6 +74,14 @@ def test_threshold_crossing_unit_disables_table_and_decode_stays_exact():
     u = _inputs(3)
     _, ok = gd.ops.v24_check_mlp_table(g, m.packed_weights().double(), u)
     assert not ok
+    # the same weights on a graph whose range stops short of the crossing (toric: R = 3; a
+    # unit crossing 20 at |u| = 3.5): valid
+    with torch.no_grad():
+        m.ggc2.mlp[0].bias[5] = 13.0           # h = 2 u + 13 reaches 20 at u = 3.5
+    _, ok = gd.ops.v24_check_mlp_table(g, m.packed_weights().double(), u)
+    assert ok
+    with torch.no_grad():
+        m.ggc2.mlp[0].bias[5] = 17.0
     x, _ = gd.data.toric_batch(H, 64, seed=3, device=torch.device(DEV), dtype=torch.float64)
     out = gd.ops.decode(g, 'v24', x, m.Nc, m.prepared_weights(torch.float64, torch.device(DEV)))
     w = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
@@ -83,12 +92,35 @@ def test_threshold_crossing_unit_disables_table_and_decode_stays_exact():
 
 
 def test_large_weights_fail_the_remainder_bound():
-    """sum |W2| |W1|^8 large enough that the Taylor remainder bound exceeds 1e-13: invalid."""
+    """sum |W2| |W1|^12 large enough that the Taylor remainder bound exceeds 1e-13: invalid."""
     import gnndecode as gd
     m, H = _model(weights='shipped')
     with torch.no_grad():
-        m.ggc2.mlp[0].weight[7, 0] = 6.0       # |W1|^8 = 1.7e6, bias keeps h below 20
+        m.ggc2.mlp[0].weight[7, 0] = 9.0       # |W1|^12 = 2.8e11: bound 1.8e-10; h stays below 20
         m.ggc2.mlp[0].bias[7] = -10.0
+        m.ggc2.mlp[2].weight[0, 7] = 1.0
     g = m.graph(torch.device(DEV))
     _, ok = gd.ops.v24_check_mlp_table(g, m.packed_weights().double(), _inputs(3))
     assert not ok
+
+
+def test_prepared_layout_and_trainer_rebuild():
+    """gnnd_prepare_weights (fp64 V24) = [plain weights | bound, R limit, pad | table]; the
+    fused trainer's epilogue (gnnd_train_update) rebuilds the table of the updated weights, so
+    its prepared buffer equals a fresh gnnd_prepare_weights of its parameters after each step."""
+    import gnndecode as gd
+    m, H = _model(L=5)
+    flat = m.packed_weights().double().detach().contiguous()
+    prep = gd.ops.prepare_weights('v24', flat)
+    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64) == 7252
+    assert torch.equal(prep[:1283], flat)
+    assert 0 < float(prep[1283]) < 1e-13 and float(prep[1284]) > 3
+    assert gd.ops.prepared_count('v24', torch.float32) == 1283
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+    tr = gd.train.FusedV24Trainer(m, lf, graph=False)
+    x, y = gd.data.toric_batch(H, 32, seed=2, device=torch.device(DEV), dtype=torch.float64)
+    for _ in range(2):
+        tr.step(gd.data.make_batch(x, m.graph(x.device)), y)
+        torch.cuda.synchronize()
+        ref = gd.ops.prepare_weights('v24', tr.flat)
+        assert torch.equal(tr.prepared, ref)
