@@ -516,6 +516,7 @@ __global__ void __launch_bounds__(128) ctab_build_kernel(const double* w, double
         if (j == 0) {
             prep[1283] = (s12 + part[kCtabNC]) * kCtabBoundCoef;
             prep[1284] = fmin(rk, part[kCtabNC + 1]);
+            for (int i = 1285; i < kV24CtabOff; ++i) prep[i] = 0.0;     // (defined padding)
         }
     }
 }
@@ -1158,6 +1159,33 @@ __device__ __forceinline__ f32x2 bp_msg_prod_f32x2(f32x2 q, f32x2 n, float hi) {
         const f32x2 r = up * f32x2{__builtin_amdgcn_rcpf(dn.x), __builtin_amdgcn_rcpf(dn.y)};
         return f32x2{__builtin_amdgcn_logf(r.x), __builtin_amdgcn_logf(r.y)} * kLn2;
     }
+}
+// RATIO form of the fp32 BP check step (the paired resident kernel, GNND_BP_RATIO): with the
+// state in base-2 units (a' = a log2 e) and t_e = tanh(a_e/2) = n_e / d_e, n_e = sign(a)(1 - E),
+// d_e = 1 + E, E = 2^-z, z = clamp(|a'|, zmin, zmax) (the reference's clamp(a, -10, 10) and
+// its |t| >= lo floor, both on t's argument), the check node forms N = prod n and D = prod d
+// (signed numerators carry the sign count: no (-1)^n parity), and the leave-one-out value is
+// p_e = (N / n_e) / (D / d_e), so the message
+//     m'_e = log2((1 + p_e) / (1 - p_e)) = log2|D n_e + N d_e| - log2|D n_e - N d_e|
+// (CBP log((1+p)/(1-p)), QBP log(1+p) - log(1-p): the same function, in base 2) takes two
+// v_log_f32 and no reciprocal: 3 transcendentals per edge (exp, 2 log) instead of the product
+// form's 5 (exp and rcp for tanh, the leave-one-out rcp, rcp and log for atanh).  |p_e| <= tanh(5)
+// ^(dc - 1) < 1 for every check of degree >= 2, so the reference's p clamp (1 - 1e-7 / 1 - 1e-12)
+// never binds and the denominators never vanish (plans with a degree-1 check keep the product
+// form: make_plan).  n_e != 0 by the z floor; products of tiny factors may underflow, exactly
+// where the true leave-one-out value is below the fp32 range anyway (m'_e -> 0, never NaN).
+// zmin = 1e-7 * 2 / ln 2 puts t's floor at the reference's 1e-7 (CBP; QBP's 1e-20 floor is
+// below fp32's resolution of 1 - E: its t floor is 1e-7 too, a message change below 3e-7).
+constexpr float kBpZmin = 2.8853900817779268e-07f;        // 2e-7 log2 e
+constexpr float kBpZmax = 14.426950408889634f;             // 10 log2 e
+#ifndef GNND_BP_RATIO
+#define GNND_BP_RATIO 1      // 0: the product form (A/B builds)
+#endif
+__device__ __forceinline__ f32x2 bp_ratio_msg(f32x2 N, f32x2 D, f32x2 n, f32x2 d) {
+    const f32x2 A = D * n, Bv = N * d;
+    const f32x2 up = A + Bv, dn = A - Bv;
+    return f32x2{__builtin_amdgcn_logf(fabsf(up.x)), __builtin_amdgcn_logf(fabsf(up.y))} -
+           f32x2{__builtin_amdgcn_logf(fabsf(dn.x)), __builtin_amdgcn_logf(fabsf(dn.y))};
 }
 __device__ __forceinline__ f32x2 rcp2(f32x2 v) {
     return f32x2{__builtin_amdgcn_rcpf(v.x), __builtin_amdgcn_rcpf(v.y)};
@@ -1999,6 +2027,12 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
 #else
     constexpr bool kProd = false;
 #endif
+    // ... in RATIO form (GNND_BP_RATIO, default): no per-edge tanh division, leave-one-out
+    // reciprocal or atanh quotient; messages and x in base-2 units (bp_ratio below)
+    constexpr bool kRatio = kProd && GNND_BP_RATIO;
+    // x and messages held in base-2 units (x' = x log2 e): the GNN models' tanh pre-op and the
+    // ratio-form BP check step start from 2^(-a')
+    constexpr bool kB2 = kBase2 || kRatio;
     // T layout (paired GNN and plain-BP models): LDS keeps ONE value per variable,
     // T_v = S_v + x_v (base-2 scaled for the GNN models: messages m' = m log2 e, so
     // T'_v = S'_v + x'_v), refreshed by the variable-sum step, plus x_v itself for that
@@ -2042,7 +2076,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         if (n < V) {
             if constexpr (!kTX) {                       // (T layout: below, in var_ord order)
                 const T xv = io_ld(xg[i]);
-                s_sx[b * V + n] = SumX<T>{T(0), kBase2 ? xv * T(kLog2e) : xv};
+                s_sx[b * V + n] = SumX<T>{T(0), kB2 ? xv * T(kLog2e) : xv};
             }
         } else {
             s_xc[b * C + n - V] = io_ld(xg[i]);
@@ -2061,7 +2095,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             const uint2 o = s_vord[j];
             const int v = GNND_DIDX((int)(o.x & 0xffffu), V, GNND_DBG_VAR);
             const T xv = io_ld(xg[b * N + v]);
-            const T xs = kBase2 ? xv * T(kLog2e) : xv;
+            const T xs = kB2 ? xv * T(kLog2e) : xv;
             s_t[b * TS + GNND_DIDX((int)(o.y >> 16), TS, GNND_DBG_VAR)] = xs;
             s_m[b * E1 + GNND_DIDX((int)(o.y & 0xffffu) + (int)(o.x >> 16) - 1, E1, GNND_DBG_LDS_POS)] = xs;
         }
@@ -2112,6 +2146,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         const int cc = c < C ? c : C - 1, bb = b < nb ? b : nb - 1;
         const int rem = cc * G + (f & (G - 1));
         sc[q] = s_xc[bb * C + cc];
+        // ratio-form QBP: the syndrome's sign factor cos(pi (1 - s_c) / 2) of quantum/BP.py:112
+        // (+-1 for s_c = +-1) multiplies the check's numerator product
+        if constexpr (kRatio && MODEL == GNND_QBP) sc[q] = cosf(3.14159265358979f * 0.5f * (1.f - (float)sc[q]));
         cb[q] = bb;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -2301,10 +2338,49 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
                     return 1.f;
                 }
             };
+            // ratio-form fp32 BP (kRatio): per slot the signed numerator n = sign(a)(1 - E) and
+            // the denominator d = 1 + E of t = tanh(a/2) (E = 2^-z, z = |a'| clamped to
+            // [kBpZmin, kBpZmax]); padding slots n = d = 1
+            auto nd2 = [&](f32x2 tt, uint32_t sa, uint32_t sb, f32x2 mprev, int ra, int rb, f32x2& n,
+                           f32x2& d) {
+                const f32x2 a = tt - mprev;
+                const f32x2 e = {__builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(a.x), kBpZmin, kBpZmax)),
+                                 __builtin_amdgcn_exp2f(-__builtin_amdgcn_fmed3f(fabsf(a.y), kBpZmin, kBpZmax))};
+                n = f32x2{1.f, 1.f} - e;
+                d = f32x2{1.f, 1.f} + e;
+                n = f32x2{__builtin_copysignf(n.x, a.x), __builtin_copysignf(n.y, a.y)};
+                if constexpr (PADR > 0) {
+                    if (ra >= R - PADR && sa >= ((uint32_t)spare << 16)) { n.x = 1.f; d.x = 1.f; }
+                    if (rb >= R - PADR && sb >= ((uint32_t)spare << 16)) { n.y = 1.f; d.y = 1.f; }
+                }
+            };
             // item pair (2j, 2j + 1)
             auto pair_step = [&](auto jc, const PX (&px)[R]) {
                 constexpr int j = decltype(jc)::value;
                 const int qa = 2 * j, qb = 2 * j + 1;
+                if constexpr (kRatio) {
+                    // the check's products N = sc prod n, D = prod d (G-lane product butterflies)
+                    // and per edge m' = log2|(D n_e + N d_e) / (D n_e - N d_e)| (bp_ratio_msg)
+                    f32x2 nv[R], dv[R], Np, Dp;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        nd2(px[r], ve[qa][r], ve[qb][r], m2[j][r], r, r, nv[r], dv[r]);
+                        Np = r == 0 ? nv[0] : Np * nv[r];
+                        Dp = r == 0 ? dv[0] : Dp * dv[r];
+                    }
+                    Np = f32x2{group_prod_c<G>(Np.x), group_prod_c<G>(Np.y)};
+                    Dp = f32x2{group_prod_c<G>(Dp.x), group_prod_c<G>(Dp.y)};
+                    if constexpr (MODEL == GNND_QBP) Np = Np * sc2[j];
+                    T* mra = s_m + cb[qa] * E1;
+                    T* mrb = s_m + cb[qb] * E1;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        m2[j][r] = bp_ratio_msg(Np, Dp, nv[r], dv[r]);
+                        mra[GNND_DIDX((int)(ve[qa][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].x;
+                        mrb[GNND_DIDX((int)(ve[qb][r] >> 16), E1, GNND_DBG_LDS_POS)] = m2[j][r].y;
+                    }
+                    return;
+                }
                 f32x2 tv[R], cv[R], tsum, csum;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
@@ -2358,6 +2434,35 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             // bitwise-identical messages)
             auto solo_step = [&](auto qc, f32x2* msp) {
                 constexpr int q = decltype(qc)::value;
+                if constexpr (kRatio) {
+                    f32x2 nv[RP], dv[RP];
+                    float Np = 1.f, Dp = 1.f;
+#pragma unroll
+                    for (int i = 0; i < RP; ++i) {
+                        const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
+                        const f32x2 tt = {s_t[cb[q] * TS + (int)(ve[q][r0] & 0xffffu)],
+                                          s_t[cb[q] * TS + (int)(ve[q][r1] & 0xffffu)]};
+                        nd2(tt, ve[q][r0], ve[q][r1], msp[i], r0, r1, nv[i], dv[i]);
+                        Np = i == 0 ? nv[0].x : Np * nv[i].x;
+                        Dp = i == 0 ? dv[0].x : Dp * dv[i].x;
+                        if (2 * i + 1 < R) {
+                            Np = Np * nv[i].y;
+                            Dp = Dp * dv[i].y;
+                        }
+                    }
+                    Np = group_prod_c<G>(Np);
+                    Dp = group_prod_c<G>(Dp);
+                    if constexpr (MODEL == GNND_QBP) Np = Np * (float)sc[q];
+                    T* mb = s_m + cb[q] * E1;
+#pragma unroll
+                    for (int i = 0; i < RP; ++i) {
+                        const int r0 = 2 * i, r1 = 2 * i + 1 < R ? 2 * i + 1 : 2 * i;
+                        msp[i] = bp_ratio_msg(f32x2{Np, Np}, f32x2{Dp, Dp}, nv[i], dv[i]);
+                        mb[GNND_DIDX((int)(ve[q][r0] >> 16), E1, GNND_DBG_LDS_POS)] = msp[i].x;
+                        if (r1 != r0) mb[GNND_DIDX((int)(ve[q][r1] >> 16), E1, GNND_DBG_LDS_POS)] = msp[i].y;
+                    }
+                    return;
+                }
                 f32x2 tv[RP], cv[RP];
                 float tsum = 0.f, csum = 0.f;
 #pragma unroll
@@ -2499,7 +2604,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         auto var_out = [&](int b, int sbase, int tbase, int v, int tp, T s) {
             if (last) {
                 T r;
-                if constexpr (kTX && kBase2) r = s * kLn2;          // (S' + x') ln2 = S + x
+                if constexpr (kTX && kB2) r = s * kLn2;             // (S' + x') ln2 = S + x
                 else if constexpr (kTX) r = s;                       // S + x
                 else r = s + (kBase2 ? io_ld(xg[b * N + v]) : s_sx[sbase + v].x);
                 out[b0 * V + sbase + v] = io_st<TI>(M::readout(r, s_w));
@@ -2812,7 +2917,10 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     const bool quantum = model == GNND_QBP || model == GNND_QGNNI || model == GNND_NBP ||
                          model == GNND_V10 || model == GNND_V22;
     const bool f64res = dtype == GNND_F64 && quantum && !f64_resident_disabled();
-    if (light && (dtype == GNND_F32 || f64res) && gr->rview.G <= 16 && !resident_disabled()) {
+    // (the ratio-form fp32 BP check step needs every check of degree >= 2: bp_ratio_msg)
+    const bool ratio_bad = GNND_BP_RATIO && dtype == GNND_F32 && (model == GNND_CBP || model == GNND_QBP) &&
+                           gr->min_dc < 2;
+    if (light && (dtype == GNND_F32 || f64res) && gr->rview.G <= 16 && !resident_disabled() && !ratio_bad) {
         const GraphView& g = gr->rview;          // instantiated group sizes 1..16
         const size_t target = dtype == GNND_F64 ? 2 * lds_target() : lds_target();
         const int IC = g.C * g.G;
