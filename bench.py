@@ -59,9 +59,13 @@ def flops_per_codeword(model, g, T):
 
 
 # Hardware transcendental ops (v_exp / v_log / v_rcp_f32) the fp32 BP check step issues per edge
-# and iteration (decode_resident_kernel, product form: tanh = exp + rcp, the leave-one-out rcp,
-# CBP log((1 + p) / (1 - p)) = rcp + log, QBP log(1 + p) - log(1 - p) = 2 log)
-HW_TRANS_PER_EDGE = {'cbp': 5, 'qbp': 5}
+# and iteration (decode_resident_kernel, ratio form since r06: E = 2^-|a'| and two v_log_f32 of
+# D n_e +- N d_e; bp_ratio_msg).  The product form it replaced issued 5 (tanh = exp + rcp, the
+# leave-one-out rcp, atanh = rcp + log) and the reference's formula 6 (tanh, log, exp, log of a
+# quotient); the line reports the same throughput priced at those counts beside `frac`.
+HW_TRANS_PER_EDGE = {'cbp': 3, 'qbp': 3}
+TRANS_PER_EDGE_PRODUCT_FORM = 5
+TRANS_PER_EDGE_REFERENCE = 6
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
 PEAK_FP64_TFLOPS = 78.6
@@ -882,7 +886,9 @@ def decode_run(a, world, rank, dev, cpu='full'):
             rf = res['roofline']
             rf.update(bound='transcendental', achieved=trans_hw['achieved'], peak=trans_hw['peak'],
                       unit=trans_hw['unit'], frac=trans_hw['frac'], frac_flop=frac_alg,
-                      trans_ops_per_edge_iteration=hw_ops)
+                      trans_ops_per_edge_iteration=hw_ops,
+                      frac_at_product_form_ops=trans_hw['frac'] * TRANS_PER_EDGE_PRODUCT_FORM / hw_ops,
+                      frac_at_reference_ops=trans_hw['frac'] * TRANS_PER_EDGE_REFERENCE / hw_ops)
         if a.cpu_seconds > 0 and world == 1 and cpu != 'off':
             # the oracle decodes the same (for bf16: widened) inputs in fp32
             res['cpu_baseline'] = cpu_baseline(a.model, H, state, x.to(dtype), pred, labels, g, T,

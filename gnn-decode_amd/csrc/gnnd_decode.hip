@@ -83,6 +83,9 @@ extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void*
     // fp64 decoder_v2_4: [plain | bound, R limit, pad | check-MLP table] (ctab_build_kernel)
     if (model == GNND_V24 && dtype == GNND_F64)
         return launch_ctab_build((const double*)d_w, (double*)d_prepared, st);
+    // fp32 CGNNI / QGNNI: [plain | pad | header | message-MLP cells] (pwl_build_kernel)
+    if ((model == GNND_CGNNI || model == GNND_QGNNI) && dtype == GNND_F32 && GNND_MLP_PWL)
+        return launch_pwl_build((const float*)d_w, (float*)d_prepared, st);
     return GNND_OK;
 }
 
@@ -90,7 +93,9 @@ extern "C" int gnnd_prepared_weights_count(int model, int dtype, int64_t* h_coun
     int n = weights_count(model);
     if (n == -1 || !h_count || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
     if (n < 0) return GNND_ERR_UNSUPPORTED;
-    *h_count = model == GNND_V24 && dtype == GNND_F64 ? kV24PreparedF64 : n;
+    *h_count = model == GNND_V24 && dtype == GNND_F64 ? kV24PreparedF64
+               : (model == GNND_CGNNI || model == GNND_QGNNI) && dtype == GNND_F32 && GNND_MLP_PWL
+                   ? kGnnPreparedF32 : n;
     return GNND_OK;
 }
 

@@ -780,6 +780,176 @@ struct Mlp10Pair {
     }
 };
 
+// ---------------------------------------------------------------------------------------
+// CGNNI / QGNNI message MLP as an exact piecewise-linear table (fp32 resident kernel,
+// GNND_MLP_PWL).  The MLP (Linear(1,10) -> ReLU -> Linear(10,1),
+// classical/CGNNI.py:238-242, quantum/QGNNI.py:207-214) of one scalar u,
+//   f(u) = b2 + sum_k W2_k relu(W1_k u + b1_k),
+// is linear between its <= 10 knots kappa_k = -b1_k / W1_k.  gnnd_prepare_weights (fp32)
+// appends it as a table (pwl_build_kernel): the knots inside [-31, 31] (|u| <= dc - 1 <= 31)
+// span [lo, hi], cut into the fewest K <= 32 equal cells holding at most two knots each (the
+// trained weights: BCH 12 cells, LDPC 28, toric QGNNI 12); a cell stores its linear part and
+// its knots' relu terms {alpha, beta, gamma1, kappa1, gamma2, kappa2} (the end cells extend to
+// -inf / +inf).  The decoder maps each entry to its own input v = R_c - r_e (u = A v + B,
+// A = -2, B = G R - 1, the output x log2 e: Mlp10Pair's folding) when it stages the table in
+// LDS, so an edge costs an index (fma, cvt, med3, address), one 24-byte LDS entry and 5 FMAs
+// (two clamped: relu of a 2^-p scaled difference, 2^p >= G R) instead of 20 packed FMAs per
+// edge pair; the same function, rounded differently (the 1e-7 level).  No K <= 32: ok = 0 and
+// the kernel keeps Mlp10Pair.
+// ---------------------------------------------------------------------------------------
+#ifndef GNND_MLP_PWL
+#define GNND_MLP_PWL 1                // 0: Mlp10Pair everywhere (A/B builds)
+#endif
+constexpr int kPwlMaxCells = 32;
+constexpr int kPwlEntry = 8;                                      // floats per cell (6 used)
+constexpr size_t kPwlBytes = (size_t)kPwlMaxCells * kPwlEntry * 4;
+constexpr int kPwlOff = 64;          // floats: prepared fp32 CGNNI / QGNNI = [62 | pad | hdr | cells]
+constexpr int kPwlHdr = 8;           // {ok, K, s, t0, 0...}: cell = clamp(int(u s + t0), 0, K - 1)
+constexpr int kGnnPreparedF32 = kPwlOff + kPwlHdr + kPwlMaxCells * kPwlEntry;   // 328
+constexpr float kPwlUmax = 31.f;
+// w = the plain 62 weights (message MLP at kMlp10Msg), prep = the prepared buffer; one wave.
+// The cells' span [lo, hi] runs between two of the knots (the outermost ones may be left to
+// the end cells, which extend to -inf / +inf and hold at most two knots like the others): the
+// wave tries lo = the 1st..3rd smallest and hi = the 1st..3rd largest knot with K = 1..32 cells
+// and keeps the fewest cells (then the first such pair)
+__global__ void __launch_bounds__(64) pwl_build_kernel(const float* __restrict__ w, float* __restrict__ prep) {
+    const float* m = w + kMlp10Msg;
+    float* hdr = prep + kPwlOff;
+    float* tab = hdr + kPwlHdr;
+    const int tid = threadIdx.x;
+    double a[10], c[10], kap[10], ks[10];
+    bool in[10];
+    int n = 0;
+    for (int k = 0; k < 10; ++k) {
+        a[k] = (double)m[k];
+        c[k] = (double)m[10 + k];
+        kap[k] = a[k] != 0.0 ? -c[k] / a[k] : 0.0;
+        in[k] = a[k] != 0.0 && fabs(kap[k]) < kPwlUmax;
+        if (in[k]) {                                           // insertion into the sorted knots
+            int i = n++;
+            while (i > 0 && ks[i - 1] > kap[k]) { ks[i] = ks[i - 1]; --i; }
+            ks[i] = kap[k];
+        }
+    }
+    auto cell = [&](double x, double lo, double span, int K) {
+        const double r = span > 0.0 ? (x - lo) / span * K : 0.0;
+        return r < 0.0 ? 0 : (r >= K ? K - 1 : (int)r);
+    };
+    // combo = (i, j, K): lo = ks[i], hi = ks[n - 1 - j]
+    int best = 1 << 30;
+    for (int cb = tid; cb < 9 * kPwlMaxCells; cb += 64) {
+        const int K = cb / 9 + 1, i = cb % 9 / 3, j = cb % 3;
+        if (n == 0 || i > n - 1 - j) continue;
+        const double lo = ks[i], span = ks[n - 1 - j] - lo;
+        bool fit = true;
+        for (int x = 0; x < n && fit; ++x) {
+            int cnt = 0;
+            const int cx = cell(ks[x], lo, span, K);
+            for (int y = 0; y < n; ++y) cnt += cell(ks[y], lo, span, K) == cx;
+            fit = cnt <= 2;
+        }
+        if (fit && cb < best) best = cb;
+    }
+    for (int o = 1; o < 64; o <<= 1) best = min(best, __shfl_xor(best, o));
+    if (n == 0) best = 0;                                      // no knot: one linear cell
+    const bool ok = best < (1 << 30);
+    const int K = ok ? best / 9 + 1 : 1;
+    const double lo = ok && n ? ks[best % 9 / 3] : 0.0;
+    const double span = ok && n ? ks[n - 1 - best % 3] - lo : 0.0;
+    if (tid == 0) {
+        hdr[0] = ok ? 1.f : 0.f;
+        hdr[1] = (float)K;
+        hdr[2] = span > 0.0 ? (float)(K / span) : 0.f;
+        hdr[3] = span > 0.0 ? (float)(-lo * (K / span)) : 0.f;
+        for (int i = 4; i < kPwlHdr; ++i) hdr[i] = 0.f;
+        prep[62] = prep[63] = 0.f;
+    }
+    if (ok && tid < kPwlMaxCells) {
+        double al = (double)m[30], be = 0.0, ga[2] = {0.0, 0.0}, ka[2] = {0.0, 0.0};
+        int nk = 0;
+        for (int k = 0; k < 10; ++k) {
+            const int ci = in[k] ? cell(kap[k], lo, span, K) : -1;
+            const double w2 = (double)m[20 + k];
+            bool lin;                                          // active as a linear term
+            if (ci == tid && nk < 2) {                         // the knot's relu term here
+                ga[nk] = w2 * fabs(a[k]);
+                ka[nk] = kap[k];
+                ++nk;
+                lin = a[k] < 0.0;                              // relu(-x) = -x + relu(x)
+            } else if (ci >= 0) {
+                lin = (a[k] > 0.0) == (ci < tid);
+            } else {
+                lin = a[k] != 0.0 ? (a[k] > 0.0) == (kap[k] < 0.0) : c[k] > 0.0;   // sign at u = 0
+            }
+            if (lin) { al = fma(w2, c[k], al); be = fma(w2, a[k], be); }
+        }
+        float* e = tab + tid * kPwlEntry;
+        e[0] = (float)al; e[1] = (float)be;
+        e[2] = (float)ga[0]; e[3] = (float)ka[0];
+        e[4] = (float)ga[1]; e[5] = (float)ka[1];
+        e[6] = 0.f; e[7] = 0.f;
+    }
+}
+struct Pwl {
+    int ok, K;
+    float s, t0, sc;     // v-domain cell = clamp(int(v s + t0), 0, K - 1); sc = 2^-p
+};
+// the decoder's v-domain copy of the prepared table (u = A v + B, output x O), entries by
+// threads < K; the caller's barrier orders them before use
+__device__ Pwl pwl_stage(const float* __restrict__ prep, float* __restrict__ tab, float vmax, float A,
+                         float B, float O, int tid) {
+    const float* hdr = prep + kPwlOff;
+    Pwl p;
+    p.ok = (int)hdr[0];
+    p.K = (int)hdr[1];
+    int e2 = 0;
+    frexpf(vmax, &e2);                                         // 2^e2 > vmax
+    p.sc = ldexpf(1.f, -e2);
+    const double s = hdr[2], t0 = hdr[3];
+    p.s = (float)(A * s);                                      // cell from v: (A v + B) s + t0
+    p.t0 = (float)fma((double)B, s, t0);
+    if (p.ok && tid < p.K) {
+        const float* e = hdr + kPwlHdr + tid * kPwlEntry;
+        double al = e[0] + (double)e[1] * B, be = (double)e[1] * A;
+        double g[2], kv[2];
+        for (int j = 0; j < 2; ++j) {
+            // gamma relu(u - kappa) = gamma relu(A (v - kv)), kv = (kappa - B) / A
+            const double ga = e[2 + 2 * j], kap = e[3 + 2 * j];
+            kv[j] = (kap - B) / A;
+            g[j] = ga * fabs((double)A);
+            if (A < 0.f) { al = fma(g[j], kv[j], al); be -= g[j]; }   // |A| relu(kv - v)
+        }
+        float* d = tab + tid * kPwlEntry;
+        d[0] = (float)(al * O);
+        d[1] = (float)(be * O);
+        d[2] = (float)(g[0] * O / p.sc);
+        d[3] = (float)(-kv[0] * p.sc);
+        d[4] = (float)(g[1] * O / p.sc);
+        d[5] = (float)(-kv[1] * p.sc);
+        d[6] = 0.f; d[7] = 0.f;
+    }
+    return p;
+}
+__device__ __forceinline__ float pwl_eval(const float* tab, const Pwl& p, float v) {
+    int k = (int)__builtin_fmaf(v, p.s, p.t0);
+    k = k < 0 ? 0 : (k >= p.K ? p.K - 1 : k);
+    const float* e = tab + k * kPwlEntry;
+    const float4 e0 = *(const float4*)e;
+    const float2 e1 = *(const float2*)(e + 4);
+    float y = __builtin_fmaf(e0.y, v, e0.x);
+    y = __builtin_fmaf(e0.z, __builtin_amdgcn_fmed3f(__builtin_fmaf(v, p.sc, e0.w), 0.f, 1.f), y);
+    return __builtin_fmaf(e1.x, __builtin_amdgcn_fmed3f(__builtin_fmaf(v, p.sc, e1.y), 0.f, 1.f), y);
+}
+__device__ __forceinline__ f32x2 pwl_eval2(const float* tab, const Pwl& p, f32x2 v) {
+    return f32x2{pwl_eval(tab, p, v.x), pwl_eval(tab, p, v.y)};
+}
+// the fp32 GNN message MLP's piecewise-linear table into the prepared buffer (w may alias prep)
+int launch_pwl_build(const float* w, float* prep, hipStream_t st) {
+    pwl_build_kernel<<<1, 64, 0, st>>>(w, prep);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}
+
 // The unit sum in a FIXED order independent of how the units are spread over lanes: chain j
 // (0..7) accumulates units k = 8i + j (i ascending), chain 0 starting from the linear part,
 // and the MLP value is ((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7)).  A call evaluates
@@ -2056,6 +2226,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
 
     T* s_w = (T*)smem;
     size_t off = ((size_t)nw * sizeof(T) + 15) & ~(size_t)15;
+    // fp32 GNN models: the message MLP's piecewise-linear table (pwl_build) after the weights
+    float* s_pwl = (float*)(smem + off);
+    if constexpr (kBase2 && GNND_MLP_PWL) off += kPwlBytes;
     uint2* s_vord = (uint2*)(smem + off);
     off += ((size_t)V * 8 + 15) & ~(size_t)15;
     T* s_m = (T*)(smem + off);                             // [CW][E+1] messages, var-major
@@ -2136,6 +2309,13 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     Mlp10Pair mlp2;
     if constexpr (kBase2)      // input v = R - r_e: u = (G R_slots - 1) - 2 v; output x log2 e
         mlp2.load((const float*)s_w + kMlp10Msg, (float)(G * R), -2.f, (float)(G * R - 1), kLog2e);
+    // the same function as a piecewise-linear table (pwl_stage: uniform ok, K and scales from
+    // the prepared weights, the graph's v-domain entries in LDS)
+    Pwl pwl{0, 1, 0.f, 0.f, 1.f};
+    if constexpr (kBase2 && GNND_MLP_PWL) {
+        pwl = pwl_stage((const float*)w, s_pwl, (float)(G * R), -2.f, (float)(G * R - 1), kLog2e, tid);
+        __syncthreads();
+    }
 #pragma unroll
     for (int q = 0; q < QMAX; ++q) {
         const int f = tid + q * GNND_BLOCK;
@@ -2313,7 +2493,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             // c->v update of two edges from the leave-one-out sums u (and sign counts n)
             auto post2 = [&](f32x2 u, f32x2 n, f32x2 scp, f32x2 mprev) {
                 if constexpr (kBase2) {
-                    const f32x2 y = mlp2(u);
+                    const f32x2 y = pwl.ok ? pwl_eval2(s_pwl, pwl, u) : mlp2(u);
                     if constexpr (MODEL == GNND_QGNNI) return __builtin_elementwise_fma(y, scp, mprev);
                     else return y + mprev;
                 } else if constexpr (WBP) {
@@ -2944,7 +3124,10 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
         // resident layout: weights, var order, then [CW][P1] messages, [CW][V] {S, x},
         // [CW][C].  Pick (CW, Q) with Q in kResidentQ maximising lane utilisation
         // CW*IC / (Q*256), ties to the larger tile.
-        const size_t fixed = wb + align16((size_t)g.V * 8);
+        // (+ the fp32 GNN message MLP's piecewise-linear table, pwl_stage)
+        const size_t fixed = wb + align16((size_t)g.V * 8) +
+                             (GNND_MLP_PWL && dtype == GNND_F32 && (model == GNND_CGNNI || model == GNND_QGNNI)
+                                  ? kPwlBytes : 0);
         auto lds_of = [&](int cw) {     // messages, then {S_v, x_v} (T layout: T_v rows), x_c
             const GraphView* l = lay_of(cw);
             return fixed + esz * (((size_t)cw * l->P1 + 1) & ~(size_t)1) +

@@ -268,8 +268,11 @@ def train_forward(graph, model, x, prepared_weights, iters):
     x = x.contiguous()
     B = x.numel() // graph.N
     dt = dtype_code(x.dtype)
-    nw = prepared_count(model, x.dtype, graph, iters)
-    if nw and (prepared_weights is None or prepared_weights.numel() != nw):
+    # (decoder_v2_4 reads its prepared layout -- fp64: with the check-MLP table; the other
+    # models' training forwards read the plain weights at its head)
+    nw = (prepared_count(model, x.dtype, graph, iters) if model == 'v24'
+          else weights_count(model, graph, iters))
+    if nw and (prepared_weights is None or prepared_weights.numel() < nw):
         raise ValueError(f'{model}: needs {nw} prepared weights (prepare_weights)')
     nb = ctypes.c_int64()
     _lib.call('gnnd_train_tape_bytes', graph.handle, _lib.VARIANT[model], dt, B, int(iters),
