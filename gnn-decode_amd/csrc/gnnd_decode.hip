@@ -76,6 +76,8 @@ extern "C" int gnnd_prepare_weights(int model, int dtype, const void* d_w, void*
     if (model == GNND_V24 && dtype == GNND_F32) {
         prepare_v24_f32_kernel<<<1, 128, 0, st>>>((const float*)d_w, (float*)d_prepared);
         GNND_LAUNCH_CHECK();
+        // [base-2 weights | bound, pad | check-MLP table (fp32)] (ctab_build_kernel)
+        if (GNND_V24_CTAB) return launch_ctab_build((const float*)d_w, (float*)d_prepared, st);
         return GNND_OK;
     }
     size_t bytes = (size_t)n * (dtype == GNND_F64 ? 8 : 4);
@@ -93,7 +95,7 @@ extern "C" int gnnd_prepared_weights_count(int model, int dtype, int64_t* h_coun
     int n = weights_count(model);
     if (n == -1 || !h_count || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
     if (n < 0) return GNND_ERR_UNSUPPORTED;
-    *h_count = model == GNND_V24 && dtype == GNND_F64 ? kV24PreparedF64
+    *h_count = model == GNND_V24 && (dtype == GNND_F64 || GNND_V24_CTAB) ? kV24PreparedF64
                : (model == GNND_CGNNI || model == GNND_QGNNI) && dtype == GNND_F32 && GNND_MLP_PWL
                    ? kGnnPreparedF32 : n;
     return GNND_OK;

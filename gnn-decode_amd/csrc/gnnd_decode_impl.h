@@ -464,14 +464,19 @@ __device__ __forceinline__ double group_min64(double v) {
     for (int o = 1; o < 64; o <<= 1) v = fmin(v, __shfl_xor(v, o));
     return v;
 }
-__global__ void __launch_bounds__(128) ctab_build_kernel(const double* w, double* prep) {
-    const double* wm = w + kV24Ggc2;
+// TP = float (the fp32 decoder's table, fp32 coefficients from the same fp64 sums): the fp32
+// kernels evaluate Softplus without torch's threshold (its jump, 2e-9, is below fp32's
+// resolution at 20), so the table is the smooth function everywhere and prep[1284] = 1e30
+template <typename TW, typename TP>
+__global__ void __launch_bounds__(128) ctab_build_kernel(const TW* w, TP* prep) {
+    constexpr bool kThr = sizeof(TP) == 8;     // torch's threshold (fp64 decoder)
+    const TW* wm = w + kV24Ggc2;
     const int k = threadIdx.x, j = blockIdx.x;
     const double c = (double)(j - kCtabInv * kCtabRcap) * (1.0 / kCtabInv);
     const double W1 = wm[k], b1 = wm[128 + k], W2 = wm[256 + k], b2 = wm[384];
     const double h = fma(W1, c, b1);
     double d[kCtabNC];
-    if (h > 20.0) {                            // torch's threshold: softplus(h) = h
+    if (kThr && h > 20.0) {                    // torch's threshold: softplus(h) = h
         d[0] = h;
         d[1] = 1.0;
 #pragma unroll
@@ -510,27 +515,30 @@ __global__ void __launch_bounds__(128) ctab_build_kernel(const double* w, double
     }
     __syncthreads();
     if (k == 0) {
-        double* en = prep + kV24CtabOff + (size_t)j * kCtabNC;
+        TP* en = prep + kV24CtabOff + (size_t)j * kCtabNC;
 #pragma unroll
-        for (int n = 0; n < kCtabNC; ++n) en[n] = (t[n] + part[n]) + (n == 0 ? b2 : 0.0);
+        for (int n = 0; n < kCtabNC; ++n) en[n] = (TP)((t[n] + part[n]) + (n == 0 ? b2 : 0.0));
         if (j == 0) {
-            prep[1283] = (s12 + part[kCtabNC]) * kCtabBoundCoef;
-            prep[1284] = fmin(rk, part[kCtabNC + 1]);
-            for (int i = 1285; i < kV24CtabOff; ++i) prep[i] = 0.0;     // (defined padding)
+            prep[1283] = (TP)((s12 + part[kCtabNC]) * kCtabBoundCoef);
+            prep[1284] = (TP)(kThr ? fmin(rk, part[kCtabNC + 1]) : 1e30);
+            for (int i = 1285; i < kV24CtabOff; ++i) prep[i] = TP(0);   // (defined padding)
         }
     }
 }
-// the table of the plain weights w into the prepared buffer prep (w may alias prep)
-int launch_ctab_build(const double* w, double* prep, hipStream_t st) {
-    ctab_build_kernel<<<kCtabCap, 128, 0, st>>>(w, prep);
+// the table of the plain weights w into the prepared buffer prep (w may alias prep for fp64;
+// fp32: w = the plain weights, prep's head holds the base-2 rescaled ones)
+template <typename TW, typename TP>
+int launch_ctab_build(const TW* w, TP* prep, hipStream_t st) {
+    ctab_build_kernel<TW, TP><<<kCtabCap, 128, 0, st>>>(w, prep);
     GNND_LAUNCH_CHECK();
     return GNND_OK;
 }
 // Whether the prepared table holds for a graph with |u| <= R (w = the prepared weights): no
 // unit's pre-activation reaches 20 for |u| <= R unless it stays above 20 there (a crossing at
 // distance rk from u = 0 lies outside [-R, R] iff R < rk), and the remainder bound <= 1e-13
-__device__ __forceinline__ bool ctab_valid(const double* __restrict__ w, int R) {
-    return GNND_V24_CTAB && R <= kCtabRcap && w[1283] <= 1e-13 && (double)R < w[1284];
+template <typename T>
+__device__ __forceinline__ bool ctab_valid(const T* __restrict__ w, int R) {
+    return GNND_V24_CTAB && R <= kCtabRcap && w[1283] <= T(1e-13) && (T)R < w[1284];
 }
 // MLP_c(u) from the staged entries (tab[0] at c = -R, R8 = kCtabInv R): the nearest centre,
 // then Horner in r = u - c_j
@@ -549,6 +557,25 @@ __device__ __forceinline__ double ctab_eval(const double* tab, double u, int R8)
     double p = a[kCtabNC - 1];
 #pragma unroll
     for (int n = kCtabNC - 2; n >= 0; --n) p = fma(p, r, a[n]);
+    return p;
+}
+// the fp32 form (fp32 V24 decoder): the same nearest centre (round to nearest by the 1.5 2^23
+// magic), three ds_read_b128 of fp32 coefficients, Horner in fp32
+__device__ __forceinline__ float ctab_eval(const float* tab, float u, int R8) {
+    const float tk = __builtin_fmaf(u, (float)kCtabInv, 12582912.f);   // 1.5 2^23
+    int k = (int)(__float_as_uint(tk) & 0x7fffffu) - 0x400000;
+    k = k < -R8 ? -R8 : (k > R8 ? R8 : k);
+    const float r = __builtin_fmaf((float)k, -1.f / kCtabInv, u);
+    const float4* e = (const float4*)(tab + (size_t)(k + R8) * kCtabNC);
+    float a[kCtabNC];
+#pragma unroll
+    for (int i = 0; i < kCtabNC / 4; ++i) {
+        const float4 v = e[i];
+        a[4 * i] = v.x; a[4 * i + 1] = v.y; a[4 * i + 2] = v.z; a[4 * i + 3] = v.w;
+    }
+    float p = a[kCtabNC - 1];
+#pragma unroll
+    for (int n = kCtabNC - 2; n >= 0; --n) p = __builtin_fmaf(p, r, a[n]);
     return p;
 }
 
@@ -1530,8 +1557,13 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     T* s_tab = nullptr;
     T* s_bias = nullptr;
     T* s_lin = nullptr;        // [3][4] {A, B, C, 0} per MLP (mlp_lin), after the biases
-    double* s_ctab = nullptr;      // [ctab_entries(max_dc)][kCtabNC] check-MLP table entries
+    T* s_ctab = nullptr;           // [ctab_entries(max_dc)][kCtabNC] check-MLP table entries
     const int Rc = g.max_dc > 1 ? g.max_dc - 1 : 0, R8 = kCtabInv * Rc;
+    constexpr bool kCtab = MODEL == GNND_V24 && GNND_V24_CTAB;
+    if constexpr (kCtab && sizeof(T) == 4) {          // fp32 V24: the table at LDS byte 0
+        s_ctab = (T*)smem;
+        off = ((size_t)ctab_entries(g.max_dc) * kCtabNC * 4 + 15) & ~(size_t)15;
+    }
     if constexpr (kTab) {
         s_tab = (T*)smem;
         s_bias = s_tab + kV24F64TabDoubles;
@@ -1563,12 +1595,12 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     }
     // the check-side MLP's table entries |c_j| <= R from the prepared weights (uniform verdict)
     bool ctab_ok = false;
-    if constexpr (kTab && GNND_V24_CTAB) {
-        ctab_ok = ctab_valid((const double*)w, Rc);
+    if constexpr (kCtab) {
+        ctab_ok = ctab_valid(w, Rc);
         if (ctab_ok) {
-            const double2* src = (const double2*)((const double*)w + kV24CtabOff +
-                                                  (size_t)(kCtabInv * kCtabRcap - R8) * kCtabNC);
-            for (int i = tid; i < ctab_entries(g.max_dc) * kCtabNC / 2; i += NT) ((double2*)s_ctab)[i] = src[i];
+            constexpr int kV = 16 / sizeof(T);            // values per 16-byte move
+            const uint4* src = (const uint4*)(w + kV24CtabOff + (size_t)(kCtabInv * kCtabRcap - R8) * kCtabNC);
+            for (int i = tid; i < ctab_entries(g.max_dc) * kCtabNC / kV; i += NT) ((uint4*)s_ctab)[i] = src[i];
         }
     }
     const int nslot = C * G * R;
@@ -1765,16 +1797,19 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 }
                 GNND_PMARK(pf, 0);
                 if constexpr (kUP) {
-                    // one edge per lane, two hidden units per packed op
+                    // one edge per lane, two hidden units per packed op (with the check MLP on its
+                    // table the var MLP's two partial-sum buffers alternate call by call)
+                    float* pb = (float*)(s_part + (ctab_ok && (pbuf++ & 1) ? US * IL : 0));
                     const float a = mlp128_upair_split<US, true>(s_up + UpairLds::kMlp0, v24.l1, ext[0], xs[0],
-                                                                 sub, (float*)s_part, itid, widle);
+                                                                 sub, pb, itid, widle);
                     tv[0] = val[0] ? tanh_half_fast(a) : 0.f;
                 } else {
 #pragma unroll
                     for (int r = 0; r < R; r += 2) {
                         const int r1 = r + 1 < R ? r + 1 : r;
+                        f32x2* pb = s_part + (ctab_ok && (pbuf++ & 1) ? US * IL : 0);
                         const f32x2 a = mlp128_split<US, true>(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
-                                                               f32x2{xs[r], xs[r1]}, sub, s_part, itid, widle
+                                                               f32x2{xs[r], xs[r1]}, sub, pb, itid, widle
                                                                GNND_PARG(pf, 1));
                         tv[r] = val[r] ? tanh_half_fast(a.x) : 0.f;
                         if (r + 1 < R) tv[r + 1] = val[r + 1] ? tanh_half_fast(a.y) : 0.f;
@@ -1885,8 +1920,9 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             if constexpr (kUP) {
                 GNND_PMARK(pf, 3);
                 const float u = Sc - tv[0];
-                const float y = mlp128_upair_split<US, false>(s_up + UpairLds::kMlp1, v24.l2, u, u, sub,
-                                                              (float*)(s_part + US * IL), itid, widle);
+                const float y = ctab_ok ? ctab_eval(s_ctab, u, R8)   // (uniform: every split wave)
+                                        : mlp128_upair_split<US, false>(s_up + UpairLds::kMlp1, v24.l2, u, u, sub,
+                                                                        (float*)(s_part + US * IL), itid, widle);
                 mn[0] = y * sc + mv[0];
             } else if constexpr (kV24F32) {
                 GNND_PMARK(pf, 3);
@@ -1894,8 +1930,9 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 for (int r = 0; r < R; r += 2) {
                     const int r1 = r + 1 < R ? r + 1 : r;
                     const f32x2 uu = {Sc - tv[r], Sc - tv[r1]};
-                    const f32x2 y = mlp128_split<US, false>(v24.g + kV24Ggc2, v24.l2, uu, uu, sub,
-                                                            s_part + US * IL, itid, widle GNND_PARG(pf, 4));
+                    const f32x2 y = ctab_ok ? f32x2{ctab_eval(s_ctab, uu.x, R8), ctab_eval(s_ctab, uu.y, R8)}
+                                            : mlp128_split<US, false>(v24.g + kV24Ggc2, v24.l2, uu, uu, sub,
+                                                                      s_part + US * IL, itid, widle GNND_PARG(pf, 4));
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
                 }
@@ -3173,10 +3210,13 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
                          : upair ? gr->view
                          : (B <= 4096 && gr->pview.R == 2) ? gr->pview : gr->rview;
     const size_t nslot = (size_t)g.C * g.G * g.R;
-    // (fp64 V24: Softplus table, biases, linear parts, then the check-MLP table entries)
+    // (fp64 V24: Softplus table, biases, linear parts, then the check-MLP table entries; fp32
+    // V24: the check-MLP table entries)
     const size_t tab = model == GNND_V24 && dtype == GNND_F64
                            ? (size_t)(kV24F64TabDoubles + 3 * 128 + 16) * 8 +
                                  (GNND_V24_CTAB ? (size_t)ctab_entries(g.max_dc) * kCtabNC * 8 : 0)
+                       : model == GNND_V24 && GNND_V24_CTAB
+                           ? align16((size_t)ctab_entries(g.max_dc) * kCtabNC * 4)
                            : 0;
     // (decode_kernel stages the unit-pair weights whenever fp32 V24 runs a one-slot plan, kUP:
     // reserve them for every such plan, not only for the upair choice above — ADVICE r05)

@@ -1660,6 +1660,8 @@ extern "C" int gnnd_train_update(int model, int dtype, const void* d_rows, int64
     // fp64 decoder_v2_4: the check-MLP table of the updated weights (the prepared layout's tail)
     if (model == GNND_V24 && dtype == GNND_F64 && d_prepared)
         return launch_ctab_build((const double*)d_prepared, (double*)d_prepared, st);
+    if (model == GNND_V24 && dtype == GNND_F32 && d_prepared && GNND_V24_CTAB)   // (from the plain weights)
+        return launch_ctab_build((const float*)d_param, (float*)d_prepared, st);
     // fp32 CGNNI / QGNNI: the message MLP's piecewise-linear table
     if ((model == GNND_CGNNI || model == GNND_QGNNI) && dtype == GNND_F32 && d_prepared && GNND_MLP_PWL)
         return launch_pwl_build((const float*)d_prepared, (float*)d_prepared, st);

@@ -186,7 +186,7 @@ int gnnd_propagate_generic_bwd(int variant, int flow, int aggr, int dtype,
  *            mlp {W1[10], b1[10], W2[10], b2}                                            = 137
  * gnnd_prepare_weights converts that layout into the kernel layout (for the fp32 V24
  * kernel the softplus layers are rescaled to base 2: layer-1 rows * log2(e), layer-2
- * weights * ln(2); fp64 V24 appends the check-MLP table and fp32 CGNNI / QGNNI the message
+ * weights * ln(2); V24 appends the check-MLP table and fp32 CGNNI / QGNNI the message
  * MLP's piecewise-linear table, gnnd_prepared_weights_count elements; every other model/dtype
  * is a plain copy).  Call it once per weights.
  * gnnd_weights_count is the graph-independent count (GNND_ERR_UNSUPPORTED for NBP/V10/V22,
@@ -196,12 +196,12 @@ int gnnd_weights_count(int model, int64_t* h_count);
 int gnnd_decode_weights_count(const gnnd_graph* g, int model, int32_t iters, int64_t* h_count);
 int gnnd_prepare_weights(int model, int dtype, const void* d_w, void* d_prepared,
                          void* stream);
-/* Elements of gnnd_prepare_weights' output: gnnd_weights_count, except fp64 V24 (7 252): the
- * plain 1 283 weights, then the check-MLP table (gnnd_v24_check_mlp_table) the fp64 decoder
- * and training forward read, and fp32 CGNNI / QGNNI (328): the plain 62, then their message
+/* Elements of gnnd_prepare_weights' output: gnnd_weights_count, except V24 (7 252): the 1 283
+ * weights (fp32: base-2 rescaled), then the check-MLP table (gnnd_v24_check_mlp_table) the
+ * decoder and training forward read, and fp32 CGNNI / QGNNI (328): the plain 62, then their message
  * MLP as a piecewise-linear table (<= 32 cells of <= 2 knots) the register-resident decoder
  * reads.  gnnd_decode needs this prepared buffer, not the plain weights (so does
- * gnnd_train_fwd for fp64 V24).                                                             */
+ * gnnd_train_fwd for V24).                                                                  */
 int gnnd_prepared_weights_count(int model, int dtype, int64_t* h_count);
 int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
                 void* d_out, int64_t batch, int32_t iters, void* stream);
