@@ -3024,6 +3024,15 @@ template <int CTRL> __device__ __forceinline__ double dpp_mov(double v) {
                     __builtin_amdgcn_update_dpp(0, h.y, CTRL, 0xf, 0xf, false)};
     return __builtin_bit_cast(double, r);
 }
+template <int G> __device__ __forceinline__ double group_prod_c(double v) {
+    if constexpr (G > 1) v *= dpp_mov<0xB1>(v);
+    if constexpr (G > 2) v *= dpp_mov<0x4E>(v);
+    if constexpr (G > 4) v *= dpp_mov<0x141>(v);
+    if constexpr (G > 8) v *= dpp_mov<0x140>(v);
+    if constexpr (G > 16) v *= __shfl_xor(v, 16);
+    if constexpr (G > 32) v *= __shfl_xor(v, 32);
+    return v;
+}
 template <int G> __device__ __forceinline__ double group_sum_c(double v) {
     if constexpr (G > 1) v += dpp_mov<0xB1>(v);
     if constexpr (G > 2) v += dpp_mov<0x4E>(v);

@@ -1373,6 +1373,10 @@ __device__ __forceinline__ f32x2 bp_msg_prod_f32x2(f32x2 q, f32x2 n, float hi) {
 // where the true leave-one-out value is below the fp32 range anyway (m'_e -> 0, never NaN).
 // zmin = 1e-7 * 2 / ln 2 puts t's floor at the reference's 1e-7 (CBP; QBP's 1e-20 floor is
 // below fp32's resolution of 1 - E: its t floor is 1e-7 too, a message change below 3e-7).
+// The fp64 resident kernel (the quantum scripts' dtype) runs the same form in natural units
+// with n = -expm1(-z), d = 2 + expm1(-z) (no cancellation: both floors exact, z >= 2 lo) and
+// the libm-free fp64 log (decode_resident_kernel, kRatio64): exp and two logs per edge
+// instead of tanh (expm1 and a division), log, exp, cos_pi and two logs.
 constexpr float kBpZmin = 2.8853900817779268e-07f;        // 2e-7 log2 e
 constexpr float kBpZmax = 14.426950408889634f;             // 10 log2 e
 #ifndef GNND_BP_RATIO
@@ -2237,6 +2241,9 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
     // ... in RATIO form (GNND_BP_RATIO, default): no per-edge tanh division, leave-one-out
     // reciprocal or atanh quotient; messages and x in base-2 units (bp_ratio below)
     constexpr bool kRatio = kProd && GNND_BP_RATIO;
+    // fp64 plain BP (the quantum scripts' dtype) in the same ratio form, natural units, with the
+    // cancellation-free expm1: n = -expm1(-z), d = 2 + expm1(-z) (bp_ratio64 below)
+    constexpr bool kRatio64 = sizeof(T) == 8 && (MODEL == GNND_CBP || MODEL == GNND_QBP) && GNND_BP_RATIO;
     // x and messages held in base-2 units (x' = x log2 e): the GNN models' tanh pre-op and the
     // ratio-form BP check step start from 2^(-a')
     constexpr bool kB2 = kBase2 || kRatio;
@@ -2366,6 +2373,7 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
         // ratio-form QBP: the syndrome's sign factor cos(pi (1 - s_c) / 2) of quantum/BP.py:112
         // (+-1 for s_c = +-1) multiplies the check's numerator product
         if constexpr (kRatio && MODEL == GNND_QBP) sc[q] = cosf(3.14159265358979f * 0.5f * (1.f - (float)sc[q]));
+        if constexpr (kRatio64 && MODEL == GNND_QBP) sc[q] = cos_pi((T(1) - sc[q]) / T(2));
         cb[q] = bb;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -2761,6 +2769,35 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             T tsum = T(0), csum = T(0);
             GNND_DCHECK(cb[q] < CW, GNND_DBG_GRID);
             const SumX<T>* sxb = s_sx + cb[q] * V;
+            if constexpr (kRatio64) {
+                // fp64 ratio form (bp_ratio64): t_e = n_e / d_e, the check's N = s prod n,
+                // D = prod d, m_e = log|D n_e + N d_e| - log|D n_e - N d_e|
+                T nv[R], dv[R], Np = T(1), Dp = T(1);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t sv = ve[q][r];
+                    const bool valid = !(PADR > 0 && r >= R - PADR) || (int)(sv >> 16) != spare;
+                    const SumX<T> p = sxb[sv & 0xffffu];
+                    const T a = (p.s - m[q][r]) + p.x;
+                    const T z = fmin(fmax(fabs(a), MODEL == GNND_QBP ? 2e-20 : 2e-7), 10.0);
+                    const T em = expm1_f64(-z);
+                    nv[r] = valid ? (a < T(0) ? em : -em) : T(1);
+                    dv[r] = valid ? T(2) + em : T(1);
+                    Np = r == 0 ? nv[0] : Np * nv[r];
+                    Dp = r == 0 ? dv[0] : Dp * dv[r];
+                }
+                Np = group_prod_c<G>(Np);
+                Dp = group_prod_c<G>(Dp);
+                if constexpr (MODEL == GNND_QBP) Np = Np * sc[q];
+                T* mb = s_m + cb[q] * E1;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const T A = Dp * nv[r], Bv = Np * dv[r];
+                    m[q][r] = g_log(fabs(A + Bv)) - g_log(fabs(A - Bv));
+                    mb[(int)(ve[q][r] >> 16)] = m[q][r];
+                }
+                continue;
+            }
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const uint32_t sv = ve[q][r];
@@ -3135,8 +3172,7 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
                          model == GNND_V10 || model == GNND_V22;
     const bool f64res = dtype == GNND_F64 && quantum && !f64_resident_disabled();
     // (the ratio-form fp32 BP check step needs every check of degree >= 2: bp_ratio_msg)
-    const bool ratio_bad = GNND_BP_RATIO && dtype == GNND_F32 && (model == GNND_CBP || model == GNND_QBP) &&
-                           gr->min_dc < 2;
+    const bool ratio_bad = GNND_BP_RATIO && (model == GNND_CBP || model == GNND_QBP) && gr->min_dc < 2;
     if (light && (dtype == GNND_F32 || f64res) && gr->rview.G <= 16 && !resident_disabled() && !ratio_bad) {
         const GraphView& g = gr->rview;          // instantiated group sizes 1..16
         const size_t target = dtype == GNND_F64 ? 2 * lds_target() : lds_target();
