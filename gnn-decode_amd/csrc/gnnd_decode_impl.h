@@ -824,8 +824,13 @@ struct Mlp10Pair {
 // edge pair; the same function, rounded differently (the 1e-7 level).  No K <= 32: ok = 0 and
 // the kernel keeps Mlp10Pair.
 // ---------------------------------------------------------------------------------------
+// MEASURED AND NOT KEPT (default 0; -DGNND_MLP_PWL=1 builds it): the table costs two LDS
+// reads per edge (24 bytes), and the register-resident kernel's LDS pipe, shared by the CU's
+// four SIMDs, is the tighter resource: same-box A/B (profiles/r06/experiments/ab_r06g_pwl.txt)
+// BCH 142.5 -> 121.8 M cw/s with the unit fallback compiled in, 124.2 M without it; LDPC 22.0
+// -> 16.7 / 17.4 M.  The ten packed unit FMAs with their weights in SGPRs stay.
 #ifndef GNND_MLP_PWL
-#define GNND_MLP_PWL 1                // 0: Mlp10Pair everywhere (A/B builds)
+#define GNND_MLP_PWL 0                // 1: the piecewise-linear table (A/B builds)
 #endif
 constexpr int kPwlMaxCells = 32;
 constexpr int kPwlEntry = 8;                                      // floats per cell (6 used)
@@ -2538,7 +2543,11 @@ decode_resident_kernel(GraphView g, const T* __restrict__ w, int nw, const TI* _
             // c->v update of two edges from the leave-one-out sums u (and sign counts n)
             auto post2 = [&](f32x2 u, f32x2 n, f32x2 scp, f32x2 mprev) {
                 if constexpr (kBase2) {
+#ifdef GNND_MLP_PWL_ONLY
+                    const f32x2 y = pwl_eval2(s_pwl, pwl, u);          // (A/B: no unit fallback)
+#else
                     const f32x2 y = pwl.ok ? pwl_eval2(s_pwl, pwl, u) : mlp2(u);
+#endif
                     if constexpr (MODEL == GNND_QGNNI) return __builtin_elementwise_fma(y, scp, mprev);
                     else return y + mprev;
                 } else if constexpr (WBP) {

@@ -115,7 +115,7 @@ def test_prepared_layout_and_trainer_rebuild():
     assert prep.numel() == gd.ops.prepared_count('v24', torch.float64) == 7252
     assert torch.equal(prep[:1283], flat)
     assert 0 < float(prep[1283]) < 1e-13 and float(prep[1284]) > 3
-    assert gd.ops.prepared_count('v24', torch.float32) == 1283
+    assert gd.ops.prepared_count('v24', torch.float32) == 7252          # (fp32: the same table in fp32)
     lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
     tr = gd.train.FusedV24Trainer(m, lf, graph=False)
     x, y = gd.data.toric_batch(H, 32, seed=2, device=torch.device(DEV), dtype=torch.float64)
