@@ -2892,6 +2892,22 @@ __device__ __forceinline__ SpIdx sg_index(double x) {
     q.j = k - kSgLo;
     return q;
 }
+// the same index for any finite h (sg_index's 32-bit index wraps for |h| >= 2^31 /
+// 40): the index from h clamped to [-64, 64] (beyond it j is an end entry either way), r from
+// h itself -- the end entries are exactly linear, so the value stays exact.  Identical to
+// sg_index wherever that one is valid; the decoder takes it only for waves whose pre-activation
+// bound reaches 2^25 (decode_kernel's MLP guard)
+__device__ __forceinline__ SpIdx sg_index_safe(double x) {
+    const double xi = __builtin_fmin(__builtin_fmax(x, -64.0), 64.0);
+    const double tk = __builtin_fma(xi, kSgScale, kRoundMagic);
+    int k = round_magic_lo(tk);
+    k = k < kSgLo ? kSgLo : k;
+    k = k > kSgHi ? kSgHi : k;
+    SpIdx q;
+    q.r = __builtin_fma((double)k, -kSgStep, x);
+    q.j = k - kSgLo;
+    return q;
+}
 // g(c + r) from the entry {f0 = g(c), sig = 1/2 - sigmoid(c)}: 8 VALU
 __device__ __forceinline__ double sg_poly(double r, double f0, double sig) {
     const double t = __builtin_fma(-sig, sig, 0.25);
@@ -2947,18 +2963,20 @@ __device__ __forceinline__ double softplus_v24(double x, const double* __restric
 #endif
 // the one-read forms in two steps (index, then the value from the read entry), so a caller can
 // issue several units' table reads together (decode_kernel mlp128d_chains_cm)
+template <bool SAFE = false>
 __device__ __forceinline__ SpIdx v24_sp_index(double x) {
-    if (GNND_F64_SGTAB) return sg_index(x);
+    if (GNND_F64_SGTAB) return SAFE ? sg_index_safe(x) : sg_index(x);
     return sp_index(x);
 }
 __device__ __forceinline__ double v24_sp_half(const SpIdx& q, const SpEntry& e, double x) {
     if (GNND_F64_SGTAB) return sg_poly(q.r, e.f0, e.s);
     return __builtin_fma(__builtin_fabs(x), 0.5, sp_poly(q.r, e.f0, e.s));
 }
+template <bool SAFE = false>
 __device__ __forceinline__ double softplus_v24_half(double x, const double* __restrict__ tab) {
     if (!GNND_F64_LINFOLD) return softplus_v24(x, tab);
     if (GNND_F64_SPTAB) {
-        const SpIdx q = v24_sp_index(x);
+        const SpIdx q = v24_sp_index<SAFE>(x);
         return v24_sp_half(q, sp_entry(tab, q.j), x);
     }
     return softplus_fast(x, tab);

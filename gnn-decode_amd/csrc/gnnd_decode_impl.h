@@ -269,7 +269,7 @@ template <int N, typename F, int I = 0> __device__ __forceinline__ void static_f
 // bl: the MLP's 128 layer-1 biases staged in LDS (a broadcast ds_read_b64 per unit: VOP3 takes
 // one scalar operand, so a bias from SGPRs costs a v_mov_b64 per unit); tab: the Softplus
 // table in LDS (softplus_v24).
-template <int NC, int J0, bool TWO>
+template <int NC, int J0, bool TWO, bool SAFE = false>
 __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, const double* bl,
                                                  double u0, double u1, const double* tab) {
     constexpr int kW2 = TWO ? 384 : 256;
@@ -285,7 +285,7 @@ __device__ __forceinline__ double mlp128d_chains(const double* __restrict__ w, c
             double h;
             if constexpr (TWO) h = fma_vsv(u0, w[k], fma_vsv(u1, w[128 + k], bl[k]));
             else h = fma_vsv(u0, w[k], bl[k]);
-            c[jj] = fma(softplus_v24_half(h, tab), w[kW2 + k], c[jj]);
+            c[jj] = fma(softplus_v24_half<SAFE>(h, tab), w[kW2 + k], c[jj]);
         });
     }
     if constexpr (NC == 4) return (c[0] + c[1]) + (c[2] + c[3]);
@@ -306,7 +306,7 @@ struct WcmEntry {
 #ifndef GNND_FWD_FAIR
 #define GNND_FWD_FAIR 1
 #endif
-template <int NC, int J0, bool TWO, bool FAIR = false>
+template <int NC, int J0, bool TWO, bool FAIR = false, bool SAFE = false>
 __device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u0, double u1,
                                                     const double* tab) {
     constexpr int UT = 4, NU = 32 * NC;       // units per stage (NC divides UT), per call
@@ -330,7 +330,7 @@ __device__ __forceinline__ double mlp128d_chains_cm(const WcmEntry* wl, double u
 #pragma unroll
         for (int s = 0; s < UT; ++s) {
             h[s] = TWO ? fma(u0, e[s].w1a, fma(u1, e[s].w1b, e[s].b1)) : fma(u0, e[s].w1a, e[s].b1);
-            q[s] = v24_sp_index(h[s]);
+            q[s] = v24_sp_index<SAFE>(h[s]);
         }
 #pragma unroll
         for (int s = 0; s < UT; ++s) t[s] = sp_entry(tab, q[s].j);
@@ -353,9 +353,18 @@ __device__ __forceinline__ double mlp_lin(const double* ln, double u0, double u1
     if (!GNND_F64_LINFOLD) return 0.0;
     return TWO ? fma(u0, ln[0], fma(u1, ln[1], ln[2])) : fma(u0, ln[0], ln[2]);
 }
+// The MLP's pre-activation bound |h_k| <= max(|u0|, |u1|, 1) ln[3], ln[3] = max_k (|W1a_k| +
+// |W1b_k| + |b1_k|) (decode_kernel prologue): a wave with a lane at 2^25 or above takes the
+// sg_index_safe units (the same bits wherever sg_index is valid)
+__device__ __forceinline__ bool mlp_wave_big(const double* ln, double u0, double u1) {
+    const bool big = fmax(fmax(fabs(u0), fabs(u1)), 1.0) * ln[3] >= 0x1p25;
+    return __builtin_amdgcn_ballot_w64(big) != 0;
+}
 __device__ __forceinline__ double mlp128_sp(const double* w, const double* bl, double u,
                                             const double* tab, const double* ln) {
-    return (mlp128d_chains<4, 0, false>(w, bl, u, u, tab) + mlp_lin<false>(ln, u, u)) + w[384];
+    const double c = mlp_wave_big(ln, u, u) ? mlp128d_chains<4, 0, false, true>(w, bl, u, u, tab)
+                                            : mlp128d_chains<4, 0, false>(w, bl, u, u, tab);
+    return (c + mlp_lin<false>(ln, u, u)) + w[384];
 }
 // unit-split evaluation of the fp64 MLPs (decode_kernel US > 1, fp64 decoder_v2_4 small
 // batches): wave `sub` evaluates chain group sub, the US partial sums meet in LDS (buf = [US][256]
@@ -369,7 +378,10 @@ __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, co
                                                 const double* ln, const WcmEntry* wl = nullptr) {
     constexpr int kB2 = TWO ? 512 : 384;
     if constexpr (US == 1) {
-        return idle ? 0.0 : (mlp128d_chains<4, 0, TWO>(w, bl, u0, u1, tab) + mlp_lin<TWO>(ln, u0, u1)) + w[kB2];
+        if (idle) return 0.0;
+        const double c = mlp_wave_big(ln, u0, u1) ? mlp128d_chains<4, 0, TWO, true>(w, bl, u0, u1, tab)
+                                                  : mlp128d_chains<4, 0, TWO>(w, bl, u0, u1, tab);
+        return (c + mlp_lin<TWO>(ln, u0, u1)) + w[kB2];
     } else {
         static_assert(US == 2 || US == 4, "fp64 unit split 1, 2 or 4");
         constexpr int NC = 4 / US, IL = GNND_BLOCK;
@@ -377,11 +389,20 @@ __device__ __forceinline__ double mlp128d_split(const double* __restrict__ w, co
         if (!idle) {
 #if GNND_F64_SPTAB
             constexpr bool F = GNND_FWD_FAIR;
-            switch (sub) {
-                case 0: p = mlp128d_chains_cm<NC, 0, TWO, F>(wl, u0, u1, tab); break;
-                case 1: p = mlp128d_chains_cm<NC, NC, TWO, F>(wl, u0, u1, tab); break;
-                case 2: if constexpr (US == 4) p = mlp128d_chains_cm<1, 2, TWO, F>(wl, u0, u1, tab); break;
-                default: if constexpr (US == 4) p = mlp128d_chains_cm<1, 3, TWO, F>(wl, u0, u1, tab); break;
+            if (mlp_wave_big(ln, u0, u1)) {
+                switch (sub) {
+                    case 0: p = mlp128d_chains_cm<NC, 0, TWO, F, true>(wl, u0, u1, tab); break;
+                    case 1: p = mlp128d_chains_cm<NC, NC, TWO, F, true>(wl, u0, u1, tab); break;
+                    case 2: if constexpr (US == 4) p = mlp128d_chains_cm<1, 2, TWO, F, true>(wl, u0, u1, tab); break;
+                    default: if constexpr (US == 4) p = mlp128d_chains_cm<1, 3, TWO, F, true>(wl, u0, u1, tab); break;
+                }
+            } else {
+                switch (sub) {
+                    case 0: p = mlp128d_chains_cm<NC, 0, TWO, F>(wl, u0, u1, tab); break;
+                    case 1: p = mlp128d_chains_cm<NC, NC, TWO, F>(wl, u0, u1, tab); break;
+                    case 2: if constexpr (US == 4) p = mlp128d_chains_cm<1, 2, TWO, F>(wl, u0, u1, tab); break;
+                    default: if constexpr (US == 4) p = mlp128d_chains_cm<1, 3, TWO, F>(wl, u0, u1, tab); break;
+                }
             }
 #else
             switch (sub) {
@@ -1593,7 +1614,14 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     }
                     if (tid == 0) s_lin[4 * m + q] = v;
                 }
-                if (tid == 0) s_lin[4 * m + 3] = T(0);
+                // the pre-activation bound's weight factor (mlp_wave_big): a 64-lane max
+                const T* b1p = wm + (m == 0 ? 256 : 128);
+                T wmx = T(0);
+                for (int k = tid; k < 128; k += 64)
+                    wmx = fmax(wmx, fabs(wm[k]) + (m == 0 ? fabs(wm[128 + k]) : T(0)) + fabs(b1p[k]));
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) wmx = fmax(wmx, __shfl_xor(wmx, o));
+                if (tid == 0) s_lin[4 * m + 3] = wmx;
             }
         }
         for (int i = tid; i < kV24F64TabDoubles; i += NT) s_tab[i] = v24_f64_tab_entry(i);

@@ -82,7 +82,23 @@ int main() {
         if (h > 20 && (q.j != kSgN - 1 || gv != 0.5 * h)) mthr = 1;
         if (h == 20.0 && q.j != kSgN - 2) mthr = 1;
     }
-    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %ld %.3e %.3e %.3e %.3e %.3e\n", me, ml, mt, mm, ms, mst, met, mlt, msl, nfast, msp, msg, msgt, mthr, msgd);
+    // sg_index_safe (ADVICE r05: sg_index's 32-bit index wraps for |h| >= 2^31 / 40): exact far
+    // beyond that, and the same entry and offset as sg_index wherever sg_index is valid
+    double msafe = 0;
+    const double big[] = {5.4e7, 6e7, 1e8, 1e12, 3e15, -5.4e7, -6e7, -1e8, -1e12, -3e15};
+    for (double h : big) {
+        const SpIdx q = sg_index_safe(h);
+        const double gv = sg_poly(q.r, kSgTab[2 * q.j], kSgTab[2 * q.j + 1]);
+        const double ref = h > 20 ? h : log1p(exp(h));
+        msafe = fmax(msafe, fabs((gv + 0.5 * h) - ref) / fmax(1.0, fabs(ref)));
+    }
+    long nsafe = 0;
+    for (int i = 0; i < 200000; ++i) {
+        const double h = U(g) * (i % 2 ? 1.0 : 1e4);
+        const SpIdx a = sg_index(h), b = sg_index_safe(h);
+        nsafe += a.j != b.j || a.r != b.r;
+    }
+    printf("%.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3f %.3e %ld %.3e %.3e %.3e %.3e %.3e %.3e %ld\n", me, ml, mt, mm, ms, mst, met, mlt, msl, nfast, msp, msg, msgt, mthr, msgd, msafe, nsafe);
 }
 '''
 
@@ -124,3 +140,7 @@ def test_fp64_fast_math_ulp(tmp_path):
     # sg_grad_poly (its sigmoid, the fp64 reverse pass since r05): <= 1e-12 absolute, exactly 1
     # above the threshold
     assert float(out[14]) <= 1e-12, out[14]
+    # sg_index_safe (the decoder's MLP guard path): |h| up to 3e15 within an ulp of
+    # torch's Softplus, and bit-identical to sg_index over |h| <= 7e6
+    assert float(out[15]) <= 2.3e-16, out[15]
+    assert int(out[16]) == 0, out[16]

@@ -124,3 +124,25 @@ def test_prepared_layout_and_trainer_rebuild():
         torch.cuda.synchronize()
         ref = gd.ops.prepare_weights('v24', tr.flat)
         assert torch.equal(tr.prepared, ref)
+
+
+def test_huge_priors_take_the_safe_softplus_index():
+    """the fp64 Softplus table index (sg_index) wraps for |h| >= 2^31 / 40; a wave
+    whose MLP pre-activation bound reaches 2^25 evaluates its units with sg_index_safe.  Priors of
+    +-1e8 on some codewords (h up to ~4e8): the decode still equals the oracle (rtol 1e-10)."""
+    import warnings
+    import gnndecode as gd
+    m, H = _model(weights='shipped')
+    x, _ = gd.data.toric_batch(H, 32, seed=4, device=torch.device(DEV), dtype=torch.float64)
+    N, V = H.shape[0] + H.shape[1], H.shape[0]
+    xv = x.view(32, N)
+    xv[::3, :V] *= 1e8 / xv[::3, :V].abs().clamp_min(1e-300)
+    g = m.graph(x.device)
+    out = gd.ops.decode(g, 'v24', x, m.Nc, m.prepared_weights(torch.float64, x.device))
+    w = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')               # (exp overflow inside the oracle's where)
+        ref = O.decode('v24', H, x.cpu().numpy(), m.Nc, w)
+    got = out.cpu().numpy()
+    assert np.isfinite(got).all()
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
