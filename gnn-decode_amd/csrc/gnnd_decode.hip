@@ -95,9 +95,39 @@ extern "C" int gnnd_prepared_weights_count(int model, int dtype, int64_t* h_coun
     int n = weights_count(model);
     if (n == -1 || !h_count || (dtype != GNND_F32 && dtype != GNND_F64)) return GNND_ERR_INVALID_ARG;
     if (n < 0) return GNND_ERR_UNSUPPORTED;
-    *h_count = model == GNND_V24 && (dtype == GNND_F64 || GNND_V24_CTAB) ? kV24PreparedF64
+    *h_count = model == GNND_V24 && (dtype == GNND_F64 || GNND_V24_CTAB) ? kV24PriorOff
                : (model == GNND_CGNNI || model == GNND_QGNNI) && dtype == GNND_F32 && GNND_MLP_PWL
                    ? kGnnPreparedF32 : n;
+    return GNND_OK;
+}
+
+extern "C" int gnnd_prepared_weights_count_priors(int model, int dtype, int32_t n_priors,
+                                                  int64_t* h_count) {
+    if (n_priors == 0) return gnnd_prepared_weights_count(model, dtype, h_count);
+    if (!h_count || n_priors < 0 || n_priors > kVtMaxPriors || weights_count(model) == -1)
+        return GNND_ERR_INVALID_ARG;
+    if (model != GNND_V24 || dtype != GNND_F64) return GNND_ERR_UNSUPPORTED;
+    *h_count = kV24PriorOff + (int64_t)(n_priors + 1) * kVtStride;   // (+ the readout MLP's table)
+    return GNND_OK;
+}
+
+extern "C" int gnnd_prepare_weights_priors(int model, int dtype, const void* d_w, void* d_prepared,
+                                           const double* h_priors, int32_t n_priors, void* stream) {
+    if (n_priors < 0 || n_priors > kVtMaxPriors || (n_priors > 0 && !h_priors)) return GNND_ERR_INVALID_ARG;
+    if (n_priors > 0 && (model != GNND_V24 || dtype != GNND_F64)) return GNND_ERR_UNSUPPORTED;
+    const int rc = gnnd_prepare_weights(model, dtype, d_w, d_prepared, stream);
+    if (rc != GNND_OK || n_priors == 0) return rc;
+    // (after gnnd_prepare_weights on the same stream: its check-MLP build zeroes the header,
+    // the table build then writes the count)
+    VtPriors pr{};
+    for (int i = 0; i < n_priors; ++i) pr.x[i] = h_priors[i];
+    vtab_build_kernel<0><<<dim3(kVtCells, n_priors), 128, 0, (hipStream_t)stream>>>(
+        (const double*)d_w, (double*)d_prepared, pr, n_priors, 0);
+    GNND_LAUNCH_CHECK();
+    // the readout MLP's table after them (same form, no prior)
+    vtab_build_kernel<1><<<dim3(kVtCells, 1), 128, 0, (hipStream_t)stream>>>(
+        (const double*)d_w, (double*)d_prepared, pr, n_priors, n_priors);
+    GNND_LAUNCH_CHECK();
     return GNND_OK;
 }
 

@@ -450,6 +450,10 @@ constexpr int kCtabRcap = 31;                // prepared table: |c_j| <= 31 (max
 constexpr int kCtabCap = 2 * kCtabInv * kCtabRcap + 1;               // 497 entries
 constexpr int kV24CtabOff = 1288;            // doubles: prepared fp64 V24 = [1283 plain | pad | table]
 constexpr int kV24PreparedF64 = kV24CtabOff + kCtabCap * kCtabNC;    // 7 252
+// then the channel-prior section (vtab_*, below): [kV24PriorHdr] = number of prior tables (0
+// unless gnnd_prepare_weights_priors built them), pad to kV24PriorOff, the tables
+constexpr int kV24PriorHdr = kV24PreparedF64;
+constexpr int kV24PriorOff = kV24PriorHdr + 12;                      // 7 264 (128-B aligned): the V24 prepared count
 // (1/16)^12 / 12! * max|sigma^(11)|: the remainder bound per unit of sum |W2| |W1|^12
 constexpr double kCtabBoundCoef = 86.375 / 479001600.0 / 281474976710656.0;
 __host__ __device__ constexpr int ctab_entries(int max_dc) {
@@ -472,6 +476,18 @@ __device__ __forceinline__ double ctab_un(int n, double q, double q2) {
         default: return q * fma(q2, fma(q2, fma(q2, fma(q2, 7087.5, -18900.0), 17482.5), -6360.0), 691.0) *
                         (1.0 / 39916800);
     }
+}
+// softplus^(n)(h) / n!, n = 0 .. kCtabNC - 1, of the smooth function (no threshold)
+__device__ __forceinline__ void softplus_taylor(double h, double (&d)[kCtabNC]) {
+    const double e = exp(-fabs(h));
+    const double sv = 1.0 / (1.0 + e);
+    const double tau = e * sv * sv;
+    const double q = h >= 0.0 ? (e - 1.0) * sv : (1.0 - e) * sv;
+    const double q2 = q * q;
+    d[0] = fmax(h, 0.0) + log1p(e);
+    d[1] = h >= 0.0 ? sv : e * sv;
+#pragma unroll
+    for (int n = 2; n < kCtabNC; ++n) d[n] = tau * ctab_un(n - 1, q, q2);
 }
 // One entry per block (blockIdx.x = j + kCtabInv kCtabRcap), one hidden unit per thread (128):
 // w = plain packed V24 weights (ggc2.mlp at kV24Ggc2; may alias prep), prep = the prepared
@@ -503,15 +519,7 @@ __global__ void __launch_bounds__(128) ctab_build_kernel(const TW* w, TP* prep) 
 #pragma unroll
         for (int n = 2; n < kCtabNC; ++n) d[n] = 0.0;
     } else {
-        const double e = exp(-fabs(h));
-        const double sv = 1.0 / (1.0 + e);
-        const double tau = e * sv * sv;
-        const double q = h >= 0.0 ? (e - 1.0) * sv : (1.0 - e) * sv;
-        const double q2 = q * q;
-        d[0] = fmax(h, 0.0) + log1p(e);
-        d[1] = h >= 0.0 ? sv : e * sv;
-#pragma unroll
-        for (int n = 2; n < kCtabNC; ++n) d[n] = tau * ctab_un(n - 1, q, q2);
+        softplus_taylor(h, d);
     }
     __shared__ double part[kCtabNC + 2];
     double t[kCtabNC];
@@ -543,6 +551,8 @@ __global__ void __launch_bounds__(128) ctab_build_kernel(const TW* w, TP* prep) 
             prep[1283] = (TP)((s12 + part[kCtabNC]) * kCtabBoundCoef);
             prep[1284] = (TP)(kThr ? fmin(rk, part[kCtabNC + 1]) : 1e30);
             for (int i = 1285; i < kV24CtabOff; ++i) prep[i] = TP(0);   // (defined padding)
+            // no channel-prior tables (a weight update leaves any earlier ones stale)
+            for (int i = kV24PriorHdr; i < kV24PriorOff; ++i) prep[i] = TP(0);
         }
     }
 }
@@ -598,6 +608,172 @@ __device__ __forceinline__ float ctab_eval(const float* tab, float u, int R8) {
 #pragma unroll
     for (int n = kCtabNC - 2; n >= 0; --n) p = __builtin_fmaf(p, r, a[n]);
     return p;
+}
+
+// ---------------------------------------------------------------------------------------
+// decoder_v2_4's variable-side MLP per channel prior (fp64).  ggc1.mlp (Linear(2, 128) ->
+// Softplus -> Linear(128, 1), quantum/decoder_v2_4.py:237-239, :253-255) takes (u, x_v), u =
+// S_v - m_e; the reference's inputs carry ONE prior per codeword, x_v = log((1 - p) / p) with p
+// from a short list (quantum/error_generate.py:252-260 gen_syn), so for a fixed x it is a
+// one-input MLP with biases b1' = W1b x + b1.  gnnd_prepare_weights_priors tabulates it per
+// prior value over |u| <= kVtR as degree-11 Taylor polynomials about c_j = j / 8, one cell per
+// centre, like the check-side table -- except that u is not bounded by the graph, so units DO
+// cross torch's Softplus threshold 20 inside the range.  Each cell classifies the units over
+// its interval |u - c_j| <= 1/16: h > 20 throughout -> the unit is exactly linear (torch's
+// softplus(h) = h); h <= 20 throughout -> smooth; otherwise the unit crosses inside the cell:
+// the polynomial takes its smooth softplus and the cell lists it ({W1a, b1', -W2 e^-20}, at most
+// kVtNX per cell), the evaluation adding torch's jump -W2 log1p(e^-h) = -W2 e^-20 e^-(h - 20)
+// (1 + O(2e-9)) on the lanes whose h = fma(u, W1a, b1') -- the decoder's own pre-activation --
+// exceeds 20.  A cell with more crossings, a crossing unit with |W1a| > 8 (h - 20 beyond [0, 1]),
+// or a remainder bound above 1e-13 is marked invalid; its lanes, |u| > kVtR + 1/16, and inputs
+// whose x_v is not the table's prior (bit-exact key) evaluate the 128 units.  Epoch-67 weights,
+// the ten priors of the reference's p list: 0-3 crossings per cell, bound 3.5e-18.
+// Table t at kV24PriorOff + t kVtStride: [0] = the prior x (key), pad to kVtHdr, then kVtCells
+// cells of kVtCell doubles (one 128-byte line each: a lookup reads one line): a_0 .. a_11, [12] =
+// crossing count (-1: invalid), pad; then per cell kVtNX crossing units {W1a, b1', -W2 e^-20}.
+// ---------------------------------------------------------------------------------------
+constexpr int kVtInv = 8;
+constexpr int kVtR = 32;                                  // centres |c_j| <= 32
+constexpr int kVtCells = 2 * kVtInv * kVtR + 1;           // 513
+constexpr int kVtNX = 3;                                  // crossing units per cell
+constexpr int kVtCell = 16;                               // doubles per cell (128 B)
+constexpr int kVtHdr = 16;
+constexpr int kVtXOff = kVtHdr + kVtCells * kVtCell;      // the crossing units [kVtCells][kVtNX][3]
+constexpr int kVtStride = (kVtXOff + kVtCells * kVtNX * 3 + 15) & ~15;   // 12 848 doubles per table
+constexpr int kVtMaxPriors = 64;
+struct VtPriors {
+    double x[kVtMaxPriors];
+};
+// The readout MLP (mlp: Linear(1,128) -> Softplus -> Linear(128,1) on every message m_e,
+// quantum/decoder_v2_4.py:291) the same way, as one more table after the prior tables (SEL = 1:
+// no key, no prior; prep[kV24PriorHdr + 1] = 1 marks it).
+// block (j, t): cell j of table t0 + t, one unit per thread; w = the plain packed fp64 weights
+// (may alias prep)
+template <int SEL>
+__global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double* prep, VtPriors pr, int n,
+                                                         int t0) {
+    const double* wm = w + (SEL == 0 ? kV24Ggc1 : kV24Mlp);
+    const int k = threadIdx.x, j = blockIdx.x, t = t0 + blockIdx.y;
+    const double x = SEL == 0 ? pr.x[blockIdx.y] : 0.0;
+    const double W1a = wm[k], W1b = SEL == 0 ? wm[128 + k] : 0.0, b1 = wm[(SEL == 0 ? 256 : 128) + k];
+    const double W2 = wm[(SEL == 0 ? 384 : 256) + k], b2 = wm[SEL == 0 ? 512 : 384];
+    // the decoder's pre-activation: ggc1 fma(u, W1a, fma(x, W1b, b1)), readout fma(m, W1, b1)
+    const double bp = SEL == 0 ? fma(x, W1b, b1) : b1;
+    const double c = (double)(j - kVtInv * kVtR) * (1.0 / kVtInv);
+    const double h = fma(W1a, c, bp);
+    const double half = fabs(W1a) * (0.5 / kVtInv) + 1e-9 * (1.0 + fabs(h));
+    const bool lin = h - half > 20.0, cross = !lin && h + half > 20.0;
+    double d[kCtabNC];
+    if (lin) {
+        d[0] = h;
+        d[1] = 1.0;
+#pragma unroll
+        for (int i = 2; i < kCtabNC; ++i) d[i] = 0.0;
+    } else {
+        softplus_taylor(h, d);
+    }
+    __shared__ double part[kCtabNC + 1];
+    __shared__ int ncross0;
+    double a[kCtabNC];
+    double p = W2;
+#pragma unroll
+    for (int i = 0; i < kCtabNC; ++i) {
+        a[i] = group_sum_c<64>(p * d[i]);
+        p *= W1a;
+    }
+    const double w2 = W1a * W1a, w4 = w2 * w2;
+    const double s12 = group_sum_c<64>(fabs(W2) * (w4 * w4 * w4));
+    const uint64_t cm = __builtin_amdgcn_ballot_w64(cross);
+    const bool wide_cross = __builtin_amdgcn_ballot_w64(cross && fabs(W1a) > 8.0) != 0;
+    __shared__ int bad;
+    if (k == 0) bad = 0;
+    __syncthreads();
+    if (k == 64) {
+#pragma unroll
+        for (int i = 0; i < kCtabNC; ++i) part[i] = a[i];
+        part[kCtabNC] = s12;
+    }
+    if (k == 0) ncross0 = __builtin_popcountll(cm);
+    if ((k & 63) == 0 && wide_cross) bad = 1;
+    __syncthreads();
+    double* tbl = prep + kV24PriorOff + (size_t)t * kVtStride;
+    double* cell = tbl + kVtHdr + (size_t)j * kVtCell;
+    double* xu = tbl + kVtXOff + (size_t)j * kVtNX * 3;   // the cell's crossing units
+    const int ntot = ncross0 + (k >= 64 ? __builtin_popcountll(cm) : 0);   // (valid in wave 1)
+    // the crossing units in unit order: rank = crossings below k
+    const int below = __builtin_popcountll(cm & ((1ull << (k & 63)) - 1ull)) + (k >= 64 ? ncross0 : 0);
+    if (cross && below < kVtNX) {
+        xu[3 * below] = W1a;
+        xu[3 * below + 1] = bp;
+        xu[3 * below + 2] = -W2 * exp(-20.0);
+    }
+    if (k == 64) {                                        // wave 1 knows the total
+        const bool ok = !bad && ntot <= kVtNX && (s12 + part[kCtabNC]) * kCtabBoundCoef <= 1e-13;
+        cell[12] = ok ? (double)ntot : -1.0;
+        for (int i = 13; i < kVtCell; ++i) cell[i] = 0.0;
+        for (int i = ntot < kVtNX ? ntot : kVtNX; i < kVtNX; ++i) {
+            xu[3 * i] = 0.0;
+            xu[3 * i + 1] = 0.0;
+            xu[3 * i + 2] = 0.0;
+        }
+        if (j == 0)                                       // (defined padding after the units)
+            for (int i = kVtXOff + kVtCells * kVtNX * 3; i < kVtStride; ++i) tbl[i] = 0.0;
+    }
+    if (k == 0) {
+#pragma unroll
+        for (int i = 0; i < kCtabNC; ++i) cell[i] = (a[i] + part[i]) + (i == 0 ? b2 : 0.0);
+        if (j == 0) {
+            double* hd = prep + kV24PriorOff + (size_t)t * kVtStride;
+            hd[0] = x;
+            for (int i = 1; i < kVtHdr; ++i) hd[i] = 0.0;
+            if (blockIdx.y == 0) prep[kV24PriorHdr + SEL] = SEL == 0 ? (double)n : 1.0;
+        }
+    }
+}
+// e^-t, 0 <= t <= 1 (degree 10: relative error < 3e-8, on a term below 2.1e-9 |W2|)
+__device__ __forceinline__ double vtab_expm(double t) {
+    double p = 1.0 / 3628800;
+    p = fma(p, -t, 1.0 / 362880);
+    p = fma(p, -t, 1.0 / 40320);
+    p = fma(p, -t, 1.0 / 5040);
+    p = fma(p, -t, 1.0 / 720);
+    p = fma(p, -t, 1.0 / 120);
+    p = fma(p, -t, 1.0 / 24);
+    p = fma(p, -t, 1.0 / 6);
+    p = fma(p, -t, 0.5);
+    p = fma(p, -t, 1.0);
+    return fma(p, -t, 1.0);
+}
+// ggc1.mlp(u, x) from prior table tb (global memory, L2-resident): false (y untouched) when x is
+// not the table's prior (KEY), |u| is outside the table or the cell is invalid
+template <bool KEY = true>
+__device__ __forceinline__ bool vtab_eval(const double* __restrict__ tb, double u, double x, double& y) {
+    if (KEY && __double_as_longlong(x) != __double_as_longlong(tb[0])) return false;
+    if (!(fabs(u) <= kVtR + 0.0625)) return false;
+    int k = round_magic_lo(__builtin_fma(u, (double)kVtInv, kRoundMagic));
+    k = k < -kVtInv * kVtR ? -kVtInv * kVtR : (k > kVtInv * kVtR ? kVtInv * kVtR : k);
+    const int jc = k + kVtInv * kVtR;
+    const double* e = tb + kVtHdr + (size_t)jc * kVtCell;
+    double a[kCtabNC + 2];
+#pragma unroll
+    for (int i = 0; i < kCtabNC / 2 + 1; ++i) {
+        const double2 v = ((const double2*)e)[i];
+        a[2 * i] = v.x;
+        a[2 * i + 1] = v.y;
+    }
+    const int nx = (int)a[kCtabNC];
+    if (nx < 0) return false;
+    const double r = __builtin_fma((double)k, -1.0 / kVtInv, u);
+    double p = a[kCtabNC - 1];
+#pragma unroll
+    for (int n = kCtabNC - 2; n >= 0; --n) p = fma(p, r, a[n]);
+    const double* xu = tb + kVtXOff + (size_t)jc * kVtNX * 3;
+    for (int i = 0; i < nx; ++i) {                        // (rare: ~10 % of the cells)
+        const double h = fma(u, xu[3 * i], xu[3 * i + 1]);
+        if (h > 20.0) p = fma(xu[3 * i + 2], vtab_expm(h - 20.0), p);
+    }
+    y = p;
+    return true;
 }
 
 // fp32 forms: TWO EDGES per call, riding the two halves of packed FMAs (the lane's
@@ -1648,13 +1824,18 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     T* s_m = (T*)(smem + off);                             // [CW][nslot] c->v messages
     SumX<T>* s_sx = (SumX<T>*)(s_m + (size_t)CW * nslot);  // [CW][V]  {S_v, x_v}
     T* s_xc = (T*)(s_sx + (size_t)CW * V);                 // [CW][C]  check-row features
+    constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
+    constexpr bool kV24F64 = MODEL == GNND_V24 && sizeof(T) == 8;
+    // fp64 V24: [CW] the codeword's channel-prior table (offset into w, -1: none; vtab_eval)
+    int* s_vto = (int*)(s_xc + (size_t)CW * C);
     // unit split: two [US][IL] f32x2 buffers for the MLP partial sums (8-byte aligned)
     // (offset arithmetic on the __shared__ base keeps the LDS address space: ds_* accesses,
     // not flat ones as through an integer cast of the pointer)
-    f32x2* s_part = (f32x2*)(smem + ((((char*)(s_xc + (size_t)CW * C) - smem) + 7) & ~(ptrdiff_t)7));
-
-    constexpr bool kV24F32 = MODEL == GNND_V24 && sizeof(T) == 4;
-    constexpr bool kV24F64 = MODEL == GNND_V24 && sizeof(T) == 8;
+    f32x2* s_part = (f32x2*)(smem + ((((char*)(s_vto + (kV24F64 ? CW : 0)) - smem) + 7) & ~(ptrdiff_t)7));
+    // channel-prior tables of the variable-side MLP (fp64 V24 decodes with one wave per item
+    // group: the unit-split and training-tape forms evaluate the units)
+    int n_pt = 0;
+    if constexpr (kV24F64 && US == 1 && !TAPE) n_pt = (int)w[kV24PriorHdr];
     // fp32 V24 on the R = 1 slot plan (B <= 4096): the unit-pair MLPs (mlp128_upair), their
     // pair-major weights staged in LDS after the unit split's partial-sum buffers
     constexpr bool kUP = kV24F32 && R == 1 && US <= 4;
@@ -1715,6 +1896,18 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
             const T* xr = x + (size_t)(b0 + b) * g.xs;
             if (n < V) s_sx[b * V + n] = SumX<T>{T(0), xr[g.xv0 + n]};
             else s_xc[b * C + n - V] = xr[g.xc0 + n - V];
+            if constexpr (kV24F64) {
+                if (n_pt > 0 && n == 0) {     // the table whose prior is the codeword's first x_v
+                    const long long xb = __double_as_longlong((double)xr[g.xv0]);
+                    int to = -1;
+                    for (int t = 0; t < n_pt; ++t)
+                        if (__double_as_longlong((double)w[kV24PriorOff + (size_t)t * kVtStride]) == xb) {
+                            to = kV24PriorOff + t * kVtStride;
+                            break;
+                        }
+                    s_vto[b] = to;
+                }
+            }
         }
     }
     for (int i = tid; i < nb * nslot; i += NT) s_m[i] = T(0);
@@ -1882,11 +2075,21 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     ext[r] = p.s - mv[r];
                     xs[r] = p.x;
                 }
+                const int vto = n_pt > 0 ? s_vto[b] : -1;
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const T a = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
-                                                        s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid, widle,
-                                                        s_tab, s_lin, s_wcm);
+                    T a = T(0);
+                    // the channel-prior table where this lane's (u, x_v) has one; the wave
+                    // evaluates the 128 units when any live lane has none (those lanes keep them)
+                    bool need = n_pt == 0 || (act && val[r]);
+                    if (n_pt > 0 && need && vto >= 0 && vtab_eval((const double*)wv + vto, ext[r], xs[r], a))
+                        need = false;
+                    if (n_pt == 0 || __builtin_amdgcn_ballot_w64(need) != 0) {
+                        const T a2 = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
+                                                             s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid, widle,
+                                                             s_tab, s_lin, s_wcm);
+                        if (need) a = a2;
+                    }
                     tv[r] = val[r] ? tanh_half_fast(a) : T(0);
                     cf[r] = T(0);
                     tsum += tv[r];
@@ -2080,6 +2283,21 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                                                      s_pd + rb * US * GNND_BLOCK, itid, widle, s_tab,
                                                      s_lin + 8, s_wcm + 256);
                 if (sub == 0 && f < n) s_m[f] = y;   // (lanes read only their own message)
+            }
+        } else if (n_pt > 0 && w[kV24PriorHdr + 1] != T(0)) {     // (uniform) the readout table
+            const double* rt = (const double*)wv + kV24PriorOff + (size_t)n_pt * kVtStride;
+            const int n = nb * nslot;
+            for (int f0 = 0; f0 < n; f0 += NT) {
+                const int f = f0 + tid;
+                const T m = s_m[f < n ? f : n - 1];
+                T y = T(0);
+                bool need = f < n;
+                if (need && vtab_eval<false>(rt, m, 0.0, y)) need = false;
+                if (__builtin_amdgcn_ballot_w64(need) != 0) {
+                    const T y2 = mlp128_sp(wv + kV24Mlp, s_bias + 256, m, s_tab, s_lin + 8);
+                    if (need) y = y2;
+                }
+                if (f < n) s_m[f] = y;
             }
         } else {
             for (int f = tid; f < nb * nslot; f += NT) s_m[f] = mlp128_sp(wv + kV24Mlp, s_bias + 256, s_m[f], s_tab, s_lin + 8);
@@ -3294,9 +3512,12 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     // (decode_kernel stages the unit-pair weights whenever fp32 V24 runs a one-slot plan, kUP:
     // reserve them for every such plan, not only for the upair choice above — ADVICE r05)
     const bool up_lds = v24f32 && g.R == 1;
-    const size_t fixed = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab +
-                         (up_lds ? (size_t)UpairLds::kFloats * 4 + 16 : 0);
-    const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C);
+    const size_t fixed0 = wb + align16((nslot + g.V + 1 + g.E) * 4) + tab +
+                          (up_lds ? (size_t)UpairLds::kFloats * 4 + 16 : 0);
+    const bool v24f64 = model == GNND_V24 && dtype == GNND_F64;
+    // (+ fp64 V24: the codeword's channel-prior table offset, s_vto, and its alignment)
+    const size_t fixed = fixed0 + (v24f64 ? 16 : 0);
+    const size_t per = esz * (nslot + 2 * (size_t)g.V + g.C) + (v24f64 ? 4 : 0);
     if (fixed + per > kLdsMax) return GNND_ERR_UNSUPPORTED;
     // fp64 decoder_v2_4 stages its 33 KB Softplus table per workgroup: a third of the CU's LDS
     // per 256-lane workgroup (3 per CU; toric-5: 4 codewords, 3 full item rounds; the default

@@ -60,3 +60,51 @@ extern "C" int gnnd_v24_check_mlp_table(const gnnd_graph* g, const void* d_w, co
     GNND_LAUNCH_CHECK();
     return GNND_OK;
 }
+
+// the variable-side MLP through the channel-prior tables (vtab_eval, gnnd_decode_impl.h), for
+// tests: y[i] = ggc1.mlp(u[i], x[i]) and hit[i] = 1 where a table covers (u[i], x[i]), else hit[i]
+// = 0 and y[i] untouched (the decoder evaluates the 128 units there); x = NULL: the readout
+// MLP's table, y[i] = mlp(u[i])
+namespace {
+__global__ void __launch_bounds__(256)
+vtab_eval_kernel(const double* __restrict__ w, const double* __restrict__ u, const double* __restrict__ xv,
+                 double* __restrict__ y, int32_t* __restrict__ hit, int64_t n) {
+    const int n_pt = (int)w[kV24PriorHdr];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int h = 0;
+        if (!xv) {                                        // the readout MLP's table
+            double v;
+            if (n_pt > 0 && w[kV24PriorHdr + 1] != 0.0 &&
+                vtab_eval<false>(w + kV24PriorOff + (size_t)n_pt * kVtStride, u[i], 0.0, v)) {
+                y[i] = v;
+                h = 1;
+            }
+            hit[i] = h;
+            continue;
+        }
+        const long long xb = __double_as_longlong(xv[i]);
+        for (int t = 0; t < n_pt; ++t) {
+            const double* tb = w + kV24PriorOff + (size_t)t * kVtStride;
+            if (__double_as_longlong(tb[0]) != xb) continue;
+            double v;
+            if (vtab_eval(tb, u[i], xv[i], v)) {
+                y[i] = v;
+                h = 1;
+            }
+            break;
+        }
+        hit[i] = h;
+    }
+}
+}  // namespace
+
+extern "C" int gnnd_v24_var_mlp_table(const void* d_w, const void* d_u, const void* d_x, void* d_y,
+                                      int32_t* d_hit, int64_t n, void* stream) {
+    if (!d_w || n < 0 || (n > 0 && (!d_u || !d_y || !d_hit))) return GNND_ERR_INVALID_ARG;
+    if (n == 0) return GNND_OK;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+    vtab_eval_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+        (const double*)d_w, (const double*)d_u, (const double*)d_x, (double*)d_y, d_hit, n);
+    GNND_LAUNCH_CHECK();
+    return GNND_OK;
+}

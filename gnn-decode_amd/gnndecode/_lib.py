@@ -48,6 +48,10 @@ SIGNATURES = {
     'gnnd_decode_weights_count': (_int, [_vp, _int, _i32, _c_i64p]),
     'gnnd_prepare_weights': (_int, [_int, _int, _vp, _vp, _vp]),
     'gnnd_prepared_weights_count': (_int, [_int, _int, _c_i64p]),
+    'gnnd_prepared_weights_count_priors': (_int, [_int, _int, _i32, _c_i64p]),
+    'gnnd_prepare_weights_priors': (_int, [_int, _int, _vp, _vp, ctypes.POINTER(ctypes.c_double), _i32,
+                                           _vp]),
+    'gnnd_v24_var_mlp_table': (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     'gnnd_decode': (_int, [_vp, _int, _int, _vp, _vp, _vp, _i64, _i32, _vp]),
     'gnnd_decode_tile': (_int, [_vp, _int, _int, _c_i32p, _c_i32p]),
     'gnnd_decode_plan': (_int, [_vp, _int, _int, _c_i32p]),

@@ -287,6 +287,7 @@ class _Decoder(torch.nn.Module):
         self.rows, self.cols = int(self.H.size(0)), int(self.H.size(1))
         self._graphs = {}
         self._wcache = None
+        self._priors = ()
 
     # ---- graph / weights on the device ------------------------------------------------
     def graph(self, device):
@@ -310,15 +311,26 @@ class _Decoder(torch.nn.Module):
         fused trainer's gnnd_adam_step.  The trainers call this after every step."""
         self._wcache = None
 
+    def set_channel_priors(self, priors):
+        """decoder_v2_4, fp64: the channel-prior LLRs x_v the inputs carry (one per codeword in
+        the reference's gen_syn data; e.g. ops.channel_priors(graph, x)).  The fused decoder then
+        reads the variable-side MLP from a table per prior (gnnd_prepare_weights_priors); inputs
+        with other priors still decode exactly (the 128 units).  () to clear."""
+        if priors and self.kind != 'v24':
+            raise ValueError('channel-prior tables: decoder_v2_4 only')
+        self._priors = tuple(float(v) for v in priors)
+        self._wcache = None
+
     def prepared_weights(self, dtype, device):
         key = (dtype, str(device), tuple(p._version for p in self.parameters()),
-               tuple(p.data_ptr() for p in self.parameters()))
+               tuple(p.data_ptr() for p in self.parameters()), self._priors)
         if self._wcache is not None and self._wcache[0] == key:
             return self._wcache[1]
         flat = self.packed_weights()
         if flat is None:
             return None
-        prep = ops.prepare_weights(self.kind, flat.detach().to(device=device, dtype=dtype))
+        pri = self._priors if dtype == torch.float64 else None
+        prep = ops.prepare_weights(self.kind, flat.detach().to(device=device, dtype=dtype), priors=pri)
         self._wcache = (key, prep)
         return prep
 

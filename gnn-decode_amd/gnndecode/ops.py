@@ -168,20 +168,24 @@ def weights_count(model, graph=None, iters=None):
     return n.value
 
 
-def prepared_count(model, dtype, graph=None, iters=None):
-    """Elements of the kernel-layout weights (gnnd_prepared_weights_count): the packed count,
-    except fp64 decoder_v2_4, whose prepared weights carry the check-MLP table."""
+def prepared_count(model, dtype, graph=None, iters=None, priors=0):
+    """Elements of the kernel-layout weights (gnnd_prepared_weights_count[_priors]): the packed
+    count, except decoder_v2_4, whose prepared weights carry the check-MLP table and the
+    channel-prior section (fp64: `priors` tables of the variable-side MLP)."""
     if model in WEIGHTED_BP:
         return weights_count(model, graph, iters)
     n = ctypes.c_int64()
-    _lib.call('gnnd_prepared_weights_count', _lib.VARIANT[model],
-              dtype_code(torch.float32 if dtype == torch.bfloat16 else dtype), ctypes.byref(n))
+    _lib.call('gnnd_prepared_weights_count_priors', _lib.VARIANT[model],
+              dtype_code(torch.float32 if dtype == torch.bfloat16 else dtype), int(priors),
+              ctypes.byref(n))
     return n.value
 
 
-def prepare_weights(model, flat):
+def prepare_weights(model, flat, priors=None):
     """Kernel-layout copy of a packed weight vector (gnnd_prepare_weights).  The weighted-BP
-    tables are used as packed."""
+    tables are used as packed.  `priors` (fp64 decoder_v2_4): the channel-prior LLRs x_v the
+    inputs will carry (e.g. channel_priors(graph, x)); the prepared weights then hold the
+    variable-side MLP tabulated per prior (gnnd_prepare_weights_priors)."""
     _require_gpu(flat)
     flat = flat.contiguous()
     if model in WEIGHTED_BP:
@@ -191,10 +195,43 @@ def prepare_weights(model, flat):
         return None
     if flat.numel() != n:
         raise ValueError(f'{model}: expected {n} packed weights, got {flat.numel()}')
-    out = torch.empty(prepared_count(model, flat.dtype), dtype=flat.dtype, device=flat.device)
-    _lib.call('gnnd_prepare_weights', _lib.VARIANT[model], dtype_code(flat.dtype), _ptr(flat),
-              _ptr(out), current_stream(flat.device))
+    pv = [float(v) for v in (priors if priors is not None else [])]
+    out = torch.empty(prepared_count(model, flat.dtype, priors=len(pv)), dtype=flat.dtype,
+                      device=flat.device)
+    arr = (ctypes.c_double * max(len(pv), 1))(*pv)
+    _lib.call('gnnd_prepare_weights_priors', _lib.VARIANT[model], dtype_code(flat.dtype), _ptr(flat),
+              _ptr(out), arr, len(pv), current_stream(flat.device))
     return out
+
+
+def channel_priors(graph, x, limit=64):
+    """The distinct variable-node inputs x_v of a batch x [B*N] (the channel-prior LLRs of the
+    reference's gen_syn inputs: one per codeword, from a short p list) -- the keys for
+    prepare_weights(priors=...).  One device-to-host copy (setup, not the decode path); raises
+    ValueError when there are more than `limit` (<= 64) distinct values."""
+    xv = x.reshape(-1, graph.N)[:, :graph.V]
+    u = torch.unique(xv).cpu().tolist()
+    if len(u) > limit:
+        raise ValueError(f'{len(u)} distinct priors (at most {limit} tables)')
+    return u
+
+
+def v24_var_mlp_table(prepared_weights, u, xv=None):
+    """gnnd_v24_var_mlp_table: decoder_v2_4's variable-side MLP through the channel-prior tables
+    at fp64 points (u, x_v) -> (y, hit); xv None: the readout MLP's table at u.  y is NaN where
+    hit is False."""
+    _require_gpu(prepared_weights, u)
+    u = u.to(torch.float64).contiguous()
+    if xv is not None:
+        xv = xv.to(torch.float64).contiguous()
+        if u.shape != xv.shape:
+            raise ValueError('u and x need the same shape')
+    y = torch.full_like(u, float('nan'))
+    hit = torch.zeros(u.shape, dtype=torch.int32, device=u.device)
+    _lib.call('gnnd_v24_var_mlp_table', _ptr(prepared_weights), _ptr(u),
+              _ptr(xv) if xv is not None else None, _ptr(y), _ptr(hit), u.numel(),
+              current_stream(u.device))
+    return y, hit.bool()
 
 
 def decode_out_rows(graph, model, B, iters=1):
@@ -222,7 +259,9 @@ def decode(graph: TannerGraph, model, x, iters, prepared_weights=None, out=None)
     B = x.numel() // graph.N
     wdt = torch.float32 if x.dtype == torch.bfloat16 else x.dtype   # bf16 storage, fp32 math
     nw = prepared_count(model, wdt, graph, iters)
-    if nw and (prepared_weights is None or prepared_weights.numel() != nw):
+    # (fp64 decoder_v2_4 prepared with channel-prior tables: more)
+    if nw and (prepared_weights is None or prepared_weights.numel() < nw or
+               (prepared_weights.numel() != nw and not (model == 'v24' and wdt == torch.float64))):
         raise ValueError(f'{model}: needs {nw} prepared weights (prepare_weights)')
     if prepared_weights is not None and prepared_weights.dtype != wdt:
         raise TypeError(f'{x.dtype} inputs need {wdt} prepared weights')

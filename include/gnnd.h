@@ -196,15 +196,40 @@ int gnnd_weights_count(int model, int64_t* h_count);
 int gnnd_decode_weights_count(const gnnd_graph* g, int model, int32_t iters, int64_t* h_count);
 int gnnd_prepare_weights(int model, int dtype, const void* d_w, void* d_prepared,
                          void* stream);
-/* Elements of gnnd_prepare_weights' output: gnnd_weights_count, except V24 (7 252): the 1 283
+/* Elements of gnnd_prepare_weights' output: gnnd_weights_count, except V24 (7 264): the 1 283
  * weights (fp32: base-2 rescaled), then the check-MLP table (gnnd_v24_check_mlp_table) the
- * decoder and training forward read, and fp32 CGNNI / QGNNI (328): the plain 62, then their message
+ * decoder and training forward read, then an 12-element channel-prior header (0 tables; see
+ * gnnd_prepare_weights_priors), and fp32 CGNNI / QGNNI (328): the plain 62, then their message
  * MLP as a piecewise-linear table (<= 32 cells of <= 2 knots) the register-resident decoder
  * reads.  gnnd_decode needs this prepared buffer, not the plain weights (so does
  * gnnd_train_fwd for V24).                                                                  */
 int gnnd_prepared_weights_count(int model, int dtype, int64_t* h_count);
 int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, const void* d_x,
                 void* d_out, int64_t batch, int32_t iters, void* stream);
+
+/* Channel-prior tables (fp64 decoder_v2_4).  The variable-side MLP ggc1.mlp (Linear(2,128) ->
+ * Softplus -> Linear(128,1), quantum/decoder_v2_4.py:237-239, :253-255) takes (S_v - m_e, x_v);
+ * the reference's inputs carry one prior LLR x_v = log((1-p)/p) per codeword, p drawn from a
+ * short list (quantum/error_generate.py:252-260).  gnnd_prepare_weights_priors = gnnd_prepare_weights
+ * plus, for each of the n_priors values h_priors[] (host fp64, <= 64; the exact x_v bits the
+ * inputs will carry), the MLP tabulated over |S_v - m_e| <= 32 (degree-11 Taylor cells of width
+ * 1/8; units crossing torch's Softplus threshold inside a cell are evaluated exactly; <= 1e-13
+ * absolute vs the MLP), into a buffer of gnnd_prepared_weights_count_priors elements.  gnnd_decode
+ * (fp64 V24, batches decoded one wave per item group) then reads a codeword's table where its
+ * x_v equals a registered prior bit for bit and evaluates the 128 units elsewhere (other priors,
+ * |S_v - m_e| > 32), and the readout MLP from one more table (n_priors > 0).  The tables
+ * depend on the weights: gnnd_train_update and
+ * gnnd_prepare_weights reset the count to 0.  Other models/dtypes: n_priors must be 0.        */
+int gnnd_prepared_weights_count_priors(int model, int dtype, int32_t n_priors, int64_t* h_count);
+int gnnd_prepare_weights_priors(int model, int dtype, const void* d_w, void* d_prepared,
+                                const double* h_priors, int32_t n_priors, void* stream);
+/* The tables as the decoder evaluates them, for tests: d_y[i] = ggc1.mlp(d_u[i], d_x[i]) and
+ * d_hit[i] = 1 where a table covers the point, else d_hit[i] = 0 and d_y[i] untouched
+ * (d_w = prepared fp64 V24 weights with tables; device fp64 d_u, d_x, d_y [n], int32 d_hit).
+ * The prepared tables end with one for the readout MLP (mlp, quantum/decoder_v2_4.py:291, over
+ * |m| <= 32, no prior): d_x = NULL evaluates that one, d_y[i] = mlp(d_u[i]).                 */
+int gnnd_v24_var_mlp_table(const void* d_w, const void* d_u, const void* d_x, void* d_y,
+                           int32_t* d_hit, int64_t n, void* stream);
 
 /* decoder_v2_4's check-side MLP (ggc2.mlp: Linear(1,128) -> Softplus -> Linear(128,1),
  * quantum/decoder_v2_4.py:241-243, :253-257) as the fp64 decoder evaluates it: its input

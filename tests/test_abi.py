@@ -78,6 +78,30 @@ def test_weights_count_and_width():
     assert w(9, 0) == -1 and w(0, 5) == -1
 
 
+def test_prepared_counts_with_channel_prior_tables():
+    """gnnd_prepared_weights_count[_priors] (host-only): decoder_v2_4 = 1 283 weights + check-MLP
+    table + prior header = 7 264; fp64 V24 adds 12 848 per channel-prior table (<= 64) and one for
+    the readout MLP; other
+    models / fp32 take no tables."""
+    lib = _lib.get()
+    n = ctypes.c_int64()
+    v24, f32, f64 = _lib.VARIANT['v24'], 0, 1
+    for dt in (f32, f64):
+        assert lib.gnnd_prepared_weights_count(v24, dt, ctypes.byref(n)) == _lib.OK and n.value == 7264
+        assert lib.gnnd_prepared_weights_count_priors(v24, dt, 0, ctypes.byref(n)) == _lib.OK and n.value == 7264
+    assert lib.gnnd_prepared_weights_count_priors(v24, f64, 10, ctypes.byref(n)) == _lib.OK
+    assert n.value == 7264 + 11 * 12848              # (+ the readout MLP's table)
+    assert lib.gnnd_prepared_weights_count_priors(v24, f64, 65, ctypes.byref(n)) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_prepared_weights_count_priors(v24, f64, -1, ctypes.byref(n)) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_prepared_weights_count_priors(v24, f32, 1, ctypes.byref(n)) == _lib.ERR_UNSUPPORTED
+    assert lib.gnnd_prepared_weights_count_priors(_lib.VARIANT['cgnni'], f32, 1, ctypes.byref(n)) == _lib.ERR_UNSUPPORTED
+    # argument checks before any device call
+    assert lib.gnnd_prepare_weights_priors(v24, f64, None, None, None, 3, None) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_prepare_weights_priors(v24, f64, None, None, None, 65, None) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_v24_var_mlp_table(None, None, None, None, None, 4, None) == _lib.ERR_INVALID_ARG
+    assert lib.gnnd_v24_var_mlp_table(ctypes.c_void_p(8), None, None, None, None, 4, None) == _lib.ERR_INVALID_ARG
+
+
 def _graph_create(v, c, V, C):
     lib = _lib.get()
     v = np.ascontiguousarray(v, np.int64)

@@ -105,17 +105,19 @@ def test_large_weights_fail_the_remainder_bound():
 
 
 def test_prepared_layout_and_trainer_rebuild():
-    """gnnd_prepare_weights (fp64 V24) = [plain weights | bound, R limit, pad | table]; the
+    """gnnd_prepare_weights (fp64 V24) = [plain weights | bound, R limit, pad | table | prior
+    header (0 tables)]; the
     fused trainer's epilogue (gnnd_train_update) rebuilds the table of the updated weights, so
     its prepared buffer equals a fresh gnnd_prepare_weights of its parameters after each step."""
     import gnndecode as gd
     m, H = _model(L=5)
     flat = m.packed_weights().double().detach().contiguous()
     prep = gd.ops.prepare_weights('v24', flat)
-    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64) == 7252
+    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64) == 7264
     assert torch.equal(prep[:1283], flat)
     assert 0 < float(prep[1283]) < 1e-13 and float(prep[1284]) > 3
-    assert gd.ops.prepared_count('v24', torch.float32) == 7252          # (fp32: the same table in fp32)
+    assert gd.ops.prepared_count('v24', torch.float32) == 7264          # (fp32: the same table in fp32)
+    assert float(prep[7252:7264].abs().sum()) == 0.0                    # (no channel-prior tables)
     lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
     tr = gd.train.FusedV24Trainer(m, lf, graph=False)
     x, y = gd.data.toric_batch(H, 32, seed=2, device=torch.device(DEV), dtype=torch.float64)

@@ -1,0 +1,194 @@
+"""decoder_v2_4 fp64: the variable-side MLP through channel-prior tables
+(gnnd_prepare_weights_priors / vtab_eval in gnnd_decode_impl.h, gnnd_v24_var_mlp_table).
+
+ggc1.mlp (Linear(2,128) -> Softplus -> Linear(128,1), quantum/decoder_v2_4.py:237-239,
+:253-255) takes (S_v - m_e, x_v); the reference's gen_syn inputs (quantum/error_generate.py:
+252-260) carry one prior LLR per codeword from a short p list, so the prepared weights can carry
+the MLP tabulated per prior.  Held here against torch's own fp64 module (Softplus threshold 20
+included: units cross it inside the table's range, and the cells evaluate the jump exactly) at
+1e-13 absolute, and the decoder with tables against the oracle (rtol 1e-10, bit-exact
+decisions) on batches mixing registered priors, other priors and per-variable priors.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import gnn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOL = 1e-13
+
+
+def _model(L=5, weights='shipped', seed=0):
+    import gnndecode as gd
+    H = gd.codes.toric_code(L)
+    torch.manual_seed(seed)
+    m = gd.MODELS['v24'](15, H)
+    if weights == 'shipped':
+        z = np.load(os.path.join(ROOT, 'gnn-decode_amd', 'gnndecode', 'weights', 'v24_toric_5.npz'))
+        m.load_state_dict({k: torch.from_numpy(z[k]) for k in z.files})
+    return m.to(DEV).double().eval(), H
+
+
+def _priors(H, B=512, seed=1):
+    import gnndecode as gd
+    x, _ = gd.data.toric_batch(H, B, seed=seed, device=torch.device(DEV), dtype=torch.float64)
+    g = gd.TannerGraph(H, device=torch.device(DEV))
+    return gd.ops.channel_priors(g, x)
+
+
+def _torch_mlp(m, u, xv):
+    with torch.no_grad():
+        return m.ggc1.mlp(torch.stack([u, xv], dim=1)).view(-1)
+
+
+def _crossings(m, xv):
+    """u where some unit's pre-activation W1a u + W1b x + b1 equals 20 (torch's threshold)."""
+    W = m.ggc1.mlp[0].weight.detach().cpu().numpy()
+    b = m.ggc1.mlp[0].bias.detach().cpu().numpy()
+    with np.errstate(divide='ignore'):
+        return (20.0 - (W[:, 1] * xv + b)) / W[:, 0]
+
+
+@pytest.mark.parametrize('weights', ['shipped', 'random'])
+def test_prior_tables_match_reference_mlp(weights):
+    import gnndecode as gd
+    m, H = _model(weights=weights)
+    pri = _priors(H)
+    assert len(pri) == 10
+    prep = gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous(), priors=pri)
+    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64, priors=10) == 7264 + 11 * 12848
+    assert int(prep[7252]) == 10 and float(prep[7253]) == 1.0
+    g = torch.Generator(device='cpu').manual_seed(2)
+    for xv in pri:
+        u = torch.cat([torch.linspace(-32, 32, 16001, dtype=torch.float64),
+                       (torch.rand(4000, generator=g, dtype=torch.float64) * 2 - 1) * 32])
+        cr = _crossings(m, xv)
+        cr = cr[np.isfinite(cr) & (np.abs(cr) < 32)]
+        # both sides of every threshold crossing inside the range, 1e-7 away
+        u = torch.cat([u, torch.from_numpy(np.concatenate([cr - 1e-7, cr + 1e-7]))])
+        # (points within 1e-9 of a crossing: the reference's own rounding of h decides the side)
+        un = u.numpy()
+        far = np.ones(un.shape, bool) if cr.size == 0 else \
+            (np.abs(un[:, None] - cr[None, :]) > 1e-9 * (1 + np.abs(un[:, None]))).all(1)
+        u = u[torch.from_numpy(far)].to(DEV)
+        xt = torch.full_like(u, xv)
+        y, hit = gd.ops.v24_var_mlp_table(prep, u, xt)
+        ref = _torch_mlp(m, u, xt)
+        if weights == 'shipped':
+            assert bool(hit.all()), int((~hit).sum())      # every cell valid (0-3 crossings)
+        assert float(hit.float().mean()) > 0.9
+        err = float((y[hit] - ref[hit]).abs().max())
+        assert err <= TOL, (xv, err)
+
+
+def test_readout_table_matches_reference_mlp():
+    """The readout MLP (mlp, quantum/decoder_v2_4.py:291) table after the prior tables:
+    |m| <= 32, torch's threshold crossings evaluated exactly, 1e-13 (relative to 1 + |mlp(m)|)."""
+    import gnndecode as gd
+    m, H = _model()
+    prep = gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous(), priors=_priors(H))
+    W = m.mlp[0].weight.detach().cpu().numpy()[:, 0]
+    b = m.mlp[0].bias.detach().cpu().numpy()
+    with np.errstate(divide='ignore'):
+        cr = (20.0 - b) / W
+    cr = cr[np.isfinite(cr) & (np.abs(cr) < 32)]
+    u = np.concatenate([np.linspace(-32, 32, 16001), cr - 1e-7, cr + 1e-7])
+    if cr.size:
+        u = u[(np.abs(u[:, None] - cr[None, :]) > 1e-9 * (1 + np.abs(u[:, None]))).all(1)]
+    u = torch.from_numpy(u).to(DEV)
+    y, hit = gd.ops.v24_var_mlp_table(prep, u)
+    assert bool(hit.all())
+    with torch.no_grad():
+        ref = m.mlp(u.view(-1, 1)).view(-1)
+    # (|mlp(m)| reaches ~700 here: torch's own 128-term fp64 sum rounds at ~1e-15 relative)
+    err = float(((y - ref).abs() / (1 + ref.abs())).max())
+    assert err <= TOL, err
+    _, hit = gd.ops.v24_var_mlp_table(prep, torch.tensor([40.0, -33.0], dtype=torch.float64, device=DEV))
+    assert not bool(hit.any())
+
+
+def test_prior_table_misses_fall_back():
+    """Points outside |u| <= 32 + 1/16 or with an unregistered prior are not covered."""
+    import gnndecode as gd
+    m, H = _model()
+    pri = _priors(H)
+    prep = gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous(), priors=pri[:3])
+    u = torch.tensor([0.0, 32.0, -32.06, 32.07, -40.0, 1e300, float('nan'), 1.5], dtype=torch.float64,
+                     device=DEV)
+    xv = torch.full_like(u, pri[0])
+    xv[-1] = pri[5]                                        # not registered
+    _, hit = gd.ops.v24_var_mlp_table(prep, u, xv)
+    assert hit.tolist() == [True, True, True, False, False, False, False, False]
+    # without tables nothing is covered
+    p0 = gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous())
+    _, hit = gd.ops.v24_var_mlp_table(p0, u, xv)
+    assert not bool(hit.any())
+
+
+def _oracle(m, H, x):
+    w = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    return O.decode('v24', H, x.cpu().numpy(), m.Nc, w)
+
+
+def test_decode_with_prior_tables_matches_oracle():
+    """B = 2048 (one wave per item group, the tables' plan): registered priors, codewords with
+    an unregistered prior, and codewords whose x_v vary per variable (those lanes evaluate the
+    units) -- all equal to the oracle at rtol 1e-10 with the same hard decisions; the tables are
+    really read (the outputs differ from the unit decode in the last bits) and the decode is
+    bitwise reproducible."""
+    import gnndecode as gd
+    m, H = _model()
+    B = 2048
+    x, _ = gd.data.toric_batch(H, B, seed=5, device=torch.device(DEV), dtype=torch.float64)
+    g = m.graph(x.device)
+    pri = gd.ops.channel_priors(g, x)
+    N, V = g.N, g.V
+    xv = x.view(B, N)
+    xv[1::7, :V] *= 1.0 + 1e-3                            # a prior no table has
+    gen = torch.Generator(device='cpu').manual_seed(6)
+    xv[2::11, :V] = (torch.rand(len(range(2, B, 11)), V, generator=gen, dtype=torch.float64) * 4 + 1).to(DEV)
+    flat = m.packed_weights().double().detach().contiguous()
+    p_tab = gd.ops.prepare_weights('v24', flat, priors=pri)
+    p_unit = gd.ops.prepare_weights('v24', flat)
+    out = gd.ops.decode(g, 'v24', x, m.Nc, p_tab)
+    out2 = gd.ops.decode(g, 'v24', x, m.Nc, p_tab)
+    ref_u = gd.ops.decode(g, 'v24', x, m.Nc, p_unit)
+    assert torch.equal(out, out2)
+    assert not torch.equal(out, ref_u)
+    # (the unit path's own Softplus table is within ~1e-11 of the oracle: DESIGN §2)
+    assert float((out - ref_u).abs().max()) < 1e-10
+    ref = _oracle(m, H, x)
+    got = out.cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-12)
+    assert ((got > 0.5) == (ref > 0.5)).all()
+
+
+def test_model_forward_uses_registered_priors_and_updates_reset_them():
+    """GNNI-style forward with set_channel_priors == ops.decode with the tables, bit for bit;
+    a fused training step's prepared weights carry no tables (gnnd_train_update resets the
+    count: the tables belong to the old weights)."""
+    import gnndecode as gd
+    m, H = _model()
+    x, y = gd.data.toric_batch(H, 1024, seed=7, device=torch.device(DEV), dtype=torch.float64)
+    g = m.graph(x.device)
+    pri = gd.ops.channel_priors(g, x)
+    m.set_channel_priors(pri)
+    with torch.no_grad():
+        out = m(gd.data.make_batch(x, g))
+    ref = gd.ops.decode(g, 'v24', x, m.Nc,
+                        gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous(),
+                                               priors=pri))
+    assert torch.equal(out, ref)
+    m.set_channel_priors(())
+    lf = gd.loss.SyndromeLoss(H, gd.codes.toric_logicals(H)).to(DEV)
+    tr = gd.train.FusedV24Trainer(m, lf, graph=False)
+    tr.prepared = gd.ops.prepare_weights('v24', tr.flat, priors=pri)[:tr.prepared.numel()].clone()
+    tr.step(gd.data.make_batch(x[:32 * g.N], g), y[:32 * g.V])
+    torch.cuda.synchronize()
+    assert float(tr.prepared[7252]) == 0.0
