@@ -630,7 +630,8 @@ __device__ __forceinline__ float ctab_eval(const float* tab, float u, int R8) {
 // the ten priors of the reference's p list: 0-3 crossings per cell, bound 3.5e-18.
 // Table t at kV24PriorOff + t kVtStride: [0] = the prior x (key), pad to kVtHdr, then kVtCells
 // cells of kVtCell doubles (one 128-byte line each: a lookup reads one line): a_0 .. a_11, [12] =
-// crossing count (-1: invalid), pad; then per cell kVtNX crossing units {W1a, b1', -W2 e^-20}.
+// crossing count (-1: invalid), [13..15] the first crossing unit {W1a, b1', -W2 e^-20}; then per
+// cell the other kVtNX - 1 crossing units.
 // ---------------------------------------------------------------------------------------
 constexpr int kVtInv = 8;
 constexpr int kVtR = 32;                                  // centres |c_j| <= 32
@@ -638,8 +639,8 @@ constexpr int kVtCells = 2 * kVtInv * kVtR + 1;           // 513
 constexpr int kVtNX = 3;                                  // crossing units per cell
 constexpr int kVtCell = 16;                               // doubles per cell (128 B)
 constexpr int kVtHdr = 16;
-constexpr int kVtXOff = kVtHdr + kVtCells * kVtCell;      // the crossing units [kVtCells][kVtNX][3]
-constexpr int kVtStride = (kVtXOff + kVtCells * kVtNX * 3 + 15) & ~15;   // 12 848 doubles per table
+constexpr int kVtXOff = kVtHdr + kVtCells * kVtCell;      // crossing units 2.. [kVtCells][kVtNX - 1][3]
+constexpr int kVtStride = (kVtXOff + kVtCells * (kVtNX - 1) * 3 + 15) & ~15;   // 11 312 doubles per table
 constexpr int kVtMaxPriors = 64;
 struct VtPriors {
     double x[kVtMaxPriors];
@@ -698,26 +699,28 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
     __syncthreads();
     double* tbl = prep + kV24PriorOff + (size_t)t * kVtStride;
     double* cell = tbl + kVtHdr + (size_t)j * kVtCell;
-    double* xu = tbl + kVtXOff + (size_t)j * kVtNX * 3;   // the cell's crossing units
+    double* xu2 = tbl + kVtXOff + (size_t)j * (kVtNX - 1) * 3;   // the cell's crossing units 2..
+    auto xslot = [&](int i) { return i == 0 ? cell + 13 : xu2 + 3 * (i - 1); };
     const int ntot = ncross0 + (k >= 64 ? __builtin_popcountll(cm) : 0);   // (valid in wave 1)
     // the crossing units in unit order: rank = crossings below k
     const int below = __builtin_popcountll(cm & ((1ull << (k & 63)) - 1ull)) + (k >= 64 ? ncross0 : 0);
     if (cross && below < kVtNX) {
-        xu[3 * below] = W1a;
-        xu[3 * below + 1] = bp;
-        xu[3 * below + 2] = -W2 * exp(-20.0);
+        double* xs = xslot(below);
+        xs[0] = W1a;
+        xs[1] = bp;
+        xs[2] = -W2 * exp(-20.0);
     }
     if (k == 64) {                                        // wave 1 knows the total
         const bool ok = !bad && ntot <= kVtNX && (s12 + part[kCtabNC]) * kCtabBoundCoef <= 1e-13;
         cell[12] = ok ? (double)ntot : -1.0;
-        for (int i = 13; i < kVtCell; ++i) cell[i] = 0.0;
         for (int i = ntot < kVtNX ? ntot : kVtNX; i < kVtNX; ++i) {
-            xu[3 * i] = 0.0;
-            xu[3 * i + 1] = 0.0;
-            xu[3 * i + 2] = 0.0;
+            double* xs = xslot(i);
+            xs[0] = 0.0;
+            xs[1] = 0.0;
+            xs[2] = 0.0;
         }
         if (j == 0)                                       // (defined padding after the units)
-            for (int i = kVtXOff + kVtCells * kVtNX * 3; i < kVtStride; ++i) tbl[i] = 0.0;
+            for (int i = kVtXOff + kVtCells * (kVtNX - 1) * 3; i < kVtStride; ++i) tbl[i] = 0.0;
     }
     if (k == 0) {
 #pragma unroll
@@ -744,37 +747,60 @@ __device__ __forceinline__ double vtab_expm(double t) {
     p = fma(p, -t, 1.0);
     return fma(p, -t, 1.0);
 }
-// ggc1.mlp(u, x) from prior table tb (global memory, L2-resident): false (y untouched) when x is
-// not the table's prior (KEY), |u| is outside the table or the cell is invalid
+// ggc1.mlp(u, x) from prior table tb (global memory, L2-resident), in two steps so the decoder can
+// issue a lookup's line read one item round ahead (GNND_VT_PREFETCH): vtab_load reads the cell's
+// 128-byte line (ok = false when x is not the table's prior (KEY) or |u| is outside the table),
+// vtab_finish evaluates it (false, y untouched, for an invalid cell)
+struct VtLine {
+    double a[kVtCell];
+    int jc;
+    bool ok;
+};
 template <bool KEY = true>
-__device__ __forceinline__ bool vtab_eval(const double* __restrict__ tb, double u, double x, double& y) {
-    if (KEY && __double_as_longlong(x) != __double_as_longlong(tb[0])) return false;
-    if (!(fabs(u) <= kVtR + 0.0625)) return false;
+__device__ __forceinline__ void vtab_load(const double* __restrict__ tb, double u, double x, VtLine& L) {
+    L.ok = (!KEY || __double_as_longlong(x) == __double_as_longlong(tb[0])) && fabs(u) <= kVtR + 0.0625;
     int k = round_magic_lo(__builtin_fma(u, (double)kVtInv, kRoundMagic));
     k = k < -kVtInv * kVtR ? -kVtInv * kVtR : (k > kVtInv * kVtR ? kVtInv * kVtR : k);
-    const int jc = k + kVtInv * kVtR;
-    const double* e = tb + kVtHdr + (size_t)jc * kVtCell;
-    double a[kCtabNC + 2];
+    L.jc = k + kVtInv * kVtR;
+    if (L.ok) {
+        const double2* e = (const double2*)(tb + kVtHdr + (size_t)L.jc * kVtCell);
 #pragma unroll
-    for (int i = 0; i < kCtabNC / 2 + 1; ++i) {
-        const double2 v = ((const double2*)e)[i];
-        a[2 * i] = v.x;
-        a[2 * i + 1] = v.y;
+        for (int i = 0; i < kVtCell / 2; ++i) {
+            const double2 v = e[i];
+            L.a[2 * i] = v.x;
+            L.a[2 * i + 1] = v.y;
+        }
     }
+}
+__device__ __forceinline__ bool vtab_finish(const double* __restrict__ tb, double u, const VtLine& L, double& y) {
+    const double* a = L.a;
     const int nx = (int)a[kCtabNC];
-    if (nx < 0) return false;
-    const double r = __builtin_fma((double)k, -1.0 / kVtInv, u);
+    if (!L.ok || nx < 0) return false;
+    const double r = __builtin_fma((double)(L.jc - kVtInv * kVtR), -1.0 / kVtInv, u);
     double p = a[kCtabNC - 1];
 #pragma unroll
     for (int n = kCtabNC - 2; n >= 0; --n) p = fma(p, r, a[n]);
-    const double* xu = tb + kVtXOff + (size_t)jc * kVtNX * 3;
-    for (int i = 0; i < nx; ++i) {                        // (rare: ~10 % of the cells)
-        const double h = fma(u, xu[3 * i], xu[3 * i + 1]);
-        if (h > 20.0) p = fma(xu[3 * i + 2], vtab_expm(h - 20.0), p);
+    if (nx > 0) {                                         // (~10 % of the cells: one unit in the line)
+        const double h = fma(u, a[13], a[14]);
+        if (h > 20.0) p = fma(a[15], vtab_expm(h - 20.0), p);
+    }
+    const double* xu = tb + kVtXOff + (size_t)L.jc * (kVtNX - 1) * 3;
+    for (int i = 1; i < nx; ++i) {                        // (~1.5 %: a second line)
+        const double h = fma(u, xu[3 * i - 3], xu[3 * i - 2]);
+        if (h > 20.0) p = fma(xu[3 * i - 1], vtab_expm(h - 20.0), p);
     }
     y = p;
     return true;
 }
+template <bool KEY = true>
+__device__ __forceinline__ bool vtab_eval(const double* __restrict__ tb, double u, double x, double& y) {
+    VtLine L;
+    vtab_load<KEY>(tb, u, x, L);
+    return vtab_finish(tb, u, L, y);
+}
+#ifndef GNND_VT_PREFETCH
+#define GNND_VT_PREFETCH 1
+#endif
 
 // fp32 forms: TWO EDGES per call, riding the two halves of packed FMAs (the lane's
 // slots are processed in pairs).  Prepared layout (gnnd_prepare_weights; base-2 rescaled:
@@ -1983,6 +2009,11 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // read of its previous contents)
     int pbuf = 0;
     for (int it = 0; it < iters; ++it) {
+        // fp64 V24 channel-prior tables, one-slot plans: the next item round's table line, read
+        // while this round computes (its S_v and message are final once the variable sums ran)
+        constexpr bool kVtPf = kV24F64 && R == 1 && US == 1 && !TAPE && GNND_VT_PREFETCH;
+        VtLine vnext;
+        bool vnext_set = false;
         for (int f0 = 0; f0 < nItem; f0 += IL) {
             const int f = f0 + itid;
             const bool act = f < nItem;
@@ -2076,14 +2107,45 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     xs[r] = p.x;
                 }
                 const int vto = n_pt > 0 ? s_vto[b] : -1;
+                VtLine vcur;
+                if constexpr (kVtPf) {
+                    if (n_pt > 0) {
+                        if (vnext_set) {
+                            vcur = vnext;
+                        } else {
+                            vcur.ok = false;
+                            if (act && val[0] && vto >= 0) vtab_load((const double*)wv + vto, ext[0], xs[0], vcur);
+                        }
+                        vnext_set = false;
+                        if (f0 + IL < nItem) {                // (uniform) the next round's item
+                            const int fn = f + IL;
+                            const bool actn = fn < nItem;
+                            const int fcn = actn ? fn : nItem - 1;
+                            const int bn = fdiv(fcn, dItem), remn = fcn - bn * IC;
+                            const uint32_t svn = s_slot[remn];
+                            const int vton = s_vto[bn];
+                            vnext.ok = false;
+                            if (actn && (int)(svn >> 16) != E && vton >= 0) {
+                                const SumX<T> pn = s_sx[bn * V + (int)(svn & 0xffffu)];
+                                vtab_load((const double*)wv + vton, pn.s - s_m[bn * nslot + remn], pn.x, vnext);
+                            }
+                            vnext_set = true;
+                        }
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     T a = T(0);
                     // the channel-prior table where this lane's (u, x_v) has one; the wave
                     // evaluates the 128 units when any live lane has none (those lanes keep them)
                     bool need = n_pt == 0 || (act && val[r]);
-                    if (n_pt > 0 && need && vto >= 0 && vtab_eval((const double*)wv + vto, ext[r], xs[r], a))
-                        need = false;
+                    if constexpr (kVtPf) {
+                        if (n_pt > 0 && need && vto >= 0 && vtab_finish((const double*)wv + vto, ext[r], vcur, a))
+                            need = false;
+                    } else {
+                        if (n_pt > 0 && need && vto >= 0 && vtab_eval((const double*)wv + vto, ext[r], xs[r], a))
+                            need = false;
+                    }
                     if (n_pt == 0 || __builtin_amdgcn_ballot_w64(need) != 0) {
                         const T a2 = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
                                                              s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid, widle,

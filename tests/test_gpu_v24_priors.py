@@ -62,7 +62,7 @@ def test_prior_tables_match_reference_mlp(weights):
     pri = _priors(H)
     assert len(pri) == 10
     prep = gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous(), priors=pri)
-    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64, priors=10) == 7264 + 11 * 12848
+    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64, priors=10) == 7264 + 11 * 11312
     assert int(prep[7252]) == 10 and float(prep[7253]) == 1.0
     g = torch.Generator(device='cpu').manual_seed(2)
     for xv in pri:
