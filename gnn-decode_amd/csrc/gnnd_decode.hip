@@ -107,7 +107,7 @@ extern "C" int gnnd_prepared_weights_count_priors(int model, int dtype, int32_t 
     if (!h_count || n_priors < 0 || n_priors > kVtMaxPriors || weights_count(model) == -1)
         return GNND_ERR_INVALID_ARG;
     if (model != GNND_V24 || dtype != GNND_F64) return GNND_ERR_UNSUPPORTED;
-    *h_count = kV24PriorOff + (int64_t)(n_priors + 1) * kVtStride;   // (+ the readout MLP's table)
+    *h_count = kV24PriorOff + (int64_t)n_priors * kVtStride + kVtStrideR;   // (+ the readout MLP's table)
     return GNND_OK;
 }
 
@@ -121,11 +121,11 @@ extern "C" int gnnd_prepare_weights_priors(int model, int dtype, const void* d_w
     // the table build then writes the count)
     VtPriors pr{};
     for (int i = 0; i < n_priors; ++i) pr.x[i] = h_priors[i];
-    vtab_build_kernel<0><<<dim3(kVtCells, n_priors), 128, 0, (hipStream_t)stream>>>(
+    vtab_build_kernel<0><<<dim3(vt_cells(kVtInvG), n_priors), 128, 0, (hipStream_t)stream>>>(
         (const double*)d_w, (double*)d_prepared, pr, n_priors, 0);
     GNND_LAUNCH_CHECK();
-    // the readout MLP's table after them (same form, no prior)
-    vtab_build_kernel<1><<<dim3(kVtCells, 1), 128, 0, (hipStream_t)stream>>>(
+    // the readout MLP's table after them (same form, no prior, finer cells)
+    vtab_build_kernel<1><<<dim3(vt_cells(kVtInvR), 1), 128, 0, (hipStream_t)stream>>>(
         (const double*)d_w, (double*)d_prepared, pr, n_priors, n_priors);
     GNND_LAUNCH_CHECK();
     return GNND_OK;

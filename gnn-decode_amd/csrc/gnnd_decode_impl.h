@@ -616,53 +616,56 @@ __device__ __forceinline__ float ctab_eval(const float* tab, float u, int R8) {
 // S_v - m_e; the reference's inputs carry ONE prior per codeword, x_v = log((1 - p) / p) with p
 // from a short list (quantum/error_generate.py:252-260 gen_syn), so for a fixed x it is a
 // one-input MLP with biases b1' = W1b x + b1.  gnnd_prepare_weights_priors tabulates it per
-// prior value over |u| <= kVtR as degree-11 Taylor polynomials about c_j = j / 8, one cell per
-// centre, like the check-side table -- except that u is not bounded by the graph, so units DO
-// cross torch's Softplus threshold 20 inside the range.  Each cell classifies the units over
-// its interval |u - c_j| <= 1/16: h > 20 throughout -> the unit is exactly linear (torch's
-// softplus(h) = h); h <= 20 throughout -> smooth; otherwise the unit crosses inside the cell:
-// the polynomial takes its smooth softplus and the cell lists it ({W1a, b1', -W2 e^-20}, at most
-// kVtNX per cell), the evaluation adding torch's jump -W2 log1p(e^-h) = -W2 e^-20 e^-(h - 20)
-// (1 + O(2e-9)) on the lanes whose h = fma(u, W1a, b1') -- the decoder's own pre-activation --
-// exceeds 20.  A cell with more crossings, a crossing unit with |W1a| > 8 (h - 20 beyond [0, 1]),
-// or a remainder bound above 1e-13 is marked invalid; its lanes, |u| > kVtR + 1/16, and inputs
-// whose x_v is not the table's prior (bit-exact key) evaluate the 128 units.  Epoch-67 weights,
-// the ten priors of the reference's p list: 0-3 crossings per cell, bound 3.5e-18.
-// Table t at kV24PriorOff + t kVtStride: [0] = the prior x (key), pad to kVtHdr, then kVtCells
-// cells of kVtCell doubles (one 128-byte line each: a lookup reads one line): a_0 .. a_11, [12] =
-// crossing count (-1: invalid), [13..15] the first crossing unit {W1a, b1', -W2 e^-20}; then per
-// cell the other kVtNX - 1 crossing units.
+// prior value over |u| <= kVtR as degree-7 Taylor polynomials about c_j = j / INV (INV = 16),
+// one cell per centre -- like the check-side table, except that u is not bounded by the graph,
+// so units DO cross torch's Softplus threshold 20 inside the range.  Each cell classifies the
+// units over its interval |u - c_j| <= 1/(2 INV): h > 20 throughout -> the unit is exactly
+// linear (torch's softplus(h) = h); h <= 20 throughout -> smooth; otherwise it crosses inside
+// the cell: the polynomial takes its smooth softplus and the cell lists the unit ({W1a, b1',
+// -W2 e^-20}, at most kVtNX), the evaluation adding torch's jump -W2 log1p(e^-h) = -W2 e^-20
+// e^-(h - 20) (1 + O(2e-9)) on the lanes whose h = fma(u, W1a, b1') -- the decoder's own
+// pre-activation -- exceeds 20.  Remainder <= (1/(2 INV))^8 / 8! * max|sigma^(7)| (= 17/16) *
+// sum_k |W2_k| |W1a_k|^8: 5.6e-15 for the epoch-67 weights.  A cell with more crossings, a
+// crossing unit with |W1a| > 4 INV (h - 20 beyond [0, 1]) or a bound above 1e-13 is invalid;
+// its lanes, |u| > kVtR + 1/(2 INV), and inputs whose x_v is not the table's prior (bit-exact
+// key) evaluate the 128 units.  The readout MLP (mlp, :291, on every message m_e; SEL = 1) gets
+// one such table too, with INV = 32 (its |W1| reaches 4.2: bound 5.3e-15), no prior.
+// A table: [0] = the prior x (key), pad to kVtHdr; cells [kVtCells(INV)][8] = a_0 .. a_7, the three
+// lowest mantissa bits of a_7 holding the cell's code (0-3 crossing units, 7 invalid: a_7 r^7 <=
+// a_7 / 2^35 changes by < 1e-25); then [kVtCells(INV)][kVtNX][3] the crossing units.  A lookup
+// reads one 64-byte cell (4 dwordx4), a crossing cell one more line.
 // ---------------------------------------------------------------------------------------
-constexpr int kVtInv = 8;
 constexpr int kVtR = 32;                                  // centres |c_j| <= 32
-constexpr int kVtCells = 2 * kVtInv * kVtR + 1;           // 513
+constexpr int kVtNC = 8;                                  // coefficients a_0 .. a_7 per cell
 constexpr int kVtNX = 3;                                  // crossing units per cell
-constexpr int kVtCell = 16;                               // doubles per cell (128 B)
 constexpr int kVtHdr = 16;
-constexpr int kVtXOff = kVtHdr + kVtCells * kVtCell;      // crossing units 2.. [kVtCells][kVtNX - 1][3]
-constexpr int kVtStride = (kVtXOff + kVtCells * (kVtNX - 1) * 3 + 15) & ~15;   // 11 312 doubles per table
+constexpr int kVtInvG = 16, kVtInvR = 32;                 // cells per unit of u: ggc1, readout
+__host__ __device__ constexpr int vt_cells(int inv) { return 2 * inv * kVtR + 1; }
+__host__ __device__ constexpr int vt_xoff(int inv) { return kVtHdr + vt_cells(inv) * kVtNC; }
+__host__ __device__ constexpr int vt_stride(int inv) { return (vt_xoff(inv) + vt_cells(inv) * kVtNX * 3 + 15) & ~15; }
+constexpr int kVtStride = vt_stride(kVtInvG);             // 17 456 doubles per prior table
+constexpr int kVtStrideR = vt_stride(kVtInvR);            // 34 864: the readout table
 constexpr int kVtMaxPriors = 64;
 struct VtPriors {
     double x[kVtMaxPriors];
 };
-// The readout MLP (mlp: Linear(1,128) -> Softplus -> Linear(128,1) on every message m_e,
-// quantum/decoder_v2_4.py:291) the same way, as one more table after the prior tables (SEL = 1:
-// no key, no prior; prep[kV24PriorHdr + 1] = 1 marks it).
 // block (j, t): cell j of table t0 + t, one unit per thread; w = the plain packed fp64 weights
-// (may alias prep)
+// (may alias prep).  SEL 0: ggc1 with prior pr.x[t]; SEL 1: the readout MLP (prep[kV24PriorHdr + 1]
+// = 1 marks it)
 template <int SEL>
 __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double* prep, VtPriors pr, int n,
                                                          int t0) {
+    constexpr int INV = SEL == 0 ? kVtInvG : kVtInvR;
     const double* wm = w + (SEL == 0 ? kV24Ggc1 : kV24Mlp);
-    const int k = threadIdx.x, j = blockIdx.x, t = t0 + blockIdx.y;
+    const int k = threadIdx.x, j = blockIdx.x;
     const double x = SEL == 0 ? pr.x[blockIdx.y] : 0.0;
     const double W1a = wm[k], W1b = SEL == 0 ? wm[128 + k] : 0.0, b1 = wm[(SEL == 0 ? 256 : 128) + k];
     const double W2 = wm[(SEL == 0 ? 384 : 256) + k], b2 = wm[SEL == 0 ? 512 : 384];
     // the decoder's pre-activation: ggc1 fma(u, W1a, fma(x, W1b, b1)), readout fma(m, W1, b1)
     const double bp = SEL == 0 ? fma(x, W1b, b1) : b1;
-    const double c = (double)(j - kVtInv * kVtR) * (1.0 / kVtInv);
+    const double c = (double)(j - INV * kVtR) * (1.0 / INV);
     const double h = fma(W1a, c, bp);
-    const double half = fabs(W1a) * (0.5 / kVtInv) + 1e-9 * (1.0 + fabs(h));
+    const double half = fabs(W1a) * (0.5 / INV) + 1e-9 * (1.0 + fabs(h));
     const bool lin = h - half > 20.0, cross = !lin && h + half > 20.0;
     double d[kCtabNC];
     if (lin) {
@@ -673,62 +676,63 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
     } else {
         softplus_taylor(h, d);
     }
-    __shared__ double part[kCtabNC + 1];
-    __shared__ int ncross0;
-    double a[kCtabNC];
+    __shared__ double part[kVtNC + 1];
+    __shared__ int ncross0, ncross1, bad;
+    double a[kVtNC];
     double p = W2;
 #pragma unroll
-    for (int i = 0; i < kCtabNC; ++i) {
+    for (int i = 0; i < kVtNC; ++i) {
         a[i] = group_sum_c<64>(p * d[i]);
         p *= W1a;
     }
     const double w2 = W1a * W1a, w4 = w2 * w2;
-    const double s12 = group_sum_c<64>(fabs(W2) * (w4 * w4 * w4));
+    const double s8 = group_sum_c<64>(fabs(W2) * (w4 * w4));
     const uint64_t cm = __builtin_amdgcn_ballot_w64(cross);
-    const bool wide_cross = __builtin_amdgcn_ballot_w64(cross && fabs(W1a) > 8.0) != 0;
-    __shared__ int bad;
+    const bool wide_cross = __builtin_amdgcn_ballot_w64(cross && fabs(W1a) > 4.0 * INV) != 0;
     if (k == 0) bad = 0;
     __syncthreads();
-    if (k == 64) {
+    if (k == 64) {                                        // wave 1's sums and crossing count
 #pragma unroll
-        for (int i = 0; i < kCtabNC; ++i) part[i] = a[i];
-        part[kCtabNC] = s12;
+        for (int i = 0; i < kVtNC; ++i) part[i] = a[i];
+        part[kVtNC] = s8;
+        ncross1 = __builtin_popcountll(cm);
     }
     if (k == 0) ncross0 = __builtin_popcountll(cm);
     if ((k & 63) == 0 && wide_cross) bad = 1;
     __syncthreads();
-    double* tbl = prep + kV24PriorOff + (size_t)t * kVtStride;
-    double* cell = tbl + kVtHdr + (size_t)j * kVtCell;
-    double* xu2 = tbl + kVtXOff + (size_t)j * (kVtNX - 1) * 3;   // the cell's crossing units 2..
-    auto xslot = [&](int i) { return i == 0 ? cell + 13 : xu2 + 3 * (i - 1); };
-    const int ntot = ncross0 + (k >= 64 ? __builtin_popcountll(cm) : 0);   // (valid in wave 1)
+
+    double* tbl = prep + kV24PriorOff + (size_t)(t0 + blockIdx.y) * kVtStride;
+    double* cell = tbl + kVtHdr + (size_t)j * kVtNC;
+    double* xu = tbl + vt_xoff(INV) + (size_t)j * kVtNX * 3;    // the cell's crossing units
     // the crossing units in unit order: rank = crossings below k
     const int below = __builtin_popcountll(cm & ((1ull << (k & 63)) - 1ull)) + (k >= 64 ? ncross0 : 0);
     if (cross && below < kVtNX) {
-        double* xs = xslot(below);
-        xs[0] = W1a;
-        xs[1] = bp;
-        xs[2] = -W2 * exp(-20.0);
+        xu[3 * below] = W1a;
+        xu[3 * below + 1] = bp;
+        xu[3 * below + 2] = -W2 * exp(-20.0);
     }
-    if (k == 64) {                                        // wave 1 knows the total
-        const bool ok = !bad && ntot <= kVtNX && (s12 + part[kCtabNC]) * kCtabBoundCoef <= 1e-13;
-        cell[12] = ok ? (double)ntot : -1.0;
+    // (1/(2 INV))^8 / 8! * 17/16
+    constexpr double kBound = 1.0625 / 40320.0 / ((2.0 * INV) * (2.0 * INV) * (2.0 * INV) * (2.0 * INV) *
+                                                  (2.0 * INV) * (2.0 * INV) * (2.0 * INV) * (2.0 * INV));
+    if (k == 0) {                                         // wave 0 + wave 1 (fixed order)
+        const int ntot = ncross0 + ncross1;
+        const bool ok = !bad && ntot <= kVtNX && (s8 + part[kVtNC]) * kBound <= 1e-13;
+        const long long code = ok ? ntot : 7;
         for (int i = ntot < kVtNX ? ntot : kVtNX; i < kVtNX; ++i) {
-            double* xs = xslot(i);
-            xs[0] = 0.0;
-            xs[1] = 0.0;
-            xs[2] = 0.0;
+            xu[3 * i] = 0.0;
+            xu[3 * i + 1] = 0.0;
+            xu[3 * i + 2] = 0.0;
         }
-        if (j == 0)                                       // (defined padding after the units)
-            for (int i = kVtXOff + kVtCells * (kVtNX - 1) * 3; i < kVtStride; ++i) tbl[i] = 0.0;
-    }
-    if (k == 0) {
+        double v[kVtNC];
 #pragma unroll
-        for (int i = 0; i < kCtabNC; ++i) cell[i] = (a[i] + part[i]) + (i == 0 ? b2 : 0.0);
+        for (int i = 0; i < kVtNC; ++i) v[i] = (a[i] + part[i]) + (i == 0 ? b2 : 0.0);
+        v[kVtNC - 1] = __longlong_as_double((__double_as_longlong(v[kVtNC - 1]) & ~7ll) | code);
+#pragma unroll
+        for (int i = 0; i < kVtNC; ++i) cell[i] = v[i];
         if (j == 0) {
-            double* hd = prep + kV24PriorOff + (size_t)t * kVtStride;
-            hd[0] = x;
-            for (int i = 1; i < kVtHdr; ++i) hd[i] = 0.0;
+            tbl[0] = x;
+            for (int i = 1; i < kVtHdr; ++i) tbl[i] = 0.0;
+            for (int i = vt_xoff(INV) + vt_cells(INV) * kVtNX * 3; i < vt_stride(INV); ++i) tbl[i] = 0.0;
             if (blockIdx.y == 0) prep[kV24PriorHdr + SEL] = SEL == 0 ? (double)n : 1.0;
         }
     }
@@ -747,60 +751,40 @@ __device__ __forceinline__ double vtab_expm(double t) {
     p = fma(p, -t, 1.0);
     return fma(p, -t, 1.0);
 }
-// ggc1.mlp(u, x) from prior table tb (global memory, L2-resident), in two steps so the decoder can
-// issue a lookup's line read one item round ahead (GNND_VT_PREFETCH): vtab_load reads the cell's
-// 128-byte line (ok = false when x is not the table's prior (KEY) or |u| is outside the table),
-// vtab_finish evaluates it (false, y untouched, for an invalid cell)
-struct VtLine {
-    double a[kVtCell];
-    int jc;
-    bool ok;
-};
-template <bool KEY = true>
-__device__ __forceinline__ void vtab_load(const double* __restrict__ tb, double u, double x, VtLine& L) {
-    L.ok = (!KEY || __double_as_longlong(x) == __double_as_longlong(tb[0])) && fabs(u) <= kVtR + 0.0625;
-    int k = round_magic_lo(__builtin_fma(u, (double)kVtInv, kRoundMagic));
-    k = k < -kVtInv * kVtR ? -kVtInv * kVtR : (k > kVtInv * kVtR ? kVtInv * kVtR : k);
-    L.jc = k + kVtInv * kVtR;
-    if (L.ok) {
-        const double2* e = (const double2*)(tb + kVtHdr + (size_t)L.jc * kVtCell);
+// ggc1.mlp(u, x) (INV = kVtInvG, KEY) or mlp(u) (kVtInvR, no key) from table tb (global memory,
+// L2-resident): false (y untouched) when x is not the table's prior, |u| is outside the table or
+// the cell is invalid
+template <int INV, bool KEY>
+__device__ __forceinline__ bool vtab_eval(const double* __restrict__ tb, double u, double x, double& y) {
+    if (KEY && __double_as_longlong(x) != __double_as_longlong(tb[0])) return false;
+    if (!(fabs(u) <= kVtR + 0.5 / INV)) return false;
+    int k = round_magic_lo(__builtin_fma(u, (double)INV, kRoundMagic));
+    k = k < -INV * kVtR ? -INV * kVtR : (k > INV * kVtR ? INV * kVtR : k);
+    const int jc = k + INV * kVtR;
+    const double2* e = (const double2*)(tb + kVtHdr + (size_t)jc * kVtNC);
+    double a[kVtNC];
 #pragma unroll
-        for (int i = 0; i < kVtCell / 2; ++i) {
-            const double2 v = e[i];
-            L.a[2 * i] = v.x;
-            L.a[2 * i + 1] = v.y;
+    for (int i = 0; i < kVtNC / 2; ++i) {
+        const double2 v = e[i];
+        a[2 * i] = v.x;
+        a[2 * i + 1] = v.y;
+    }
+    const int code = (int)(__double_as_longlong(a[kVtNC - 1]) & 7);
+    if (code > kVtNX) return false;
+    const double r = __builtin_fma((double)k, -1.0 / INV, u);
+    double p = a[kVtNC - 1];
+#pragma unroll
+    for (int n = kVtNC - 2; n >= 0; --n) p = fma(p, r, a[n]);
+    if (code > 0) {                                       // (a few % of the cells)
+        const double* xu = tb + vt_xoff(INV) + (size_t)jc * kVtNX * 3;
+        for (int i = 0; i < code; ++i) {
+            const double h = fma(u, xu[3 * i], xu[3 * i + 1]);
+            if (h > 20.0) p = fma(xu[3 * i + 2], vtab_expm(h - 20.0), p);
         }
-    }
-}
-__device__ __forceinline__ bool vtab_finish(const double* __restrict__ tb, double u, const VtLine& L, double& y) {
-    const double* a = L.a;
-    const int nx = (int)a[kCtabNC];
-    if (!L.ok || nx < 0) return false;
-    const double r = __builtin_fma((double)(L.jc - kVtInv * kVtR), -1.0 / kVtInv, u);
-    double p = a[kCtabNC - 1];
-#pragma unroll
-    for (int n = kCtabNC - 2; n >= 0; --n) p = fma(p, r, a[n]);
-    if (nx > 0) {                                         // (~10 % of the cells: one unit in the line)
-        const double h = fma(u, a[13], a[14]);
-        if (h > 20.0) p = fma(a[15], vtab_expm(h - 20.0), p);
-    }
-    const double* xu = tb + kVtXOff + (size_t)L.jc * (kVtNX - 1) * 3;
-    for (int i = 1; i < nx; ++i) {                        // (~1.5 %: a second line)
-        const double h = fma(u, xu[3 * i - 3], xu[3 * i - 2]);
-        if (h > 20.0) p = fma(xu[3 * i - 1], vtab_expm(h - 20.0), p);
     }
     y = p;
     return true;
 }
-template <bool KEY = true>
-__device__ __forceinline__ bool vtab_eval(const double* __restrict__ tb, double u, double x, double& y) {
-    VtLine L;
-    vtab_load<KEY>(tb, u, x, L);
-    return vtab_finish(tb, u, L, y);
-}
-#ifndef GNND_VT_PREFETCH
-#define GNND_VT_PREFETCH 1
-#endif
 
 // fp32 forms: TWO EDGES per call, riding the two halves of packed FMAs (the lane's
 // slots are processed in pairs).  Prepared layout (gnnd_prepare_weights; base-2 rescaled:
@@ -2009,11 +1993,6 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // read of its previous contents)
     int pbuf = 0;
     for (int it = 0; it < iters; ++it) {
-        // fp64 V24 channel-prior tables, one-slot plans: the next item round's table line, read
-        // while this round computes (its S_v and message are final once the variable sums ran)
-        constexpr bool kVtPf = kV24F64 && R == 1 && US == 1 && !TAPE && GNND_VT_PREFETCH;
-        VtLine vnext;
-        bool vnext_set = false;
         for (int f0 = 0; f0 < nItem; f0 += IL) {
             const int f = f0 + itid;
             const bool act = f < nItem;
@@ -2107,45 +2086,15 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     xs[r] = p.x;
                 }
                 const int vto = n_pt > 0 ? s_vto[b] : -1;
-                VtLine vcur;
-                if constexpr (kVtPf) {
-                    if (n_pt > 0) {
-                        if (vnext_set) {
-                            vcur = vnext;
-                        } else {
-                            vcur.ok = false;
-                            if (act && val[0] && vto >= 0) vtab_load((const double*)wv + vto, ext[0], xs[0], vcur);
-                        }
-                        vnext_set = false;
-                        if (f0 + IL < nItem) {                // (uniform) the next round's item
-                            const int fn = f + IL;
-                            const bool actn = fn < nItem;
-                            const int fcn = actn ? fn : nItem - 1;
-                            const int bn = fdiv(fcn, dItem), remn = fcn - bn * IC;
-                            const uint32_t svn = s_slot[remn];
-                            const int vton = s_vto[bn];
-                            vnext.ok = false;
-                            if (actn && (int)(svn >> 16) != E && vton >= 0) {
-                                const SumX<T> pn = s_sx[bn * V + (int)(svn & 0xffffu)];
-                                vtab_load((const double*)wv + vton, pn.s - s_m[bn * nslot + remn], pn.x, vnext);
-                            }
-                            vnext_set = true;
-                        }
-                    }
-                }
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     T a = T(0);
                     // the channel-prior table where this lane's (u, x_v) has one; the wave
                     // evaluates the 128 units when any live lane has none (those lanes keep them)
                     bool need = n_pt == 0 || (act && val[r]);
-                    if constexpr (kVtPf) {
-                        if (n_pt > 0 && need && vto >= 0 && vtab_finish((const double*)wv + vto, ext[r], vcur, a))
-                            need = false;
-                    } else {
-                        if (n_pt > 0 && need && vto >= 0 && vtab_eval((const double*)wv + vto, ext[r], xs[r], a))
-                            need = false;
-                    }
+                    if (n_pt > 0 && need && vto >= 0 &&
+                        vtab_eval<kVtInvG, true>((const double*)wv + vto, ext[r], xs[r], a))
+                        need = false;
                     if (n_pt == 0 || __builtin_amdgcn_ballot_w64(need) != 0) {
                         const T a2 = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
                                                              s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid, widle,
@@ -2354,7 +2303,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const T m = s_m[f < n ? f : n - 1];
                 T y = T(0);
                 bool need = f < n;
-                if (need && vtab_eval<false>(rt, m, 0.0, y)) need = false;
+                if (need && vtab_eval<kVtInvR, false>(rt, m, 0.0, y)) need = false;
                 if (__builtin_amdgcn_ballot_w64(need) != 0) {
                     const T y2 = mlp128_sp(wv + kV24Mlp, s_bias + 256, m, s_tab, s_lin + 8);
                     if (need) y = y2;

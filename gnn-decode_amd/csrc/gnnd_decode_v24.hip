@@ -75,7 +75,7 @@ vtab_eval_kernel(const double* __restrict__ w, const double* __restrict__ u, con
         if (!xv) {                                        // the readout MLP's table
             double v;
             if (n_pt > 0 && w[kV24PriorHdr + 1] != 0.0 &&
-                vtab_eval<false>(w + kV24PriorOff + (size_t)n_pt * kVtStride, u[i], 0.0, v)) {
+                vtab_eval<kVtInvR, false>(w + kV24PriorOff + (size_t)n_pt * kVtStride, u[i], 0.0, v)) {
                 y[i] = v;
                 h = 1;
             }
@@ -87,7 +87,7 @@ vtab_eval_kernel(const double* __restrict__ w, const double* __restrict__ u, con
             const double* tb = w + kV24PriorOff + (size_t)t * kVtStride;
             if (__double_as_longlong(tb[0]) != xb) continue;
             double v;
-            if (vtab_eval(tb, u[i], xv[i], v)) {
+            if (vtab_eval<kVtInvG, true>(tb, u[i], xv[i], v)) {
                 y[i] = v;
                 h = 1;
             }

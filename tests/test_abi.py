@@ -80,7 +80,7 @@ def test_weights_count_and_width():
 
 def test_prepared_counts_with_channel_prior_tables():
     """gnnd_prepared_weights_count[_priors] (host-only): decoder_v2_4 = 1 283 weights + check-MLP
-    table + prior header = 7 264; fp64 V24 adds 11 312 per channel-prior table (<= 64) and one for
+    table + prior header = 7 264; fp64 V24 adds 17 456 per channel-prior table (<= 64) and 34 864 for
     the readout MLP; other
     models / fp32 take no tables."""
     lib = _lib.get()
@@ -90,7 +90,7 @@ def test_prepared_counts_with_channel_prior_tables():
         assert lib.gnnd_prepared_weights_count(v24, dt, ctypes.byref(n)) == _lib.OK and n.value == 7264
         assert lib.gnnd_prepared_weights_count_priors(v24, dt, 0, ctypes.byref(n)) == _lib.OK and n.value == 7264
     assert lib.gnnd_prepared_weights_count_priors(v24, f64, 10, ctypes.byref(n)) == _lib.OK
-    assert n.value == 7264 + 11 * 11312              # (+ the readout MLP's table)
+    assert n.value == 7264 + 10 * 17456 + 34864       # (+ the readout MLP's table)
     assert lib.gnnd_prepared_weights_count_priors(v24, f64, 65, ctypes.byref(n)) == _lib.ERR_INVALID_ARG
     assert lib.gnnd_prepared_weights_count_priors(v24, f64, -1, ctypes.byref(n)) == _lib.ERR_INVALID_ARG
     assert lib.gnnd_prepared_weights_count_priors(v24, f32, 1, ctypes.byref(n)) == _lib.ERR_UNSUPPORTED

@@ -62,7 +62,7 @@ def test_prior_tables_match_reference_mlp(weights):
     pri = _priors(H)
     assert len(pri) == 10
     prep = gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous(), priors=pri)
-    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64, priors=10) == 7264 + 11 * 11312
+    assert prep.numel() == gd.ops.prepared_count('v24', torch.float64, priors=10) == 7264 + 10 * 17456 + 34864
     assert int(prep[7252]) == 10 and float(prep[7253]) == 1.0
     g = torch.Generator(device='cpu').manual_seed(2)
     for xv in pri:
@@ -81,7 +81,7 @@ def test_prior_tables_match_reference_mlp(weights):
         y, hit = gd.ops.v24_var_mlp_table(prep, u, xt)
         ref = _torch_mlp(m, u, xt)
         if weights == 'shipped':
-            assert bool(hit.all()), int((~hit).sum())      # every cell valid (0-3 crossings)
+            assert bool(hit.all()), int((~hit).sum())      # every cell valid (<= 3 crossings)
         assert float(hit.float().mean()) > 0.9
         err = float((y[hit] - ref[hit]).abs().max())
         assert err <= TOL, (xv, err)
