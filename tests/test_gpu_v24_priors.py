@@ -114,12 +114,13 @@ def test_readout_table_matches_reference_mlp():
 
 
 def test_prior_table_misses_fall_back():
-    """Points outside |u| <= 32 + 1/16 or with an unregistered prior are not covered."""
+    """Points outside |u| <= 32 + 1/32 (cells of width 1/16 centred on j/16) or with an
+    unregistered prior are not covered."""
     import gnndecode as gd
     m, H = _model()
     pri = _priors(H)
     prep = gd.ops.prepare_weights('v24', m.packed_weights().double().detach().contiguous(), priors=pri[:3])
-    u = torch.tensor([0.0, 32.0, -32.06, 32.07, -40.0, 1e300, float('nan'), 1.5], dtype=torch.float64,
+    u = torch.tensor([0.0, 32.0, -32.03, 32.032, -40.0, 1e300, float('nan'), 1.5], dtype=torch.float64,
                      device=DEV)
     xv = torch.full_like(u, pri[0])
     xv[-1] = pri[5]                                        # not registered
