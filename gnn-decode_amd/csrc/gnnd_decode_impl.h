@@ -753,37 +753,63 @@ __device__ __forceinline__ double vtab_expm(double t) {
 }
 // ggc1.mlp(u, x) (INV = kVtInvG, KEY) or mlp(u) (kVtInvR, no key) from table tb (global memory,
 // L2-resident): false (y untouched) when x is not the table's prior, |u| is outside the table or
-// the cell is invalid
-template <int INV, bool KEY>
-__device__ __forceinline__ bool vtab_eval(const double* __restrict__ tb, double u, double x, double& y) {
-    if (KEY && __double_as_longlong(x) != __double_as_longlong(tb[0])) return false;
-    if (!(fabs(u) <= kVtR + 0.5 / INV)) return false;
-    int k = round_magic_lo(__builtin_fma(u, (double)INV, kRoundMagic));
-    k = k < -INV * kVtR ? -INV * kVtR : (k > INV * kVtR ? INV * kVtR : k);
-    const int jc = k + INV * kVtR;
-    const double2* e = (const double2*)(tb + kVtHdr + (size_t)jc * kVtNC);
+// the cell is invalid.  The cell index is clamped into the table before any test (NaN and huge
+// |u| included), so the key, the cell's four 16-byte loads and the range test issue together --
+// one L2 round trip per evaluation, not the key's and then the cell's -- and the tests select
+// the result instead of branching around the loads.
+struct VtCell {
     double a[kVtNC];
+    double key;
+    int k;
+};
+// phase 1: the cell's loads (and the key's) from the clamped index -- straight-line, so the
+// fetches of several evaluations issue back to back
+template <int INV, bool KEY>
+__device__ __forceinline__ VtCell vtab_fetch(const double* __restrict__ tb, double u) {
+    VtCell c;
+    int k = round_magic_lo(__builtin_fma(u, (double)INV, kRoundMagic));
+    c.k = k < -INV * kVtR ? -INV * kVtR : (k > INV * kVtR ? INV * kVtR : k);
+    const double2* e = (const double2*)(tb + kVtHdr + (size_t)(c.k + INV * kVtR) * kVtNC);
 #pragma unroll
     for (int i = 0; i < kVtNC / 2; ++i) {
         const double2 v = e[i];
-        a[2 * i] = v.x;
-        a[2 * i + 1] = v.y;
+        c.a[2 * i] = v.x;
+        c.a[2 * i + 1] = v.y;
     }
-    const int code = (int)(__double_as_longlong(a[kVtNC - 1]) & 7);
-    if (code > kVtNX) return false;
-    const double r = __builtin_fma((double)k, -1.0 / INV, u);
-    double p = a[kVtNC - 1];
+    c.key = KEY ? tb[0] : 0.0;
+    return c;
+}
+// phase 2: the tests and the polynomial (the rare threshold-crossing units of the cell last)
+template <int INV, bool KEY>
+__device__ __forceinline__ bool vtab_finish(const double* __restrict__ tb, const VtCell& c, double u, double x,
+                                            double& y) {
+    const bool key_ok = !KEY || __double_as_longlong(x) == __double_as_longlong(c.key);
+    const int code = (int)(__double_as_longlong(c.a[kVtNC - 1]) & 7);
+    const bool hit = key_ok && fabs(u) <= kVtR + 0.5 / INV && code <= kVtNX;
+    const double r = __builtin_fma((double)c.k, -1.0 / INV, u);
+    double p = c.a[kVtNC - 1];
 #pragma unroll
-    for (int n = kVtNC - 2; n >= 0; --n) p = fma(p, r, a[n]);
-    if (code > 0) {                                       // (a few % of the cells)
-        const double* xu = tb + vt_xoff(INV) + (size_t)jc * kVtNX * 3;
+    for (int n = kVtNC - 2; n >= 0; --n) p = fma(p, r, c.a[n]);
+    if (hit && code > 0) {                                // (a few % of the cells)
+        const double* xu = tb + vt_xoff(INV) + (size_t)(c.k + INV * kVtR) * kVtNX * 3;
         for (int i = 0; i < code; ++i) {
             const double h = fma(u, xu[3 * i], xu[3 * i + 1]);
             if (h > 20.0) p = fma(xu[3 * i + 2], vtab_expm(h - 20.0), p);
         }
     }
-    y = p;
-    return true;
+    if (hit) y = p;
+    return hit;
+}
+// ggc1.mlp(u, x) (INV = kVtInvG, KEY) or mlp(u) (kVtInvR, no key) from table tb (global memory,
+// L2-resident): false (y untouched) when x is not the table's prior, |u| is outside the table or
+// the cell is invalid.  The cell index is clamped into the table before any test (NaN and huge
+// |u| included), so the key, the cell's four 16-byte loads and the range test issue together --
+// one L2 round trip per evaluation, not the key's and then the cell's -- and the tests select
+// the result instead of branching around the loads.
+template <int INV, bool KEY>
+__device__ __forceinline__ bool vtab_eval(const double* __restrict__ tb, double u, double x, double& y) {
+    const VtCell c = vtab_fetch<INV, KEY>(tb, u);
+    return vtab_finish<INV, KEY>(tb, c, u, x, y);
 }
 
 // fp32 forms: TWO EDGES per call, riding the two halves of packed FMAs (the lane's
@@ -1992,8 +2018,84 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // alternate call by call, so a buffer is rewritten only after a barrier that follows every
     // read of its previous contents)
     int pbuf = 0;
+    // fp64 decoder_v2_4 with channel-prior tables (one slot per item): TWO work items per lane per
+    // pass (rounds f0 and f0 + IL), their LDS reads, table fetches and check-MLP entries issued
+    // together -- the variable-side MLP is one L2 round trip per edge, and one item per lane left
+    // the waves waiting on it (SQ_WAIT_ANY 0.60, profiles/pmc_classes_v24_toric_5_T15_f64_ptab)
+    constexpr bool kPt2 = kV24F64 && US == 1 && !TAPE && R == 1;
+    const bool pt2 = kPt2 && n_pt > 0;
     for (int it = 0; it < iters; ++it) {
-        for (int f0 = 0; f0 < nItem; f0 += IL) {
+        if constexpr (kPt2) {
+            // one pass: items A (round f0) and, when TWO, B (round f0 + IL); a wave with no live
+            // second item runs the one-item instantiation (no work on clamped copies)
+            auto pass2 = [&](int f0, auto twoC) {
+                constexpr bool TWO = decltype(twoC)::value;
+                const int fA = f0 + itid, fB = fA + IL;
+                const bool actA = fA < nItem, actB = TWO && fB < nItem;
+                const bool idleA = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= nItem;
+                const int fcA = actA ? fA : nItem - 1, fcB = actB ? fB : nItem - 1;
+                const int bA = fdiv(fcA, dItem), bB = TWO ? fdiv(fcB, dItem) : bA;
+                const int remA = fcA - bA * IC, remB = TWO ? fcB - bB * IC : remA;
+                const uint32_t svA = s_slot[remA], svB = TWO ? s_slot[remB] : svA;
+                T* mbA = s_m + bA * nslot + remA;
+                T* mbB = s_m + bB * nslot + remB;
+                const bool valA = (int)(svA >> 16) != E, valB = (int)(svB >> 16) != E;
+                const T mvA = *mbA, mvB = TWO ? *mbB : mvA;
+                const SumX<T> pA = s_sx[bA * V + GNND_DIDX((int)(svA & 0xffffu), V, GNND_DBG_VAR)];
+                const SumX<T> pB = TWO ? s_sx[bB * V + GNND_DIDX((int)(svB & 0xffffu), V, GNND_DBG_VAR)] : pA;
+                const T extA = pA.s - mvA, extB = pB.s - mvB;
+                const int vtoA = s_vto[bA], vtoB = TWO ? s_vto[bB] : vtoA;
+                const double* tbA = (const double*)wv + (vtoA >= 0 ? vtoA : kV24PriorOff);
+                const double* tbB = (const double*)wv + (vtoB >= 0 ? vtoB : kV24PriorOff);
+                const VtCell cA = vtab_fetch<kVtInvG, true>(tbA, extA);
+                VtCell cB;
+                if constexpr (TWO) cB = vtab_fetch<kVtInvG, true>(tbB, extB);
+                const T scA = s_xc[bA * C + (remA >> logG)];
+                const T scB = TWO ? s_xc[bB * C + (remB >> logG)] : scA;
+                T aA = T(0), aB = T(0);
+                const bool needA = actA && valA && !vtab_finish<kVtInvG, true>(tbA, cA, extA, pA.x, aA);
+                bool needB = false;
+                if constexpr (TWO) needB = actB && valB && !vtab_finish<kVtInvG, true>(tbB, cB, extB, pB.x, aB);
+                // (the wave evaluates the 128 units where a live lane's (u, x_v) has no table)
+                if (__builtin_amdgcn_ballot_w64(needA) != 0) {
+                    const T a2 = mlp128d_split<1, true>(wv + kV24Ggc1, s_bias, extA, pA.x, 0, s_pd, itid, idleA,
+                                                        s_tab, s_lin, s_wcm);
+                    if (needA) aA = a2;
+                }
+                if constexpr (TWO) {
+                    if (__builtin_amdgcn_ballot_w64(needB) != 0) {
+                        const T a2 = mlp128d_split<1, true>(wv + kV24Ggc1, s_bias, extB, pB.x, 0, s_pd, itid, false,
+                                                            s_tab, s_lin, s_wcm);
+                        if (needB) aB = a2;
+                    }
+                }
+                const T tvA = valA ? tanh_half_fast(aA) : T(0);
+                const T tvB = TWO && valB ? tanh_half_fast(aB) : T(0);
+                const T ScA = group_sum(tvA, G);
+                const T ScB = TWO ? group_sum(tvB, G) : T(0);
+                const T uA = ScA - tvA, uB = ScB - tvB;
+                T yA, yB = T(0);
+                if (ctab_ok) {               // (uniform)
+                    yA = ctab_eval(s_ctab, uA, R8);
+                    if constexpr (TWO) yB = ctab_eval(s_ctab, uB, R8);
+                } else {
+                    yA = mlp128d_split<1, false>(wv + kV24Ggc2, s_bias + 128, uA, uA, 0, s_pd, itid, idleA, s_tab,
+                                                 s_lin + 4, s_wcm + 128);
+                    if constexpr (TWO)
+                        yB = mlp128d_split<1, false>(wv + kV24Ggc2, s_bias + 128, uB, uB, 0, s_pd, itid, false, s_tab,
+                                                     s_lin + 4, s_wcm + 128);
+                }
+                if (actA) *mbA = yA * scA + mvA;
+                if (TWO && actB) *mbB = yB * scB + mvB;
+            };
+            for (int f0 = 0; f0 < (pt2 ? nItem : 0); f0 += 2 * IL) {
+                if (__builtin_amdgcn_readfirstlane(f0 + IL + (itid & ~63)) < nItem)
+                    pass2(f0, std::true_type{});
+                else
+                    pass2(f0, std::false_type{});
+            }
+        }
+        for (int f0 = 0; f0 < (pt2 ? 0 : nItem); f0 += IL) {
             const int f = f0 + itid;
             const bool act = f < nItem;
             const bool own = act && sub == 0;            // the unit-split waves' writer
@@ -2092,8 +2194,10 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     // the channel-prior table where this lane's (u, x_v) has one; the wave
                     // evaluates the 128 units when any live lane has none (those lanes keep them)
                     bool need = n_pt == 0 || (act && val[r]);
-                    if (n_pt > 0 && need && vto >= 0 &&
-                        vtab_eval<kVtInvG, true>((const double*)wv + vto, ext[r], xs[r], a))
+                    // (no table for the codeword's first prior: table 0, whose key then decides --
+                    // a variable whose x_v is table 0's prior is covered by it all the same)
+                    if (n_pt > 0 && vtab_eval<kVtInvG, true>((const double*)wv + (vto >= 0 ? vto : kV24PriorOff),
+                                                             ext[r], xs[r], a))
                         need = false;
                     if (n_pt == 0 || __builtin_amdgcn_ballot_w64(need) != 0) {
                         const T a2 = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
@@ -2303,7 +2407,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const T m = s_m[f < n ? f : n - 1];
                 T y = T(0);
                 bool need = f < n;
-                if (need && vtab_eval<kVtInvR, false>(rt, m, 0.0, y)) need = false;
+                if (vtab_eval<kVtInvR, false>(rt, m, 0.0, y)) need = false;   // (f >= n: need false)
                 if (__builtin_amdgcn_ballot_w64(need) != 0) {
                     const T y2 = mlp128_sp(wv + kV24Mlp, s_bias + 256, m, s_tab, s_lin + 8);
                     if (need) y = y2;
@@ -3562,13 +3666,18 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
     // tiles down to half the LDS-limited size take the one wasting the fewest lanes (ties:
     // larger).  toric-5 V24 fp32 (C*G = 48): 19 -> 16 codewords (3 full rounds, and 4
     // workgroups per CU instead of 3)
+    // (fp64 V24 wide plans with channel-prior tables run two rounds per pass (kPt2); choosing the
+    // tile by round-pair utilisation instead -- toric-5: 10 codewords, 0.94 of two passes, for 8 =
+    // 3 rounds -- measured 1.8182 vs 1.8325 ms at B = 65 536 (noise) and moved B = 4 096 off the
+    // wide form, 0.155 -> 0.208 ms: not kept)
     {
         const size_t IC = (size_t)g.C * g.G;
+        const size_t span = lanes;
         size_t best = n;
         double bu = 0;
         for (size_t c = n; c >= 1 && 2 * c >= n; --c) {
-            const size_t items = c * IC, rounds = (items + lanes - 1) / lanes;
-            const double u = (double)items / (double)(rounds * lanes);
+            const size_t items = c * IC, rounds = (items + span - 1) / span;
+            const double u = (double)items / (double)(rounds * span);
             if (u > bu + 1e-9) { bu = u; best = c; }
         }
         n = best;

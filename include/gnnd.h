@@ -212,9 +212,11 @@ int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, cons
  * the reference's inputs carry one prior LLR x_v = log((1-p)/p) per codeword, p drawn from a
  * short list (quantum/error_generate.py:252-260).  gnnd_prepare_weights_priors = gnnd_prepare_weights
  * plus, for each of the n_priors values h_priors[] (host fp64, <= 64; the exact x_v bits the
- * inputs will carry), the MLP tabulated over |S_v - m_e| <= 32 (degree-11 Taylor cells of width
- * 1/8; units crossing torch's Softplus threshold inside a cell are evaluated exactly; <= 1e-13
- * absolute vs the MLP), into a buffer of gnnd_prepared_weights_count_priors elements.  gnnd_decode
+ * inputs will carry), the MLP tabulated over |S_v - m_e| <= 32 (64-byte cells: degree-7 Taylor
+ * polynomials about j/16, the readout's about j/32; up to 3 units crossing torch's Softplus
+ * threshold inside a cell are stored aside and evaluated exactly; a cell whose remainder bound
+ * exceeds 1e-13 or that holds more crossings is marked invalid and its points take the 128
+ * units), into a buffer of gnnd_prepared_weights_count_priors elements.  gnnd_decode
  * (fp64 V24, batches decoded one wave per item group) then reads a codeword's table where its
  * x_v equals a registered prior bit for bit and evaluates the 128 units elsewhere (other priors,
  * |S_v - m_e| > 32), and the readout MLP from one more table (n_priors > 0).  The tables
