@@ -676,7 +676,7 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
     } else {
         softplus_taylor(h, d);
     }
-    __shared__ double part[kVtNC + 1];
+    __shared__ double part[kVtNC + 3];
     __shared__ int ncross0, ncross1, bad;
     double a[kVtNC];
     double p = W2;
@@ -687,6 +687,16 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
     }
     const double w2 = W1a * W1a, w4 = w2 * w2;
     const double s8 = group_sum_c<64>(fabs(W2) * (w4 * w4));
+    // SEL 0: the smooth function at the cell's two edges (lin units exactly h, the others
+    // log1p(e^h) -- what the polynomial holds), to check the tanh composition below
+    double fe[2] = {0.0, 0.0};
+    if constexpr (SEL == 0) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const double he = fma(W1a, c + (q ? 0.5 : -0.5) / INV, bp);
+            fe[q] = group_sum_c<64>(W2 * (lin ? he : log1p(exp(he))));
+        }
+    }
     const uint64_t cm = __builtin_amdgcn_ballot_w64(cross);
     const bool wide_cross = __builtin_amdgcn_ballot_w64(cross && fabs(W1a) > 4.0 * INV) != 0;
     if (k == 0) bad = 0;
@@ -695,6 +705,8 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
 #pragma unroll
         for (int i = 0; i < kVtNC; ++i) part[i] = a[i];
         part[kVtNC] = s8;
+        part[kVtNC + 1] = fe[0];
+        part[kVtNC + 2] = fe[1];
         ncross1 = __builtin_popcountll(cm);
     }
     if (k == 0) ncross0 = __builtin_popcountll(cm);
@@ -716,8 +728,7 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
                                                   (2.0 * INV) * (2.0 * INV) * (2.0 * INV) * (2.0 * INV));
     if (k == 0) {                                         // wave 0 + wave 1 (fixed order)
         const int ntot = ncross0 + ncross1;
-        const bool ok = !bad && ntot <= kVtNX && (s8 + part[kVtNC]) * kBound <= 1e-13;
-        const long long code = ok ? ntot : 7;
+        bool ok = !bad && ntot <= kVtNX && (s8 + part[kVtNC]) * kBound <= 1e-13;
         for (int i = ntot < kVtNX ? ntot : kVtNX; i < kVtNX; ++i) {
             xu[3 * i] = 0.0;
             xu[3 * i + 1] = 0.0;
@@ -726,6 +737,47 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
         double v[kVtNC];
 #pragma unroll
         for (int i = 0; i < kVtNC; ++i) v[i] = (a[i] + part[i]) + (i == 0 ? b2 : 0.0);
+        if constexpr (SEL == 0) {
+            // the decoder needs t = tanh(f/2) of ggc1's output (the check step's pre-op,
+            // quantum/decoder_v2_4.py:135-136): the cell holds t's own degree-7 Taylor series,
+            // composed here -- w = (f - f(c))/2 has no constant term, so tanh(w) = w - w^3/3 +
+            // 2w^5/15 - 17w^7/315 is exact to r^8, and T = (t0 + tanh w)/(1 + t0 tanh w) by series
+            // division (constant term 1).  No composed remainder bound is derived: the cell is
+            // valid only if the polynomial meets tanh of the directly summed f at both cell edges
+            // (where the r^8 term peaks) within 2e-14, on top of f's own bound above.
+            double wv[kVtNC], w2v[kVtNC], w3v[kVtNC], w5v[kVtNC], w7v[kVtNC], tb[kVtNC], q[kVtNC];
+            auto smul = [](const double* A, const double* B, double* C) {
+                for (int n2 = 0; n2 < kVtNC; ++n2) {
+                    double acc = 0.0;
+                    for (int i = 0; i <= n2; ++i) acc = fma(A[i], B[n2 - i], acc);
+                    C[n2] = acc;
+                }
+            };
+            wv[0] = 0.0;
+            for (int i = 1; i < kVtNC; ++i) wv[i] = 0.5 * v[i];
+            smul(wv, wv, w2v);
+            smul(w2v, wv, w3v);
+            smul(w3v, w2v, w5v);
+            smul(w5v, w2v, w7v);
+            for (int i = 0; i < kVtNC; ++i)
+                tb[i] = ((wv[i] - w3v[i] * (1.0 / 3.0)) + w5v[i] * (2.0 / 15.0)) - w7v[i] * (17.0 / 315.0);
+            const double t0 = tanh(0.5 * v[0]);
+            for (int n2 = 0; n2 < kVtNC; ++n2) {          // q = (t0 + tb) / (1 + t0 tb)
+                double acc = (n2 == 0 ? t0 : 0.0) + tb[n2];
+                for (int i = 1; i <= n2; ++i) acc = fma(-t0 * tb[i], q[n2 - i], acc);
+                q[n2] = acc;
+            }
+#pragma unroll
+            for (int e2 = 0; e2 < 2; ++e2) {
+                const double r = (e2 ? 0.5 : -0.5) / INV;
+                double pv = q[kVtNC - 1];
+                for (int n2 = kVtNC - 2; n2 >= 0; --n2) pv = fma(pv, r, q[n2]);
+                const double te = tanh(0.5 * ((fe[e2] + part[kVtNC + 1 + e2]) + b2));
+                ok = ok && fabs(pv - te) <= 2e-14;
+            }
+            for (int i = 0; i < kVtNC; ++i) v[i] = q[i];
+        }
+        const long long code = ok ? ntot : 7;
         v[kVtNC - 1] = __longlong_as_double((__double_as_longlong(v[kVtNC - 1]) & ~7ll) | code);
 #pragma unroll
         for (int i = 0; i < kVtNC; ++i) cell[i] = v[i];
@@ -751,12 +803,6 @@ __device__ __forceinline__ double vtab_expm(double t) {
     p = fma(p, -t, 1.0);
     return fma(p, -t, 1.0);
 }
-// ggc1.mlp(u, x) (INV = kVtInvG, KEY) or mlp(u) (kVtInvR, no key) from table tb (global memory,
-// L2-resident): false (y untouched) when x is not the table's prior, |u| is outside the table or
-// the cell is invalid.  The cell index is clamped into the table before any test (NaN and huge
-// |u| included), so the key, the cell's four 16-byte loads and the range test issue together --
-// one L2 round trip per evaluation, not the key's and then the cell's -- and the tests select
-// the result instead of branching around the loads.
 struct VtCell {
     double a[kVtNC];
     double key;
@@ -792,16 +838,20 @@ __device__ __forceinline__ bool vtab_finish(const double* __restrict__ tb, const
     for (int n = kVtNC - 2; n >= 0; --n) p = fma(p, r, c.a[n]);
     if (hit && code > 0) {                                // (a few % of the cells)
         const double* xu = tb + vt_xoff(INV) + (size_t)(c.k + INV * kVtR) * kVtNX * 3;
+        double dj = 0.0;
         for (int i = 0; i < code; ++i) {
             const double h = fma(u, xu[3 * i], xu[3 * i + 1]);
-            if (h > 20.0) p = fma(xu[3 * i + 2], vtab_expm(h - 20.0), p);
+            if (h > 20.0) dj = fma(xu[3 * i + 2], vtab_expm(h - 20.0), dj);
         }
+        // the jumps dj (|dj| <= 2.1e-9 |W2| per unit) on f, or on t = tanh(f/2) to first order:
+        // t + dj (1 - t^2)/2, the next term below dj^2 / 10 ~ 1e-18
+        p = KEY ? fma(0.5 * dj, fma(-p, p, 1.0), p) : p + dj;
     }
     if (hit) y = p;
     return hit;
 }
-// ggc1.mlp(u, x) (INV = kVtInvG, KEY) or mlp(u) (kVtInvR, no key) from table tb (global memory,
-// L2-resident): false (y untouched) when x is not the table's prior, |u| is outside the table or
+// tanh(ggc1.mlp(u, x)/2) (INV = kVtInvG, KEY: the prior tables hold the check step's pre-op
+// directly) or mlp(u) (kVtInvR, no key) from table tb (global memory, L2-resident): false (y untouched) when x is not the table's prior, |u| is outside the table or
 // the cell is invalid.  The cell index is clamped into the table before any test (NaN and huge
 // |u| included), so the key, the cell's four 16-byte loads and the range test issue together --
 // one L2 round trip per evaluation, not the key's and then the cell's -- and the tests select
@@ -2052,10 +2102,13 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 if constexpr (TWO) cB = vtab_fetch<kVtInvG, true>(tbB, extB);
                 const T scA = s_xc[bA * C + (remA >> logG)];
                 const T scB = TWO ? s_xc[bB * C + (remB >> logG)] : scA;
+                // (a hit gives t = tanh(ggc1.mlp/2) itself; the units give the MLP output)
                 T aA = T(0), aB = T(0);
-                const bool needA = actA && valA && !vtab_finish<kVtInvG, true>(tbA, cA, extA, pA.x, aA);
-                bool needB = false;
-                if constexpr (TWO) needB = actB && valB && !vtab_finish<kVtInvG, true>(tbB, cB, extB, pB.x, aB);
+                const bool hitA = vtab_finish<kVtInvG, true>(tbA, cA, extA, pA.x, aA);
+                bool hitB = false;
+                if constexpr (TWO) hitB = vtab_finish<kVtInvG, true>(tbB, cB, extB, pB.x, aB);
+                const bool needA = actA && valA && !hitA;
+                const bool needB = TWO && actB && valB && !hitB;
                 // (the wave evaluates the 128 units where a live lane's (u, x_v) has no table)
                 if (__builtin_amdgcn_ballot_w64(needA) != 0) {
                     const T a2 = mlp128d_split<1, true>(wv + kV24Ggc1, s_bias, extA, pA.x, 0, s_pd, itid, idleA,
@@ -2069,8 +2122,8 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                         if (needB) aB = a2;
                     }
                 }
-                const T tvA = valA ? tanh_half_fast(aA) : T(0);
-                const T tvB = TWO && valB ? tanh_half_fast(aB) : T(0);
+                const T tvA = valA ? (hitA ? aA : tanh_half_fast(aA)) : T(0);
+                const T tvB = TWO && valB ? (hitB ? aB : tanh_half_fast(aB)) : T(0);
                 const T ScA = group_sum(tvA, G);
                 const T ScB = TWO ? group_sum(tvB, G) : T(0);
                 const T uA = ScA - tvA, uB = ScB - tvB;
@@ -2196,16 +2249,17 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     bool need = n_pt == 0 || (act && val[r]);
                     // (no table for the codeword's first prior: table 0, whose key then decides --
                     // a variable whose x_v is table 0's prior is covered by it all the same)
-                    if (n_pt > 0 && vtab_eval<kVtInvG, true>((const double*)wv + (vto >= 0 ? vto : kV24PriorOff),
-                                                             ext[r], xs[r], a))
-                        need = false;
+                    // (a hit gives t = tanh(ggc1.mlp/2) itself; the units give the MLP output)
+                    const bool hit = n_pt > 0 && vtab_eval<kVtInvG, true>(
+                                                     (const double*)wv + (vto >= 0 ? vto : kV24PriorOff), ext[r], xs[r], a);
+                    if (hit) need = false;
                     if (n_pt == 0 || __builtin_amdgcn_ballot_w64(need) != 0) {
                         const T a2 = mlp128d_split<US, true>(wv + kV24Ggc1, s_bias, ext[r], xs[r], sub,
                                                              s_pd + (pbuf++ & 1) * US * GNND_BLOCK, itid, widle,
                                                              s_tab, s_lin, s_wcm);
                         if (need) a = a2;
                     }
-                    tv[r] = val[r] ? tanh_half_fast(a) : T(0);
+                    tv[r] = val[r] ? (hit ? a : tanh_half_fast(a)) : T(0);
                     cf[r] = T(0);
                     tsum += tv[r];
                     if constexpr (TAPE) {

@@ -62,9 +62,9 @@ extern "C" int gnnd_v24_check_mlp_table(const gnnd_graph* g, const void* d_w, co
 }
 
 // the variable-side MLP through the channel-prior tables (vtab_eval, gnnd_decode_impl.h), for
-// tests: y[i] = ggc1.mlp(u[i], x[i]) and hit[i] = 1 where a table covers (u[i], x[i]), else hit[i]
-// = 0 and y[i] untouched (the decoder evaluates the 128 units there); x = NULL: the readout
-// MLP's table, y[i] = mlp(u[i])
+// tests: y[i] = tanh(ggc1.mlp(u[i], x[i]) / 2) (the check step's pre-op, what the tables hold)
+// and hit[i] = 1 where a table covers (u[i], x[i]), else hit[i] = 0 and y[i] untouched (the
+// decoder evaluates the 128 units there); x = NULL: the readout MLP's table, y[i] = mlp(u[i])
 namespace {
 __global__ void __launch_bounds__(256)
 vtab_eval_kernel(const double* __restrict__ w, const double* __restrict__ u, const double* __restrict__ xv,

@@ -218,8 +218,9 @@ def channel_priors(graph, x, limit=64):
 
 def v24_var_mlp_table(prepared_weights, u, xv=None):
     """gnnd_v24_var_mlp_table: decoder_v2_4's variable-side MLP through the channel-prior tables
-    at fp64 points (u, x_v) -> (y, hit); xv None: the readout MLP's table at u.  y is NaN where
-    hit is False."""
+    at fp64 points (u, x_v) -> (y, hit) with y = tanh(ggc1.mlp(u, x_v) / 2), the check step's
+    pre-op of the MLP output that the tables hold; xv None: the readout MLP's table at u,
+    y = mlp(u).  y is NaN where hit is False."""
     _require_gpu(prepared_weights, u)
     u = u.to(torch.float64).contiguous()
     if xv is not None:

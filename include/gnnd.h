@@ -212,11 +212,13 @@ int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, cons
  * the reference's inputs carry one prior LLR x_v = log((1-p)/p) per codeword, p drawn from a
  * short list (quantum/error_generate.py:252-260).  gnnd_prepare_weights_priors = gnnd_prepare_weights
  * plus, for each of the n_priors values h_priors[] (host fp64, <= 64; the exact x_v bits the
- * inputs will carry), the MLP tabulated over |S_v - m_e| <= 32 (64-byte cells: degree-7 Taylor
- * polynomials about j/16, the readout's about j/32; up to 3 units crossing torch's Softplus
- * threshold inside a cell are stored aside and evaluated exactly; a cell whose remainder bound
- * exceeds 1e-13 or that holds more crossings is marked invalid and its points take the 128
- * units), into a buffer of gnnd_prepared_weights_count_priors elements.  gnnd_decode
+ * inputs will carry), tanh(MLP/2) -- the check step's pre-op of its output -- tabulated over
+ * |S_v - m_e| <= 32 (64-byte cells: degree-7 Taylor polynomials about j/16; the readout MLP's
+ * about j/32; up to 3 units crossing torch's Softplus threshold inside a cell are stored aside and
+ * their jumps added exactly; a cell whose MLP remainder bound exceeds 1e-13, whose tanh series
+ * misses the directly evaluated tanh(MLP/2) at a cell edge by more than 2e-14, or that holds more
+ * crossings is marked invalid and its points take the 128 units), into a buffer of
+ * gnnd_prepared_weights_count_priors elements.  gnnd_decode
  * (fp64 V24, batches decoded one wave per item group) then reads a codeword's table where its
  * x_v equals a registered prior bit for bit and evaluates the 128 units elsewhere (other priors,
  * |S_v - m_e| > 32), and the readout MLP from one more table (n_priors > 0).  The tables
@@ -225,7 +227,9 @@ int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, cons
 int gnnd_prepared_weights_count_priors(int model, int dtype, int32_t n_priors, int64_t* h_count);
 int gnnd_prepare_weights_priors(int model, int dtype, const void* d_w, void* d_prepared,
                                 const double* h_priors, int32_t n_priors, void* stream);
-/* The tables as the decoder evaluates them, for tests: d_y[i] = ggc1.mlp(d_u[i], d_x[i]) and
+/* The tables as the decoder evaluates them, for tests: d_y[i] = tanh(ggc1.mlp(d_u[i], d_x[i]) / 2)
+ * (the prior tables hold the check step's pre-op tanh(m/2) of ggc1's output directly, as degree-7
+ * series composed from the MLP's; quantum/decoder_v2_4.py:135-136) and
  * d_hit[i] = 1 where a table covers the point, else d_hit[i] = 0 and d_y[i] untouched
  * (d_w = prepared fp64 V24 weights with tables; device fp64 d_u, d_x, d_y [n], int32 d_hit).
  * The prepared tables end with one for the readout MLP (mlp, quantum/decoder_v2_4.py:291, over

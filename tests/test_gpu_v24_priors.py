@@ -1,12 +1,13 @@
 """decoder_v2_4 fp64: the variable-side MLP through channel-prior tables
-(gnnd_prepare_weights_priors / vtab_eval in gnnd_decode_impl.h, gnnd_v24_var_mlp_table).
+(gnnd_prepare_weights_priors / vtab_eval in gnnd_decode_impl.h, gnnd_v24_var_mlp_table); the
+prior tables hold tanh(ggc1.mlp/2), the check step's pre-op of the MLP output.
 
 ggc1.mlp (Linear(2,128) -> Softplus -> Linear(128,1), quantum/decoder_v2_4.py:237-239,
 :253-255) takes (S_v - m_e, x_v); the reference's gen_syn inputs (quantum/error_generate.py:
 252-260) carry one prior LLR per codeword from a short p list, so the prepared weights can carry
 the MLP tabulated per prior.  Held here against torch's own fp64 module (Softplus threshold 20
-included: units cross it inside the table's range, and the cells evaluate the jump exactly) at
-1e-13 absolute, and the decoder with tables against the oracle (rtol 1e-10, bit-exact
+included: units cross it inside the table's range, and the cells evaluate the jump exactly), the
+prior tables as tanh(mlp/2), at 1e-13 absolute, and the decoder with tables against the oracle (rtol 1e-10, bit-exact
 decisions) on batches mixing registered priors, other priors and per-variable priors.
 """
 import os
@@ -47,6 +48,12 @@ def _torch_mlp(m, u, xv):
         return m.ggc1.mlp(torch.stack([u, xv], dim=1)).view(-1)
 
 
+def _torch_pre(m, u, xv):
+    """What the prior tables hold: the check step's pre-op tanh(m/2) of ggc1's output
+    (quantum/decoder_v2_4.py:135-136)."""
+    return torch.tanh(_torch_mlp(m, u, xv) / 2)
+
+
 def _crossings(m, xv):
     """u where some unit's pre-activation W1a u + W1b x + b1 equals 20 (torch's threshold)."""
     W = m.ggc1.mlp[0].weight.detach().cpu().numpy()
@@ -79,7 +86,7 @@ def test_prior_tables_match_reference_mlp(weights):
         u = u[torch.from_numpy(far)].to(DEV)
         xt = torch.full_like(u, xv)
         y, hit = gd.ops.v24_var_mlp_table(prep, u, xt)
-        ref = _torch_mlp(m, u, xt)
+        ref = _torch_pre(m, u, xt)
         if weights == 'shipped':
             assert bool(hit.all()), int((~hit).sum())      # every cell valid (<= 3 crossings)
         assert float(hit.float().mean()) > 0.9
