@@ -1811,7 +1811,11 @@ __device__ __forceinline__ double fwd_wave_sum(double v) {
 // views[k]; the component's rows are addressed through its GraphView addressing fields.
 // WIDE (US = 1 only): WIDE x 256 work-item lanes per workgroup, so several waves' worth of items
 // share one copy of the workgroup's LDS tables (fp64 decoder_v2_4: the 33 KB Softplus table)
-template <int MODEL, typename T, int R, bool TAPE = false, int US = 1, int WIDE = 1>
+// IW3 (unit split only): rounds of 192 work-item lanes (three item waves x US) instead of 256 --
+// a workgroup with one toric-7 component-codeword (192 edges, one per lane) then has no item
+// wave without work (launched with 192 US threads; the launch bound and thus the register
+// allocation stay those of the 256-lane form)
+template <int MODEL, typename T, int R, bool TAPE = false, int US = 1, int WIDE = 1, bool IW3 = false>
 __global__ void __launch_bounds__(unit_split_lanes<US>() * US * WIDE)
 decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict__ x,
               T* __restrict__ out, int64_t B, int iters, int CW, FastDiv dItem, FastDiv dV,
@@ -1832,7 +1836,10 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     const int V = g.V, C = g.C, E = g.E, N = g.N, G = g.G, logG = g.logG;
     const int tid = threadIdx.x;
     static_assert(WIDE == 1 || US == 1, "wide workgroups: no unit split");
-    constexpr int IL = unit_split_lanes<US>() * WIDE;  // work-item lanes
+    static_assert(!IW3 || (US > 1 && US < 8), "192-lane rounds: unit split 2 or 4");
+    // ILB: the partial-sum buffers' row stride (the unit-split MLPs index them by it)
+    constexpr int ILB = unit_split_lanes<US>() * WIDE;
+    constexpr int IL = IW3 ? 192 : ILB;                // work-item lanes
     constexpr int NT = IL * US;
     static_assert(US == 1 || (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2) ||
                       (MODEL == GNND_V24 && sizeof(T) == 8 && US <= 4),
@@ -1925,7 +1932,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // fp32 V24 on the R = 1 slot plan (B <= 4096): the unit-pair MLPs (mlp128_upair), their
     // pair-major weights staged in LDS after the unit split's partial-sum buffers
     constexpr bool kUP = kV24F32 && R == 1 && US <= 4;
-    float* s_up = (float*)(smem + ((((char*)(s_part + (US > 1 ? 2 * US * IL : 0))) - smem) + 15 & ~(ptrdiff_t)15));
+    float* s_up = (float*)(smem + ((((char*)(s_part + (US > 1 ? 2 * US * ILB : 0))) - smem) + 15 & ~(ptrdiff_t)15));
     if constexpr (kUP) stage_upair((const float*)w, s_up, tid);
     double* s_pd = (double*)s_part;                        // fp64 unit split: [2][US][256]
     // fp64 unit split: the three MLPs' chain-major weights [3][128] (16-byte aligned) after it
@@ -2194,7 +2201,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 if constexpr (kUP) {
                     // one edge per lane, two hidden units per packed op (with the check MLP on its
                     // table the var MLP's two partial-sum buffers alternate call by call)
-                    float* pb = (float*)(s_part + (ctab_ok && (pbuf++ & 1) ? US * IL : 0));
+                    float* pb = (float*)(s_part + (ctab_ok && (pbuf++ & 1) ? US * ILB : 0));
                     const float a = mlp128_upair_split<US, true>(s_up + UpairLds::kMlp0, v24.l1, ext[0], xs[0],
                                                                  sub, pb, itid, widle);
                     tv[0] = val[0] ? tanh_half_fast(a) : 0.f;
@@ -2202,7 +2209,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
 #pragma unroll
                     for (int r = 0; r < R; r += 2) {
                         const int r1 = r + 1 < R ? r + 1 : r;
-                        f32x2* pb = s_part + (ctab_ok && (pbuf++ & 1) ? US * IL : 0);
+                        f32x2* pb = s_part + (ctab_ok && (pbuf++ & 1) ? US * ILB : 0);
                         const f32x2 a = mlp128_split<US, true>(v24.g + kV24Ggc1, v24.l1, f32x2{ext[r], ext[r1]},
                                                                f32x2{xs[r], xs[r1]}, sub, pb, itid, widle
                                                                GNND_PARG(pf, 1));
@@ -2331,7 +2338,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const float u = Sc - tv[0];
                 const float y = ctab_ok ? ctab_eval(s_ctab, u, R8)   // (uniform: every split wave)
                                         : mlp128_upair_split<US, false>(s_up + UpairLds::kMlp1, v24.l2, u, u, sub,
-                                                                        (float*)(s_part + US * IL), itid, widle);
+                                                                        (float*)(s_part + US * ILB), itid, widle);
                 mn[0] = y * sc + mv[0];
             } else if constexpr (kV24F32) {
                 GNND_PMARK(pf, 3);
@@ -2341,7 +2348,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                     const f32x2 uu = {Sc - tv[r], Sc - tv[r1]};
                     const f32x2 y = ctab_ok ? f32x2{ctab_eval(s_ctab, uu.x, R8), ctab_eval(s_ctab, uu.y, R8)}
                                             : mlp128_split<US, false>(v24.g + kV24Ggc2, v24.l2, uu, uu, sub,
-                                                                      s_part + US * IL, itid, widle GNND_PARG(pf, 4));
+                                                                      s_part + US * ILB, itid, widle GNND_PARG(pf, 4));
                     mn[r] = y.x * sc + mv[r];
                     if (r + 1 < R) mn[r + 1] = y.y * sc + mv[r + 1];
                 }
@@ -2409,7 +2416,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const bool widle = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= n;
                 const float m = s_m[f < n ? f : n - 1];
                 const float y = mlp128_upair_split<US, false>(s_up + UpairLds::kMlp2, v24.l3, m, m, sub,
-                                                              (float*)(s_part + rb * US * IL), itid, widle);
+                                                              (float*)(s_part + rb * US * ILB), itid, widle);
                 if (sub == 0 && f < n) s_m[f] = y;
             }
         } else if constexpr (kV24F32 && US > 1) {
@@ -2425,7 +2432,7 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
                 const int f1 = fa + 1 < n ? fa + 1 : fa;
                 const f32x2 m2 = {s_m[fa], s_m[f1]};
                 const f32x2 y = mlp128_split<US, false>(v24.g + kV24Mlp, v24.l3, m2, m2, sub,
-                                                        s_part + rb * US * IL, itid, widle);
+                                                        s_part + rb * US * ILB, itid, widle);
                 if (sub == 0 && f < n) {
                     s_m[f] = y.x;
                     if (f + 1 < n) s_m[f + 1] = y.y;
@@ -3499,6 +3506,7 @@ struct Plan {
     size_t lds;   // bytes of dynamic LDS
     int us = 1;   // unit split of the streaming kernel (fp32 decoder_v2_4, small batches)
     int wide = 1; // work-item lanes / 256 of the streaming kernel (fp64 decoder_v2_4, GNND_V24F64_WIDE)
+    bool iw3 = false;  // unit split in rounds of 192 item lanes (decode_kernel IW3)
     int ncomp = 1;                       // split graph: components per codeword (streaming)
     const GraphView* dviews = nullptr;   // device [ncomp] views of the plan's kind
 };
@@ -3563,6 +3571,13 @@ int v24f64_wide() {
 bool v24_upair_disabled() {
     static bool v = [] {
         const char* e = gnnd_tune_env("GNND_V24_UPAIR");
+        return e && e[0] == '0';
+    }();
+    return v;
+}
+bool v24_iw3_disabled() {
+    static bool v = [] {
+        const char* e = gnnd_tune_env("GNND_V24_IW3");
         return e && e[0] == '0';
     }();
     return v;
@@ -3780,6 +3795,14 @@ int make_plan(int model, int dtype, const gnnd_graph* gr, Plan* p, int64_t B = I
             p->lds = align16(p->lds) + (size_t)2 * us * GNND_BLOCK * 8 + 8 + wcm;
         }
     }
+    // unit split with a tile of 129..192 work items (toric-7: one component-codeword of 192
+    // edges, one per lane): rounds of three item waves, so no item wave (and none of its US - 1
+    // unit-split partners) sits at the barriers without work -- a quarter of the 256-lane
+    // form's waves
+    if ((p->us == 2 || p->us == 4) && !v24_iw3_disabled()) {
+        const size_t items = n * (size_t)g.C * g.G;
+        p->iw3 = items > 128 && items <= 192;
+    }
     return GNND_OK;
 }
 
@@ -3831,13 +3854,13 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
     // the streaming kernel: every component of a split graph in the same launch
     // persist: one workgroup per resident slot (occupancy x CUs), each looping over tiles
     // (decode_kernel's tile loop); split graphs never
-    auto go_s = [&](auto kern, int us = 1, int wide = 1, bool persist = false) -> int {
+    auto go_s = [&](auto kern, int us = 1, int wide = 1, bool persist = false, bool iw3 = false) -> int {
         if (p.lds > 64 * 1024)
             GNND_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds));
         int64_t grid = blocks * p.ncomp;
         if (grid > 0x7fffffff) return GNND_ERR_UNSUPPORTED;
-        const int il = (us == 8 ? 128 : GNND_BLOCK) * wide;  // unit_split_lanes<US>() * WIDE
+        const int il = iw3 ? 192 : (us == 8 ? 128 : GNND_BLOCK) * wide;  // decode_kernel's IL
         if (persist && p.ncomp == 1) {
             int per_cu = 0;
             GNND_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, il * us, p.lds));
@@ -3885,6 +3908,14 @@ int launch_decode(const Plan& p, const void* w, const void* x, void* out, int64_
         // bf16 I/O and decoder_v2_2's per-iteration readout: register-resident plans only
         return GNND_ERR_UNSUPPORTED;
     } else {
+        if constexpr (MODEL == GNND_V24 && R <= 2) {
+            if (p.iw3 && p.us == 4)
+                return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 4, 1, true>, 4, 1, false, true)
+                                : go_s(decode_kernel<MODEL, T, R, false, 4, 1, true>, 4, 1, false, true);
+            if (p.iw3 && p.us == 2)
+                return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 2, 1, true>, 2, 1, false, true)
+                                : go_s(decode_kernel<MODEL, T, R, false, 2, 1, true>, 2, 1, false, true);
+        }
         if constexpr (MODEL == GNND_V24 && sizeof(T) == 4 && R <= 2) {
             if (p.us == 8) return tape.ext ? go_s(decode_kernel<MODEL, T, R, true, 8>, 8)
                                            : go_s(decode_kernel<MODEL, T, R, false, 8>, 8);
