@@ -676,7 +676,7 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
     } else {
         softplus_taylor(h, d);
     }
-    __shared__ double part[kVtNC + 3];
+    __shared__ double part[kVtNC + 1];
     __shared__ int ncross0, ncross1, bad;
     double a[kVtNC];
     double p = W2;
@@ -687,16 +687,6 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
     }
     const double w2 = W1a * W1a, w4 = w2 * w2;
     const double s8 = group_sum_c<64>(fabs(W2) * (w4 * w4));
-    // SEL 0: the smooth function at the cell's two edges (lin units exactly h, the others
-    // log1p(e^h) -- what the polynomial holds), to check the tanh composition below
-    double fe[2] = {0.0, 0.0};
-    if constexpr (SEL == 0) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const double he = fma(W1a, c + (q ? 0.5 : -0.5) / INV, bp);
-            fe[q] = group_sum_c<64>(W2 * (lin ? he : log1p(exp(he))));
-        }
-    }
     const uint64_t cm = __builtin_amdgcn_ballot_w64(cross);
     const bool wide_cross = __builtin_amdgcn_ballot_w64(cross && fabs(W1a) > 4.0 * INV) != 0;
     if (k == 0) bad = 0;
@@ -705,8 +695,6 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
 #pragma unroll
         for (int i = 0; i < kVtNC; ++i) part[i] = a[i];
         part[kVtNC] = s8;
-        part[kVtNC + 1] = fe[0];
-        part[kVtNC + 2] = fe[1];
         ncross1 = __builtin_popcountll(cm);
     }
     if (k == 0) ncross0 = __builtin_popcountll(cm);
@@ -743,8 +731,9 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
             // composed here -- w = (f - f(c))/2 has no constant term, so tanh(w) = w - w^3/3 +
             // 2w^5/15 - 17w^7/315 is exact to r^8, and T = (t0 + tanh w)/(1 + t0 tanh w) by series
             // division (constant term 1).  No composed remainder bound is derived: the cell is
-            // valid only if the polynomial meets tanh of the directly summed f at both cell edges
-            // (where the r^8 term peaks) within 2e-14, on top of f's own bound above.
+            // valid only if T's polynomial meets tanh(P_f/2) of f's own polynomial P_f at both
+            // cell edges (where the r^8 terms peak) within 2e-14; P_f is within f's bound above
+            // (<= 1e-13) of f, and tanh halves that, so T stays within 7e-14 of tanh(f/2).
             double wv[kVtNC], w2v[kVtNC], w3v[kVtNC], w5v[kVtNC], w7v[kVtNC], tb[kVtNC], q[kVtNC];
             auto smul = [](const double* A, const double* B, double* C) {
                 for (int n2 = 0; n2 < kVtNC; ++n2) {
@@ -770,10 +759,12 @@ __global__ void __launch_bounds__(128) vtab_build_kernel(const double* w, double
 #pragma unroll
             for (int e2 = 0; e2 < 2; ++e2) {
                 const double r = (e2 ? 0.5 : -0.5) / INV;
-                double pv = q[kVtNC - 1];
-                for (int n2 = kVtNC - 2; n2 >= 0; --n2) pv = fma(pv, r, q[n2]);
-                const double te = tanh(0.5 * ((fe[e2] + part[kVtNC + 1 + e2]) + b2));
-                ok = ok && fabs(pv - te) <= 2e-14;
+                double pv = q[kVtNC - 1], pf = v[kVtNC - 1];
+                for (int n2 = kVtNC - 2; n2 >= 0; --n2) {
+                    pv = fma(pv, r, q[n2]);
+                    pf = fma(pf, r, v[n2]);
+                }
+                ok = ok && fabs(pv - tanh(0.5 * pf)) <= 2e-14;
             }
             for (int i = 0; i < kVtNC; ++i) v[i] = q[i];
         }

@@ -216,8 +216,8 @@ int gnnd_decode(const gnnd_graph* g, int model, int dtype, const void* d_w, cons
  * |S_v - m_e| <= 32 (64-byte cells: degree-7 Taylor polynomials about j/16; the readout MLP's
  * about j/32; up to 3 units crossing torch's Softplus threshold inside a cell are stored aside and
  * their jumps added exactly; a cell whose MLP remainder bound exceeds 1e-13, whose tanh series
- * misses the directly evaluated tanh(MLP/2) at a cell edge by more than 2e-14, or that holds more
- * crossings is marked invalid and its points take the 128 units), into a buffer of
+ * misses tanh(P/2) of the MLP's own cell polynomial P at a cell edge by more than 2e-14, or that
+ * holds more crossings is marked invalid and its points take the 128 units), into a buffer of
  * gnnd_prepared_weights_count_priors elements.  gnnd_decode
  * (fp64 V24, batches decoded one wave per item group) then reads a codeword's table where its
  * x_v equals a registered prior bit for bit and evaluates the 128 units elsewhere (other priors,
