@@ -145,6 +145,29 @@ def test_config3_toric5_v24_B65536(dtype):
         assert ((got > 0.5) == (ref > 0.5))[far].all()
 
 
+def test_config3_toric5_v24_B65536_prior_tables():
+    """Config 3 as the bench runs it: fp64 decoder_v2_4 at B = 65 536 with the batch's channel
+    priors registered (the variable-side and readout MLPs from the prepared tables) -- rtol
+    1e-10 and bit-exact decisions against the oracle on sampled codewords."""
+    import gnndecode as gd
+    w = _shipped('v24_toric_5')
+    m, H = _model('v24', 'toric_5', 15, w)
+    B = 65536
+    x, _ = gd.data.toric_batch(H, B, seed=26, device=DEV, dtype=torch.float64)
+    g = m.graph(x.device)
+    pri = gd.ops.channel_priors(g, x)
+    assert len(pri) == 10
+    m.set_channel_priors(pri)
+    g, out = _decode(m, x)
+    m.set_channel_priors(())
+    pick = _sample(B)
+    xs = _rows(x, B, g.N, pick).reshape(-1, 1)
+    ref = O.decode('v24', H, xs, 15, w).reshape(len(pick), g.V)
+    got = _rows(out, B, g.V, pick)
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-13)
+    assert ((got > 0.5) == (ref > 0.5)).all()
+
+
 def test_config5_toric7_v24_decode_B16384_fp64():
     """Config 5's architecture (decoder_v2_4 at L = 7, seeded reference init) decoded at
     B = 16 384 in fp64: bit-exact decisions on 64 sampled codewords."""

@@ -144,15 +144,16 @@ def _oracle(m, H, x):
     return O.decode('v24', H, x.cpu().numpy(), m.Nc, w)
 
 
-def test_decode_with_prior_tables_matches_oracle():
-    """B = 2048 (one wave per item group, the tables' plan): registered priors, codewords with
+@pytest.mark.parametrize('B', [2048, 777])
+def test_decode_with_prior_tables_matches_oracle(B):
+    """B = 2048 (512-lane workgroups, two items per lane per pass) and a ragged B = 777 (256-lane
+    workgroups, a partial last tile): registered priors, codewords with
     an unregistered prior, and codewords whose x_v vary per variable (those lanes evaluate the
     units) -- all equal to the oracle at rtol 1e-10 with the same hard decisions; the tables are
     really read (the outputs differ from the unit decode in the last bits) and the decode is
     bitwise reproducible."""
     import gnndecode as gd
     m, H = _model()
-    B = 2048
     x, _ = gd.data.toric_batch(H, B, seed=5, device=torch.device(DEV), dtype=torch.float64)
     g = m.graph(x.device)
     pri = gd.ops.channel_priors(g, x)
