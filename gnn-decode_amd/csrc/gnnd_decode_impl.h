@@ -2070,80 +2070,91 @@ decode_kernel(GraphView g0, const T* __restrict__ w, int nw, const T* __restrict
     // pass (rounds f0 and f0 + IL), their LDS reads, table fetches and check-MLP entries issued
     // together -- the variable-side MLP is one L2 round trip per edge, and one item per lane left
     // the waves waiting on it (SQ_WAIT_ANY 0.60, profiles/pmc_classes_v24_toric_5_T15_f64_ptab)
+#ifndef GNND_PT_ITEMS
+#define GNND_PT_ITEMS 2            // work items per lane per pass (2 or 3; 3 measured slower:
+#endif                             // 147 VGPRs = 3 waves per SIMD, or spills at 128 -- r06m)
     constexpr bool kPt2 = kV24F64 && US == 1 && !TAPE && R == 1;
     const bool pt2 = kPt2 && n_pt > 0;
     for (int it = 0; it < iters; ++it) {
         if constexpr (kPt2) {
-            // one pass: items A (round f0) and, when TWO, B (round f0 + IL); a wave with no live
-            // second item runs the one-item instantiation (no work on clamped copies)
-            auto pass2 = [&](int f0, auto twoC) {
-                constexpr bool TWO = decltype(twoC)::value;
-                const int fA = f0 + itid, fB = fA + IL;
-                const bool actA = fA < nItem, actB = TWO && fB < nItem;
-                const bool idleA = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= nItem;
-                const int fcA = actA ? fA : nItem - 1, fcB = actB ? fB : nItem - 1;
-                const int bA = fdiv(fcA, dItem), bB = TWO ? fdiv(fcB, dItem) : bA;
-                const int remA = fcA - bA * IC, remB = TWO ? fcB - bB * IC : remA;
-                const uint32_t svA = s_slot[remA], svB = TWO ? s_slot[remB] : svA;
-                T* mbA = s_m + bA * nslot + remA;
-                T* mbB = s_m + bB * nslot + remB;
-                const bool valA = (int)(svA >> 16) != E, valB = (int)(svB >> 16) != E;
-                const T mvA = *mbA, mvB = TWO ? *mbB : mvA;
-                const SumX<T> pA = s_sx[bA * V + GNND_DIDX((int)(svA & 0xffffu), V, GNND_DBG_VAR)];
-                const SumX<T> pB = TWO ? s_sx[bB * V + GNND_DIDX((int)(svB & 0xffffu), V, GNND_DBG_VAR)] : pA;
-                const T extA = pA.s - mvA, extB = pB.s - mvB;
-                const int vtoA = s_vto[bA], vtoB = TWO ? s_vto[bB] : vtoA;
-                const double* tbA = (const double*)wv + (vtoA >= 0 ? vtoA : kV24PriorOff);
-                const double* tbB = (const double*)wv + (vtoB >= 0 ? vtoB : kV24PriorOff);
-                const VtCell cA = vtab_fetch<kVtInvG, true>(tbA, extA);
-                VtCell cB;
-                if constexpr (TWO) cB = vtab_fetch<kVtInvG, true>(tbB, extB);
-                const T scA = s_xc[bA * C + (remA >> logG)];
-                const T scB = TWO ? s_xc[bB * C + (remB >> logG)] : scA;
-                // (a hit gives t = tanh(ggc1.mlp/2) itself; the units give the MLP output)
-                T aA = T(0), aB = T(0);
-                const bool hitA = vtab_finish<kVtInvG, true>(tbA, cA, extA, pA.x, aA);
-                bool hitB = false;
-                if constexpr (TWO) hitB = vtab_finish<kVtInvG, true>(tbB, cB, extB, pB.x, aB);
-                const bool needA = actA && valA && !hitA;
-                const bool needB = TWO && actB && valB && !hitB;
-                // (the wave evaluates the 128 units where a live lane's (u, x_v) has no table)
-                if (__builtin_amdgcn_ballot_w64(needA) != 0) {
-                    const T a2 = mlp128d_split<1, true>(wv + kV24Ggc1, s_bias, extA, pA.x, 0, s_pd, itid, idleA,
-                                                        s_tab, s_lin, s_wcm);
-                    if (needA) aA = a2;
+            // one pass: items i = 0 .. NI-1 of rounds f0 + i IL; a wave whose later rounds hold no
+            // live item runs the instantiation with fewer items (no work on clamped copies)
+            auto pass_n = [&](int f0, auto nC) {
+                constexpr int NI = decltype(nC)::value;
+                bool act[NI], val[NI], need[NI], hit[NI];
+                int bI[NI], rem[NI];
+                T* mb[NI];
+                T mv[NI], ext[NI], xs[NI], sc[NI], a[NI], tv[NI], y[NI];
+                const double* tb[NI];
+                VtCell cell[NI];
+                const bool idle0 = __builtin_amdgcn_readfirstlane(f0 + (itid & ~63)) >= nItem;
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    const int f = f0 + i * IL + itid;
+                    act[i] = f < nItem;
+                    const int fc = act[i] ? f : nItem - 1;
+                    bI[i] = fdiv(fc, dItem);
+                    rem[i] = fc - bI[i] * IC;
+                    const uint32_t sv = s_slot[rem[i]];
+                    mb[i] = s_m + bI[i] * nslot + rem[i];
+                    val[i] = (int)(sv >> 16) != E;
+                    mv[i] = *mb[i];
+                    const SumX<T> p = s_sx[bI[i] * V + GNND_DIDX((int)(sv & 0xffffu), V, GNND_DBG_VAR)];
+                    ext[i] = p.s - mv[i];
+                    xs[i] = p.x;
+                    const int vto = s_vto[bI[i]];
+                    tb[i] = (const double*)wv + (vto >= 0 ? vto : kV24PriorOff);
                 }
-                if constexpr (TWO) {
-                    if (__builtin_amdgcn_ballot_w64(needB) != 0) {
-                        const T a2 = mlp128d_split<1, true>(wv + kV24Ggc1, s_bias, extB, pB.x, 0, s_pd, itid, false,
-                                                            s_tab, s_lin, s_wcm);
-                        if (needB) aB = a2;
+#pragma unroll
+                for (int i = 0; i < NI; ++i) cell[i] = vtab_fetch<kVtInvG, true>(tb[i], ext[i]);
+#pragma unroll
+                for (int i = 0; i < NI; ++i) sc[i] = s_xc[bI[i] * C + (rem[i] >> logG)];
+                // (a hit gives t = tanh(ggc1.mlp/2) itself; the units give the MLP output)
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    a[i] = T(0);
+                    hit[i] = vtab_finish<kVtInvG, true>(tb[i], cell[i], ext[i], xs[i], a[i]);
+                    need[i] = act[i] && val[i] && !hit[i];
+                }
+                // (the wave evaluates the 128 units where a live lane's (u, x_v) has no table)
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    if (__builtin_amdgcn_ballot_w64(need[i]) != 0) {
+                        const T a2 = mlp128d_split<1, true>(wv + kV24Ggc1, s_bias, ext[i], xs[i], 0, s_pd, itid,
+                                                            i == 0 ? idle0 : false, s_tab, s_lin, s_wcm);
+                        if (need[i]) a[i] = a2;
                     }
                 }
-                const T tvA = valA ? (hitA ? aA : tanh_half_fast(aA)) : T(0);
-                const T tvB = TWO && valB ? (hitB ? aB : tanh_half_fast(aB)) : T(0);
-                const T ScA = group_sum(tvA, G);
-                const T ScB = TWO ? group_sum(tvB, G) : T(0);
-                const T uA = ScA - tvA, uB = ScB - tvB;
-                T yA, yB = T(0);
-                if (ctab_ok) {               // (uniform)
-                    yA = ctab_eval(s_ctab, uA, R8);
-                    if constexpr (TWO) yB = ctab_eval(s_ctab, uB, R8);
-                } else {
-                    yA = mlp128d_split<1, false>(wv + kV24Ggc2, s_bias + 128, uA, uA, 0, s_pd, itid, idleA, s_tab,
-                                                 s_lin + 4, s_wcm + 128);
-                    if constexpr (TWO)
-                        yB = mlp128d_split<1, false>(wv + kV24Ggc2, s_bias + 128, uB, uB, 0, s_pd, itid, false, s_tab,
-                                                     s_lin + 4, s_wcm + 128);
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    tv[i] = val[i] ? (hit[i] ? a[i] : tanh_half_fast(a[i])) : T(0);
+                    const T Sc = group_sum(tv[i], G);
+                    a[i] = Sc - tv[i];                       // the check-side MLP's input u
                 }
-                if (actA) *mbA = yA * scA + mvA;
-                if (TWO && actB) *mbB = yB * scB + mvB;
+                if (ctab_ok) {               // (uniform)
+#pragma unroll
+                    for (int i = 0; i < NI; ++i) y[i] = ctab_eval(s_ctab, a[i], R8);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+                        y[i] = mlp128d_split<1, false>(wv + kV24Ggc2, s_bias + 128, a[i], a[i], 0, s_pd, itid,
+                                                       i == 0 ? idle0 : false, s_tab, s_lin + 4, s_wcm + 128);
+                }
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+                    if (act[i]) *mb[i] = y[i] * sc[i] + mv[i];
             };
-            for (int f0 = 0; f0 < (pt2 ? nItem : 0); f0 += 2 * IL) {
-                if (__builtin_amdgcn_readfirstlane(f0 + IL + (itid & ~63)) < nItem)
-                    pass2(f0, std::true_type{});
-                else
-                    pass2(f0, std::false_type{});
+            constexpr int kNI = GNND_PT_ITEMS;
+            for (int f0 = 0; f0 < (pt2 ? nItem : 0); f0 += kNI * IL) {
+                // live rounds in this wave's pass (uniform)
+                int live = 1;
+                for (int i = 1; i < kNI; ++i)
+                    live += __builtin_amdgcn_readfirstlane(f0 + i * IL + (itid & ~63)) < nItem ? 1 : 0;
+                if constexpr (kNI >= 3) {
+                    if (live == 3) { pass_n(f0, std::integral_constant<int, 3>{}); continue; }
+                }
+                if (live == 2) pass_n(f0, std::integral_constant<int, 2>{});
+                else pass_n(f0, std::integral_constant<int, 1>{});
             }
         }
         for (int f0 = 0; f0 < (pt2 ? 0 : nItem); f0 += IL) {
