@@ -218,6 +218,27 @@ def test_decision_errors_kernel_on_decoder_outputs(golden):
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_v24_unit_split_192_lane_rounds_bit_identical(dtype):
+    """toric-7 (a component-codeword holds 192 edges): the unit split runs 192-lane rounds
+    (decode_kernel IW3: US = 4 at B*ncomp <= 256, US = 2 at <= 512) -- slices decoded alone give
+    the same bits as the B = 1 024 decode (US = 1, whole graph)."""
+    import gnndecode as gd
+    H = gd.codes.get_code('toric_7')
+    torch.manual_seed(7)
+    m = gd.MODELS['v24'](15, H).to(DEV).eval()
+    if dtype == torch.float64:
+        m = m.double()
+    B = 1024
+    x, _ = gd.data.toric_batch(H, B, seed=8, device=DEV, dtype=dtype)
+    _, full = _decode(m, x)
+    full = full.view(B, -1)
+    xb = x.view(B, -1)
+    for b0, n in ((0, 128), (128, 200), (700, 77), (1023, 1)):
+        _, part = _decode(m, xb[b0:b0 + n].reshape(-1, 1).contiguous())
+        assert torch.equal(part.view(n, -1), full[b0:b0 + n]), (b0, n)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
 def test_v24_unit_split_bit_identical(dtype):
     """decoder_v2_4 small-batch unit split: decode_kernel runs US = 4 (B*ncomp <= 256), 2
     (<= 512) waves per item wave at one codeword per workgroup (fp32 also US = 8 when a
